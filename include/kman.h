@@ -1,0 +1,168 @@
+/*
+ * kman.h — C ABI of the MI355X (gfx950) k-mer extract / sort / join engine.
+ *
+ * The reference (ggirelli/kman, package kmermaid 1.0.0) is pure Python and has
+ * no FFI of its own; its "operator API" is the class surface
+ * FastaBatcher.do / Batch.sorted / Crawler.do_batch / KJoiner.join.  Every
+ * entry point below replaces the arithmetic of one of those functions and is
+ * what kman_amd/_native.py binds through ctypes:
+ *
+ *   kman_parse_fasta   SmartFastaParser.parse            kmermaid/parsers.py:86-128
+ *                      + record name rule                 kmermaid/batcher.py:551
+ *   kman_extract       Sequence.yield_kmers / kmerator    kmermaid/seq.py:285-359
+ *                      + alphabet check / mkrc            kmermaid/seq.py:279,318,500-509
+ *   kman_sort          Batch.sorted (stable, by .seq)     kmermaid/batch.py:156-168
+ *                      + BatcherBase.write_all re-sort    kmermaid/batcher.py:133-153,392
+ *   kman_rle_count     Crawler.do_batch + join_sequence_count
+ *                                                         kmermaid/join.py:95-130,266-285
+ *   kman_rle_uniq      Crawler.do_batch + join_unique     kmermaid/join.py:95-130,244-263
+ *   kman_merge_runs    Crawler.do_records heapq.merge     kmermaid/join.py:63-93
+ *   kman_format_*      the output writers                 kmermaid/join.py:262,284; seq.py:489-495
+ *
+ * Conventions
+ *   - Plain C, no exceptions cross the boundary.  Every call returns 0 on
+ *     success or a negative KMAN_E* code; kman_last_error() has the message.
+ *   - Device buffers are raw device pointers obtained from kman_malloc and
+ *     owned by the caller (freed with kman_free).  Host buffers are borrowed
+ *     for the duration of the call.
+ *   - One context per GPU and host thread; a context is not re-entrant.  All
+ *     device work of a context runs in order on its own HIP stream.
+ *   - Keys are k-mers packed 2 bits per base MSB-first (A=0 C=1 G=2 T=3), so
+ *     numeric order of keys == the reference's Python str order of the
+ *     upper-case sequences (for a fixed k <= 32).
+ *   - "pos" payloads are (global base index << 1) | strand, where the global
+ *     base index addresses the cleaned, concatenated sequence of all records
+ *     (see kman_parse_fasta) and strand 1 means the '-' (reverse-complement)
+ *     record of seq.py:274-282.
+ */
+#ifndef KMAN_H
+#define KMAN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KMAN_ABI_VERSION 1
+
+/* error codes */
+#define KMAN_OK 0
+#define KMAN_EINVAL (-1)   /* bad argument (maps to AssertionError like the reference) */
+#define KMAN_EHIP (-2)     /* HIP runtime error */
+#define KMAN_ENOMEM (-3)   /* device or host allocation failed */
+#define KMAN_EFORMAT (-4)  /* input is not parsable FASTA (parsers.py:105-107) */
+#define KMAN_ETIMEOUT (-5) /* a device-side wait exceeded its bound (engine bug) */
+#define KMAN_ECOMM (-6)    /* RCCL error */
+#define KMAN_ECAP (-7)     /* output capacity too small; *needed reports the size */
+
+/* kman_extract flags */
+#define KMAN_RC 1u          /* also emit reverse complements (kmer -r, seq.py:274-282) */
+#define KMAN_WANT_POS 2u    /* also emit the pos payload (uniq / batch modes) */
+#define KMAN_CANONICAL 4u   /* emit min(fwd, rc) instead (not in the reference) */
+
+typedef struct kman_ctx kman_ctx;
+
+/* parse result (host struct) */
+typedef struct {
+    uint64_t n_bases;   /* cleaned sequence characters over all records */
+    uint64_t n_records; /* header lines ('>' at a line start) */
+} kman_parse_info;
+
+/* ------------------------------------------------------------------ context */
+int kman_abi_version(void);
+int kman_device_count(int *n);
+int kman_create(int device, kman_ctx **out);
+void kman_destroy(kman_ctx *ctx);
+const char *kman_last_error(const kman_ctx *ctx);
+int kman_sync(kman_ctx *ctx);
+
+/* ------------------------------------------------------------------- memory */
+int kman_malloc(kman_ctx *ctx, void **dptr, size_t bytes);
+int kman_free(kman_ctx *ctx, void *dptr);
+int kman_host_alloc(kman_ctx *ctx, void **hptr, size_t bytes); /* pinned */
+int kman_host_free(kman_ctx *ctx, void *hptr);
+int kman_memcpy_h2d(kman_ctx *ctx, void *dst, const void *src, size_t bytes);
+int kman_memcpy_d2h(kman_ctx *ctx, void *dst, const void *src, size_t bytes);
+int kman_memset(kman_ctx *ctx, void *dst, int value, size_t bytes);
+
+/* ------------------------------------------------------------------- timing
+ * Optional per-kernel timing with HIP events recorded on the context's own
+ * stream around every launch (bench.py's live roofline).  Tags: "parse",
+ * "extract", "sort_hist", "sort_pass", "rle_count", "rle_uniq".
+ * kman_timing_query synchronises and returns launches and summed ms. */
+int kman_timing_enable(kman_ctx *ctx, int enable);
+int kman_timing_query(kman_ctx *ctx, const char *tag, uint64_t *launches, double *total_ms);
+
+/* ------------------------------------------------------------------- stages */
+
+/* FASTA text -> cleaned base codes + record table  (parsers.py:86-128)
+ *   d_text     n_bytes of FASTA text (uncompressed)
+ *   d_codes    out, capacity >= n_bytes + 64: one byte per kept sequence char:
+ *              bits 0-1 base (A/a=0 C/c=1 G/g=2 T/t=3), bit 2 set = not ACGT,
+ *              bit 3 set = first char of a record.  64 pad bytes (value 4)
+ *              follow the last code.
+ *   d_rec_hdr  out, byte offset of each record's '>'
+ *   d_rec_seq  out, global base index of each record's first char
+ *   rec_cap    capacity of the two record arrays; KMAN_ECAP if exceeded
+ * Returns KMAN_EFORMAT when no line starts with '>' (empty file included). */
+int kman_parse_fasta(kman_ctx *ctx, const uint8_t *d_text, uint64_t n_bytes, uint8_t *d_codes,
+                     uint64_t *d_rec_hdr, uint64_t *d_rec_seq, uint64_t rec_cap,
+                     kman_parse_info *info);
+
+/* Number of k-mers kman_extract will emit (valid windows x (RC ? 2 : 1)). */
+int kman_count_kmers(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k,
+                     uint32_t flags, uint64_t *n_kmers);
+
+/* base codes -> packed keys in stream order (seq.py:285-328), k in [2, 32].
+ *   d_keys     out, capacity cap keys
+ *   d_pos      out (flags & KMAN_WANT_POS), u32 if pos_bytes == 4 else u64
+ *   d_hist     optional out (may be NULL): the radix-digit histograms that
+ *              kman_sort would compute, for the pass plan of kman_sort_plan(2k)
+ *              (npass x 256 u64, must be zeroed by the caller) */
+int kman_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k,
+                 uint32_t flags, uint64_t *d_keys, void *d_pos, uint32_t pos_bytes, uint64_t cap,
+                 uint64_t *d_hist, uint64_t *n_kmers);
+
+/* LSD radix sort plan for keys with key_bits significant bits:
+ * npass digit passes of bits[i] bits each, starting at bit shift[i]. */
+int kman_sort_plan(uint32_t key_bits, uint32_t *npass, uint32_t *shift, uint32_t *bits);
+
+/* Stable LSD radix sort (onesweep, decoupled look-back) of n keys with an
+ * optional payload (val_bytes 0, 4 or 8).  Ping-pongs between the two
+ * buffers; *result_in_alt is set to 1 when the sorted data ended in the alt
+ * buffers.  d_hist may be NULL (then computed) or the histogram filled by
+ * kman_extract for the same key_bits.  Stability == the reference's Timsort
+ * stability (batch.py:165). */
+int kman_sort(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, void *d_vals, void *d_vals_alt,
+              uint32_t val_bytes, uint64_t n, uint32_t key_bits, const uint64_t *d_hist,
+              int *result_in_alt);
+
+/* Run-length count of sorted keys (join.py:95-130 + 266-285):
+ * d_ukeys[j], d_counts[j] (u32 if count_bytes == 4 else u64). */
+int kman_rle_count(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint64_t *d_ukeys,
+                   void *d_counts, uint32_t count_bytes, uint64_t *n_unique);
+
+/* Keys that occur exactly once, with their payload (join.py:244-263). */
+int kman_rle_uniq(kman_ctx *ctx, const uint64_t *d_keys, const void *d_vals, uint32_t val_bytes,
+                  uint64_t n, uint64_t *d_okeys, void *d_ovals, uint64_t *n_out);
+
+/* ------------------------------------------------------------- formatting
+ * Host-side writers that produce the reference's exact bytes.  They run on
+ * host threads over host copies of the device results.
+ *   names      concatenated record names, name r at names[name_off[r] .. name_off[r+1])
+ *   rec_seq    host copy of d_rec_seq (sorted ascending)
+ * Each returns the number of bytes written to out (<= cap) in *used, or
+ * KMAN_ECAP with the required size in *used. */
+int kman_format_count(const uint64_t *ukeys, const void *counts, uint32_t count_bytes, uint64_t n,
+                      uint32_t k, char *out, size_t cap, size_t *used, int threads);
+int kman_format_uniq(const uint64_t *keys, const void *pos, uint32_t pos_bytes, uint64_t n,
+                     uint32_t k, const char *names, const uint64_t *name_off,
+                     const uint64_t *rec_seq, uint64_t n_records, char *out, size_t cap,
+                     size_t *used, int threads);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KMAN_H */

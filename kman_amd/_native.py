@@ -1,0 +1,137 @@
+"""ctypes binding of libkman.so (the C ABI declared in include/kman.h).
+
+This module is the only place Python touches the native library.  Loading is
+strict: if the in-tree ``kman_amd/lib/libkman.so`` is missing the import of any
+engine entry point raises — there is no CPU fallback on the product path.
+
+Error mapping follows the reference: argument errors the reference raises as
+``AssertionError`` (k <= 1, empty FASTA, ...) stay ``AssertionError``; device
+and runtime failures become ``RuntimeError``.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from ctypes import POINTER, c_char_p, c_int, c_size_t, c_uint32, c_uint64, c_void_p
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("KMAN_LIB", os.path.join(HERE, "lib", "libkman.so"))
+
+KMAN_OK = 0
+KMAN_EINVAL = -1
+KMAN_EHIP = -2
+KMAN_ENOMEM = -3
+KMAN_EFORMAT = -4
+KMAN_ETIMEOUT = -5
+KMAN_ECOMM = -6
+KMAN_ECAP = -7
+
+KMAN_RC = 1
+KMAN_WANT_POS = 2
+KMAN_CANONICAL = 4
+
+
+class ParseInfo(ctypes.Structure):
+    _fields_ = [("n_bases", c_uint64), ("n_records", c_uint64)]
+
+
+# name -> (restype, argtypes); every symbol include/kman.h declares
+SIGNATURES = {
+    "kman_abi_version": (c_int, []),
+    "kman_device_count": (c_int, [POINTER(c_int)]),
+    "kman_create": (c_int, [c_int, POINTER(c_void_p)]),
+    "kman_destroy": (None, [c_void_p]),
+    "kman_last_error": (c_char_p, [c_void_p]),
+    "kman_sync": (c_int, [c_void_p]),
+    "kman_malloc": (c_int, [c_void_p, POINTER(c_void_p), c_size_t]),
+    "kman_free": (c_int, [c_void_p, c_void_p]),
+    "kman_host_alloc": (c_int, [c_void_p, POINTER(c_void_p), c_size_t]),
+    "kman_host_free": (c_int, [c_void_p, c_void_p]),
+    "kman_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+    "kman_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+    "kman_memset": (c_int, [c_void_p, c_void_p, c_int, c_size_t]),
+    "kman_timing_enable": (c_int, [c_void_p, c_int]),
+    "kman_timing_query": (c_int, [c_void_p, c_char_p, POINTER(c_uint64), POINTER(ctypes.c_double)]),
+    "kman_parse_fasta": (
+        c_int,
+        [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_void_p, c_uint64, POINTER(ParseInfo)],
+    ),
+    "kman_count_kmers": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, POINTER(c_uint64)]),
+    "kman_extract": (
+        c_int,
+        [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p,
+         POINTER(c_uint64)],
+    ),
+    "kman_sort_plan": (c_int, [c_uint32, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]),
+    "kman_sort": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, POINTER(c_int)],
+    ),
+    "kman_rle_count": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, POINTER(c_uint64)]),
+    "kman_rle_uniq": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, POINTER(c_uint64)],
+    ),
+    "kman_format_count": (
+        c_int,
+        [c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_size_t, POINTER(c_size_t), c_int],
+    ),
+    "kman_format_uniq": (
+        c_int,
+        [c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p,
+         c_size_t, POINTER(c_size_t), c_int],
+    ),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def header_symbols() -> list:
+    """Function names declared in include/kman.h (parsed, for the ABI test)."""
+    import re
+
+    path = os.path.join(os.path.dirname(HERE), "include", "kman.h")
+    with open(path) as fh:
+        text = fh.read()
+    return sorted(set(re.findall(r"\b(kman_[a-z0-9_]+)\s*\(", text)))
+
+
+def lib() -> ctypes.CDLL:
+    """Load libkman.so once; raise loudly if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.isfile(LIB_PATH):
+                raise RuntimeError(
+                    "libkman.so not found at %s: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                    "(the MI355X engine has no CPU fallback)" % LIB_PATH
+                )
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(ctx, rc: int, what: str) -> None:
+    if rc == KMAN_OK:
+        return
+    msg = lib().kman_last_error(ctx).decode(errors="replace") if ctx else ""
+    if rc in (KMAN_EINVAL, KMAN_EFORMAT):
+        raise AssertionError(msg or what)
+    if rc == KMAN_ENOMEM:
+        raise MemoryError("%s: %s" % (what, msg))
+    raise RuntimeError("%s failed (%d): %s" % (what, rc, msg))
+
+
+def device_count() -> int:
+    n = c_int(0)
+    lib().kman_device_count(ctypes.byref(n))
+    return n.value

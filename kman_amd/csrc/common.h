@@ -1,0 +1,244 @@
+// common.h — shared device helpers for the kman gfx950 kernels.
+//
+// Everything here is wave64-native: lane masks are 64-bit, scans use
+// 6-step __shfl_up ladders, block scans combine wave totals through LDS.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <string>
+#include <type_traits>
+#include <vector>
+
+#include "../../include/kman.h"
+
+#define KMAN_DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------- context
+struct kman_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    // look-back scratch: status words (flag:2 | epoch:6 | value:56)
+    uint64_t *d_status = nullptr;
+    size_t status_words = 0;
+    uint32_t *d_counters = nullptr; // one dynamic-tile counter per epoch (64)
+    uint32_t *d_err = nullptr;      // device-side error word (spin timeouts)
+    uint32_t epoch = 63;            // last epoch handed out; wraps 63 -> 1 with a reset
+    // small pinned host area for results
+    uint64_t *h_small = nullptr;
+    // generic device scratch
+    void *d_scratch = nullptr;
+    size_t scratch_bytes = 0;
+    // optional launch timing (kman_timing_*)
+    bool timing = false;
+    struct TimedLaunch {
+        const char *tag;
+        hipEvent_t a, b;
+    };
+    std::vector<TimedLaunch> launches;
+    std::vector<hipEvent_t> event_pool;
+};
+
+// RAII launch timer: records an event pair around the launches in its scope.
+struct KTimer {
+    kman_ctx *ctx;
+    size_t idx;
+    KTimer(kman_ctx *c, const char *tag);
+    ~KTimer();
+};
+
+int kman_fail(kman_ctx *ctx, int code, const char *fmt, ...);
+int kman_hip_fail(kman_ctx *ctx, hipError_t e, const char *what);
+// status buffer with >= words entries; returns epoch to use (1..63) and the
+// counter for dynamic tile ids of that epoch.
+int kman_lookback_begin(kman_ctx *ctx, size_t words, uint32_t *epoch, uint32_t **counter);
+int kman_scratch(kman_ctx *ctx, size_t bytes, void **p);
+int kman_check_device_error(kman_ctx *ctx);
+// synchronises; reads the inclusive value of the last tile of the most recent
+// look-back launch (checks its epoch) and the device error word.
+int kman_lookback_total(kman_ctx *ctx, uint64_t n_tiles, uint64_t *total);
+
+#define HIP_TRY(ctx, expr)                                      \
+    do {                                                        \
+        hipError_t _e = (expr);                                 \
+        if (_e != hipSuccess) return kman_hip_fail(ctx, _e, #expr); \
+    } while (0)
+
+#define KMAN_TRY(expr)              \
+    do {                            \
+        int _r = (expr);            \
+        if (_r != KMAN_OK) return _r; \
+    } while (0)
+
+// ------------------------------------------------------------ status words
+constexpr uint64_t ST_AGG = 1ull;
+constexpr uint64_t ST_INCL = 2ull;
+constexpr uint64_t ST_VMASK = (1ull << 56) - 1;
+constexpr uint32_t SPIN_LIMIT = 1u << 20; // ~1 s of polling; a hit is an engine bug
+
+// true when this waiter must give up: its own bound is spent, or another wave
+// already flagged an error (so one fault does not cascade into serial timeouts)
+KMAN_DEV bool spin_give_up(uint32_t &spins, uint32_t *err, uint32_t code) {
+    ++spins;
+    if ((spins & 255u) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return true;
+    if (spins > SPIN_LIMIT) {
+        atomicOr(err, code);
+        return true;
+    }
+    return false;
+}
+
+KMAN_DEV uint64_t st_make(uint64_t flag, uint32_t epoch, uint64_t v) {
+    return (flag << 62) | ((uint64_t)epoch << 56) | (v & ST_VMASK);
+}
+KMAN_DEV void st_store(uint64_t *p, uint64_t w) {
+    __hip_atomic_store(p, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+KMAN_DEV uint64_t st_load(const uint64_t *p) {
+    return __hip_atomic_load(const_cast<uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+KMAN_DEV uint64_t st_flag(uint64_t w, uint32_t epoch) {
+    return (((w >> 56) & 63u) == epoch) ? (w >> 62) : 0ull;
+}
+
+// --------------------------------------------------------------- lanes
+KMAN_DEV int lane_id() { return __lane_id(); }
+KMAN_DEV uint64_t lanemask_lt() {
+    const int l = lane_id();
+    return l ? (~0ull >> (64 - l)) : 0ull;
+}
+
+template <typename T>
+KMAN_DEV T shfl_up_any(T v, int d) {
+    static_assert(sizeof(T) % 4 == 0, "32-bit granular");
+    constexpr int W = sizeof(T) / 4;
+    uint32_t w[W];
+    memcpy(w, &v, sizeof(T));
+#pragma unroll
+    for (int i = 0; i < W; i++) w[i] = (uint32_t)__shfl_up((int)w[i], d, 64);
+    T r;
+    memcpy(&r, w, sizeof(T));
+    return r;
+}
+
+template <typename T>
+KMAN_DEV T shfl_any(T v, int src) {
+    static_assert(sizeof(T) % 4 == 0, "32-bit granular");
+    constexpr int W = sizeof(T) / 4;
+    uint32_t w[W];
+    memcpy(w, &v, sizeof(T));
+#pragma unroll
+    for (int i = 0; i < W; i++) w[i] = (uint32_t)__shfl((int)w[i], src, 64);
+    T r;
+    memcpy(&r, w, sizeof(T));
+    return r;
+}
+
+// Inclusive scan across the 64 lanes; op(a, b) with a the earlier element.
+template <typename T, typename Op>
+KMAN_DEV T wave_inclusive_scan(T v, Op op) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        T o = shfl_up_any(v, d);
+        if (lane >= d) v = op(o, v);
+    }
+    return v;
+}
+
+// Exclusive block scan for NT threads (NT multiple of 64, <= 1024).
+// lds must hold NT/64 elements.  Returns the exclusive prefix; *total (if not
+// null) receives the block aggregate in every thread.
+template <int NT, typename T, typename Op>
+KMAN_DEV T block_exclusive_scan(T v, Op op, T identity, T *lds, T *total) {
+    constexpr int NW = NT / 64;
+    const int lane = lane_id();
+    const int w = threadIdx.x >> 6;
+    T inc = wave_inclusive_scan(v, op);
+    if (lane == 63) lds[w] = inc;
+    __syncthreads();
+    if (w == 0) {
+        T x = lane < NW ? lds[lane] : identity;
+        x = wave_inclusive_scan(x, op);
+        if (lane < NW) lds[lane] = x;
+    }
+    __syncthreads();
+    T ex = shfl_up_any(inc, 1);
+    if (lane == 0) ex = identity;
+    T res = w ? op(lds[w - 1], ex) : ex;
+    if (total) *total = lds[NW - 1];
+    __syncthreads();
+    return res;
+}
+
+struct SumU64 {
+    KMAN_DEV uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; }
+};
+struct SumU32 {
+    KMAN_DEV uint32_t operator()(uint32_t a, uint32_t b) const { return a + b; }
+};
+
+// ------------------------------------------------------ decoupled look-back
+// Called by ONE full wave of the tile (all 64 lanes active).  Publishes the
+// tile aggregate, looks back over up to 64 predecessors per round (one status
+// word per lane, sc1 loads), publishes the inclusive prefix and returns the
+// exclusive prefix (wave-uniform).  op: 0 = sum, 1 = max.
+template <int OP>
+KMAN_DEV uint64_t wave_lookback(uint64_t *status, int64_t tile, uint64_t agg, uint32_t epoch,
+                                uint32_t *err) {
+    const int lane = lane_id();
+    if (tile == 0) {
+        if (lane == 0) st_store(&status[0], st_make(ST_INCL, epoch, agg));
+        return 0;
+    }
+    if (lane == 0) st_store(&status[tile], st_make(ST_AGG, epoch, agg));
+    uint64_t excl = 0;
+    int64_t end = tile; // exclusive upper bound of the window still to fold
+    uint32_t spins = 0;
+    for (;;) {
+        const int64_t j = end - 1 - lane;
+        uint64_t w = 0, f = ST_INCL;
+        if (j >= 0) {
+            w = st_load(&status[j]);
+            f = st_flag(w, epoch);
+        }
+        const uint64_t notready = __ballot(f == 0);
+        const uint64_t incl = __ballot(f == ST_INCL && j >= 0);
+        // lanes 0..first_incl must all be ready; fold them
+        const int first_incl = incl ? __ffsll((unsigned long long)incl) - 1 : 64;
+        const uint64_t need = first_incl == 64 ? ~0ull : (~0ull >> (63 - first_incl));
+        if (notready & need) {
+            if (spin_give_up(spins, err, 1u)) break;
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint64_t v = (j >= 0 && (need >> lane) & 1ull) ? (w & ST_VMASK) : 0ull;
+        // wave reduce
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            uint64_t o = shfl_any(v, lane ^ d);
+            v = OP == 0 ? v + o : (v > o ? v : o);
+        }
+        excl = OP == 0 ? excl + v : (excl > v ? excl : v);
+        if (first_incl < 64 || end - 64 <= 0) break;
+        end -= 64;
+    }
+    const uint64_t inc = OP == 0 ? excl + agg : (excl > agg ? excl : agg);
+    if (lane == 0) st_store(&status[tile], st_make(ST_INCL, epoch, inc));
+    return excl;
+}
+
+// dynamic tile id: tiles are numbered in the order they start, so every
+// predecessor of a tile is resident or finished (forward progress).
+KMAN_DEV int64_t grab_tile(uint32_t *counter, uint32_t *lds_slot) {
+    if (threadIdx.x == 0) *lds_slot = atomicAdd(counter, 1u);
+    __syncthreads();
+    const int64_t t = *lds_slot;
+    __syncthreads();
+    return t;
+}
+
+inline uint64_t ceil_div(uint64_t a, uint64_t b) { return (a + b - 1) / b; }

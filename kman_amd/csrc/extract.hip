@@ -1,0 +1,297 @@
+// extract.hip — sliding-window k-mer enumeration on the GPU.
+//
+// Restates Sequence.yield_kmers (kmermaid/seq.py:285-328) over the cleaned
+// codes written by kman_parse_fasta:
+//   * every window [i, i+k) of a record is visited in order (seq.py:317);
+//   * the window is skipped unless all k chars are in "ACGT" after upper()
+//     (seq.py:313,318 -> om.check_ab; kmer.is_ab_checked, batcher.py:560);
+//   * a kept window yields KMer(+) and, with -r, KMer(-) = mkrc(window) with
+//     the same coordinates (seq.py:274-282), in that order.
+// Keys are packed 2 bits/base MSB-first, so key order == Python str order of
+// the upper-case window (A<C<G<T).  Output order == the reference's stream
+// order (record, position, strand): tiles are compacted in order with a
+// decoupled look-back over tile counts.
+//
+// Layout per tile: 256 threads x EI consecutive window starts (EI = 16, or 8
+// with -r so a tile emits at most 4096 keys).  The tile's codes (+64 halo) are
+// staged in LDS with 16-byte loads; each thread rolls its windows from LDS;
+// keys are staged in LDS at their compacted tile offsets and written out
+// coalesced.  The radix-digit histograms of every sort pass are accumulated in
+// LDS across the tiles a persistent block processes and flushed once per
+// block, so kman_sort needs no histogram pass over the keys.
+//
+// Algorithmic bytes: 1 B code read + 8 B key write (+ 4/8 B pos) per k-mer.
+#include "common.h"
+
+namespace {
+
+constexpr int ET = 256;
+constexpr int MAXPASS = 8;
+
+struct Plan {
+    int npass;
+    uint8_t shift[MAXPASS];
+    uint8_t bits[MAXPASS];
+};
+
+struct NoPos {};
+
+template <int EI>
+KMAN_DEV void stage_codes(const uint8_t *__restrict__ codes, uint64_t n_bases, uint64_t tb, uint8_t *s) {
+    constexpr int BYTES = ET * EI + 64;
+    const uint64_t limit = n_bases + 64;  // padded region is valid memory, value 4
+    for (int v = threadIdx.x; v < BYTES / 16; v += ET) {
+        const uint64_t off = tb + (uint64_t)v * 16;
+        if (off + 16 <= limit) {
+            *reinterpret_cast<uint4 *>(s + v * 16) = *reinterpret_cast<const uint4 *>(codes + off);
+        } else {
+#pragma unroll
+            for (int b = 0; b < 16; b++) s[v * 16 + b] = (off + b < limit) ? codes[off + b] : 4;
+        }
+    }
+}
+
+// Roll the EI windows starting at s[base .. base+EI) (k from LDS bytes).
+template <int EI, bool CANON>
+KMAN_DEV uint32_t roll(const uint8_t *s, int base, int k, uint64_t mask, uint64_t p0, uint64_t n_bases,
+                       uint64_t (&kf)[EI], uint64_t (&kr)[EI]) {
+    uint64_t f = 0, r = 0;
+    uint32_t run = 0;
+    const int rsh = 2 * k - 2;
+    for (int q = 0; q < k - 1; q++) {
+        const uint32_t c = s[base + q];
+        run = (c & 8) ? 0 : run;
+        run = (c & 4) ? 0 : run + 1;
+        f = (f << 2) | (c & 3);
+        r = (r >> 2) | ((uint64_t)(3 - (c & 3)) << rsh);
+    }
+    uint32_t valid = 0;
+#pragma unroll
+    for (int j = 0; j < EI; j++) {
+        const uint32_t c = s[base + k - 1 + j];
+        run = (c & 8) ? 0 : run;
+        run = (c & 4) ? 0 : run + 1;
+        f = (f << 2) | (c & 3);
+        r = (r >> 2) | ((uint64_t)(3 - (c & 3)) << rsh);
+        const uint64_t fm = f & mask;
+        if (CANON) {
+            kf[j] = fm < r ? fm : r;
+        } else {
+            kf[j] = fm;
+            kr[j] = r;
+        }
+        valid |= (uint32_t)(run >= (uint32_t)k && p0 + j < n_bases) << j;
+    }
+    return valid;
+}
+
+template <int EI, bool RC, bool CANON, typename P>
+__global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__ codes, uint64_t n_bases,
+                                                     uint64_t n_tiles, int k, uint64_t *__restrict__ keys,
+                                                     P *__restrict__ pos, uint64_t *__restrict__ status,
+                                                     uint32_t *__restrict__ counter, uint32_t epoch,
+                                                     uint32_t *__restrict__ err, uint64_t *__restrict__ hist,
+                                                     Plan plan) {
+    constexpr int TILE = ET * EI;
+    constexpr int KPT = RC && !CANON ? 2 * EI : EI;  // keys per thread, max
+    constexpr int MAXKEYS = ET * KPT;
+    constexpr bool HAS_POS = !std::is_same<P, NoPos>::value;
+    __shared__ __attribute__((aligned(16))) uint8_t scodes[TILE + 64];
+    __shared__ __attribute__((aligned(16))) uint64_t skeys[MAXKEYS];
+    __shared__ uint32_t lhist[MAXPASS][256];
+    __shared__ uint32_t lds_scan[ET / 64];
+    __shared__ uint64_t lds_base;
+    __shared__ uint32_t lds_tile;
+
+    const uint64_t mask = k == 32 ? ~0ull : ((1ull << (2 * k)) - 1);
+    if (hist) {
+        for (int i = threadIdx.x; i < MAXPASS * 256; i += ET) (&lhist[0][0])[i] = 0;
+    }
+    for (;;) {
+        const int64_t tile = grab_tile(counter, &lds_tile);
+        if ((uint64_t)tile >= n_tiles) break;
+        const uint64_t tb = (uint64_t)tile * TILE;
+        stage_codes<EI>(codes, n_bases, tb, scodes);
+        __syncthreads();
+        uint64_t kf[EI], kr[EI];
+        const uint64_t p0 = tb + (uint64_t)threadIdx.x * EI;
+        const uint32_t valid = roll<EI, CANON>(scodes, threadIdx.x * EI, k, mask, p0, n_bases, kf, kr);
+        const uint32_t cnt = __popc(valid) * (RC && !CANON ? 2 : 1);
+        uint32_t total;
+        const uint32_t loff = block_exclusive_scan<ET>(cnt, SumU32(), 0u, lds_scan, &total);
+        if (threadIdx.x < 64) {
+            const uint64_t b = wave_lookback<0>(status, tile, total, epoch, err);
+            if (threadIdx.x == 0) lds_base = b;
+        }
+        // stage keys at compacted offsets
+        {
+            uint32_t o = loff;
+#pragma unroll
+            for (int j = 0; j < EI; j++) {
+                if ((valid >> j) & 1u) {
+                    skeys[o++] = kf[j];
+                    if (RC && !CANON) skeys[o++] = kr[j];
+                }
+            }
+        }
+        __syncthreads();
+        const uint64_t base = lds_base;
+        for (uint32_t q = threadIdx.x; q < total; q += ET) {
+            const uint64_t key = skeys[q];
+            keys[base + q] = key;
+            if (hist) {
+                for (int p = 0; p < plan.npass; p++) {
+                    const uint32_t d = (uint32_t)(key >> plan.shift[p]) & ((1u << plan.bits[p]) - 1);
+                    atomicAdd(&lhist[p][d], 1u);
+                }
+            }
+        }
+        if constexpr (HAS_POS) {
+            __syncthreads();
+            P *spos = reinterpret_cast<P *>(skeys);
+            uint32_t o = loff;
+#pragma unroll
+            for (int j = 0; j < EI; j++) {
+                if ((valid >> j) & 1u) {
+                    const P pv = (P)((p0 + j) << 1);
+                    spos[o++] = pv;
+                    if (RC && !CANON) spos[o++] = pv | 1;
+                }
+            }
+            __syncthreads();
+            for (uint32_t q = threadIdx.x; q < total; q += ET) pos[base + q] = spos[q];
+        }
+        __syncthreads();
+    }
+    if (hist) {
+        __syncthreads();
+        for (int p = 0; p < plan.npass; p++) {
+            const uint32_t c = lhist[p][threadIdx.x];
+            if (c) atomicAdd((unsigned long long *)&hist[p * 256 + threadIdx.x], (unsigned long long)c);
+        }
+    }
+}
+
+// valid-window count only (sizing)
+template <int EI>
+__global__ __launch_bounds__(ET) void count_kernel(const uint8_t *__restrict__ codes, uint64_t n_bases,
+                                                   uint64_t n_tiles, int k, unsigned long long *__restrict__ out) {
+    constexpr int TILE = ET * EI;
+    __shared__ __attribute__((aligned(16))) uint8_t scodes[TILE + 64];
+    __shared__ uint32_t lds_scan[ET / 64];
+    const uint64_t mask = k == 32 ? ~0ull : ((1ull << (2 * k)) - 1);
+    uint64_t acc = 0;
+    for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const uint64_t tb = tile * TILE;
+        stage_codes<EI>(codes, n_bases, tb, scodes);
+        __syncthreads();
+        uint64_t kf[EI], kr[EI];
+        const uint64_t p0 = tb + (uint64_t)threadIdx.x * EI;
+        acc += __popc(roll<EI, true>(scodes, threadIdx.x * EI, k, mask, p0, n_bases, kf, kr));
+        __syncthreads();
+    }
+    uint32_t tot;
+    block_exclusive_scan<ET>((uint32_t)acc, SumU32(), 0u, lds_scan, &tot);
+    if (threadIdx.x == 0 && tot) atomicAdd(out, (unsigned long long)tot);
+}
+
+int persistent_grid(kman_ctx *ctx, const void *fn, int threads, uint64_t n_tiles) {
+    int per_cu = 1, cus = 256;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    uint64_t g = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
+    if (g > n_tiles) g = n_tiles;
+    return (int)(g ? g : 1);
+}
+
+template <int EI, bool RC, bool CANON, typename P>
+int launch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k, uint64_t *keys, P *pos,
+                   uint64_t *hist, const Plan &plan) {
+    const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * EI);
+    uint32_t epoch, *counter;
+    KMAN_TRY(kman_lookback_begin(ctx, n_tiles, &epoch, &counter));
+    auto fn = extract_kernel<EI, RC, CANON, P>;
+    const int grid = persistent_grid(ctx, (const void *)fn, ET, n_tiles);
+    KTimer kt_(ctx, "extract");
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(ET), 0, ctx->stream, codes, n_bases, n_tiles, k, keys, pos,
+                       ctx->d_status, counter, epoch, ctx->d_err, hist, plan);
+    HIP_TRY(ctx, hipGetLastError());
+    return KMAN_OK;
+}
+
+template <typename P>
+int dispatch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k, uint32_t flags, uint64_t *keys,
+                     P *pos, uint64_t *hist, const Plan &plan) {
+    if (flags & KMAN_CANONICAL) return launch_extract<16, false, true, P>(ctx, codes, n_bases, k, keys, pos, hist, plan);
+    if (flags & KMAN_RC) return launch_extract<8, true, false, P>(ctx, codes, n_bases, k, keys, pos, hist, plan);
+    return launch_extract<16, false, false, P>(ctx, codes, n_bases, k, keys, pos, hist, plan);
+}
+
+}  // namespace
+
+extern "C" int kman_count_kmers(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                                uint64_t *n_kmers) {
+    if (!ctx || !n_kmers) return KMAN_EINVAL;
+    if (k < 2 || k > 32) return kman_fail(ctx, KMAN_EINVAL, "k must be in [2, 32] on the GPU path, got %u", k);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    *n_kmers = 0;
+    if (n_bases == 0) return KMAN_OK;
+    void *scr;
+    KMAN_TRY(kman_scratch(ctx, 256, &scr));
+    HIP_TRY(ctx, hipMemsetAsync(scr, 0, 8, ctx->stream));
+    const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * 16);
+    uint64_t grid = n_tiles < 4096 ? n_tiles : 4096;
+    hipLaunchKernelGGL(count_kernel<16>, dim3((uint32_t)grid), dim3(ET), 0, ctx->stream, d_codes, n_bases, n_tiles,
+                       (int)k, (unsigned long long *)scr);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small, scr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    const uint64_t w = ctx->h_small[0];
+    *n_kmers = (flags & KMAN_RC) && !(flags & KMAN_CANONICAL) ? 2 * w : w;
+    return KMAN_OK;
+}
+
+extern "C" int kman_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                            uint64_t *d_keys, void *d_pos, uint32_t pos_bytes, uint64_t cap, uint64_t *d_hist,
+                            uint64_t *n_kmers) {
+    if (!ctx || !n_kmers) return KMAN_EINVAL;
+    if (k < 2 || k > 32) return kman_fail(ctx, KMAN_EINVAL, "k must be in [2, 32] on the GPU path, got %u", k);
+    const bool want_pos = flags & KMAN_WANT_POS;
+    if (want_pos && pos_bytes != 4 && pos_bytes != 8)
+        return kman_fail(ctx, KMAN_EINVAL, "pos_bytes must be 4 or 8");
+    if (want_pos && pos_bytes == 4 && (n_bases << 1) > 0xffffffffull)
+        return kman_fail(ctx, KMAN_EINVAL, "u32 pos payload cannot address %llu bases", (unsigned long long)n_bases);
+    if (((uintptr_t)d_codes & 15) != 0) return kman_fail(ctx, KMAN_EINVAL, "codes must be 16-byte aligned");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    *n_kmers = 0;
+    if (n_bases == 0) return KMAN_OK;
+    const uint64_t bound = (flags & KMAN_RC) && !(flags & KMAN_CANONICAL) ? 2 * n_bases : n_bases;
+    if (cap < bound) {
+        // only size exactly when the caller's buffer is below the trivial bound
+        uint64_t need;
+        KMAN_TRY(kman_count_kmers(ctx, d_codes, n_bases, k, flags, &need));
+        if (need > cap)
+            return kman_fail(ctx, KMAN_ECAP, "key capacity %llu < %llu", (unsigned long long)cap,
+                             (unsigned long long)need);
+    }
+    Plan plan{};
+    uint32_t np, sh[MAXPASS], bi[MAXPASS];
+    KMAN_TRY(kman_sort_plan(2 * k, &np, sh, bi));
+    plan.npass = (int)np;
+    for (uint32_t i = 0; i < np; i++) {
+        plan.shift[i] = (uint8_t)sh[i];
+        plan.bits[i] = (uint8_t)bi[i];
+    }
+    if (!want_pos) {
+        KMAN_TRY(dispatch_extract<NoPos>(ctx, d_codes, n_bases, (int)k, flags, d_keys, nullptr, d_hist, plan));
+    } else if (pos_bytes == 4) {
+        KMAN_TRY(dispatch_extract<uint32_t>(ctx, d_codes, n_bases, (int)k, flags, d_keys, (uint32_t *)d_pos, d_hist,
+                                            plan));
+    } else {
+        KMAN_TRY(dispatch_extract<uint64_t>(ctx, d_codes, n_bases, (int)k, flags, d_keys, (uint64_t *)d_pos, d_hist,
+                                            plan));
+    }
+    // the last tile's inclusive prefix is the number of k-mers written
+    const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * ((flags & KMAN_RC) && !(flags & KMAN_CANONICAL) ? 8 : 16));
+    return kman_lookback_total(ctx, n_tiles, n_kmers);
+}

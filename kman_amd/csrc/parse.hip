@@ -1,0 +1,392 @@
+// parse.hip — FASTA text -> cleaned base codes + record table, on the GPU.
+//
+// Restates SmartFastaParser.parse (kmermaid/parsers.py:86-128) byte-parallel:
+//   * the file is read in text mode, so "\n", "\r\n" and a lone "\r" end a line
+//     (universal newlines);
+//   * lines before the first line that starts with '>' are skipped
+//     (__skip_blank_and_comments, parsers.py:43-56); no such line at all ->
+//     AssertionError("premature end of file or empty file") (parsers.py:105-107);
+//   * a line starting with '>' opens a record; every other line is a sequence
+//     line whose content is line.rstrip() (parsers.py:72), joined, with " " and
+//     "\r" removed (parsers.py:114).
+//
+// Per byte the only non-local facts are (a) which kind of line it sits in,
+// which depends on bytes to its left, and (b) for the rare non-space
+// whitespace chars (\t \v \f \x1c-\x1f), whether a non-whitespace char follows
+// later in the same line (rstrip).  (a) is a scan over a 3-state machine
+//   PRE (no header seen yet) / HDR (inside a header line) / SEQ (sequence line)
+// whose per-chunk summary is a transformer "incoming state -> (outgoing state,
+// kept chars)"; transformers compose associatively, so the whole file is
+// parsed with a reduce -> scan -> downsweep over 16 KiB tiles.  (b) is resolved
+// right-to-left inside each thread's 64-byte chunk plus, only when a chunk
+// ends inside a whitespace run, a forward probe past the chunk.
+//
+// Memory traffic: the text is read twice (reduce + downsweep), codes written
+// once: 3 B per input byte (algorithmic bytes in DESIGN.md).
+#include "common.h"
+
+namespace {
+
+constexpr int PT = 256;           // threads per tile
+constexpr int PB = 64;            // bytes per thread
+constexpr int PTILE = PT * PB;    // 16 KiB per tile
+constexpr int SCAN_T = 1024;      // threads of the single-block tile scan
+constexpr uint32_t XF_ID_OUTS = 0u | (1u << 2) | (2u << 4);
+
+enum : uint32_t { S_PRE = 0, S_HDR = 1, S_SEQ = 2 };
+
+struct Xf {  // 3-state transformer over a thread chunk (counts fit 32 bits)
+    uint32_t outs;
+    uint32_t kept[3];
+    uint32_t nhdr;
+};
+struct Xf64 {  // the same over tiles / tile ranges
+    uint32_t outs;
+    uint32_t pad;
+    uint64_t kept[3];
+    uint64_t nhdr;
+};
+struct TileIn {  // concrete state entering a tile
+    uint64_t kept;
+    uint64_t nhdr;
+    uint32_t state;
+    uint32_t pad;
+};
+
+KMAN_DEV uint32_t xf_out(uint32_t outs, uint32_t s) { return (outs >> (2 * s)) & 3u; }
+// select without runtime array indexing (which would go to scratch)
+template <typename T>
+KMAN_DEV T sel3(const T (&a)[3], uint32_t s) { return s == 0 ? a[0] : (s == 1 ? a[1] : a[2]); }
+
+struct ComposeXf {
+    KMAN_DEV Xf operator()(const Xf &a, const Xf &b) const {
+        Xf r;
+        r.outs = 0;
+#pragma unroll
+        for (uint32_t s = 0; s < 3; s++) {
+            const uint32_t m = xf_out(a.outs, s);
+            r.outs |= xf_out(b.outs, m) << (2 * s);
+            r.kept[s] = a.kept[s] + sel3(b.kept, m);
+        }
+        r.nhdr = a.nhdr + b.nhdr;
+        return r;
+    }
+};
+struct ComposeXf64 {
+    KMAN_DEV Xf64 operator()(const Xf64 &a, const Xf64 &b) const {
+        Xf64 r;
+        r.outs = 0;
+        r.pad = 0;
+#pragma unroll
+        for (uint32_t s = 0; s < 3; s++) {
+            const uint32_t m = xf_out(a.outs, s);
+            r.outs |= xf_out(b.outs, m) << (2 * s);
+            r.kept[s] = a.kept[s] + sel3(b.kept, m);
+        }
+        r.nhdr = a.nhdr + b.nhdr;
+        return r;
+    }
+};
+
+KMAN_DEV bool is_term(uint32_t c) { return c == '\n' || c == '\r'; }
+// Python str.isspace() over ASCII: what str.rstrip() strips.
+KMAN_DEV bool py_space(uint32_t c) { return c == ' ' || (c >= 9 && c <= 13) || (c >= 0x1c && c <= 0x1f); }
+// whitespace that is kept unless it is trailing (terminators and ' ' never kept)
+KMAN_DEV bool exotic_ws(uint32_t c) { return c == 9 || c == 11 || c == 12 || (c >= 0x1c && c <= 0x1f); }
+KMAN_DEV uint8_t base_code(uint32_t c) {
+    switch (c | 0x20u) {  // case-insensitive for letters
+        case 'a': return 0;
+        case 'c': return 1;
+        case 'g': return 2;
+        case 't': return 3;
+        default: return 4;
+    }
+}
+
+// A thread's 64-byte chunk of the text, reduced to bit masks (bit i = byte i).
+// Bytes are kept in 16 registers and only ever indexed at compile time.
+struct Chunk {
+    uint32_t w[PB / 4];
+    int cnt;
+    uint64_t ls;     // byte starts a line (universal newlines)
+    uint64_t hls;    // byte starts a header line ('>' at a line start)
+    uint64_t keep;   // content byte (not a terminator, not ' ', not trailing ws)
+    uint64_t hdr;    // byte lies in a header line
+};
+
+KMAN_DEV uint32_t byte_at(const uint32_t (&w)[PB / 4], int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xffu; }
+KMAN_DEV uint64_t bits_from(int i) { return i >= 64 ? 0ull : (~0ull << i); }
+KMAN_DEV uint64_t bits_below(int i) { return i >= 64 ? ~0ull : ((1ull << i) - 1); }
+
+KMAN_DEV void load_chunk(const uint8_t *text, uint64_t n, uint64_t pos, Chunk &ch) {
+    ch.cnt = pos < n ? (int)((n - pos) < (uint64_t)PB ? (n - pos) : (uint64_t)PB) : 0;
+    if (ch.cnt == PB) {
+        const uint4 *p = reinterpret_cast<const uint4 *>(text + pos);
+#pragma unroll
+        for (int v = 0; v < PB / 16; v++) {
+            const uint4 x = p[v];
+            ch.w[4 * v + 0] = x.x;
+            ch.w[4 * v + 1] = x.y;
+            ch.w[4 * v + 2] = x.z;
+            ch.w[4 * v + 3] = x.w;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < PB / 4; q++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const int i = 4 * q + b;
+                v |= (i < ch.cnt ? (uint32_t)text[pos + i] : 0u) << (8 * b);
+            }
+            ch.w[q] = v;
+        }
+    }
+    const uint32_t prev = pos ? text[pos - 1] : '\n';  // position 0 starts a line
+    uint64_t keep = 0, ls = 0, gt = 0, exo = 0, term = 0, nonws = 0;
+    uint32_t pc = prev;
+#pragma unroll
+    for (int i = 0; i < PB; i++) {
+        const uint32_t c = byte_at(ch.w, i);
+        const uint64_t in = i < ch.cnt;
+        ls |= (in & (uint64_t)(pc == '\n' || (pc == '\r' && c != '\n'))) << i;
+        keep |= (in & (uint64_t)!(c == '\n' || c == '\r' || c == ' ')) << i;
+        gt |= (uint64_t)(c == '>') << i;
+        exo |= (in & (uint64_t)exotic_ws(c)) << i;
+        term |= (uint64_t)is_term(c) << i;
+        nonws |= (uint64_t)!py_space(c) << i;
+        pc = c;
+    }
+    if (exo) {
+        // rstrip: an exotic whitespace byte survives only if a non-whitespace
+        // byte follows it in the same line (possibly beyond this chunk).
+        bool later = false;
+        for (uint64_t j = pos + ch.cnt; j < n; j++) {
+            const uint32_t c = text[j];
+            if (is_term(c)) break;
+            if (!py_space(c)) {
+                later = true;
+                break;
+            }
+        }
+#pragma unroll
+        for (int i = PB - 1; i >= 0; i--) {
+            if (i < ch.cnt) {
+                if (((exo >> i) & 1ull) && !later) keep &= ~(1ull << i);
+                if ((term >> i) & 1ull) later = false;
+                else if ((nonws >> i) & 1ull) later = true;
+            }
+        }
+    }
+    // bytes of header lines: from each header line start to the next line start
+    const uint64_t hls = ls & gt;
+    uint64_t hdr = 0;
+    for (uint64_t m = hls; m; m &= m - 1) {
+        const int h = __ffsll((unsigned long long)m) - 1;
+        const uint64_t after = ls & bits_from(h + 1);
+        const int nx = after ? __ffsll((unsigned long long)after) - 1 : 64;
+        hdr |= bits_from(h) & bits_below(nx);
+    }
+    ch.ls = ls;
+    ch.hls = hls;
+    ch.keep = keep;
+    ch.hdr = hdr;
+}
+
+// content bytes that land in the cleaned sequence, per incoming state
+struct Emit {
+    uint64_t lead;  // bytes before the first line start (kept iff incoming SEQ)
+    uint64_t mid;   // non-header lines before the first header (kept iff incoming != PRE)
+    uint64_t all;   // non-header lines after a header (always kept)
+};
+
+KMAN_DEV Emit chunk_emit(const Chunk &ch) {
+    const int F = ch.ls ? __ffsll((unsigned long long)ch.ls) - 1 : 64;
+    const int H = ch.hls ? __ffsll((unsigned long long)ch.hls) - 1 : 64;
+    const uint64_t body = ch.keep & ~ch.hdr;
+    Emit e;
+    e.lead = ch.keep & bits_below(F);
+    e.mid = body & bits_from(F) & bits_below(H);
+    e.all = body & bits_from(H);
+    return e;
+}
+
+KMAN_DEV uint64_t emit_mask(const Emit &e, uint32_t s) {
+    return e.all | (s != S_PRE ? e.mid : 0ull) | (s == S_SEQ ? e.lead : 0ull);
+}
+
+KMAN_DEV Xf chunk_xf(const Chunk &ch) {
+    const Emit e = chunk_emit(ch);
+    Xf x;
+    x.kept[S_PRE] = __popcll(e.all);
+    x.kept[S_HDR] = __popcll(e.all | e.mid);
+    x.kept[S_SEQ] = __popcll(e.all | e.mid | e.lead);
+    x.nhdr = __popcll(ch.hls);
+    if (!ch.ls) {
+        x.outs = XF_ID_OUTS;
+    } else {
+        const int L = 63 - __clzll((unsigned long long)ch.ls);
+        if ((ch.hls >> L) & 1ull) {
+            x.outs = S_HDR | (S_HDR << 2) | (S_HDR << 4);
+        } else if (ch.hls) {
+            x.outs = S_SEQ | (S_SEQ << 2) | (S_SEQ << 4);
+        } else {
+            x.outs = S_PRE | (S_SEQ << 2) | (S_SEQ << 4);
+        }
+    }
+    return x;
+}
+
+__global__ __launch_bounds__(PT) void parse_reduce(const uint8_t *__restrict__ text, uint64_t n,
+                                                   Xf64 *__restrict__ tiles) {
+    __shared__ Xf lds[PT / 64];
+    const uint64_t pos = (uint64_t)blockIdx.x * PTILE + (uint64_t)threadIdx.x * PB;
+    Chunk ch;
+    load_chunk(text, n, pos, ch);
+    Xf x = chunk_xf(ch);
+    Xf id;
+    id.outs = XF_ID_OUTS;
+    id.kept[0] = id.kept[1] = id.kept[2] = 0;
+    id.nhdr = 0;
+    Xf tot;
+    block_exclusive_scan<PT>(x, ComposeXf(), id, lds, &tot);
+    if (threadIdx.x == 0) {
+        Xf64 t;
+        t.outs = tot.outs;
+        t.pad = 0;
+        for (int s = 0; s < 3; s++) t.kept[s] = tot.kept[s];
+        t.nhdr = tot.nhdr;
+        tiles[blockIdx.x] = t;
+    }
+}
+
+// Single block: turn per-tile transformers into concrete incoming states.
+__global__ __launch_bounds__(SCAN_T) void parse_scan(const Xf64 *__restrict__ tiles, uint64_t T,
+                                                     TileIn *__restrict__ tin, uint64_t *__restrict__ info) {
+    __shared__ Xf64 lds[SCAN_T / 64];
+    const uint64_t chunk = (T + SCAN_T - 1) / SCAN_T;
+    const uint64_t b = threadIdx.x * chunk;
+    const uint64_t e = b + chunk < T ? b + chunk : T;
+    Xf64 id;
+    id.outs = XF_ID_OUTS;
+    id.pad = 0;
+    id.kept[0] = id.kept[1] = id.kept[2] = 0;
+    id.nhdr = 0;
+    Xf64 acc = id;
+    ComposeXf64 op;
+    for (uint64_t t = b; t < e; t++) acc = op(acc, tiles[t]);
+    Xf64 tot;
+    Xf64 pre = block_exclusive_scan<SCAN_T>(acc, op, id, lds, &tot);
+    uint32_t s = xf_out(pre.outs, S_PRE);
+    uint64_t kept = pre.kept[S_PRE];
+    uint64_t nh = pre.nhdr;
+    for (uint64_t t = b; t < e; t++) {
+        TileIn ti;
+        ti.kept = kept;
+        ti.nhdr = nh;
+        ti.state = s;
+        ti.pad = 0;
+        tin[t] = ti;
+        const Xf64 x = tiles[t];
+        kept += s == 0 ? x.kept[0] : (s == 1 ? x.kept[1] : x.kept[2]);
+        nh += x.nhdr;
+        s = xf_out(x.outs, s);
+    }
+    if (threadIdx.x == 0) {
+        info[0] = tot.kept[S_PRE];  // n_bases
+        info[1] = tot.nhdr;         // n_records
+    }
+}
+
+__global__ __launch_bounds__(PT) void parse_emit(const uint8_t *__restrict__ text, uint64_t n,
+                                                 const TileIn *__restrict__ tin, uint8_t *__restrict__ codes,
+                                                 uint64_t *__restrict__ rec_hdr, uint64_t *__restrict__ rec_seq) {
+    __shared__ Xf lds[PT / 64];
+    __shared__ uint8_t stage[PTILE];
+    const uint64_t pos = (uint64_t)blockIdx.x * PTILE + (uint64_t)threadIdx.x * PB;
+    Chunk ch;
+    load_chunk(text, n, pos, ch);
+    const Xf x = chunk_xf(ch);
+    Xf id;
+    id.outs = XF_ID_OUTS;
+    id.kept[0] = id.kept[1] = id.kept[2] = 0;
+    id.nhdr = 0;
+    Xf tot;
+    const Xf pre = block_exclusive_scan<PT>(x, ComposeXf(), id, lds, &tot);
+    const TileIn ti = tin[blockIdx.x];
+    const uint32_t s = xf_out(pre.outs, ti.state);  // state entering this thread's chunk
+    const uint32_t lk0 = ti.state == 0 ? pre.kept[0] : (ti.state == 1 ? pre.kept[1] : pre.kept[2]);        // tile-local kept offset of this thread
+    const uint64_t nh0 = ti.nhdr + pre.nhdr;
+    const uint32_t tile_kept = ti.state == 0 ? tot.kept[0] : (ti.state == 1 ? tot.kept[1] : tot.kept[2]);
+    const uint64_t em = emit_mask(chunk_emit(ch), s);
+    // records opened in this chunk: '>' offset and the global index of the next kept char
+    {
+        uint64_t nh = nh0;
+        for (uint64_t m = ch.hls; m; m &= m - 1) {
+            const int h = __ffsll((unsigned long long)m) - 1;
+            rec_hdr[nh] = pos + h;
+            rec_seq[nh] = ti.kept + lk0 + __popcll(em & bits_below(h));
+            nh++;
+        }
+    }
+    uint32_t lk = lk0;
+#pragma unroll
+    for (int i = 0; i < PB; i++) {
+        if ((em >> i) & 1ull) stage[lk++] = base_code(byte_at(ch.w, i));
+    }
+    __syncthreads();
+    uint8_t *dst = codes + ti.kept;
+    for (uint32_t q = threadIdx.x; q < tile_kept; q += PT) dst[q] = stage[q];
+}
+
+// bit 3 on the first code of every non-empty record
+__global__ void mark_records(uint8_t *__restrict__ codes, const uint64_t *__restrict__ rec_seq, uint64_t R,
+                             uint64_t n_bases) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < R) {
+        const uint64_t p = rec_seq[r];
+        if (p < n_bases) codes[p] |= 8;
+    }
+}
+
+}  // namespace
+
+extern "C" int kman_parse_fasta(kman_ctx *ctx, const uint8_t *d_text, uint64_t n_bytes, uint8_t *d_codes,
+                                uint64_t *d_rec_hdr, uint64_t *d_rec_seq, uint64_t rec_cap,
+                                kman_parse_info *info) {
+    if (!ctx || !info) return KMAN_EINVAL;
+    if (n_bytes && (!d_text || !d_codes)) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    if (((uintptr_t)d_text & 15) != 0) return kman_fail(ctx, KMAN_EINVAL, "text must be 16-byte aligned");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const uint64_t T = n_bytes ? ceil_div(n_bytes, PTILE) : 0;
+    if (T == 0) return kman_fail(ctx, KMAN_EFORMAT, "premature end of file or empty file");
+    // scratch: tiles (Xf64) + tile-in + info
+    const size_t xf_bytes = ((T * sizeof(Xf64)) + 255) & ~size_t(255);
+    const size_t ti_bytes = ((T * sizeof(TileIn)) + 255) & ~size_t(255);
+    void *scr;
+    KMAN_TRY(kman_scratch(ctx, xf_bytes + ti_bytes + 256, &scr));
+    Xf64 *d_xf = (Xf64 *)scr;
+    TileIn *d_ti = (TileIn *)((char *)scr + xf_bytes);
+    uint64_t *d_info = (uint64_t *)((char *)scr + xf_bytes + ti_bytes);
+    { KTimer kt_(ctx, "parse");
+    hipLaunchKernelGGL(parse_reduce, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf);
+    hipLaunchKernelGGL(parse_scan, dim3(1), dim3(SCAN_T), 0, ctx->stream, d_xf, T, d_ti, d_info); }
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small, d_info, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    info->n_bases = ctx->h_small[0];
+    info->n_records = ctx->h_small[1];
+    if (info->n_records == 0) return kman_fail(ctx, KMAN_EFORMAT, "premature end of file or empty file");
+    if (info->n_records > rec_cap)
+        return kman_fail(ctx, KMAN_ECAP, "record capacity %llu < %llu", (unsigned long long)rec_cap,
+                         (unsigned long long)info->n_records);
+    { KTimer kt_(ctx, "parse");
+    hipLaunchKernelGGL(parse_emit, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_ti, d_codes,
+                       d_rec_hdr, d_rec_seq);
+    const uint64_t R = info->n_records;
+    hipLaunchKernelGGL(mark_records, dim3((uint32_t)ceil_div(R, 256)), dim3(256), 0, ctx->stream, d_codes,
+                       d_rec_seq, R, info->n_bases); }
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipMemsetAsync(d_codes + info->n_bases, 4, 64, ctx->stream));
+    return KMAN_OK;
+}

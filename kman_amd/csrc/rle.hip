@@ -1,0 +1,237 @@
+// rle.hip — run-length grouping of sorted keys: count and uniq.
+//
+// Replaces the group loop of Crawler.do_batch (kmermaid/join.py:95-130) fed
+// by the heap merge, and the two join functions on the hot path:
+//   join_sequence_count (join.py:266-285): one (key, group size) per group;
+//   join_unique         (join.py:244-263): the group only if it has exactly one
+//                                          member, with that member's header.
+// Both are single-pass tile kernels (256 threads x 16 keys) with decoupled
+// look-back: count needs the number of groups before the tile (sum) and, for
+// a tile that starts inside a group, the position of that group's head (max
+// of head positions; a tile holding any head publishes it as inclusive at
+// once, so the chain is short).  uniq keeps keys that differ from both
+// neighbours and needs only the sum.
+//
+// Algorithmic bytes: count 8 B read + (8 + 4|8) B per group written;
+// uniq 8 B key read (+ payload of kept keys) + (8 + 4|8) B per kept key.
+#include "common.h"
+
+namespace {
+
+constexpr int RT = 256;
+constexpr int RI = 16;
+constexpr int RTILE = RT * RI;
+
+struct MaxU64 {
+    KMAN_DEV uint64_t operator()(uint64_t a, uint64_t b) const { return a > b ? a : b; }
+};
+
+KMAN_DEV void stage_keys(const uint64_t *__restrict__ keys, uint64_t n, uint64_t tb, uint64_t *s) {
+    for (int i = threadIdx.x; i < RTILE; i += RT) {
+        const uint64_t idx = tb + i;
+        s[i] = idx < n ? keys[idx] : 0;
+    }
+}
+
+// look-back for "position of the last group head + 1" (max); a tile with a head
+// publishes its own value as inclusive immediately.
+KMAN_DEV uint64_t wave_lookback_lasthead(uint64_t *status, int64_t tile, uint64_t agg, bool need, uint32_t epoch,
+                                         uint32_t *err) {
+    const int lane = lane_id();
+    if (agg != 0 || tile == 0) {
+        if (lane == 0) st_store(&status[tile], st_make(ST_INCL, epoch, agg));
+        if (!need || tile == 0) return 0;
+    }
+    if (agg == 0 && lane == 0) st_store(&status[tile], st_make(ST_AGG, epoch, 0));
+    uint64_t best = 0;
+    int64_t end = tile;
+    uint32_t spins = 0;
+    for (;;) {
+        const int64_t j = end - 1 - lane;
+        uint64_t w = 0, f = ST_INCL;
+        if (j >= 0) {
+            w = st_load(&status[j]);
+            f = st_flag(w, epoch);
+        }
+        const uint64_t v = j >= 0 ? (w & ST_VMASK) : 0;
+        const uint64_t notready = __ballot(j >= 0 && f == 0);
+        // stop at the nearest tile whose value is final: INCL, or AGG with a head
+        const uint64_t fin = __ballot(j >= 0 && (f == ST_INCL || (f == ST_AGG && v != 0)));
+        const int first = fin ? __ffsll((unsigned long long)fin) - 1 : 64;
+        const uint64_t need_m = first == 64 ? ~0ull : (~0ull >> (63 - first));
+        if (notready & need_m) {
+            if (spin_give_up(spins, err, 4u)) break;
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        if (first < 64) {
+            best = shfl_any(v, first);
+            break;
+        }
+        if (end - 64 <= 0) break;
+        end -= 64;
+    }
+    if (agg == 0 && lane == 0) st_store(&status[tile], st_make(ST_INCL, epoch, best));
+    return best;
+}
+
+template <typename C>
+__global__ __launch_bounds__(RT) void rle_count_kernel(const uint64_t *__restrict__ keys, uint64_t n,
+                                                       uint64_t *__restrict__ ukeys, C *__restrict__ counts,
+                                                       uint64_t *__restrict__ st_sum, uint64_t *__restrict__ st_max,
+                                                       uint32_t *__restrict__ counter, uint32_t epoch,
+                                                       uint32_t *__restrict__ err) {
+    __shared__ __attribute__((aligned(16))) uint64_t s[RTILE];
+    __shared__ uint32_t lds_scan[RT / 64];
+    __shared__ uint64_t lds_scan64[RT / 64];
+    __shared__ uint64_t lds_base, lds_head;
+    __shared__ uint32_t lds_tile;
+    const int64_t tile = grab_tile(counter, &lds_tile);
+    const uint64_t tb = (uint64_t)tile * RTILE;
+    stage_keys(keys, n, tb, s);
+    const uint64_t prev_key = tb ? keys[tb - 1] : 0;
+    const uint64_t next_key = tb + RTILE < n ? keys[tb + RTILE] : 0;
+    __syncthreads();
+    const uint32_t t0 = threadIdx.x * RI;
+    uint64_t k[RI];
+#pragma unroll
+    for (int j = 0; j < RI; j++) k[j] = s[t0 + j];
+    uint32_t heads = 0, tails = 0;
+#pragma unroll
+    for (int j = 0; j < RI; j++) {
+        const uint64_t i = tb + t0 + j;
+        const uint64_t pk = j ? k[j - 1] : (t0 ? s[t0 - 1] : prev_key);
+        const uint64_t nk = j + 1 < RI ? k[j + 1] : (t0 + RI < (uint32_t)RTILE ? s[t0 + RI] : next_key);
+        const bool in = i < n;
+        heads |= (uint32_t)(in && (i == 0 || k[j] != pk)) << j;
+        tails |= (uint32_t)(in && (i == n - 1 || k[j] != nk)) << j;
+    }
+    const uint32_t nh = __popc(heads);
+    // last head position + 1 within this thread (0 = none)
+    const uint64_t lh = heads ? tb + t0 + (31 - __clz(heads)) + 1 : 0;
+    uint32_t tile_heads;
+    const uint32_t hoff = block_exclusive_scan<RT>(nh, SumU32(), 0u, lds_scan, &tile_heads);
+    uint64_t tile_lh;
+    const uint64_t lh_before = block_exclusive_scan<RT>(lh, MaxU64(), (uint64_t)0, lds_scan64, &tile_lh);
+    if (threadIdx.x < 64) {
+        const uint64_t b = wave_lookback<0>(st_sum, tile, tile_heads, epoch, err);
+        const bool first_is_head = tb == 0 || s[0] != prev_key;
+        const uint64_t h = wave_lookback_lasthead(st_max, tile, tile_lh, !first_is_head, epoch, err);
+        if (threadIdx.x == 0) {
+            lds_base = b;
+            lds_head = h;
+        }
+    }
+    __syncthreads();
+    const uint64_t base = lds_base;
+    uint64_t cur_head = lh_before ? lh_before : lds_head;  // head position + 1 of the open group
+    uint64_t slot = base + hoff;                           // groups opened before this key
+#pragma unroll
+    for (int j = 0; j < RI; j++) {
+        const uint64_t i = tb + t0 + j;
+        if ((heads >> j) & 1u) {
+            cur_head = i + 1;
+            slot++;
+        }
+        if ((tails >> j) & 1u) {
+            ukeys[slot - 1] = k[j];
+            counts[slot - 1] = (C)(i + 2 - cur_head);
+        }
+    }
+}
+
+template <typename V>
+__global__ __launch_bounds__(RT) void rle_uniq_kernel(const uint64_t *__restrict__ keys, const V *__restrict__ vals,
+                                                      uint64_t n, uint64_t *__restrict__ okeys, V *__restrict__ ovals,
+                                                      uint64_t *__restrict__ st_sum, uint32_t *__restrict__ counter,
+                                                      uint32_t epoch, uint32_t *__restrict__ err) {
+    __shared__ __attribute__((aligned(16))) uint64_t s[RTILE];
+    __shared__ uint32_t lds_scan[RT / 64];
+    __shared__ uint64_t lds_base;
+    __shared__ uint32_t lds_tile;
+    const int64_t tile = grab_tile(counter, &lds_tile);
+    const uint64_t tb = (uint64_t)tile * RTILE;
+    stage_keys(keys, n, tb, s);
+    const uint64_t prev_key = tb ? keys[tb - 1] : 0;
+    const uint64_t next_key = tb + RTILE < n ? keys[tb + RTILE] : 0;
+    __syncthreads();
+    const uint32_t t0 = threadIdx.x * RI;
+    uint64_t k[RI];
+#pragma unroll
+    for (int j = 0; j < RI; j++) k[j] = s[t0 + j];
+    uint32_t single = 0;
+#pragma unroll
+    for (int j = 0; j < RI; j++) {
+        const uint64_t i = tb + t0 + j;
+        const uint64_t pk = j ? k[j - 1] : (t0 ? s[t0 - 1] : prev_key);
+        const uint64_t nk = j + 1 < RI ? k[j + 1] : (t0 + RI < (uint32_t)RTILE ? s[t0 + RI] : next_key);
+        const bool in = i < n;
+        const bool h = i == 0 || k[j] != pk;
+        const bool t = i == n - 1 || k[j] != nk;
+        single |= (uint32_t)(in && h && t) << j;
+    }
+    uint32_t tile_cnt;
+    const uint32_t off = block_exclusive_scan<RT>((uint32_t)__popc(single), SumU32(), 0u, lds_scan, &tile_cnt);
+    if (threadIdx.x < 64) {
+        const uint64_t b = wave_lookback<0>(st_sum, tile, tile_cnt, epoch, err);
+        if (threadIdx.x == 0) lds_base = b;
+    }
+    __syncthreads();
+    uint64_t o = lds_base + off;
+#pragma unroll
+    for (int j = 0; j < RI; j++) {
+        if ((single >> j) & 1u) {
+            okeys[o] = k[j];
+            ovals[o] = vals[tb + t0 + j];
+            o++;
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" int kman_rle_count(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint64_t *d_ukeys, void *d_counts,
+                              uint32_t count_bytes, uint64_t *n_unique) {
+    if (!ctx || !n_unique) return KMAN_EINVAL;
+    if (count_bytes != 4 && count_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "count_bytes must be 4 or 8");
+    if (count_bytes == 4 && n > 0xffffffffull)
+        return kman_fail(ctx, KMAN_EINVAL, "u32 counts cannot hold groups of %llu keys", (unsigned long long)n);
+    *n_unique = 0;
+    if (n == 0) return KMAN_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const uint64_t T = ceil_div(n, RTILE);
+    uint32_t epoch, *counter;
+    KMAN_TRY(kman_lookback_begin(ctx, 2 * T, &epoch, &counter));
+    KTimer kt_(ctx, "rle_count");
+    if (count_bytes == 4)
+        hipLaunchKernelGGL(rle_count_kernel<uint32_t>, dim3((uint32_t)T), dim3(RT), 0, ctx->stream, d_keys, n, d_ukeys,
+                           (uint32_t *)d_counts, ctx->d_status, ctx->d_status + T, counter, epoch, ctx->d_err);
+    else
+        hipLaunchKernelGGL(rle_count_kernel<uint64_t>, dim3((uint32_t)T), dim3(RT), 0, ctx->stream, d_keys, n, d_ukeys,
+                           (uint64_t *)d_counts, ctx->d_status, ctx->d_status + T, counter, epoch, ctx->d_err);
+    HIP_TRY(ctx, hipGetLastError());
+    return kman_lookback_total(ctx, T, n_unique);
+}
+
+extern "C" int kman_rle_uniq(kman_ctx *ctx, const uint64_t *d_keys, const void *d_vals, uint32_t val_bytes, uint64_t n,
+                             uint64_t *d_okeys, void *d_ovals, uint64_t *n_out) {
+    if (!ctx || !n_out) return KMAN_EINVAL;
+    if (val_bytes != 4 && val_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "val_bytes must be 4 or 8");
+    *n_out = 0;
+    if (n == 0) return KMAN_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const uint64_t T = ceil_div(n, RTILE);
+    uint32_t epoch, *counter;
+    KMAN_TRY(kman_lookback_begin(ctx, T, &epoch, &counter));
+    KTimer kt_(ctx, "rle_uniq");
+    if (val_bytes == 4)
+        hipLaunchKernelGGL(rle_uniq_kernel<uint32_t>, dim3((uint32_t)T), dim3(RT), 0, ctx->stream, d_keys,
+                           (const uint32_t *)d_vals, n, d_okeys, (uint32_t *)d_ovals, ctx->d_status, counter, epoch,
+                           ctx->d_err);
+    else
+        hipLaunchKernelGGL(rle_uniq_kernel<uint64_t>, dim3((uint32_t)T), dim3(RT), 0, ctx->stream, d_keys,
+                           (const uint64_t *)d_vals, n, d_okeys, (uint64_t *)d_ovals, ctx->d_status, counter, epoch,
+                           ctx->d_err);
+    HIP_TRY(ctx, hipGetLastError());
+    return kman_lookback_total(ctx, T, n_out);
+}

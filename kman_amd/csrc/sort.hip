@@ -1,0 +1,287 @@
+// sort.hip — stable LSD radix sort of packed k-mer keys (+ optional payload).
+//
+// Replaces Batch.sorted (kmermaid/batch.py:156-168: a stable Timsort by .seq)
+// as forced for every batch by BatcherBase.write_all (batcher.py:133-153,392).
+// Stable because tied keys must keep stream order, exactly as Timsort keeps
+// them (this is what makes `kmer batch` files and Crawler group member order
+// match the reference).
+//
+// One "onesweep" pass per digit (Adinets & Merrill's single-pass LSD scheme,
+// re-derived for wave64 / gfx950):
+//   1. a tile of 4096 keys is read coalesced (wave-striped: item i of lane l of
+//      wave w is key tile*4096 + w*1024 + i*64 + l);
+//   2. each wave ranks its 16 items stably with 64-bit ballot match-any over
+//      the digit bits and per-wave LDS counters (no LDS atomics);
+//   3. the tile's per-digit counts are published and every digit looks back
+//      across predecessor tiles (decoupled look-back, agent-scope sc1 status
+//      words flag:2|epoch:6|count:56) for its exclusive global offset;
+//   4. keys are scattered into LDS in tile-sorted order and written out so
+//      consecutive lanes write consecutive addresses of one digit run.
+// The digit histograms of all passes come from kman_extract (fused) or from
+// one histogram pass, so a pass reads and writes every key exactly once:
+// 16 B/key (+ 2x payload bytes) — the figure the roofline is quoted against.
+#include "common.h"
+
+namespace {
+
+constexpr int ST = 256;         // threads per tile
+constexpr int SI = 16;          // keys per thread
+constexpr int STILE = ST * SI;  // 4096 keys
+constexpr int RADIX = 256;
+constexpr int NWAVE = ST / 64;
+constexpr int MAXPASS = 8;
+
+struct NoVal {};
+
+// per-thread (one digit) sequential look-back over the tile chain of that digit
+KMAN_DEV uint64_t digit_lookback(uint64_t *st, int64_t tile, uint64_t agg, uint32_t epoch, uint32_t *err) {
+    if (tile == 0) {
+        st_store(&st[0], st_make(ST_INCL, epoch, agg));
+        return 0;
+    }
+    st_store(&st[(uint64_t)tile * RADIX], st_make(ST_AGG, epoch, agg));
+    uint64_t excl = 0;
+    int64_t j = tile - 1;
+    uint32_t spins = 0;
+    while (j >= 0) {
+        const uint64_t w = st_load(&st[(uint64_t)j * RADIX]);
+        const uint64_t f = st_flag(w, epoch);
+        if (f == 0) {
+            if (spin_give_up(spins, err, 2u)) break;
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        excl += w & ST_VMASK;
+        if (f == ST_INCL) break;
+        --j;
+    }
+    st_store(&st[(uint64_t)tile * RADIX], st_make(ST_INCL, epoch, excl + agg));
+    return excl;
+}
+
+template <typename V>
+__global__ __launch_bounds__(ST) void onesweep_pass(const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
+                                                    const V *__restrict__ vin, V *__restrict__ vout, uint64_t n,
+                                                    uint32_t shift, uint32_t bits,
+                                                    const uint64_t *__restrict__ bucket_base,
+                                                    uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
+                                                    uint32_t epoch, uint32_t *__restrict__ err) {
+    constexpr bool HAS_V = !std::is_same<V, NoVal>::value;
+    __shared__ __attribute__((aligned(16))) uint64_t skeys[STILE];
+    __shared__ uint8_t sdig[STILE];
+    __shared__ uint32_t whist[NWAVE][RADIX];
+    __shared__ uint32_t lstart[RADIX];
+    __shared__ uint64_t gstart[RADIX];
+    __shared__ uint32_t lds_scan[ST / 64];
+    __shared__ uint32_t lds_tile;
+
+    const int64_t tile = grab_tile(counter, &lds_tile);
+    const int lane = lane_id();
+    const int w = threadIdx.x >> 6;
+    const uint32_t radix = 1u << bits;
+    const uint32_t dmask = radix - 1;
+    for (int i = threadIdx.x; i < NWAVE * RADIX; i += ST) (&whist[0][0])[i] = 0;
+
+    const uint64_t tb = (uint64_t)tile * STILE;
+    const uint64_t ib = tb + (uint64_t)w * (SI * 64) + lane;
+    uint64_t key[SI];
+    uint32_t rank[SI];
+#pragma unroll
+    for (int i = 0; i < SI; i++) {
+        const uint64_t idx = ib + (uint64_t)i * 64;
+        key[i] = idx < n ? kin[idx] : 0;
+    }
+    __syncthreads();
+
+    // stable in-wave ranking: items in order, lanes in order
+#pragma unroll
+    for (int i = 0; i < SI; i++) {
+        const bool valid = ib + (uint64_t)i * 64 < n;
+        const uint32_t d = (uint32_t)(key[i] >> shift) & dmask;
+        uint64_t peers = __ballot(valid);
+        for (uint32_t b = 0; b < bits; b++) {
+            const bool set = (d >> b) & 1u;
+            const uint64_t m = __ballot(set);
+            peers &= set ? m : ~m;
+        }
+        uint32_t before = 0;
+        if (valid) before = whist[w][d];
+        rank[i] = before + (uint32_t)__popcll(peers & lanemask_lt());
+        const int leader = __ffsll((unsigned long long)peers) - 1;
+        if (valid && lane == leader) whist[w][d] = before + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+
+    // per-digit tile counts and per-wave exclusive offsets (thread = digit)
+    const uint32_t d0 = threadIdx.x;
+    uint32_t tot = 0;
+#pragma unroll
+    for (int ww = 0; ww < NWAVE; ww++) {
+        const uint32_t c = whist[ww][d0];
+        whist[ww][d0] = tot;
+        tot += c;
+    }
+    uint32_t tile_total;
+    const uint32_t ls = block_exclusive_scan<ST>(tot, SumU32(), 0u, lds_scan, &tile_total);
+    lstart[d0] = ls;
+    if (d0 < radix) {
+        const uint64_t excl = digit_lookback(status + d0, tile, tot, epoch, err);
+        gstart[d0] = bucket_base[d0] + excl - ls;
+    }
+    __syncthreads();
+
+    // scatter into LDS in tile order
+    uint32_t lp[SI];
+#pragma unroll
+    for (int i = 0; i < SI; i++) {
+        const bool valid = ib + (uint64_t)i * 64 < n;
+        const uint32_t d = (uint32_t)(key[i] >> shift) & dmask;
+        lp[i] = valid ? lstart[d] + whist[w][d] + rank[i] : 0xffffffffu;
+        if (valid) {
+            skeys[lp[i]] = key[i];
+            sdig[lp[i]] = (uint8_t)d;
+        }
+    }
+    __syncthreads();
+    const uint32_t cnt = (uint32_t)(n - tb < (uint64_t)STILE ? n - tb : (uint64_t)STILE);
+    for (uint32_t q = threadIdx.x; q < cnt; q += ST) kout[gstart[sdig[q]] + q] = skeys[q];
+    if constexpr (HAS_V) {
+        V val[SI];
+#pragma unroll
+        for (int i = 0; i < SI; i++) {
+            const uint64_t idx = ib + (uint64_t)i * 64;
+            val[i] = idx < n ? vin[idx] : (V)0;
+        }
+        __syncthreads();
+        V *sval = reinterpret_cast<V *>(skeys);
+#pragma unroll
+        for (int i = 0; i < SI; i++)
+            if (lp[i] != 0xffffffffu) sval[lp[i]] = val[i];
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < cnt; q += ST) vout[gstart[sdig[q]] + q] = sval[q];
+    }
+}
+
+__global__ __launch_bounds__(256) void histogram_kernel(const uint64_t *__restrict__ keys, uint64_t n, int npass,
+                                                        const uint32_t *__restrict__ shift_bits,
+                                                        unsigned long long *__restrict__ hist) {
+    __shared__ uint32_t lh[MAXPASS][RADIX];
+    for (int i = threadIdx.x; i < MAXPASS * RADIX; i += 256) (&lh[0][0])[i] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t k = keys[i];
+        for (int p = 0; p < npass; p++) {
+            const uint32_t sh = shift_bits[p] & 0xff, b = shift_bits[p] >> 8;
+            atomicAdd(&lh[p][(uint32_t)(k >> sh) & ((1u << b) - 1)], 1u);
+        }
+    }
+    __syncthreads();
+    for (int p = 0; p < npass; p++) {
+        const uint32_t c = lh[p][threadIdx.x];
+        if (c) atomicAdd(&hist[p * RADIX + threadIdx.x], (unsigned long long)c);
+    }
+}
+
+template <typename V>
+int run_passes(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, V *v0, V *v1, uint64_t n, uint32_t np, const uint32_t *sh,
+               const uint32_t *bi, const uint64_t *h_hist, int *result_in_alt) {
+    // bucket bases per pass (host: 256 x npass), skipping single-bucket passes
+    uint64_t bases[MAXPASS][RADIX];
+    bool skip[MAXPASS];
+    for (uint32_t p = 0; p < np; p++) {
+        uint64_t acc = 0;
+        skip[p] = false;
+        for (int d = 0; d < RADIX; d++) {
+            bases[p][d] = acc;
+            const uint64_t c = h_hist[p * RADIX + d];
+            if (c == n) skip[p] = true;
+            acc += c;
+        }
+        if (acc != n)
+            return kman_fail(ctx, KMAN_EINVAL, "histogram of pass %u sums to %llu, expected %llu", p,
+                             (unsigned long long)acc, (unsigned long long)n);
+    }
+    void *scr;
+    KMAN_TRY(kman_scratch(ctx, sizeof(bases), &scr));
+    HIP_TRY(ctx, hipMemcpyAsync(scr, bases, sizeof(bases), hipMemcpyHostToDevice, ctx->stream));
+    const uint64_t n_tiles = ceil_div(n, STILE);
+    int cur = 0;
+    uint64_t *kb[2] = {k0, k1};
+    V *vb[2] = {v0, v1};
+    for (uint32_t p = 0; p < np; p++) {
+        if (skip[p]) continue;
+        uint32_t epoch, *counter;
+        KMAN_TRY(kman_lookback_begin(ctx, n_tiles * RADIX, &epoch, &counter));
+        KTimer kt_(ctx, "sort_pass");
+        hipLaunchKernelGGL(onesweep_pass<V>, dim3((uint32_t)n_tiles), dim3(ST), 0, ctx->stream, kb[cur], kb[cur ^ 1],
+                           vb[cur], vb[cur ^ 1], n, sh[p], bi[p], (const uint64_t *)scr + p * RADIX, ctx->d_status,
+                           counter, epoch, ctx->d_err);
+        HIP_TRY(ctx, hipGetLastError());
+        cur ^= 1;
+    }
+    *result_in_alt = cur;
+    return KMAN_OK;
+}
+
+}  // namespace
+
+extern "C" int kman_sort_plan(uint32_t key_bits, uint32_t *npass, uint32_t *shift, uint32_t *bits) {
+    if (!npass || !shift || !bits || key_bits == 0 || key_bits > 64) return KMAN_EINVAL;
+    // as few passes of <= 8 bits as possible, bits spread evenly (k=21: 6 x 7)
+    const uint32_t np = (key_bits + 7) / 8;
+    uint32_t at = 0;
+    for (uint32_t p = 0; p < np; p++) {
+        const uint32_t b = (key_bits - at + (np - p) - 1) / (np - p);
+        shift[p] = at;
+        bits[p] = b;
+        at += b;
+    }
+    *npass = np;
+    return KMAN_OK;
+}
+
+extern "C" int kman_sort(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, void *d_vals, void *d_vals_alt,
+                         uint32_t val_bytes, uint64_t n, uint32_t key_bits, const uint64_t *d_hist,
+                         int *result_in_alt) {
+    if (!ctx || !result_in_alt) return KMAN_EINVAL;
+    if (val_bytes != 0 && val_bytes != 4 && val_bytes != 8)
+        return kman_fail(ctx, KMAN_EINVAL, "val_bytes must be 0, 4 or 8");
+    *result_in_alt = 0;
+    if (n <= 1) return KMAN_OK;
+    if (!d_keys || !d_keys_alt || (val_bytes && (!d_vals || !d_vals_alt)))
+        return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    uint32_t np, sh[MAXPASS], bi[MAXPASS];
+    KMAN_TRY(kman_sort_plan(key_bits, &np, sh, bi));
+    // histograms of every pass (device), then to the host for the bucket bases
+    unsigned long long *hist;
+    void *scr;
+    KMAN_TRY(kman_scratch(ctx, MAXPASS * RADIX * 8 + 256, &scr));
+    hist = (unsigned long long *)scr;
+    if (d_hist) {
+        HIP_TRY(ctx, hipMemcpyAsync(hist, d_hist, np * RADIX * 8, hipMemcpyDeviceToDevice, ctx->stream));
+    } else {
+        uint32_t *d_sb = (uint32_t *)((char *)scr + MAXPASS * RADIX * 8);
+        uint32_t sb[MAXPASS];
+        for (uint32_t p = 0; p < np; p++) sb[p] = sh[p] | (bi[p] << 8);
+        HIP_TRY(ctx, hipMemsetAsync(hist, 0, np * RADIX * 8, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(d_sb, sb, sizeof(sb), hipMemcpyHostToDevice, ctx->stream));
+        const uint64_t blocks = ceil_div(n, 256 * 16);
+        KTimer kt_(ctx, "sort_hist");
+        hipLaunchKernelGGL(histogram_kernel, dim3((uint32_t)(blocks < 2048 ? blocks : 2048)), dim3(256), 0,
+                           ctx->stream, d_keys, n, (int)np, d_sb, hist);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    static thread_local uint64_t h_hist[MAXPASS * RADIX];
+    HIP_TRY(ctx, hipMemcpyAsync(h_hist, hist, np * RADIX * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    if (val_bytes == 0)
+        KMAN_TRY(run_passes<NoVal>(ctx, d_keys, d_keys_alt, nullptr, nullptr, n, np, sh, bi, h_hist, result_in_alt));
+    else if (val_bytes == 4)
+        KMAN_TRY(run_passes<uint32_t>(ctx, d_keys, d_keys_alt, (uint32_t *)d_vals, (uint32_t *)d_vals_alt, n, np, sh,
+                                      bi, h_hist, result_in_alt));
+    else
+        KMAN_TRY(run_passes<uint64_t>(ctx, d_keys, d_keys_alt, (uint64_t *)d_vals, (uint64_t *)d_vals_alt, n, np, sh,
+                                      bi, h_hist, result_in_alt));
+    return kman_check_device_error(ctx);
+}

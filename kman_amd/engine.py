@@ -1,0 +1,538 @@
+"""Device-side engine: FASTA bytes -> parse -> extract -> sort -> count/uniq.
+
+Thin Python orchestration over the C ABI (``_native``).  All per-base and
+per-k-mer arithmetic runs in the gfx950 kernels of libkman.so; Python only
+moves handles, sizes and the (small) record-name table.
+
+The mapping to the reference (kmermaid 1.0.0):
+
+=====================  ==========================================  ============================
+engine function        reference                                   kernel(s)
+=====================  ==========================================  ============================
+``parse``              SmartFastaParser.parse, parsers.py:86-128   parse_reduce/scan/emit
+``record names``       record[0].split(" ")[0], batcher.py:551     host (names only)
+``extract``            Sequence.yield_kmers, seq.py:285-328        extract_kernel
+``sort``               Batch.sorted, batch.py:156-168              onesweep_pass x P
+``count``              Crawler.do_batch + join_sequence_count      rle_count_kernel
+``uniq``               Crawler.do_batch + join_unique              rle_uniq_kernel
+``format_*``           join.py:262,284 / seq.py:489-495            host threads (C++)
+=====================  ==========================================  ============================
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import byref, c_int, c_size_t, c_uint32, c_uint64, c_void_p
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+
+from . import _native as N
+
+MAX_K = 32  # 2-bit keys in one u64 on the GPU path
+
+
+def host_threads() -> int:
+    n = os.cpu_count() or 1
+    return max(1, min(n, int(os.environ.get("KMAN_HOST_THREADS", "16"))))
+
+
+class DeviceBuffer:
+    """A device allocation owned by a :class:`Device`."""
+
+    __slots__ = ("dev", "ptr", "nbytes")
+
+    def __init__(self, dev: "Device", nbytes: int):
+        self.dev = dev
+        p = c_void_p()
+        N.check(dev.ctx, N.lib().kman_malloc(dev.ctx, byref(p), max(1, int(nbytes))), "kman_malloc(%d)" % nbytes)
+        self.ptr = p.value
+        self.nbytes = int(nbytes)
+
+    def free(self) -> None:
+        if self.ptr and self.dev is not None and self.dev.ctx:
+            N.lib().kman_free(self.dev.ctx, c_void_p(self.ptr))
+        self.ptr = None
+
+    def __del__(self):  # pragma: no cover - best effort at teardown
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def offset(self, nbytes: int) -> int:
+        return self.ptr + int(nbytes)
+
+
+class Device:
+    """One HIP context (stream, look-back scratch) on one GPU."""
+
+    def __init__(self, device: int = 0):
+        L = N.lib()
+        ctx = c_void_p()
+        rc = L.kman_create(int(device), byref(ctx))
+        if rc != N.KMAN_OK:
+            raise RuntimeError(
+                "kman_create(device=%d) failed (%d): no usable MI355X/HIP device (%d visible)"
+                % (device, rc, N.device_count())
+            )
+        self.ctx = ctx.value
+        self.index = device
+
+    def close(self) -> None:
+        if self.ctx:
+            N.lib().kman_destroy(c_void_p(self.ctx))
+            self.ctx = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- memory
+    def alloc(self, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    def upload(self, buf: DeviceBuffer, data, offset: int = 0) -> None:
+        mv = memoryview(data).cast("B")
+        if offset + mv.nbytes > buf.nbytes:
+            raise ValueError("upload overflows the device buffer")
+        src = (ctypes.c_char * mv.nbytes).from_buffer_copy(mv) if mv.readonly else (ctypes.c_char * mv.nbytes).from_buffer(mv)
+        N.check(self.ctx, N.lib().kman_memcpy_h2d(self.ctx, c_void_p(buf.ptr + offset), src, mv.nbytes), "h2d")
+
+    def download(self, buf: DeviceBuffer, count: int, dtype, offset: int = 0) -> np.ndarray:
+        out = np.empty(int(count), dtype=dtype)
+        if out.nbytes:
+            N.check(
+                self.ctx,
+                N.lib().kman_memcpy_d2h(self.ctx, out.ctypes.data_as(c_void_p), c_void_p(buf.ptr + offset), out.nbytes),
+                "d2h",
+            )
+        return out
+
+    def memset(self, buf: DeviceBuffer, value: int, nbytes: int, offset: int = 0) -> None:
+        N.check(self.ctx, N.lib().kman_memset(self.ctx, c_void_p(buf.ptr + offset), value, nbytes), "memset")
+
+    def sync(self) -> None:
+        N.check(self.ctx, N.lib().kman_sync(self.ctx), "sync")
+
+
+_DEFAULT: Optional[Device] = None
+
+
+def default_device() -> Device:
+    """Process-wide device (LOCAL_RANK when launched one process per GPU)."""
+    global _DEFAULT
+    if _DEFAULT is None:
+        _DEFAULT = Device(int(os.environ.get("KMAN_DEVICE", os.environ.get("LOCAL_RANK", "0"))))
+    return _DEFAULT
+
+
+# --------------------------------------------------------------------- parse
+
+
+def _title_name(text: bytes, hdr: int) -> bytes:
+    """``title = line[1:].rstrip()``; ``name = title.split(" ")[0]``.
+
+    parsers.py:85 and batcher.py:551.  Decoded like the reference's text-mode
+    file (UTF-8), so Python's own rstrip/split semantics apply verbatim."""
+    i = hdr + 1
+    n = len(text)
+    j = i
+    # universal newlines: the header line ends at \n or \r
+    while j < n and text[j] != 0x0A and text[j] != 0x0D:
+        j += 1
+    title = text[i:j].decode("utf-8", errors="surrogateescape").rstrip()
+    return title.split(" ")[0].encode("utf-8", errors="surrogateescape")
+
+
+@dataclass
+class Parsed:
+    dev: Device
+    codes: DeviceBuffer  # n_bases codes + 64 pad (see include/kman.h)
+    n_bases: int
+    n_records: int
+    rec_hdr: np.ndarray  # u64 byte offset of each '>'
+    rec_seq: np.ndarray  # u64 first base index of each record
+    names: List[bytes]
+    names_blob: bytes
+    name_off: np.ndarray  # u64, len n_records + 1
+
+    def record_of(self, base: int) -> int:
+        return int(np.searchsorted(self.rec_seq, base, side="right")) - 1
+
+    def free(self) -> None:
+        self.codes.free()
+
+
+def parse(dev: Device, text: bytes) -> Parsed:
+    """FASTA bytes -> device codes + record table (kman_parse_fasta)."""
+    n = len(text)
+    if n == 0:
+        raise AssertionError("premature end of file or empty file")
+    L = N.lib()
+    d_text = dev.alloc(n + 64)
+    codes = dev.alloc(n + 64)
+    try:
+        dev.upload(d_text, text)
+        # record capacity: one record per 2 bytes at most ('>' + terminator)
+        cap = n // 2 + 1
+        d_hdr = dev.alloc(8 * cap)
+        d_seq = dev.alloc(8 * cap)
+        info = N.ParseInfo()
+        rc = L.kman_parse_fasta(dev.ctx, c_void_p(d_text.ptr), n, c_void_p(codes.ptr), c_void_p(d_hdr.ptr),
+                                c_void_p(d_seq.ptr), cap, byref(info))
+        N.check(dev.ctx, rc, "kman_parse_fasta")
+        R = int(info.n_records)
+        rec_hdr = dev.download(d_hdr, R, np.uint64)
+        rec_seq = dev.download(d_seq, R, np.uint64)
+        d_hdr.free()
+        d_seq.free()
+    finally:
+        d_text.free()
+    names = [_title_name(text, int(h)) for h in rec_hdr]
+    name_off = np.zeros(R + 1, dtype=np.uint64)
+    if R:
+        name_off[1:] = np.cumsum([len(x) for x in names], dtype=np.uint64)
+    return Parsed(dev, codes, int(info.n_bases), R, rec_hdr, rec_seq, names, b"".join(names), name_off)
+
+
+def check_empty_names(p: Parsed, k: int) -> None:
+    """The reference re-reads every k-mer header through
+    ``SequenceCoords.from_str`` (seq.py:106-127, via batch.py:170-186) whose
+    regex needs a non-empty record name: a record with an empty name that
+    yields any k-mer raises AssertionError before any output is written."""
+    for r, nm in enumerate(p.names):
+        if nm:
+            continue
+        b = int(p.rec_seq[r])
+        e = int(p.rec_seq[r + 1]) if r + 1 < p.n_records else p.n_bases
+        if e - b < k:
+            continue
+        codes = p.dev.download(p.codes, e - b, np.uint8, offset=b) & 7
+        run = 0
+        for i, c in enumerate(codes.tolist()):
+            run = run + 1 if c < 4 else 0
+            if run >= k:
+                st = i - k + 1
+                raise AssertionError("incompatible string: :%d-%d:+" % (st, st + k))
+
+
+# ------------------------------------------------------------------- extract
+
+
+@dataclass
+class Kmers:
+    """k-mer keys (+ pos payload) in the reference's stream order."""
+
+    keys: DeviceBuffer
+    alt: DeviceBuffer
+    pos: Optional[DeviceBuffer]
+    pos_alt: Optional[DeviceBuffer]
+    pos_bytes: int
+    n: int
+    k: int
+    hist: DeviceBuffer
+    sorted: bool = False
+
+    def free(self) -> None:
+        for b in (self.keys, self.alt, self.pos, self.pos_alt, self.hist):
+            if b is not None:
+                b.free()
+
+
+def flags_for(rc: bool, want_pos: bool, canonical: bool = False) -> int:
+    return (N.KMAN_RC if rc else 0) | (N.KMAN_WANT_POS if want_pos else 0) | (N.KMAN_CANONICAL if canonical else 0)
+
+
+def count_kmers(p: Parsed, k: int, rc: bool, canonical: bool = False) -> int:
+    _check_k(k)
+    out = c_uint64(0)
+    N.check(p.dev.ctx, N.lib().kman_count_kmers(p.dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
+                                                 flags_for(rc, False, canonical), byref(out)), "kman_count_kmers")
+    return int(out.value)
+
+
+def _check_k(k: int) -> None:
+    if k <= 1:
+        raise AssertionError("k must be >= 1, got %d instead." % k)
+    if k > MAX_K:
+        raise NotImplementedError("k=%d: the MI355X path packs k-mers in 64-bit keys (k <= %d)" % (k, MAX_K))
+
+
+def extract(p: Parsed, k: int, rc: bool, want_pos: bool, canonical: bool = False) -> Kmers:
+    """kman_extract: keys (+ pos) in stream order, plus the radix histograms."""
+    _check_k(k)
+    dev = p.dev
+    L = N.lib()
+    bound = p.n_bases * (2 if rc and not canonical else 1)
+    n = max(bound, 1)
+    pos_bytes = 4 if 2 * p.n_bases <= 0xFFFFFFFF else 8
+    keys = dev.alloc(8 * n)
+    alt = dev.alloc(8 * n)
+    pos = dev.alloc(pos_bytes * n) if want_pos else None
+    pos_alt = dev.alloc(pos_bytes * n) if want_pos else None
+    hist = dev.alloc(8 * 256 * 8)
+    dev.memset(hist, 0, 8 * 256 * 8)
+    out = c_uint64(0)
+    rc_ = L.kman_extract(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k, flags_for(rc, want_pos, canonical),
+                         c_void_p(keys.ptr), c_void_p(pos.ptr if pos else None), pos_bytes, bound,
+                         c_void_p(hist.ptr), byref(out))
+    N.check(dev.ctx, rc_, "kman_extract")
+    return Kmers(keys, alt, pos, pos_alt, pos_bytes if want_pos else 0, int(out.value), k, hist)
+
+
+def sort(km: Kmers, dev: Device) -> None:
+    """kman_sort (stable LSD radix) in place: afterwards km.keys/km.pos are sorted."""
+    if km.sorted:
+        return
+    res = c_int(0)
+    rc = N.lib().kman_sort(dev.ctx, c_void_p(km.keys.ptr), c_void_p(km.alt.ptr),
+                           c_void_p(km.pos.ptr if km.pos else None), c_void_p(km.pos_alt.ptr if km.pos_alt else None),
+                           km.pos_bytes, km.n, 2 * km.k, c_void_p(km.hist.ptr), byref(res))
+    N.check(dev.ctx, rc, "kman_sort")
+    if res.value:
+        km.keys, km.alt = km.alt, km.keys
+        km.pos, km.pos_alt = km.pos_alt, km.pos
+    km.sorted = True
+
+
+@dataclass
+class CountResult:
+    ukeys: DeviceBuffer
+    counts: DeviceBuffer
+    count_bytes: int
+    n: int
+    k: int
+
+
+def rle_count(km: Kmers, dev: Device) -> CountResult:
+    cb = 4 if km.n <= 0xFFFFFFFF else 8
+    ukeys = dev.alloc(8 * max(km.n, 1))
+    counts = dev.alloc(cb * max(km.n, 1))
+    out = c_uint64(0)
+    N.check(dev.ctx, N.lib().kman_rle_count(dev.ctx, c_void_p(km.keys.ptr), km.n, c_void_p(ukeys.ptr),
+                                             c_void_p(counts.ptr), cb, byref(out)), "kman_rle_count")
+    return CountResult(ukeys, counts, cb, int(out.value), km.k)
+
+
+@dataclass
+class UniqResult:
+    keys: DeviceBuffer
+    pos: DeviceBuffer
+    pos_bytes: int
+    n: int
+    k: int
+
+
+def rle_uniq(km: Kmers, dev: Device) -> UniqResult:
+    if km.pos is None:
+        raise ValueError("uniq needs the pos payload (extract with want_pos=True)")
+    okeys = dev.alloc(8 * max(km.n, 1))
+    opos = dev.alloc(km.pos_bytes * max(km.n, 1))
+    out = c_uint64(0)
+    N.check(dev.ctx, N.lib().kman_rle_uniq(dev.ctx, c_void_p(km.keys.ptr), c_void_p(km.pos.ptr), km.pos_bytes,
+                                            km.n, c_void_p(okeys.ptr), c_void_p(opos.ptr), byref(out)),
+            "kman_rle_uniq")
+    return UniqResult(okeys, opos, km.pos_bytes, int(out.value), km.k)
+
+
+# ------------------------------------------------------------------ formatting
+
+
+def _format(fn, *args) -> bytes:
+    used = c_size_t(0)
+    rc = fn(*args, None, 0, byref(used), host_threads())
+    if rc not in (N.KMAN_OK, N.KMAN_ECAP):
+        raise RuntimeError("formatter failed (%d)" % rc)
+    buf = ctypes.create_string_buffer(max(1, used.value))
+    rc = fn(*args, buf, used.value, byref(used), host_threads())
+    if rc != N.KMAN_OK:
+        raise RuntimeError("formatter failed (%d)" % rc)
+    return buf.raw[: used.value]
+
+
+def format_count(ukeys: np.ndarray, counts: np.ndarray, k: int) -> bytes:
+    """``"%s\\t%d\\n" % (seq, count)`` per group (join.py:283-284)."""
+    ukeys = np.ascontiguousarray(ukeys, dtype=np.uint64)
+    cb = counts.dtype.itemsize
+    return _format(N.lib().kman_format_count, ukeys.ctypes.data_as(c_void_p),
+                   np.ascontiguousarray(counts).ctypes.data_as(c_void_p), cb, len(ukeys), k)
+
+
+def format_fasta(keys: np.ndarray, pos: np.ndarray, k: int, p: Parsed) -> bytes:
+    """``">%s\\n%s\\n" % (header, seq)`` (join.py:262 / seq.py:495)."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    pos = np.ascontiguousarray(pos)
+    names = ctypes.create_string_buffer(p.names_blob, max(1, len(p.names_blob)))
+    off = np.ascontiguousarray(p.name_off, dtype=np.uint64)
+    rs = np.ascontiguousarray(p.rec_seq, dtype=np.uint64)
+    return _format(N.lib().kman_format_uniq, keys.ctypes.data_as(c_void_p), pos.ctypes.data_as(c_void_p),
+                   pos.dtype.itemsize, len(keys), k, names, off.ctypes.data_as(c_void_p),
+                   rs.ctypes.data_as(c_void_p), p.n_records)
+
+
+def download_count(dev: Device, r: CountResult):
+    ukeys = dev.download(r.ukeys, r.n, np.uint64)
+    counts = dev.download(r.counts, r.n, np.uint32 if r.count_bytes == 4 else np.uint64)
+    return ukeys, counts
+
+
+def download_uniq(dev: Device, r: UniqResult):
+    keys = dev.download(r.keys, r.n, np.uint64)
+    pos = dev.download(r.pos, r.n, np.uint32 if r.pos_bytes == 4 else np.uint64)
+    return keys, pos
+
+
+# ------------------------------------------------------------------ pipelines
+
+
+def read_input(path: str) -> bytes:
+    """Bytes of a FASTA file; ``.gz`` is decompressed (batcher.py:480)."""
+    if path.endswith(".gz"):
+        import gzip
+
+        with gzip.open(path, "rb") as fh:
+            return fh.read()
+    with open(path, "rb") as fh:
+        return fh.read()
+
+
+def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = None) -> bytes:
+    """``kmer count`` output bytes for a FASTA text (SEQ_COUNT mode)."""
+    dev = dev or default_device()
+    _check_k(k)
+    p = parse(dev, text)
+    try:
+        check_empty_names(p, k)
+        km = extract(p, k, rc, want_pos=False)
+        try:
+            if km.n == 0:
+                return b""
+            sort(km, dev)
+            r = rle_count(km, dev)
+            try:
+                ukeys, counts = download_count(dev, r)
+            finally:
+                r.ukeys.free()
+                r.counts.free()
+        finally:
+            km.free()
+        return format_count(ukeys, counts, k)
+    finally:
+        p.free()
+
+
+def uniq_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = None) -> bytes:
+    """``kmer uniq`` output bytes for a FASTA text (UNIQUE mode)."""
+    dev = dev or default_device()
+    _check_k(k)
+    p = parse(dev, text)
+    try:
+        check_empty_names(p, k)
+        km = extract(p, k, rc, want_pos=True)
+        try:
+            if km.n == 0:
+                return b""
+            sort(km, dev)
+            r = rle_uniq(km, dev)
+            try:
+                keys, pos = download_uniq(dev, r)
+            finally:
+                r.keys.free()
+                r.pos.free()
+        finally:
+            km.free()
+        return format_fasta(keys, pos, k, p)
+    finally:
+        p.free()
+
+
+# ------------------------------------------------------- resident pipeline
+
+
+class ResidentPipeline:
+    """One FASTA text resident in HBM, every buffer preallocated: ``step()``
+    runs parse -> extract -> sort -> count|uniq with no allocation, leaving
+    the result device-resident (what bench.py times)."""
+
+    def __init__(self, dev: Device, text: bytes, k: int, mode: str = "uniq", rc: bool = False):
+        _check_k(k)
+        if mode not in ("count", "uniq"):
+            raise ValueError(mode)
+        self.dev, self.k, self.mode, self.rc = dev, k, mode, rc
+        n = len(text)
+        self.n_bytes = n
+        self.text = dev.alloc(n + 64)
+        dev.upload(self.text, text)
+        self.codes = dev.alloc(n + 64)
+        self.rec_cap = n // 2 + 1
+        self.rec_hdr = dev.alloc(8 * self.rec_cap)
+        self.rec_seq = dev.alloc(8 * self.rec_cap)
+        self.bound = max(1, n * (2 if rc else 1))
+        self.pos_bytes = 4 if 2 * n <= 0xFFFFFFFF else 8
+        want_pos = mode == "uniq"
+        self.keys = dev.alloc(8 * self.bound)
+        self.alt = dev.alloc(8 * self.bound)
+        self.pos = dev.alloc(self.pos_bytes * self.bound) if want_pos else None
+        self.pos_alt = dev.alloc(self.pos_bytes * self.bound) if want_pos else None
+        self.hist = dev.alloc(8 * 256 * 8)
+        self.out_keys = dev.alloc(8 * self.bound)
+        self.count_bytes = 4 if self.bound <= 0xFFFFFFFF else 8
+        self.out_vals = dev.alloc((self.pos_bytes if want_pos else self.count_bytes) * self.bound)
+        self.flags = flags_for(rc, want_pos)
+        self.n_kmers = 0
+        self.n_out = 0
+        self.n_bases = 0
+        self.sorted_in_alt = False
+
+    def step(self) -> int:
+        L, ctx = N.lib(), self.dev.ctx
+        info = N.ParseInfo()
+        N.check(ctx, L.kman_parse_fasta(ctx, c_void_p(self.text.ptr), self.n_bytes, c_void_p(self.codes.ptr),
+                                        c_void_p(self.rec_hdr.ptr), c_void_p(self.rec_seq.ptr), self.rec_cap,
+                                        byref(info)), "kman_parse_fasta")
+        self.n_bases = int(info.n_bases)
+        N.check(ctx, L.kman_memset(ctx, c_void_p(self.hist.ptr), 0, 8 * 256 * 8), "memset")
+        n = c_uint64(0)
+        pos = c_void_p(self.pos.ptr) if self.pos else c_void_p(None)
+        N.check(ctx, L.kman_extract(ctx, c_void_p(self.codes.ptr), self.n_bases, self.k, self.flags,
+                                    c_void_p(self.keys.ptr), pos, self.pos_bytes, self.bound,
+                                    c_void_p(self.hist.ptr), byref(n)), "kman_extract")
+        self.n_kmers = int(n.value)
+        res = c_int(0)
+        N.check(ctx, L.kman_sort(ctx, c_void_p(self.keys.ptr), c_void_p(self.alt.ptr), pos,
+                                 c_void_p(self.pos_alt.ptr if self.pos_alt else None),
+                                 self.pos_bytes if self.pos else 0, self.n_kmers, 2 * self.k,
+                                 c_void_p(self.hist.ptr), byref(res)), "kman_sort")
+        self.sorted_in_alt = bool(res.value)
+        skeys = self.alt if res.value else self.keys
+        out = c_uint64(0)
+        if self.mode == "count":
+            N.check(ctx, L.kman_rle_count(ctx, c_void_p(skeys.ptr), self.n_kmers, c_void_p(self.out_keys.ptr),
+                                          c_void_p(self.out_vals.ptr), self.count_bytes, byref(out)),
+                    "kman_rle_count")
+        else:
+            spos = self.pos_alt if res.value else self.pos
+            N.check(ctx, L.kman_rle_uniq(ctx, c_void_p(skeys.ptr), c_void_p(spos.ptr), self.pos_bytes,
+                                         self.n_kmers, c_void_p(self.out_keys.ptr), c_void_p(self.out_vals.ptr),
+                                         byref(out)), "kman_rle_uniq")
+        self.n_out = int(out.value)
+        return self.n_kmers
+
+    def timing(self, enable: bool) -> None:
+        N.check(self.dev.ctx, N.lib().kman_timing_enable(self.dev.ctx, 1 if enable else 0), "timing")
+
+    def timed(self, tag: str):
+        n, ms = c_uint64(0), ctypes.c_double(0)
+        N.check(self.dev.ctx, N.lib().kman_timing_query(self.dev.ctx, tag.encode(), byref(n), byref(ms)), "timing")
+        return int(n.value), float(ms.value)
+
+    def free(self) -> None:
+        for b in (self.text, self.codes, self.rec_hdr, self.rec_seq, self.keys, self.alt, self.pos, self.pos_alt,
+                  self.hist, self.out_keys, self.out_vals):
+            if b is not None:
+                b.free()

@@ -1,0 +1,51 @@
+"""Shared fixtures: golden manifest, deterministic inputs, oracle binary."""
+
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, ROOT)
+sys.path.insert(0, GOLDEN)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
+
+
+@pytest.fixture(scope="session")
+def manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as fh:
+        return json.load(fh)
+
+
+@pytest.fixture(scope="session")
+def golden_inputs(tmp_path_factory):
+    """Rebuild every golden input from its seed; check it against the sha256
+    recorded when the reference ran on it."""
+    import inputs
+
+    d = tmp_path_factory.mktemp("inputs")
+    paths = inputs.build_inputs(str(d))
+    return paths
+
+
+@pytest.fixture(scope="session")
+def oracle_bin():
+    exe = os.path.join(ROOT, "oracle", "kman_oracle")
+    if not os.path.isfile(exe):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    return exe
+
+
+def sha256_bytes(data: bytes) -> str:
+    import hashlib
+
+    return hashlib.sha256(data).hexdigest()
