@@ -82,6 +82,7 @@ __global__ __launch_bounds__(RT) void rle_count_kernel(const uint64_t *__restric
                                                        uint32_t *__restrict__ counter, uint32_t epoch,
                                                        uint32_t *__restrict__ err) {
     __shared__ __attribute__((aligned(16))) uint64_t s[RTILE];
+    __shared__ __attribute__((aligned(16))) C sc[RTILE];
     __shared__ uint32_t lds_scan[RT / 64];
     __shared__ uint64_t lds_scan64[RT / 64];
     __shared__ uint64_t lds_base, lds_head;
@@ -126,6 +127,12 @@ __global__ __launch_bounds__(RT) void rle_count_kernel(const uint64_t *__restric
     const uint64_t base = lds_base;
     uint64_t cur_head = lh_before ? lh_before : lds_head;  // head position + 1 of the open group
     uint64_t slot = base + hoff;                           // groups opened before this key
+    // the tile's tails fill global slots [out0, out0 + tile_tails): stage them
+    // in LDS (keys over s, counts in sc) and write both out coalesced
+    const bool first_is_head = tb == 0 || s[0] != prev_key;
+    const uint64_t out0 = base - (first_is_head ? 0 : 1);
+    uint32_t tile_tails;
+    block_exclusive_scan<RT>((uint32_t)__popc(tails), SumU32(), 0u, lds_scan, &tile_tails);
 #pragma unroll
     for (int j = 0; j < RI; j++) {
         const uint64_t i = tb + t0 + j;
@@ -134,9 +141,15 @@ __global__ __launch_bounds__(RT) void rle_count_kernel(const uint64_t *__restric
             slot++;
         }
         if ((tails >> j) & 1u) {
-            ukeys[slot - 1] = k[j];
-            counts[slot - 1] = (C)(i + 2 - cur_head);
+            const uint32_t q = (uint32_t)(slot - 1 - out0);
+            s[q] = k[j];
+            sc[q] = (C)(i + 2 - cur_head);
         }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < tile_tails; q += RT) {
+        ukeys[out0 + q] = s[q];
+        counts[out0 + q] = sc[q];
     }
 }
 
@@ -146,19 +159,28 @@ __global__ __launch_bounds__(RT) void rle_uniq_kernel(const uint64_t *__restrict
                                                       uint64_t *__restrict__ st_sum, uint32_t *__restrict__ counter,
                                                       uint32_t epoch, uint32_t *__restrict__ err) {
     __shared__ __attribute__((aligned(16))) uint64_t s[RTILE];
+    __shared__ __attribute__((aligned(16))) V sv[RTILE];
     __shared__ uint32_t lds_scan[RT / 64];
     __shared__ uint64_t lds_base;
     __shared__ uint32_t lds_tile;
     const int64_t tile = grab_tile(counter, &lds_tile);
     const uint64_t tb = (uint64_t)tile * RTILE;
     stage_keys(keys, n, tb, s);
+    for (int i = threadIdx.x; i < RTILE; i += RT) {
+        const uint64_t idx = tb + i;
+        sv[i] = idx < n ? vals[idx] : (V)0;
+    }
     const uint64_t prev_key = tb ? keys[tb - 1] : 0;
     const uint64_t next_key = tb + RTILE < n ? keys[tb + RTILE] : 0;
     __syncthreads();
     const uint32_t t0 = threadIdx.x * RI;
     uint64_t k[RI];
+    V v[RI];
 #pragma unroll
-    for (int j = 0; j < RI; j++) k[j] = s[t0 + j];
+    for (int j = 0; j < RI; j++) {
+        k[j] = s[t0 + j];
+        v[j] = sv[t0 + j];
+    }
     uint32_t single = 0;
 #pragma unroll
     for (int j = 0; j < RI; j++) {
@@ -176,15 +198,22 @@ __global__ __launch_bounds__(RT) void rle_uniq_kernel(const uint64_t *__restrict
         const uint64_t b = wave_lookback<0>(st_sum, tile, tile_cnt, epoch, err);
         if (threadIdx.x == 0) lds_base = b;
     }
-    __syncthreads();
-    uint64_t o = lds_base + off;
+    // stage the kept keys / payloads at their tile-local slots (the scan's
+    // barriers ordered every read of s / sv above before these writes)
+    uint32_t o = off;
 #pragma unroll
     for (int j = 0; j < RI; j++) {
         if ((single >> j) & 1u) {
-            okeys[o] = k[j];
-            ovals[o] = vals[tb + t0 + j];
+            s[o] = k[j];
+            sv[o] = v[j];
             o++;
         }
+    }
+    __syncthreads();
+    const uint64_t base = lds_base;
+    for (uint32_t q = threadIdx.x; q < tile_cnt; q += RT) {
+        okeys[base + q] = s[q];
+        ovals[base + q] = sv[q];
     }
 }
 

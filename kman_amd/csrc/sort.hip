@@ -24,55 +24,80 @@
 
 namespace {
 
-constexpr int ST = 256;         // threads per tile
-constexpr int SI = 16;          // keys per thread
-constexpr int STILE = ST * SI;  // 4096 keys
 constexpr int RADIX = 256;
-constexpr int NWAVE = ST / 64;
 constexpr int MAXPASS = 8;
+#ifndef KMAN_LB
+#define KMAN_LB 8
+#endif
+constexpr int LB = KMAN_LB;  // predecessor status words fetched per look-back round
 
 struct NoVal {};
 
-// per-thread (one digit) sequential look-back over the tile chain of that digit
+// One thread per digit walks back along that digit's tile chain, LB
+// predecessors per round (independent sc1 loads in flight), summing AGG
+// counts until it meets an INCL prefix.
+KMAN_DEV void digit_publish(uint64_t *st, int64_t tile, uint64_t agg, uint32_t epoch) {
+    st_store(&st[(uint64_t)tile * RADIX], st_make(tile == 0 ? ST_INCL : ST_AGG, epoch, agg));
+}
+
+template <bool PUBLISHED>
 KMAN_DEV uint64_t digit_lookback(uint64_t *st, int64_t tile, uint64_t agg, uint32_t epoch, uint32_t *err) {
     if (tile == 0) {
-        st_store(&st[0], st_make(ST_INCL, epoch, agg));
+        if (!PUBLISHED) st_store(&st[0], st_make(ST_INCL, epoch, agg));
         return 0;
     }
-    st_store(&st[(uint64_t)tile * RADIX], st_make(ST_AGG, epoch, agg));
+    if (!PUBLISHED) st_store(&st[(uint64_t)tile * RADIX], st_make(ST_AGG, epoch, agg));
     uint64_t excl = 0;
     int64_t j = tile - 1;
     uint32_t spins = 0;
     while (j >= 0) {
-        const uint64_t w = st_load(&st[(uint64_t)j * RADIX]);
-        const uint64_t f = st_flag(w, epoch);
-        if (f == 0) {
+        uint64_t w[LB];
+#pragma unroll
+        for (int q = 0; q < LB; q++)
+            w[q] = (j - q >= 0) ? st_load(&st[(uint64_t)(j - q) * RADIX]) : st_make(ST_INCL, epoch, 0);
+        bool done = false, stall = false;
+        int used = 0;
+#pragma unroll
+        for (int q = 0; q < LB; q++) {
+            if (done || stall) continue;
+            const uint64_t f = st_flag(w[q], epoch);
+            if (f == 0) {
+                stall = true;
+                continue;
+            }
+            excl += w[q] & ST_VMASK;
+            used++;
+            if (f == ST_INCL) done = true;
+        }
+        if (done) break;
+        j -= used;
+        if (stall) {
             if (spin_give_up(spins, err, 2u)) break;
             __builtin_amdgcn_s_sleep(1);
-            continue;
         }
-        excl += w & ST_VMASK;
-        if (f == ST_INCL) break;
-        --j;
     }
     st_store(&st[(uint64_t)tile * RADIX], st_make(ST_INCL, epoch, excl + agg));
     return excl;
 }
 
-template <typename V>
-__global__ __launch_bounds__(ST) void onesweep_pass(const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
+// One LSD digit pass over a tile of NT*SI keys.
+template <int NT, int SI, bool EARLY, typename V>
+__global__ __launch_bounds__(NT) void onesweep_pass(const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
                                                     const V *__restrict__ vin, V *__restrict__ vout, uint64_t n,
                                                     uint32_t shift, uint32_t bits,
                                                     const uint64_t *__restrict__ bucket_base,
                                                     uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
                                                     uint32_t epoch, uint32_t *__restrict__ err) {
     constexpr bool HAS_V = !std::is_same<V, NoVal>::value;
-    __shared__ __attribute__((aligned(16))) uint64_t skeys[STILE];
-    __shared__ uint8_t sdig[STILE];
+    constexpr int TILE = NT * SI;
+    constexpr int NWAVE = NT / 64;
+    static_assert(NT >= RADIX, "one thread per digit");
+    __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
     __shared__ uint32_t whist[NWAVE][RADIX];
+    __shared__ uint32_t thist[RADIX];
     __shared__ uint32_t lstart[RADIX];
     __shared__ uint64_t gstart[RADIX];
-    __shared__ uint32_t lds_scan[ST / 64];
+    __shared__ uint32_t lds_scan[NT / 64];
     __shared__ uint32_t lds_tile;
 
     const int64_t tile = grab_tile(counter, &lds_tile);
@@ -80,9 +105,10 @@ __global__ __launch_bounds__(ST) void onesweep_pass(const uint64_t *__restrict__
     const int w = threadIdx.x >> 6;
     const uint32_t radix = 1u << bits;
     const uint32_t dmask = radix - 1;
-    for (int i = threadIdx.x; i < NWAVE * RADIX; i += ST) (&whist[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&whist[0][0])[i] = 0;
+    if (EARLY && threadIdx.x < RADIX) thist[threadIdx.x] = 0;
 
-    const uint64_t tb = (uint64_t)tile * STILE;
+    const uint64_t tb = (uint64_t)tile * TILE;
     const uint64_t ib = tb + (uint64_t)w * (SI * 64) + lane;
     uint64_t key[SI];
     uint32_t rank[SI];
@@ -92,6 +118,15 @@ __global__ __launch_bounds__(ST) void onesweep_pass(const uint64_t *__restrict__
         key[i] = idx < n ? kin[idx] : 0;
     }
     __syncthreads();
+    if (EARLY) {
+        // publish this tile's digit counts as soon as its keys have landed, so
+        // successors' look-backs are not held up by the ranking below
+#pragma unroll
+        for (int i = 0; i < SI; i++)
+            if (ib + (uint64_t)i * 64 < n) atomicAdd(&thist[(uint32_t)(key[i] >> shift) & dmask], 1u);
+        __syncthreads();
+        if (threadIdx.x < radix) digit_publish(status + threadIdx.x, tile, thist[threadIdx.x], epoch);
+    }
 
     // stable in-wave ranking: items in order, lanes in order
 #pragma unroll
@@ -115,17 +150,24 @@ __global__ __launch_bounds__(ST) void onesweep_pass(const uint64_t *__restrict__
     // per-digit tile counts and per-wave exclusive offsets (thread = digit)
     const uint32_t d0 = threadIdx.x;
     uint32_t tot = 0;
+    if (d0 < RADIX) {
 #pragma unroll
-    for (int ww = 0; ww < NWAVE; ww++) {
-        const uint32_t c = whist[ww][d0];
-        whist[ww][d0] = tot;
-        tot += c;
+        for (int ww = 0; ww < NWAVE; ww++) {
+            const uint32_t c = whist[ww][d0];
+            whist[ww][d0] = tot;
+            tot += c;
+        }
     }
     uint32_t tile_total;
-    const uint32_t ls = block_exclusive_scan<ST>(tot, SumU32(), 0u, lds_scan, &tile_total);
-    lstart[d0] = ls;
+    const uint32_t ls = block_exclusive_scan<NT>(tot, SumU32(), 0u, lds_scan, &tile_total);
+    if (d0 < RADIX) lstart[d0] = ls;
     if (d0 < radix) {
-        const uint64_t excl = digit_lookback(status + d0, tile, tot, epoch, err);
+#if defined(KMAN_ABL) && (KMAN_ABL & 1)
+        // ablation build only: no look-back (wrong offsets, measures the rest)
+        const uint64_t excl = (uint64_t)tile * TILE / radix;
+#else
+        const uint64_t excl = digit_lookback<EARLY>(status + d0, tile, tot, epoch, err);
+#endif
         gstart[d0] = bucket_base[d0] + excl - ls;
     }
     __syncthreads();
@@ -137,14 +179,22 @@ __global__ __launch_bounds__(ST) void onesweep_pass(const uint64_t *__restrict__
         const bool valid = ib + (uint64_t)i * 64 < n;
         const uint32_t d = (uint32_t)(key[i] >> shift) & dmask;
         lp[i] = valid ? lstart[d] + whist[w][d] + rank[i] : 0xffffffffu;
-        if (valid) {
-            skeys[lp[i]] = key[i];
-            sdig[lp[i]] = (uint8_t)d;
-        }
+        if (valid) skeys[lp[i]] = key[i];
     }
     __syncthreads();
-    const uint32_t cnt = (uint32_t)(n - tb < (uint64_t)STILE ? n - tb : (uint64_t)STILE);
-    for (uint32_t q = threadIdx.x; q < cnt; q += ST) kout[gstart[sdig[q]] + q] = skeys[q];
+    const uint32_t cnt = (uint32_t)(n - tb < (uint64_t)TILE ? n - tb : (uint64_t)TILE);
+#if defined(KMAN_ABL) && (KMAN_ABL & 2)
+    // ablation build only: contiguous writes instead of the digit scatter
+    for (uint32_t q = threadIdx.x; q < cnt; q += NT) {
+        const uint64_t kk = skeys[q];
+        kout[tb + q] = kk + gstart[(uint32_t)(kk >> shift) & dmask];
+    }
+#else
+    for (uint32_t q = threadIdx.x; q < cnt; q += NT) {
+        const uint64_t kk = skeys[q];
+        kout[gstart[(uint32_t)(kk >> shift) & dmask] + q] = kk;
+    }
+#endif
     if constexpr (HAS_V) {
         V val[SI];
 #pragma unroll
@@ -152,13 +202,24 @@ __global__ __launch_bounds__(ST) void onesweep_pass(const uint64_t *__restrict__
             const uint64_t idx = ib + (uint64_t)i * 64;
             val[i] = idx < n ? vin[idx] : (V)0;
         }
+        // digits of the tile-ordered keys, before skeys is reused for values
+        uint8_t dq[(TILE + NT - 1) / NT];
+#pragma unroll
+        for (int r = 0; r < (TILE + NT - 1) / NT; r++) {
+            const uint32_t q = threadIdx.x + r * NT;
+            dq[r] = q < cnt ? (uint8_t)((uint32_t)(skeys[q] >> shift) & dmask) : 0;
+        }
         __syncthreads();
         V *sval = reinterpret_cast<V *>(skeys);
 #pragma unroll
         for (int i = 0; i < SI; i++)
             if (lp[i] != 0xffffffffu) sval[lp[i]] = val[i];
         __syncthreads();
-        for (uint32_t q = threadIdx.x; q < cnt; q += ST) vout[gstart[sdig[q]] + q] = sval[q];
+#pragma unroll
+        for (int r = 0; r < (TILE + NT - 1) / NT; r++) {
+            const uint32_t q = threadIdx.x + r * NT;
+            if (q < cnt) vout[gstart[dq[r]] + q] = sval[q];
+        }
     }
 }
 
@@ -182,7 +243,7 @@ __global__ __launch_bounds__(256) void histogram_kernel(const uint64_t *__restri
     }
 }
 
-template <typename V>
+template <int NT, int SI, bool EARLY, typename V>
 int run_passes(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, V *v0, V *v1, uint64_t n, uint32_t np, const uint32_t *sh,
                const uint32_t *bi, const uint64_t *h_hist, int *result_in_alt) {
     // bucket bases per pass (host: 256 x npass), skipping single-bucket passes
@@ -204,7 +265,7 @@ int run_passes(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, V *v0, V *v1, uint64_t
     void *scr;
     KMAN_TRY(kman_scratch(ctx, sizeof(bases), &scr));
     HIP_TRY(ctx, hipMemcpyAsync(scr, bases, sizeof(bases), hipMemcpyHostToDevice, ctx->stream));
-    const uint64_t n_tiles = ceil_div(n, STILE);
+    const uint64_t n_tiles = ceil_div(n, (uint64_t)NT * SI);
     int cur = 0;
     uint64_t *kb[2] = {k0, k1};
     V *vb[2] = {v0, v1};
@@ -213,7 +274,7 @@ int run_passes(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, V *v0, V *v1, uint64_t
         uint32_t epoch, *counter;
         KMAN_TRY(kman_lookback_begin(ctx, n_tiles * RADIX, &epoch, &counter));
         KTimer kt_(ctx, "sort_pass");
-        hipLaunchKernelGGL(onesweep_pass<V>, dim3((uint32_t)n_tiles), dim3(ST), 0, ctx->stream, kb[cur], kb[cur ^ 1],
+        hipLaunchKernelGGL((onesweep_pass<NT, SI, EARLY, V>), dim3((uint32_t)n_tiles), dim3(NT), 0, ctx->stream, kb[cur], kb[cur ^ 1],
                            vb[cur], vb[cur ^ 1], n, sh[p], bi[p], (const uint64_t *)scr + p * RADIX, ctx->d_status,
                            counter, epoch, ctx->d_err);
         HIP_TRY(ctx, hipGetLastError());
@@ -221,6 +282,17 @@ int run_passes(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, V *v0, V *v1, uint64_t
     }
     *result_in_alt = cur;
     return KMAN_OK;
+}
+
+template <int NT, int SI, bool EARLY = true>
+int dispatch_vals(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, void *v0, void *v1, uint32_t vb, uint64_t n, uint32_t np,
+                  const uint32_t *sh, const uint32_t *bi, const uint64_t *h_hist, int *res) {
+    if (vb == 0) return run_passes<NT, SI, EARLY, NoVal>(ctx, k0, k1, nullptr, nullptr, n, np, sh, bi, h_hist, res);
+    if (vb == 4)
+        return run_passes<NT, SI, EARLY, uint32_t>(ctx, k0, k1, (uint32_t *)v0, (uint32_t *)v1, n, np, sh, bi, h_hist,
+                                                   res);
+    return run_passes<NT, SI, EARLY, uint64_t>(ctx, k0, k1, (uint64_t *)v0, (uint64_t *)v1, n, np, sh, bi, h_hist,
+                                               res);
 }
 
 }  // namespace
@@ -275,13 +347,19 @@ extern "C" int kman_sort(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, 
     static thread_local uint64_t h_hist[MAXPASS * RADIX];
     HIP_TRY(ctx, hipMemcpyAsync(h_hist, hist, np * RADIX * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    if (val_bytes == 0)
-        KMAN_TRY(run_passes<NoVal>(ctx, d_keys, d_keys_alt, nullptr, nullptr, n, np, sh, bi, h_hist, result_in_alt));
-    else if (val_bytes == 4)
-        KMAN_TRY(run_passes<uint32_t>(ctx, d_keys, d_keys_alt, (uint32_t *)d_vals, (uint32_t *)d_vals_alt, n, np, sh,
-                                      bi, h_hist, result_in_alt));
-    else
-        KMAN_TRY(run_passes<uint64_t>(ctx, d_keys, d_keys_alt, (uint64_t *)d_vals, (uint64_t *)d_vals_alt, n, np, sh,
-                                      bi, h_hist, result_in_alt));
+    static const int cfg = [] {
+        const char *e = getenv("KMAN_SORT_CFG");  // tuning experiments only
+        return e ? atoi(e) : 0;
+    }();
+    switch (cfg) {
+        case 1: KMAN_TRY((dispatch_vals<512, 16>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
+        case 2: KMAN_TRY((dispatch_vals<256, 24>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
+        case 3: KMAN_TRY((dispatch_vals<1024, 8>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
+        case 4: KMAN_TRY((dispatch_vals<256, 16>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
+        case 6: KMAN_TRY((dispatch_vals<256, 16, false>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
+        case 7: KMAN_TRY((dispatch_vals<512, 12, false>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
+        case 5: KMAN_TRY((dispatch_vals<256, 8>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
+        default: KMAN_TRY((dispatch_vals<512, 12>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
+    }
     return kman_check_device_error(ctx);
 }

@@ -240,7 +240,11 @@ def test_full_size_properties(dev):
     del text
     km = engine.extract(p, 21, rc=False, want_pos=False)
     n = km.n
-    assert n == 1_000_000_000 - 3 * 20  # 4 records of <= 256 Mbp
+    assert p.n_records == 4 and n == 1_000_000_000 - 4 * 20  # records of <= 256 Mi bases
+    unsorted = dev.download(km.keys, n, np.uint64)
+    checksum = int(np.sum(unsorted, dtype=np.uint64))
+    xor = int(np.bitwise_xor.reduce(unsorted))
+    del unsorted
     engine.sort(km, dev)
     r = engine.rle_count(km, dev)
     uk, uc = engine.download_count(dev, r)
@@ -250,7 +254,9 @@ def test_full_size_properties(dev):
     assert abs((n - len(uk)) - n * n / 2 / 4**21) < 5 * np.sqrt(n * n / 2 / 4**21) + 10
     sorted_keys = dev.download(km.keys, n, np.uint64)
     assert (sorted_keys[1:] >= sorted_keys[:-1]).all()
-    assert int(np.sum(uk * uc.astype(np.uint64), dtype=np.uint64)) == int(np.sum(sorted_keys, dtype=np.uint64))
+    assert int(np.sum(sorted_keys, dtype=np.uint64)) == checksum
+    assert int(np.bitwise_xor.reduce(sorted_keys)) == xor
+    assert int(np.sum(uk * uc.astype(np.uint64), dtype=np.uint64)) == checksum
     km.free()
     r.ukeys.free()
     r.counts.free()
