@@ -148,6 +148,18 @@ int kman_rle_count(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint64_t *
 int kman_rle_uniq(kman_ctx *ctx, const uint64_t *d_keys, const void *d_vals, uint32_t val_bytes,
                   uint64_t n, uint64_t *d_okeys, void *d_ovals, uint64_t *n_out);
 
+/* ------------------------------------------------------------ helpers
+ * kman_tag_batches: keys[i] |= ((first_index + i) / batch_size) << key_bits,
+ *   so one stable kman_sort over key_bits + tag bits sorts every stream chunk
+ *   of batch_size k-mers on its own (BatcherBase.new_batch, batcher.py:118-131,
+ *   then Batch.sorted per batch).  KMAN_EINVAL if the tag does not fit.
+ * kman_or_u64 / kman_widen_u32: payload tagging (multi-source joins). */
+int kman_tag_batches(kman_ctx *ctx, uint64_t *d_keys, uint64_t n, uint32_t key_bits, uint64_t first_index,
+                     uint64_t batch_size);
+int kman_or_u64(kman_ctx *ctx, uint64_t *d_v, uint64_t n, uint64_t value);
+int kman_widen_u32(kman_ctx *ctx, const uint32_t *d_in, uint64_t *d_out, uint64_t n, uint64_t value);
+int kman_memcpy_d2d(kman_ctx *ctx, void *dst, const void *src, size_t bytes);
+
 /* ------------------------------------------------------------- formatting
  * Host-side writers that produce the reference's exact bytes.  They run on
  * host threads over host copies of the device results.

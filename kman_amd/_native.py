@@ -74,6 +74,10 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, POINTER(c_uint64)],
     ),
+    "kman_tag_batches": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint64, c_uint64]),
+    "kman_or_u64": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64]),
+    "kman_widen_u32": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_uint64]),
+    "kman_memcpy_d2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
     "kman_format_count": (
         c_int,
         [c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_size_t, POINTER(c_size_t), c_int],

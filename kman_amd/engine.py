@@ -390,6 +390,44 @@ def download_uniq(dev: Device, r: UniqResult):
 # ------------------------------------------------------------------ pipelines
 
 
+_CODE_TABLE = np.full(128, 4, dtype=np.uint8)
+for _i, _c in enumerate("ACGT"):
+    _CODE_TABLE[ord(_c)] = _i
+    _CODE_TABLE[ord(_c.lower())] = _i
+
+
+def decode_key(key: int, k: int) -> str:
+    """2-bit MSB-first key -> upper-case sequence."""
+    return "".join("ACGT"[(int(key) >> (2 * (k - 1 - j))) & 3] for j in range(k))
+
+
+def kmers_of_sequence(seq: str, k: int, rc: bool, dev: Optional[Device] = None):
+    """Keys + pos payloads of every valid window of one sequence string
+    (Sequence.yield_kmers, seq.py:285-328), enumerated by kman_extract."""
+    _check_k(k)
+    dev = dev or default_device()
+    cp = np.frombuffer(seq.encode("utf-32-le"), dtype=np.uint32)
+    codes = np.where(cp < 128, _CODE_TABLE[np.minimum(cp, 127)], 4).astype(np.uint8)
+    n = len(codes)
+    if n < k:
+        return np.zeros(0, np.uint64), np.zeros(0, np.uint64)
+    codes[0] |= 8
+    buf = dev.alloc(n + 64)
+    try:
+        dev.upload(buf, np.concatenate([codes, np.full(64, 4, np.uint8)]))
+        p = Parsed(dev, buf, n, 1, np.zeros(1, np.uint64), np.zeros(1, np.uint64), [b""], b"",
+                   np.zeros(2, np.uint64))
+        km = extract(p, k, rc, want_pos=True)
+        try:
+            keys = dev.download(km.keys, km.n, np.uint64)
+            pos = dev.download(km.pos, km.n, np.uint32 if km.pos_bytes == 4 else np.uint64).astype(np.uint64)
+        finally:
+            km.free()
+    finally:
+        buf.free()
+    return keys, pos
+
+
 def read_input(path: str) -> bytes:
     """Bytes of a FASTA file; ``.gz`` is decompressed (batcher.py:480)."""
     if path.endswith(".gz"):

@@ -1,0 +1,251 @@
+"""K-way join of k-mer batches (kmermaid/join.py).
+
+``KJoiner.join(batches, outpath)`` is the reference's n-way heap merge +
+run-length grouping + count/uniq writer (join.py:63-130, 244-285, 376-391).
+On the GPU the n-way merge of sorted batches is one stable radix sort of the
+union of the batches' k-mers (its result is exactly the merged order — ties
+in batch, then in-batch order, i.e. stream order) followed by the RLE kernel:
+
+* SEQ_COUNT -> kman_rle_count  -> ``"%s\\t%d\\n"``
+* UNIQUE    -> kman_rle_uniq   -> ``">%s\\n%s\\n"`` (groups of exactly one)
+
+Outputs do not depend on how the stream was cut into batches (verified on
+the reference), so batches that come from one FastaBatcher run
+are joined as the whole device-resident stream without materialising them.
+
+VEC_COUNT / VEC_COUNT_MASKED: the reference always raises
+NotImplementedError from its abstract abundance vector (abundance.py:60,123);
+they are out of this path's scope and raise the same way here.
+"""
+
+from __future__ import annotations
+
+import logging
+import os
+import tempfile
+from enum import Enum
+from typing import Dict, Iterator, List, Tuple
+
+import numpy as np
+
+from . import engine
+from .batch import Batch
+
+
+def _entries(batches: List[Batch]):
+    """(source, start, end) of every non-empty device batch, in batch order."""
+    out = []
+    for b in batches:
+        if b is None or b.current_size == 0:
+            continue
+        if not b.on_device:
+            raise AssertionError("host-mode batches are not k-mer batches")
+        s, e = b.stream_range
+        out.append((b.source, s, e))
+    return out
+
+
+class Crawler:
+    """Merged crawl over batches (join.py:36-130)."""
+
+    doSort = False
+    doSmart = False
+    verbose = True
+    desc = ""
+
+    @staticmethod
+    def count_records(batches: List[Batch]) -> int:
+        return sum(b.current_size for b in batches)
+
+    def do_records(self, batches: List[Batch]) -> Iterator[Tuple[str, str]]:
+        """(header, seq) of every record in merged order (heap-merge order),
+        from one stable device sort of the union of the batches."""
+        if any(type(b) is not Batch for b in batches):
+            raise AssertionError()
+        entries = _entries(batches)
+        if not entries:
+            return
+        from .source import gather_sorted
+
+        km, srcs, tagged = gather_sorted(entries, want_pos=True)
+        try:
+            dev = srcs[0].dev
+            keys = dev.download(km.keys, km.n, np.uint64)
+            pos = dev.download(km.pos, km.n, np.uint32 if km.pos_bytes == 4 else np.uint64)
+        finally:
+            km.free()
+        k = srcs[0].k
+        for key, p in zip(keys.tolist(), pos.tolist()):
+            src = srcs[p >> 56] if tagged else srcs[0]
+            yield (src.header(p & ((1 << 56) - 1)), engine.decode_key(key, k))
+
+    def do_batch(self, batches: List[Batch]) -> Iterator[Tuple[List[str], str]]:
+        crawler = self.do_records(batches)
+        try:
+            first = next(crawler)
+        except StopIteration:
+            logging.error("nothing to crawl")
+            return
+        cur_seq, cur_headers = first[1], [first[0]]
+        for header, seq in crawler:
+            if seq == cur_seq:
+                cur_headers.append(header)
+            else:
+                yield (cur_headers, cur_seq)
+                cur_seq, cur_headers = seq, [header]
+        yield (cur_headers, cur_seq)
+
+
+class KJoiner:
+    class MODE(Enum):
+        UNIQUE = 1
+        SEQ_COUNT = 2
+        VEC_COUNT = 3
+        VEC_COUNT_MASKED = 4
+
+    class MEMORY(Enum):
+        NORMAL = 1
+        LOCAL = 2
+
+    DEFAULT_MODE = MODE.UNIQUE
+    DEFAULT_MEMORY = MEMORY.NORMAL
+
+    def __init__(self, mode: "KJoiner.MODE" = None, memory: "KJoiner.MEMORY" = None):
+        self.__mode = self.DEFAULT_MODE
+        self.__memory = self.DEFAULT_MEMORY
+        if mode is not None:
+            if not isinstance(mode, self.MODE):
+                raise AssertionError
+            self.__mode = mode
+        if memory is not None:
+            if not isinstance(memory, self.MEMORY):
+                raise AssertionError
+            self.__memory = memory
+
+    @property
+    def mode(self):
+        return self.__mode
+
+    @mode.setter
+    def mode(self, mode) -> None:
+        if not isinstance(mode, self.MODE):
+            raise AssertionError
+        self.__mode = mode
+
+    @property
+    def memory(self):
+        return self.__memory
+
+    @memory.setter
+    def memory(self, memory) -> None:
+        if not isinstance(memory, self.MEMORY):
+            raise AssertionError
+        self.__memory = memory
+
+    @staticmethod
+    def join_unique(headers: List[str], seq: str, OH, **kwargs):
+        if len(headers) != 1:
+            return None
+        OH.write(">%s\n%s\n" % (headers[0], seq))
+        return (headers[0], seq)
+
+    @staticmethod
+    def join_sequence_count(headers: List[str], seq: str, OH, **kwargs):
+        OH.write("%s\t%d\n" % (seq, len(headers)))
+        return (seq, len(headers))
+
+    @property
+    def join_function(self):
+        return {self.MODE.UNIQUE: self.join_unique, self.MODE.SEQ_COUNT: self.join_sequence_count}.get(self.mode)
+
+    def join(self, batches: List[Batch], outpath: str) -> None:
+        """Join batches into ``outpath`` on the GPU (join.py:376-391)."""
+        if self.mode.name.startswith("VEC_"):
+            raise NotImplementedError(
+                "abundance vectors (VEC_*) are out of this engine's scope; the reference raises the same "
+                "NotImplementedError (kmermaid/abundance.py:60,123)")
+        print("Joining...")
+        data = join_bytes(batches, self.mode == self.MODE.SEQ_COUNT)
+        with open(outpath, "wb") as OH:
+            OH.write(data)
+
+
+def join_bytes(batches: List[Batch], count: bool) -> bytes:
+    """Device join of the batches: gather + stable sort + RLE, then format."""
+    entries = _entries(batches)
+    if not entries:
+        logging.error("nothing to crawl")  # join.py:110; the output stays empty
+        return b""
+    from .source import gather_sorted
+
+    km, srcs, tagged = gather_sorted(entries, want_pos=not count)
+    dev = srcs[0].dev
+    k = srcs[0].k
+    try:
+        if count:
+            r = engine.rle_count(km, dev)
+            try:
+                ukeys, counts = engine.download_count(dev, r)
+            finally:
+                r.ukeys.free()
+                r.counts.free()
+            return engine.format_count(ukeys, counts, k)
+        r = engine.rle_uniq(km, dev)
+        try:
+            keys, pos = engine.download_uniq(dev, r)
+        finally:
+            r.keys.free()
+            r.pos.free()
+    finally:
+        km.free()
+    if not tagged:
+        return srcs[0].format_fasta(keys, pos)
+    out = []
+    for key, p in zip(keys.tolist(), pos.tolist()):
+        out.append(">%s\n%s\n" % (srcs[p >> 56].header(p & ((1 << 56) - 1)), engine.decode_key(key, k)))
+    return "".join(out).encode("utf-8", "surrogateescape")
+
+
+class KJoinerThreading(KJoiner):
+    """Same surface as the reference's parallel joiner (join.py:394-480);
+    ``threads`` and ``batch_size`` are accepted (the GPU join has no host
+    threads to spread) — the reference's own parallel path returns wrong
+    counts (§A-3), the single-thread result is the contract."""
+
+    _threads = 1
+    __batch_size = 10
+    __doSort = False
+
+    @property
+    def doSort(self) -> bool:
+        return self.__doSort
+
+    @doSort.setter
+    def doSort(self, doSort) -> None:
+        if type(doSort) is not bool:
+            raise AssertionError
+        self.__doSort = doSort
+
+    @property
+    def threads(self) -> int:
+        return self._threads
+
+    @threads.setter
+    def threads(self, t) -> None:
+        self._threads = max(1, min(int(t), os.cpu_count() or 1))
+
+    @property
+    def batch_size(self) -> int:
+        return self.__batch_size
+
+    @batch_size.setter
+    def batch_size(self, batch_size) -> None:
+        if type(batch_size) is not int or batch_size < 2:
+            raise AssertionError
+        self.__batch_size = batch_size
+
+    @property
+    def tmp(self):
+        if getattr(self, "_tmp", None) is None:
+            self._tmp = tempfile.TemporaryDirectory(prefix="kmermaidJoin")
+        return self._tmp

@@ -1,0 +1,264 @@
+"""Device-resident k-mer sources behind the Batch objects.
+
+A ``FastaSource`` is one parsed FASTA input on one GPU (one
+``FastaBatcher.do`` call): the cleaned base codes and the record table stay in
+HBM, k-mer keys (+ pos payloads) are extracted on demand in the reference's
+stream order.  A ``Batch`` of the reference is a view ``[start, end)`` of that
+stream (BatcherBase.new_batch/add_record, batcher.py:118-131).
+
+A ``BatchFileSource`` is a folder of batch FASTA files written by
+``kmer batch`` (records ``>ref:start-end:strand`` / k-mer), loaded back for
+``-B``: every record is one k-mer whose header is its title.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import byref, c_int, c_void_p
+from typing import List, Optional
+
+import numpy as np
+
+from . import _native as N
+from . import engine
+
+
+class FastaSource:
+    def __init__(self, dev: engine.Device, text: bytes, k: int, rc: bool):
+        engine._check_k(k)
+        self.dev, self.k, self.rc = dev, k, rc
+        self.parsed = engine.parse(dev, text)
+        engine.check_empty_names(self.parsed, k)
+        self.n_kmers = engine.count_kmers(self.parsed, k, rc)
+        self._km = {}  # want_pos -> engine.Kmers (stream order)
+
+    # ------------------------------------------------------------ extraction
+    def kmers(self, want_pos: bool) -> engine.Kmers:
+        """Keys (+ pos) in stream order; the cached arrays are never sorted in
+        place (sorts work on copies)."""
+        km = self._km.get(want_pos) or (self._km.get(True) if not want_pos else None)
+        if km is None:
+            km = engine.extract(self.parsed, self.k, self.rc, want_pos=want_pos)
+            self._km[want_pos] = km
+        return km
+
+    def header(self, pos: int) -> str:
+        p = int(pos) >> 1
+        r = self.parsed.record_of(p)
+        st = p - int(self.parsed.rec_seq[r])
+        name = self.parsed.names[r].decode("utf-8", "surrogateescape")
+        return "%s:%d-%d:%s" % (name, st, st + self.k, "-" if int(pos) & 1 else "+")
+
+    def format_fasta(self, keys: np.ndarray, pos: np.ndarray) -> bytes:
+        return engine.format_fasta(keys, pos, self.k, self.parsed)
+
+    def free(self) -> None:
+        for km in self._km.values():
+            km.free()
+        self._km.clear()
+        self.parsed.free()
+
+
+class BatchFileSource:
+    """Batch FASTA files (``kmer batch`` output) loaded back onto the GPU."""
+
+    def __init__(self, dev: engine.Device, paths: List[str]):
+        self.dev = dev
+        self.paths = list(paths)
+        texts = [engine.read_input(p) for p in self.paths]
+        self.file_of_record: List[int] = []
+        blob = []
+        for i, t in enumerate(texts):
+            if t and not t.endswith(b"\n"):
+                t += b"\n"
+            blob.append(t)
+        text = b"".join(blob)
+        self.k = 0
+        self.n_kmers = 0
+        self._km = None
+        if not text.strip():
+            self.parsed = None
+            self.titles: List[str] = []
+            self.file_sizes = [0] * len(paths)
+            return
+        self.parsed = engine.parse(dev, text)
+        lens = np.diff(np.append(self.parsed.rec_seq, np.uint64(self.parsed.n_bases))).astype(np.int64)
+        if len(lens) and (lens != lens[0]).any():
+            raise AssertionError("batch files mix k-mer lengths")
+        self.k = int(lens[0]) if len(lens) else 0
+        self.titles = [self._title(text, int(h)) for h in self.parsed.rec_hdr]
+        self.n_kmers = engine.count_kmers(self.parsed, self.k, False) if self.k > 1 else 0
+        # records per file, for Batch sizes
+        ends = np.cumsum([len(b) for b in blob])
+        self.file_sizes = list(np.bincount(np.searchsorted(ends, self.parsed.rec_hdr, side="right"),
+                                           minlength=len(paths)))
+
+    @staticmethod
+    def _title(text: bytes, h: int) -> str:
+        j = h + 1
+        while j < len(text) and text[j] not in (10, 13):
+            j += 1
+        return text[h + 1 : j].decode("utf-8", "surrogateescape").rstrip()
+
+    def kmers(self, want_pos: bool) -> engine.Kmers:
+        if self._km is None:
+            self._km = engine.extract(self.parsed, self.k, False, want_pos=True)
+        return self._km
+
+    def header(self, pos: int) -> str:
+        return self.titles[self.parsed.record_of(int(pos) >> 1)]
+
+    def format_fasta(self, keys: np.ndarray, pos: np.ndarray) -> bytes:
+        out = []
+        for key, p in zip(keys.tolist(), pos.tolist()):
+            out.append(">%s\n%s\n" % (self.header(p), engine.decode_key(key, self.k)))
+        return "".join(out).encode("utf-8", "surrogateescape")
+
+    def free(self) -> None:
+        if self._km is not None:
+            self._km.free()
+        if self.parsed is not None:
+            self.parsed.free()
+
+
+# ------------------------------------------------------------------ sorting
+
+
+def sorted_copy(src, start: int, end: int, want_pos: bool, per_batch: Optional[int] = None):
+    """Stable sort of stream range [start, end) of a source (device copy).
+
+    With ``per_batch`` the range is cut into consecutive chunks of that many
+    k-mers, counted from stream index 0, and every chunk is sorted on its own
+    (the reference sorts each Batch separately, batch.py:156-168)."""
+    dev = src.dev
+    km = src.kmers(want_pos)
+    n = end - start
+    L = N.lib()
+    out = engine.Kmers(dev.alloc(8 * max(n, 1)), dev.alloc(8 * max(n, 1)), None, None, 0, n, src.k,
+                       dev.alloc(8 * 256 * 8))
+    N.check(dev.ctx, L.kman_memcpy_d2d(dev.ctx, c_void_p(out.keys.ptr), c_void_p(km.keys.ptr + 8 * start), 8 * n),
+            "d2d")
+    if want_pos:
+        pb = km.pos_bytes
+        out.pos, out.pos_alt, out.pos_bytes = dev.alloc(pb * max(n, 1)), dev.alloc(pb * max(n, 1)), pb
+        N.check(dev.ctx, L.kman_memcpy_d2d(dev.ctx, c_void_p(out.pos.ptr), c_void_p(km.pos.ptr + pb * start),
+                                            pb * n), "d2d")
+    key_bits = 2 * src.k
+    if per_batch is not None and n:
+        nb_last = (start + n - 1) // per_batch
+        tag_bits = max(1, int(nb_last).bit_length())
+        if key_bits + tag_bits <= 64:
+            N.check(dev.ctx, L.kman_tag_batches(dev.ctx, c_void_p(out.keys.ptr), n, key_bits, start, per_batch),
+                    "tag")
+            _sort(out, dev, key_bits + tag_bits)
+            return out
+        # no room for a tag: sort each chunk on its own
+        b = start
+        while b < end:
+            e = min(end, (b // per_batch + 1) * per_batch)
+            sub = engine.Kmers(_Ptr(out.keys.ptr + 8 * (b - start)), _Ptr(out.alt.ptr + 8 * (b - start)),
+                               _Ptr(out.pos.ptr + out.pos_bytes * (b - start)) if out.pos else None,
+                               _Ptr(out.pos_alt.ptr + out.pos_bytes * (b - start)) if out.pos else None,
+                               out.pos_bytes, e - b, src.k, out.hist)
+            flipped = _sort(sub, dev, key_bits, copy_back=True)
+            assert not flipped
+            b = e
+        return out
+    _sort(out, dev, key_bits)
+    return out
+
+
+class _Ptr:
+    """A raw device pointer viewed like a DeviceBuffer (no ownership)."""
+
+    def __init__(self, ptr):
+        self.ptr = ptr
+
+    def free(self):
+        pass
+
+
+def _sort(km: engine.Kmers, dev: engine.Device, key_bits: int, copy_back: bool = False) -> bool:
+    res = c_int(0)
+    L = N.lib()
+    rc = L.kman_sort(dev.ctx, c_void_p(km.keys.ptr), c_void_p(km.alt.ptr), c_void_p(km.pos.ptr if km.pos else None),
+                     c_void_p(km.pos_alt.ptr if km.pos_alt else None), km.pos_bytes, km.n, key_bits, None,
+                     byref(res))
+    N.check(dev.ctx, rc, "kman_sort")
+    if res.value:
+        if copy_back:
+            L.kman_memcpy_d2d(dev.ctx, c_void_p(km.keys.ptr), c_void_p(km.alt.ptr), 8 * km.n)
+            if km.pos is not None:
+                L.kman_memcpy_d2d(dev.ctx, c_void_p(km.pos.ptr), c_void_p(km.pos_alt.ptr), km.pos_bytes * km.n)
+            return False
+        km.keys, km.alt = km.alt, km.keys
+        km.pos, km.pos_alt = km.pos_alt, km.pos
+    km.sorted = True
+    return bool(res.value) and not copy_back
+
+
+def download_sorted(src, start: int, end: int, want_pos: bool, per_batch: Optional[int] = None):
+    km = sorted_copy(src, start, end, want_pos, per_batch)
+    try:
+        mask = np.uint64((1 << (2 * src.k)) - 1) if src.k < 32 else np.uint64(0xFFFFFFFFFFFFFFFF)
+        keys = src.dev.download(km.keys, km.n, np.uint64) & mask
+        pos = None
+        if want_pos:
+            pos = src.dev.download(km.pos, km.n, np.uint32 if km.pos_bytes == 4 else np.uint64)
+    finally:
+        km.free()
+    return keys, pos
+
+
+# ------------------------------------------------------------- gather + sort
+
+
+def gather_sorted(entries, want_pos: bool):
+    """Concatenate stream ranges ``(src, start, end)`` (in batch order) into
+    one device array and sort it stably: the device form of the reference's
+    heap n-way merge of sorted batches (join.py:63-93; ties by batch order,
+    then in-batch order).  With several sources the pos payload becomes u64
+    tagged with the source index in bits 56-63.
+
+    Returns (engine.Kmers sorted on device, list of sources, tagged)."""
+    srcs = []
+    for s, _, _ in entries:
+        if not any(s is x for x in srcs):
+            srcs.append(s)
+    ks = {s.k for s in srcs}
+    if len(ks) != 1:
+        raise AssertionError("batches of different k cannot be joined")
+    k = ks.pop()
+    tagged = len(srcs) > 1
+    if tagged and len(srcs) > 255:
+        raise AssertionError("at most 255 sources per join")
+    dev = srcs[0].dev
+    L = N.lib()
+    n = sum(e - s for _, s, e in entries)
+    pb = 8 if tagged else (srcs[0].kmers(want_pos).pos_bytes if want_pos else 0)
+    out = engine.Kmers(dev.alloc(8 * max(n, 1)), dev.alloc(8 * max(n, 1)), None, None, 0, n, k,
+                       dev.alloc(8 * 256 * 8))
+    if want_pos:
+        out.pos, out.pos_alt, out.pos_bytes = dev.alloc(pb * max(n, 1)), dev.alloc(pb * max(n, 1)), pb
+    at = 0
+    for src, s, e in entries:
+        m = e - s
+        if m <= 0:
+            continue
+        km = src.kmers(want_pos)
+        N.check(dev.ctx, L.kman_memcpy_d2d(dev.ctx, c_void_p(out.keys.ptr + 8 * at), c_void_p(km.keys.ptr + 8 * s),
+                                            8 * m), "d2d")
+        if want_pos:
+            tag = next(i for i, x in enumerate(srcs) if x is src) << 56 if tagged else 0
+            if km.pos_bytes == pb:
+                N.check(dev.ctx, L.kman_memcpy_d2d(dev.ctx, c_void_p(out.pos.ptr + pb * at),
+                                                    c_void_p(km.pos.ptr + pb * s), pb * m), "d2d")
+                if tag:
+                    N.check(dev.ctx, L.kman_or_u64(dev.ctx, c_void_p(out.pos.ptr + 8 * at), m, tag), "tag")
+            else:  # u32 source payload into the u64 tagged array
+                N.check(dev.ctx, L.kman_widen_u32(dev.ctx, c_void_p(km.pos.ptr + 4 * s),
+                                                   c_void_p(out.pos.ptr + 8 * at), m, tag), "widen")
+        at += m
+    _sort(out, dev, 2 * k)
+    return out, srcs, tagged

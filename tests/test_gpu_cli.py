@@ -1,0 +1,166 @@
+"""The drop-in surface on the GPU: the ``kmer`` CLI and the FastaBatcher /
+Batch / Crawler / KJoiner API produce the reference's bytes (golden sha256 /
+batch-file contents from tests/golden/manifest.json)."""
+
+from __future__ import annotations
+
+import gzip
+import hashlib
+import json
+import os
+
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+
+def _manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as fh:
+        return json.load(fh)
+
+
+def _cli(argv):
+    from kman_amd.scripts.kmer import main
+
+    main(argv, standalone_mode=False)
+
+
+def _sha(path):
+    with open(path, "rb") as fh:
+        return hashlib.sha256(fh.read()).hexdigest()
+
+
+@pytest.mark.parametrize("case", [c for c in _manifest()["cases"] if c["k"] <= 32], ids=lambda c: c["name"])
+def test_cli_matches_reference(case, golden_inputs, tmp_path):
+    out = str(tmp_path / "out.txt")
+    _cli([case["cmd"], golden_inputs[case["input"]], out, str(case["k"])] + case["flags"])
+    assert _sha(out) == case["sha256"]
+
+
+@pytest.mark.parametrize("case", _manifest()["batch_cases"], ids=lambda c: c["name"])
+def test_cli_batch_files_match_reference(case, golden_inputs, tmp_path):
+    outdir = str(tmp_path / "batches")
+    _cli(["batch", golden_inputs[case["input"]], outdir, str(case["k"])] + case["flags"])
+    got = []
+    for fn in sorted(os.listdir(outdir)):
+        with open(os.path.join(outdir, fn)) as fh:
+            got.append(fh.read())
+    assert sorted(got) == case["files"]
+
+
+def test_cli_batch_compressed(golden_inputs, tmp_path):
+    case = _manifest()["batch_cases"][0]
+    outdir = str(tmp_path / "b")
+    _cli(["batch", golden_inputs[case["input"]], outdir, str(case["k"]), "-C"] + case["flags"])
+    got = []
+    for fn in os.listdir(outdir):
+        assert fn.endswith(".fa.gz")
+        with gzip.open(os.path.join(outdir, fn), "rt") as fh:
+            got.append(fh.read())
+    assert sorted(got) == case["files"]
+
+
+@pytest.mark.parametrize("cmd", ["count", "uniq"])
+def test_previous_batches_roundtrip(cmd, golden_inputs, tmp_path):
+    """-B: batches written by `kmer batch`, loaded back, joined == joining the
+    FASTA directly (the reference's loader is broken, §A-5: evident intent)."""
+    case = [c for c in _manifest()["cases"] if c["name"] == "messy2__%s__k21__r" % cmd][0]
+    outdir = str(tmp_path / "batches")
+    _cli(["batch", golden_inputs["messy2"], outdir, "21", "-r", "-b", "777"])
+    out = str(tmp_path / "out.txt")
+    _cli([cmd, golden_inputs["messy2"], out, "21", "-B", outdir])
+    assert _sha(out) == case["sha256"]
+
+
+@pytest.mark.parametrize("cmd", ["count", "uniq"])
+def test_records_scan_mode_same_output(cmd, golden_inputs, tmp_path):
+    case = [c for c in _manifest()["cases"] if c["name"] == "messy1__%s__k5__r" % cmd][0]
+    out = str(tmp_path / "out.txt")
+    _cli([cmd, golden_inputs["messy1"], out, "5", "-r", "-s", "RECORDS", "-b", "50"])
+    assert _sha(out) == case["sha256"]
+
+
+def test_cli_errors(golden_inputs, tmp_path):
+    out = str(tmp_path / "o.txt")
+    with pytest.raises(AssertionError, match="k must be >= 1, got 1 instead."):
+        _cli(["count", golden_inputs["edge"], out, "1"])
+    with pytest.raises(AssertionError, match="premature end of file or empty file"):
+        _cli(["count", golden_inputs["empty"], out, "3"])
+    with pytest.raises(AssertionError, match="premature end of file or empty file"):
+        _cli(["uniq", golden_inputs["noheader"], out, "3"])
+    with pytest.raises(AssertionError, match="incompatible string"):
+        _cli(["count", golden_inputs["emptyname"], out, "3"])
+    assert not os.path.exists(out)
+    d = tmp_path / "full"
+    d.mkdir()
+    (d / "x").write_text("x")
+    with pytest.raises(AssertionError, match="output folder must be empty"):
+        _cli(["batch", golden_inputs["edge"], str(d), "3"])
+
+
+def test_crawler_groups_match_oracle(golden_inputs):
+    """Crawler.do_batch: every group with all its headers, in merged order
+    (join.py:95-130), against the numpy restatement."""
+    import numpy as np
+    import np_oracle
+
+    from kman_amd.batcher import FastaBatcher
+    from kman_amd.join import Crawler
+
+    path = golden_inputs["messy1"]
+    batches = FastaBatcher(reverse=True, size=101).do(path, 5).collection
+    got = list(Crawler().do_batch(batches))
+    with open(path, "rb") as fh:
+        recs = np_oracle.parse_fasta(fh.read())
+    keys, pos = np_oracle.stream_kmers(recs, 5, rc=True)
+    order = np.argsort(keys, kind="stable")
+    names = [np_oracle.record_name(t).decode() for t, _ in recs]
+    starts = np.cumsum([0] + [len(s) for _, s in recs])
+    want = []
+    for i in order:
+        g = int(pos[i]) >> 1
+        r = int(np.searchsorted(starts, g, side="right")) - 1
+        hdr = "%s:%d-%d:%s" % (names[r], g - starts[r], g - starts[r] + 5, "-" if int(pos[i]) & 1 else "+")
+        seq = np_oracle.decode(keys[i], 5).decode()
+        if want and want[-1][1] == seq:
+            want[-1][0].append(hdr)
+        else:
+            want.append(([hdr], seq))
+    assert got == want
+
+
+def test_batch_objects(golden_inputs):
+    from kman_amd.batcher import FastaBatcher
+
+    fb = FastaBatcher(size=40).do(golden_inputs["edge"], 3)
+    col = fb.collection
+    assert col[0].current_size == 0  # the batcher's own initial batch, as in the reference
+    sizes = [b.current_size for b in col[1:]]
+    assert sum(sizes) == fb.source.n_kmers and all(s == 40 for s in sizes[:-1])
+    recs = col[1].sorted()
+    assert [r.seq for r in recs] == sorted(r.seq for r in recs)
+    assert list(col[1].record_gen()) == recs
+
+
+def test_sequence_kmerator_known_answers():
+    """Known answers of the reference's tests/test_seq.py:117-181."""
+    from kman_amd.seq import NATYPES, KMer, Sequence, SequenceCoords
+
+    s = Sequence("ACGAT", NATYPES.DNA, "stest")
+    assert list(s.kmers(4)) == [KMer("stest", 0, 4, "ACGA"), KMer("stest", 1, 5, "CGAT")]
+    s = Sequence("ACGATCGATCG", NATYPES.DNA, "ref")
+    m = SequenceCoords.STRAND.MINUS
+    want = [
+        [KMer("ref", 0, 4, "ACGA"), KMer("ref", 0, 4, "TCGT", strand=m),
+         KMer("ref", 1, 5, "CGAT"), KMer("ref", 1, 5, "ATCG", strand=m)],
+        [KMer("ref", 2, 6, "GATC"), KMer("ref", 2, 6, "GATC", strand=m),
+         KMer("ref", 3, 7, "ATCG"), KMer("ref", 3, 7, "CGAT", strand=m)],
+        [KMer("ref", 4, 8, "TCGA"), KMer("ref", 4, 8, "TCGA", strand=m),
+         KMer("ref", 5, 9, "CGAT"), KMer("ref", 5, 9, "ATCG", strand=m)],
+        [KMer("ref", 6, 10, "GATC"), KMer("ref", 6, 10, "GATC", strand=m),
+         KMer("ref", 7, 11, "ATCG"), KMer("ref", 7, 11, "CGAT", strand=m)],
+    ]
+    assert [list(g) for g in s.kmerator_batched(s.text, 4, s.natype, 5, s.name, True)] == want
+    assert [k.seq for k in Sequence.kmerator("ACGNACGT", 3, NATYPES.DNA)] == ["ACG", "ACG", "CGT"]
