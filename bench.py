@@ -97,7 +97,15 @@ def main() -> None:
     text = inputs.syn_numpy(args.bases, 1 + rank)
     log("rank %d: generated %.2f GB FASTA in %.1f s" % (rank, len(text) / 1e9, time.time() - t0))
     dev = engine.Device(local)
-    pipe = engine.ResidentPipeline(dev, text, args.k, mode=args.mode)
+    if world > 1:
+        # prefix-range partition + one RCCL all-to-all over xGMI (kman_amd/dist.py)
+        from kman_amd import dist as kd
+
+        uid = [kd.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        pipe = kd.DistPipeline(dev, text, args.k, args.mode, world, rank, uid[0])
+    else:
+        pipe = engine.ResidentPipeline(dev, text, args.k, mode=args.mode)
     fasta_bytes = len(text)
     del text
 
@@ -129,13 +137,13 @@ def main() -> None:
     # live roofline of the dominant kernel (sort pass), from HIP events
     n_pass, pass_ms = pipe.timed("sort_pass")
     stages = {}
-    for tag in ("parse", "extract", "sort_pass", "rle_count", "rle_uniq"):
+    for tag in ("parse", "extract", "prefix_hist", "partition", "sort_hist", "sort_pass", "rle_count", "rle_uniq"):
         c, ms = pipe.timed(tag)
         if c:
             stages[tag] = round(ms / args.steps, 3)
     avg_pass_s = pass_ms / n_pass / 1e3
     bytes_per_key = 16 + (2 * pipe.pos_bytes if args.mode == "uniq" else 0)
-    achieved = bytes_per_key * pipe.n_kmers / avg_pass_s / 1e9
+    achieved = bytes_per_key * pipe.n_sorted / avg_pass_s / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_sort_pass.json")
     if os.path.isfile(pmc):
@@ -168,7 +176,7 @@ def main() -> None:
             "kmers_per_step_per_gpu": pipe.n_kmers,
             "k": args.k,
             "mode": args.mode,
-            "parallelism": "replicas" if world > 1 else "single",
+            "parallelism": "dp%d: prefix-range partition + RCCL all-to-all" % world if world > 1 else "single",
             "stages_ms_per_step": stages,
         },
         "roofline": {

@@ -148,6 +148,32 @@ int kman_rle_count(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint64_t *
 int kman_rle_uniq(kman_ctx *ctx, const uint64_t *d_keys, const void *d_vals, uint32_t val_bytes,
                   uint64_t n, uint64_t *d_okeys, void *d_ovals, uint64_t *n_out);
 
+/* ------------------------------------------------------------ multi-GPU
+ * One process per GPU over RCCL (xGMI).  The reference has no collective
+ * (joblib pools over temp files); this is the single exchange step that
+ * splits the global join by prefix range.
+ *   kman_comm_unique_id  rank 0 creates the 128-byte id, the launcher shares it
+ *   kman_comm_init       ncclCommInitRank on the context's device
+ *   kman_prefix_hist     d_hist[(key >> shift) & (2^bits - 1)] += 1 (bits <= 14)
+ *   kman_allreduce_u64   in-place sum (histograms)
+ *   kman_allgather_u64   per-rank counts
+ *   kman_alltoallv       grouped send/recv of contiguous per-destination runs
+ *   kman_partition       stable partition of keys (+ vals) into nbuckets
+ *                        destinations, bucket = d_lut[key >> lut_shift]; one
+ *                        onesweep pass; bucket_counts is a host array */
+int kman_comm_unique_id(uint8_t *out128);
+int kman_comm_init(kman_ctx *ctx, const uint8_t *id128, int nranks, int rank);
+int kman_comm_destroy(kman_ctx *ctx);
+int kman_prefix_hist(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint32_t shift, uint32_t bits,
+                     uint64_t *d_hist);
+int kman_allreduce_u64(kman_ctx *ctx, uint64_t *d_buf, uint64_t n);
+int kman_allgather_u64(kman_ctx *ctx, const uint64_t *d_send, uint64_t *d_recv, uint64_t n);
+int kman_alltoallv(kman_ctx *ctx, const void *d_send, const uint64_t *send_counts, const uint64_t *send_offsets,
+                   void *d_recv, const uint64_t *recv_counts, const uint64_t *recv_offsets, uint32_t elem_bytes);
+int kman_partition(kman_ctx *ctx, const uint64_t *d_keys, uint64_t *d_keys_out, const void *d_vals,
+                   void *d_vals_out, uint32_t val_bytes, uint64_t n, const uint8_t *d_lut, uint32_t lut_shift,
+                   uint32_t nbuckets, const uint64_t *bucket_counts);
+
 /* ------------------------------------------------------------ helpers
  * kman_tag_batches: keys[i] |= ((first_index + i) / batch_size) << key_bits,
  *   so one stable kman_sort over key_bits + tag bits sorts every stream chunk

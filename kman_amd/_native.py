@@ -74,6 +74,18 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, POINTER(c_uint64)],
     ),
+    "kman_comm_unique_id": (c_int, [c_void_p]),
+    "kman_comm_init": (c_int, [c_void_p, c_void_p, c_int, c_int]),
+    "kman_comm_destroy": (c_int, [c_void_p]),
+    "kman_prefix_hist": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_void_p]),
+    "kman_allreduce_u64": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "kman_allgather_u64": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64]),
+    "kman_alltoallv": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32]),
+    "kman_partition": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_uint32, c_uint32,
+         c_void_p],
+    ),
     "kman_tag_batches": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint64, c_uint64]),
     "kman_or_u64": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64]),
     "kman_widen_u32": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_uint64]),

@@ -40,6 +40,8 @@ struct kman_ctx {
     };
     std::vector<TimedLaunch> launches;
     std::vector<hipEvent_t> event_pool;
+    // RCCL communicator (comm.hip), null on a single GPU
+    void *comm = nullptr;
 };
 
 // RAII launch timer: records an event pair around the launches in its scope.

@@ -184,6 +184,7 @@ void kman_destroy(kman_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->comm) kman_comm_destroy(ctx);
     timing_clear(ctx);
     for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->d_status) (void)hipFree(ctx->d_status);

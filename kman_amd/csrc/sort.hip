@@ -80,14 +80,17 @@ KMAN_DEV uint64_t digit_lookback(uint64_t *st, int64_t tile, uint64_t agg, uint3
     return excl;
 }
 
-// One LSD digit pass over a tile of NT*SI keys.
-template <int NT, int SI, bool EARLY, typename V>
+// One LSD digit pass over a tile of NT*SI keys.  With LUT the digit is
+// lut[key >> shift] (destination rank of a prefix range: kman_partition).
+template <int NT, int SI, bool EARLY, typename V, bool LUT = false>
 __global__ __launch_bounds__(NT) void onesweep_pass(const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
                                                     const V *__restrict__ vin, V *__restrict__ vout, uint64_t n,
                                                     uint32_t shift, uint32_t bits,
                                                     const uint64_t *__restrict__ bucket_base,
                                                     uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
-                                                    uint32_t epoch, uint32_t *__restrict__ err) {
+                                                    uint32_t epoch, uint32_t *__restrict__ err,
+                                                    const uint8_t *__restrict__ lut = nullptr) {
+#define DIGIT(x) (LUT ? (uint32_t)lut[(x) >> shift] : ((uint32_t)((x) >> shift) & dmask))
     constexpr bool HAS_V = !std::is_same<V, NoVal>::value;
     constexpr int TILE = NT * SI;
     constexpr int NWAVE = NT / 64;
@@ -123,7 +126,7 @@ __global__ __launch_bounds__(NT) void onesweep_pass(const uint64_t *__restrict__
         // successors' look-backs are not held up by the ranking below
 #pragma unroll
         for (int i = 0; i < SI; i++)
-            if (ib + (uint64_t)i * 64 < n) atomicAdd(&thist[(uint32_t)(key[i] >> shift) & dmask], 1u);
+            if (ib + (uint64_t)i * 64 < n) atomicAdd(&thist[DIGIT(key[i])], 1u);
         __syncthreads();
         if (threadIdx.x < radix) digit_publish(status + threadIdx.x, tile, thist[threadIdx.x], epoch);
     }
@@ -132,7 +135,7 @@ __global__ __launch_bounds__(NT) void onesweep_pass(const uint64_t *__restrict__
 #pragma unroll
     for (int i = 0; i < SI; i++) {
         const bool valid = ib + (uint64_t)i * 64 < n;
-        const uint32_t d = (uint32_t)(key[i] >> shift) & dmask;
+        const uint32_t d = DIGIT(key[i]);
         uint64_t peers = __ballot(valid);
         for (uint32_t b = 0; b < bits; b++) {
             const bool set = (d >> b) & 1u;
@@ -177,7 +180,7 @@ __global__ __launch_bounds__(NT) void onesweep_pass(const uint64_t *__restrict__
 #pragma unroll
     for (int i = 0; i < SI; i++) {
         const bool valid = ib + (uint64_t)i * 64 < n;
-        const uint32_t d = (uint32_t)(key[i] >> shift) & dmask;
+        const uint32_t d = DIGIT(key[i]);
         lp[i] = valid ? lstart[d] + whist[w][d] + rank[i] : 0xffffffffu;
         if (valid) skeys[lp[i]] = key[i];
     }
@@ -187,12 +190,12 @@ __global__ __launch_bounds__(NT) void onesweep_pass(const uint64_t *__restrict__
     // ablation build only: contiguous writes instead of the digit scatter
     for (uint32_t q = threadIdx.x; q < cnt; q += NT) {
         const uint64_t kk = skeys[q];
-        kout[tb + q] = kk + gstart[(uint32_t)(kk >> shift) & dmask];
+        kout[tb + q] = kk + gstart[DIGIT(kk)];
     }
 #else
     for (uint32_t q = threadIdx.x; q < cnt; q += NT) {
         const uint64_t kk = skeys[q];
-        kout[gstart[(uint32_t)(kk >> shift) & dmask] + q] = kk;
+        kout[gstart[DIGIT(kk)] + q] = kk;
     }
 #endif
     if constexpr (HAS_V) {
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(NT) void onesweep_pass(const uint64_t *__restrict__
 #pragma unroll
         for (int r = 0; r < (TILE + NT - 1) / NT; r++) {
             const uint32_t q = threadIdx.x + r * NT;
-            dq[r] = q < cnt ? (uint8_t)((uint32_t)(skeys[q] >> shift) & dmask) : 0;
+            dq[r] = q < cnt ? (uint8_t)DIGIT(skeys[q]) : 0;
         }
         __syncthreads();
         V *sval = reinterpret_cast<V *>(skeys);
@@ -361,5 +364,56 @@ extern "C" int kman_sort(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, 
         case 5: KMAN_TRY((dispatch_vals<256, 8>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
         default: KMAN_TRY((dispatch_vals<512, 12>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
     }
+    return kman_check_device_error(ctx);
+}
+
+namespace {
+template <typename V>
+int launch_partition(kman_ctx *ctx, const uint64_t *kin, uint64_t *kout, const V *vin, V *vout, uint64_t n,
+                     const uint8_t *lut, uint32_t lut_shift, uint32_t bits, const uint64_t *d_base) {
+    constexpr int NT = 512, SI = 12;
+    const uint64_t n_tiles = ceil_div(n, (uint64_t)NT * SI);
+    uint32_t epoch, *counter;
+    KMAN_TRY(kman_lookback_begin(ctx, n_tiles * RADIX, &epoch, &counter));
+    KTimer kt_(ctx, "partition");
+    hipLaunchKernelGGL((onesweep_pass<NT, SI, true, V, true>), dim3((uint32_t)n_tiles), dim3(NT), 0, ctx->stream,
+                       kin, kout, vin, vout, n, lut_shift, bits, d_base, ctx->d_status, counter, epoch, ctx->d_err,
+                       lut);
+    HIP_TRY(ctx, hipGetLastError());
+    return KMAN_OK;
+}
+}  // namespace
+
+extern "C" int kman_partition(kman_ctx *ctx, const uint64_t *d_keys, uint64_t *d_keys_out, const void *d_vals,
+                              void *d_vals_out, uint32_t val_bytes, uint64_t n, const uint8_t *d_lut,
+                              uint32_t lut_shift, uint32_t nbuckets, const uint64_t *bucket_counts) {
+    if (!ctx || !bucket_counts || nbuckets < 1 || nbuckets > 256) return KMAN_EINVAL;
+    if (val_bytes != 0 && val_bytes != 4 && val_bytes != 8)
+        return kman_fail(ctx, KMAN_EINVAL, "val_bytes must be 0, 4 or 8");
+    if (n == 0) return KMAN_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    uint64_t base[RADIX] = {0}, acc = 0;
+    for (uint32_t b = 0; b < nbuckets; b++) {
+        base[b] = acc;
+        acc += bucket_counts[b];
+    }
+    if (acc != n)
+        return kman_fail(ctx, KMAN_EINVAL, "bucket counts sum to %llu, expected %llu", (unsigned long long)acc,
+                         (unsigned long long)n);
+    uint32_t bits = 1;
+    while ((1u << bits) < nbuckets) bits++;
+    void *scr;
+    KMAN_TRY(kman_scratch(ctx, sizeof(base), &scr));
+    HIP_TRY(ctx, hipMemcpyAsync(scr, base, sizeof(base), hipMemcpyHostToDevice, ctx->stream));
+    const uint64_t *d_base = (const uint64_t *)scr;
+    if (val_bytes == 0)
+        KMAN_TRY(launch_partition<NoVal>(ctx, d_keys, d_keys_out, nullptr, nullptr, n, d_lut, lut_shift, bits, d_base));
+    else if (val_bytes == 4)
+        KMAN_TRY(launch_partition<uint32_t>(ctx, d_keys, d_keys_out, (const uint32_t *)d_vals, (uint32_t *)d_vals_out,
+                                            n, d_lut, lut_shift, bits, d_base));
+    else
+        KMAN_TRY(launch_partition<uint64_t>(ctx, d_keys, d_keys_out, (const uint64_t *)d_vals, (uint64_t *)d_vals_out,
+                                            n, d_lut, lut_shift, bits, d_base));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     return kman_check_device_error(ctx);
 }

@@ -497,7 +497,8 @@ class ResidentPipeline:
     runs parse -> extract -> sort -> count|uniq with no allocation, leaving
     the result device-resident (what bench.py times)."""
 
-    def __init__(self, dev: Device, text: bytes, k: int, mode: str = "uniq", rc: bool = False):
+    def __init__(self, dev: Device, text: bytes, k: int, mode: str = "uniq", rc: bool = False,
+                 pos_bytes: Optional[int] = None):
         _check_k(k)
         if mode not in ("count", "uniq"):
             raise ValueError(mode)
@@ -511,7 +512,7 @@ class ResidentPipeline:
         self.rec_hdr = dev.alloc(8 * self.rec_cap)
         self.rec_seq = dev.alloc(8 * self.rec_cap)
         self.bound = max(1, n * (2 if rc else 1))
-        self.pos_bytes = 4 if 2 * n <= 0xFFFFFFFF else 8
+        self.pos_bytes = pos_bytes or (4 if 2 * n <= 0xFFFFFFFF else 8)
         want_pos = mode == "uniq"
         self.keys = dev.alloc(8 * self.bound)
         self.alt = dev.alloc(8 * self.bound)
@@ -526,6 +527,22 @@ class ResidentPipeline:
         self.n_out = 0
         self.n_bases = 0
         self.sorted_in_alt = False
+
+    def extract_only(self) -> int:
+        """parse + extract (stream-order keys / pos in self.keys / self.pos)."""
+        L, ctx = N.lib(), self.dev.ctx
+        info = N.ParseInfo()
+        N.check(ctx, L.kman_parse_fasta(ctx, c_void_p(self.text.ptr), self.n_bytes, c_void_p(self.codes.ptr),
+                                        c_void_p(self.rec_hdr.ptr), c_void_p(self.rec_seq.ptr), self.rec_cap,
+                                        byref(info)), "kman_parse_fasta")
+        self.n_bases = int(info.n_bases)
+        n = c_uint64(0)
+        pos = c_void_p(self.pos.ptr) if self.pos else c_void_p(None)
+        N.check(ctx, L.kman_extract(ctx, c_void_p(self.codes.ptr), self.n_bases, self.k, self.flags,
+                                    c_void_p(self.keys.ptr), pos, self.pos_bytes, self.bound, None, byref(n)),
+                "kman_extract")
+        self.n_kmers = int(n.value)
+        return self.n_kmers
 
     def step(self) -> int:
         L, ctx = N.lib(), self.dev.ctx
@@ -559,6 +576,10 @@ class ResidentPipeline:
                                          self.n_kmers, c_void_p(self.out_keys.ptr), c_void_p(self.out_vals.ptr),
                                          byref(out)), "kman_rle_uniq")
         self.n_out = int(out.value)
+        return self.n_kmers
+
+    @property
+    def n_sorted(self) -> int:
         return self.n_kmers
 
     def timing(self, enable: bool) -> None:

@@ -1,0 +1,85 @@
+"""GPU pieces of the multi-GPU join that a 1-GPU box can check: the prefix
+histogram, the LUT-digit stable partition kernel, and the whole RCCL
+pipeline at world size 1 (N>1 runs on the driver's 8-GPU node; the exchange
+logic is rehearsed on CPU in tests/test_dist_cpu.py)."""
+
+from __future__ import annotations
+
+import ctypes
+from ctypes import c_void_p
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from kman_amd import engine
+
+    return engine.default_device()
+
+
+@pytest.mark.parametrize("n", [1, 5000, 1_000_003])
+@pytest.mark.parametrize("buckets", [1, 3, 8])
+def test_prefix_hist_and_partition(dev, n, buckets):
+    from kman_amd import _native as N
+    from kman_amd.dist import bucket_counts, plan_lut
+
+    L = N.lib()
+    rng = np.random.default_rng(n + buckets)
+    keys = rng.integers(0, 1 << 42, size=n, dtype=np.uint64)
+    keys[: n // 3] &= np.uint64((1 << 30) - 1)  # skew
+    vals = np.arange(n, dtype=np.uint64) * np.uint64(7)
+    dk, dk2, dv, dv2 = dev.alloc(8 * n), dev.alloc(8 * n), dev.alloc(8 * n), dev.alloc(8 * n)
+    dh = dev.alloc(8 << 14)
+    dl = dev.alloc(1 << 14)
+    dev.upload(dk, keys)
+    dev.upload(dv, vals)
+    dev.memset(dh, 0, 8 << 14)
+    N.check(dev.ctx, L.kman_prefix_hist(dev.ctx, c_void_p(dk.ptr), n, 42 - 14, 14, c_void_p(dh.ptr)), "hist")
+    h = dev.download(dh, 1 << 14, np.uint64)
+    want_h = np.bincount((keys >> np.uint64(28)).astype(np.int64), minlength=1 << 14)
+    np.testing.assert_array_equal(h, want_h)
+    lut = plan_lut(h, buckets)
+    dev.upload(dl, lut)
+    counts = bucket_counts(h, lut, buckets)
+    N.check(dev.ctx, L.kman_partition(dev.ctx, c_void_p(dk.ptr), c_void_p(dk2.ptr), c_void_p(dv.ptr),
+                                      c_void_p(dv2.ptr), 8, n, c_void_p(dl.ptr), 28, buckets,
+                                      counts.ctypes.data_as(c_void_p)), "partition")
+    dest = lut[(keys >> np.uint64(28)).astype(np.int64)]
+    order = np.argsort(dest, kind="stable")
+    np.testing.assert_array_equal(dev.download(dk2, n, np.uint64), keys[order])
+    np.testing.assert_array_equal(dev.download(dv2, n, np.uint64), vals[order])
+    for b in (dk, dk2, dv, dv2, dh, dl):
+        b.free()
+
+
+@pytest.mark.parametrize("mode", ["count", "uniq"])
+def test_dist_pipeline_world1_equals_single(dev, mode):
+    import sys, os
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import inputs
+    import np_oracle
+    from kman_amd import dist
+
+    text = inputs.messy_records(7, n_records=40, max_len=20000)
+    p = dist.DistPipeline(dev, text, 13, mode, 1, 0, dist.unique_id())
+    try:
+        p.step()
+        keys, vals = p.results()
+    finally:
+        p.free()
+    recs = np_oracle.parse_fasta(text)
+    kk, pp = np_oracle.stream_kmers(recs, 13)
+    sk, sp = np_oracle.stable_sort(kk, pp)
+    if mode == "count":
+        wk, wc = np_oracle.rle_count(sk)
+        np.testing.assert_array_equal(keys, wk)
+        np.testing.assert_array_equal(vals, wc)
+    else:
+        wk, wv = np_oracle.rle_uniq(sk, sp)
+        np.testing.assert_array_equal(keys, wk)
+        np.testing.assert_array_equal(vals, wv)
