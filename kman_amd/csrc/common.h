@@ -42,6 +42,10 @@ struct kman_ctx {
     std::vector<hipEvent_t> event_pool;
     // RCCL communicator (comm.hip), null on a single GPU
     void *comm = nullptr;
+    // probed at kman_create: same-address LDS atomics of one wave return in
+    // lane order on this device (observed on gfx950, not architectural); the
+    // sort uses atomic ranking only when true
+    bool lds_atomic_ordered = false;
 };
 
 // RAII launch timer: records an event pair around the launches in its scope.

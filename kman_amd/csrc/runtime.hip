@@ -87,6 +87,42 @@ int kman_lookback_total(kman_ctx *ctx, uint64_t n_tiles, uint64_t *total) {
     return KMAN_OK;
 }
 
+// Probe: do same-address LDS atomics of one wave return old values in lane
+// order?  (Stable atomic ranking in sort.hip depends on it.)
+__global__ void lds_order_probe(uint32_t *bad) {
+    __shared__ uint32_t c[256];
+    for (int i = threadIdx.x; i < 256; i += blockDim.x) c[i] = 0;
+    __syncthreads();
+    uint32_t nbad = 0;
+    const int lane = threadIdx.x & 63;
+    for (int it = 0; it < 32; it++) {
+        uint32_t h = (lane * 2654435761u) ^ (it * 40503u) ^ (blockIdx.x * 97u) ^ (threadIdx.x >> 6);
+        h ^= h >> 13;
+        const uint32_t d = h % (1u + (it & 127));
+        const uint32_t old = atomicAdd(&c[d], 1u);
+        for (int o = 0; o < lane; o++) {
+            const uint32_t od = (uint32_t)__shfl((int)d, o, 64);
+            const uint32_t ov = (uint32_t)__shfl((int)old, o, 64);
+            nbad += (od == d && ov > old);
+        }
+    }
+    if (nbad) atomicAdd(bad, nbad);
+}
+
+static bool probe_lds_order(kman_ctx *ctx) {
+    uint32_t *d = nullptr, h = 1;
+    if (hipMalloc(&d, 4) != hipSuccess) return false;
+    bool ok = hipMemsetAsync(d, 0, 4, ctx->stream) == hipSuccess;
+    if (ok) {
+        hipLaunchKernelGGL(lds_order_probe, dim3(512), dim3(256), 0, ctx->stream, d);
+        ok = hipGetLastError() == hipSuccess &&
+             hipMemcpyAsync(&h, d, 4, hipMemcpyDeviceToHost, ctx->stream) == hipSuccess &&
+             hipStreamSynchronize(ctx->stream) == hipSuccess;
+    }
+    (void)hipFree(d);
+    return ok && h == 0;
+}
+
 static hipEvent_t pool_event(kman_ctx *ctx) {
     if (!ctx->event_pool.empty()) {
         hipEvent_t e = ctx->event_pool.back();
@@ -176,6 +212,8 @@ int kman_create(int device, kman_ctx **out) {
     ctx->d_err = ctx->d_counters + 64;
     if ((e = hipMemset(ctx->d_counters, 0, 64 * sizeof(uint32_t) + 256)) != hipSuccess) return bail(e, "hipMemset");
     if ((e = hipHostMalloc(&ctx->h_small, 4096, hipHostMallocDefault)) != hipSuccess) return bail(e, "hipHostMalloc");
+    const char *force = getenv("KMAN_RANK");  // "ballot" forces the probe-free ranking
+    ctx->lds_atomic_ordered = !(force && strcmp(force, "ballot") == 0) && probe_lds_order(ctx);
     *out = ctx;
     return KMAN_OK;
 }

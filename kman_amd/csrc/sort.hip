@@ -33,6 +33,20 @@ constexpr int LB = KMAN_LB;  // predecessor status words fetched per look-back r
 
 struct NoVal {};
 
+#if defined(KMAN_ABL) && (KMAN_ABL & 4)
+// diagnostic build only: per-tile s_memrealtime stamps (100 MHz) at phase
+// boundaries, thread 0, into a buffer set with kman_debug_set
+__device__ uint64_t *g_dbg;
+#define STAMP(i)                                                                         \
+    do {                                                                                 \
+        if (threadIdx.x == 0 && g_dbg) g_dbg[(uint64_t)tile * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define STAMP(i) \
+    do {         \
+    } while (0)
+#endif
+
 // One thread per digit walks back along that digit's tile chain, LB
 // predecessors per round (independent sc1 loads in flight), summing AGG
 // counts until it meets an INCL prefix.
@@ -80,9 +94,85 @@ KMAN_DEV uint64_t digit_lookback(uint64_t *st, int64_t tile, uint64_t agg, uint3
     return excl;
 }
 
+// TPD adjacent lanes walk one digit's chain together: lane `sub` of the group
+// loads predecessors base - sub*LB - q (q < LB), so one round covers TPD*LB
+// tiles.  With many tiles in flight the inclusive-prefix frontier lags by
+// (look-back time / tile start interval) tiles, so the pass runs at about
+// (predecessors per round) / (round latency) tiles per unit time: widening the
+// round is what raises it.  The aggregate has been published already (EARLY).
+template <int TPD>
+KMAN_DEV uint64_t group_lookback(uint64_t *st, int64_t tile, uint64_t agg, uint32_t epoch, uint32_t *err) {
+    const int lane = lane_id();
+    const int sub = lane % TPD;
+    const int g0 = lane - sub;
+    if (tile == 0) return 0;  // tile 0 published its inclusive count with the aggregate
+    uint64_t excl = 0;
+    int64_t base = tile - 1;
+    uint32_t spins = 0;
+#if defined(KMAN_ABL) && (KMAN_ABL & 4)
+    uint64_t rounds_dbg = 0;
+#endif
+    while (base >= 0) {
+#if defined(KMAN_ABL) && (KMAN_ABL & 4)
+        rounds_dbg++;
+#endif
+        uint64_t w[LB];
+#pragma unroll
+        for (int q = 0; q < LB; q++) {
+            const int64_t j = base - (int64_t)sub * LB - q;
+            w[q] = j >= 0 ? st_load(&st[(uint64_t)j * RADIX]) : st_make(ST_INCL, epoch, 0);
+        }
+        // this lane's segment, in distance order: 0 all AGG, 1 met INCL, 2 stalled
+        uint32_t state = 0, used = 0;
+        uint64_t sum = 0;
+#pragma unroll
+        for (int q = 0; q < LB; q++) {
+            if (state) continue;
+            const uint64_t f = st_flag(w[q], epoch);
+            if (f == 0) {
+                state = 2;
+                continue;
+            }
+            sum += w[q] & ST_VMASK;
+            used++;
+            if (f == ST_INCL) state = 1;
+        }
+        // combine the group's segments in distance order
+        const uint64_t m = (__ballot(state != 0) >> g0) & ((1ull << TPD) - 1);
+        const int first = m ? __ffsll((unsigned long long)m) - 1 : TPD;
+        uint64_t tot = 0;
+        int64_t adv = 0;
+#pragma unroll
+        for (int s = 0; s < TPD; s++) {
+            const uint64_t ss = shfl_any(sum, g0 + s);
+            const uint32_t su = (uint32_t)__shfl((int)used, g0 + s, 64);
+            if (s <= first) {
+                tot += ss;
+                adv += su;
+            }
+        }
+        const uint32_t fstate = first < TPD ? (uint32_t)__shfl((int)state, g0 + first, 64) : 0;
+        excl += tot;
+        if (fstate == 1) break;
+        base -= first < TPD ? adv : (int64_t)TPD * LB;
+        if (fstate == 2) {
+            if (spin_give_up(spins, err, 2u)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    if (sub == 0) st_store(&st[(uint64_t)tile * RADIX], st_make(ST_INCL, epoch, excl + agg));
+#if defined(KMAN_ABL) && (KMAN_ABL & 4)
+    if (threadIdx.x == 0 && g_dbg) {
+        g_dbg[(uint64_t)tile * 8 + 6] = rounds_dbg;
+        g_dbg[(uint64_t)tile * 8 + 7] = spins;
+    }
+#endif
+    return excl;
+}
+
 // One LSD digit pass over a tile of NT*SI keys.  With LUT the digit is
 // lut[key >> shift] (destination rank of a prefix range: kman_partition).
-template <int NT, int SI, bool EARLY, typename V, bool LUT = false>
+template <int NT, int SI, bool EARLY, typename V, bool LUT = false, bool ATOMIC = false>
 __global__ __launch_bounds__(NT) void onesweep_pass(const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
                                                     const V *__restrict__ vin, V *__restrict__ vout, uint64_t n,
                                                     uint32_t shift, uint32_t bits,
@@ -104,6 +194,7 @@ __global__ __launch_bounds__(NT) void onesweep_pass(const uint64_t *__restrict__
     __shared__ uint32_t lds_tile;
 
     const int64_t tile = grab_tile(counter, &lds_tile);
+    STAMP(0);
     const int lane = lane_id();
     const int w = threadIdx.x >> 6;
     const uint32_t radix = 1u << bits;
@@ -120,35 +211,72 @@ __global__ __launch_bounds__(NT) void onesweep_pass(const uint64_t *__restrict__
         const uint64_t idx = ib + (uint64_t)i * 64;
         key[i] = idx < n ? kin[idx] : 0;
     }
-    __syncthreads();
-    if (EARLY) {
-        // publish this tile's digit counts as soon as its keys have landed, so
-        // successors' look-backs are not held up by the ranking below
+    // payloads are loaded up front too, so their latency hides under the ranking
+    using VL = typename std::conditional<HAS_V, V, uint8_t>::type;
+    VL val[HAS_V ? SI : 1];
+    if constexpr (HAS_V) {
 #pragma unroll
-        for (int i = 0; i < SI; i++)
-            if (ib + (uint64_t)i * 64 < n) atomicAdd(&thist[DIGIT(key[i])], 1u);
-        __syncthreads();
-        if (threadIdx.x < radix) digit_publish(status + threadIdx.x, tile, thist[threadIdx.x], epoch);
-    }
-
-    // stable in-wave ranking: items in order, lanes in order
-#pragma unroll
-    for (int i = 0; i < SI; i++) {
-        const bool valid = ib + (uint64_t)i * 64 < n;
-        const uint32_t d = DIGIT(key[i]);
-        uint64_t peers = __ballot(valid);
-        for (uint32_t b = 0; b < bits; b++) {
-            const bool set = (d >> b) & 1u;
-            const uint64_t m = __ballot(set);
-            peers &= set ? m : ~m;
+        for (int i = 0; i < SI; i++) {
+            const uint64_t idx = ib + (uint64_t)i * 64;
+            val[i] = idx < n ? vin[idx] : (V)0;
         }
-        uint32_t before = 0;
-        if (valid) before = whist[w][d];
-        rank[i] = before + (uint32_t)__popcll(peers & lanemask_lt());
-        const int leader = __ffsll((unsigned long long)peers) - 1;
-        if (valid && lane == leader) whist[w][d] = before + (uint32_t)__popcll(peers);
+    }
+#if defined(KMAN_ABL) && (KMAN_ABL & 4)
+    {
+        uint64_t x = key[0] ^ key[SI - 1];
+        asm volatile("" ::"v"(x));
+    }
+#endif
+    __syncthreads();
+    STAMP(1);
+    if (ATOMIC) {
+        // stable in-wave ranking with LDS atomics: one ds_add_rtn per item, all
+        // in flight together; items in program order, same-address lanes in
+        // lane order (probed per device at kman_create)
+#pragma unroll
+        for (int i = 0; i < SI; i++) {
+            const bool valid = ib + (uint64_t)i * 64 < n;
+            rank[i] = valid ? atomicAdd(&whist[w][DIGIT(key[i])], 1u) : 0u;
+        }
+        __syncthreads();
+        if (EARLY && threadIdx.x < radix) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int ww = 0; ww < NWAVE; ww++) c += whist[ww][threadIdx.x];
+            thist[threadIdx.x] = c;
+            digit_publish(status + threadIdx.x, tile, c, epoch);
+        }
+    } else {
+        if (EARLY) {
+            // publish this tile's digit counts as soon as its keys have landed, so
+            // successors' look-backs are not held up by the ranking below
+#pragma unroll
+            for (int i = 0; i < SI; i++)
+                if (ib + (uint64_t)i * 64 < n) atomicAdd(&thist[DIGIT(key[i])], 1u);
+            __syncthreads();
+            if (threadIdx.x < radix) digit_publish(status + threadIdx.x, tile, thist[threadIdx.x], epoch);
+        }
+
+        // stable in-wave ranking: items in order, lanes in order (ballot match-any)
+#pragma unroll
+        for (int i = 0; i < SI; i++) {
+            const bool valid = ib + (uint64_t)i * 64 < n;
+            const uint32_t d = DIGIT(key[i]);
+            uint64_t peers = __ballot(valid);
+            for (uint32_t b = 0; b < bits; b++) {
+                const bool set = (d >> b) & 1u;
+                const uint64_t m = __ballot(set);
+                peers &= set ? m : ~m;
+            }
+            uint32_t before = 0;
+            if (valid) before = whist[w][d];
+            rank[i] = before + (uint32_t)__popcll(peers & lanemask_lt());
+            const int leader = __ffsll((unsigned long long)peers) - 1;
+            if (valid && lane == leader) whist[w][d] = before + (uint32_t)__popcll(peers);
+        }
     }
     __syncthreads();
+    STAMP(2);
 
     // per-digit tile counts and per-wave exclusive offsets (thread = digit)
     const uint32_t d0 = threadIdx.x;
@@ -164,16 +292,29 @@ __global__ __launch_bounds__(NT) void onesweep_pass(const uint64_t *__restrict__
     uint32_t tile_total;
     const uint32_t ls = block_exclusive_scan<NT>(tot, SumU32(), 0u, lds_scan, &tile_total);
     if (d0 < RADIX) lstart[d0] = ls;
-    if (d0 < radix) {
 #if defined(KMAN_ABL) && (KMAN_ABL & 1)
-        // ablation build only: no look-back (wrong offsets, measures the rest)
-        const uint64_t excl = (uint64_t)tile * TILE / radix;
+    // ablation build only: no look-back (wrong offsets, measures the rest)
+    if (d0 < radix) gstart[d0] = bucket_base[d0] + (uint64_t)tile * TILE / radix - ls;
 #else
+    if constexpr (EARLY) {
+        // several lanes per digit walk the chain (see group_lookback)
+        __syncthreads();
+        const uint32_t tpd = NT / radix >= 4 ? 4 : (NT / radix >= 2 ? 2 : 1);
+        if (threadIdx.x < radix * tpd) {
+            const uint32_t d = threadIdx.x / tpd;
+            uint64_t excl;
+            if (tpd == 4) excl = group_lookback<4>(status + d, tile, thist[d], epoch, err);
+            else if (tpd == 2) excl = group_lookback<2>(status + d, tile, thist[d], epoch, err);
+            else excl = group_lookback<1>(status + d, tile, thist[d], epoch, err);
+            if (threadIdx.x % tpd == 0) gstart[d] = bucket_base[d] + excl - lstart[d];
+        }
+    } else if (d0 < radix) {
         const uint64_t excl = digit_lookback<EARLY>(status + d0, tile, tot, epoch, err);
-#endif
         gstart[d0] = bucket_base[d0] + excl - ls;
     }
+#endif
     __syncthreads();
+    STAMP(3);
 
     // scatter into LDS in tile order
     uint32_t lp[SI];
@@ -198,13 +339,8 @@ __global__ __launch_bounds__(NT) void onesweep_pass(const uint64_t *__restrict__
         kout[gstart[DIGIT(kk)] + q] = kk;
     }
 #endif
+    STAMP(4);
     if constexpr (HAS_V) {
-        V val[SI];
-#pragma unroll
-        for (int i = 0; i < SI; i++) {
-            const uint64_t idx = ib + (uint64_t)i * 64;
-            val[i] = idx < n ? vin[idx] : (V)0;
-        }
         // digits of the tile-ordered keys, before skeys is reused for values
         uint8_t dq[(TILE + NT - 1) / NT];
 #pragma unroll
@@ -224,6 +360,7 @@ __global__ __launch_bounds__(NT) void onesweep_pass(const uint64_t *__restrict__
             if (q < cnt) vout[gstart[dq[r]] + q] = sval[q];
         }
     }
+    STAMP(5);
 }
 
 __global__ __launch_bounds__(256) void histogram_kernel(const uint64_t *__restrict__ keys, uint64_t n, int npass,
@@ -277,9 +414,14 @@ int run_passes(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, V *v0, V *v1, uint64_t
         uint32_t epoch, *counter;
         KMAN_TRY(kman_lookback_begin(ctx, n_tiles * RADIX, &epoch, &counter));
         KTimer kt_(ctx, "sort_pass");
-        hipLaunchKernelGGL((onesweep_pass<NT, SI, EARLY, V>), dim3((uint32_t)n_tiles), dim3(NT), 0, ctx->stream, kb[cur], kb[cur ^ 1],
-                           vb[cur], vb[cur ^ 1], n, sh[p], bi[p], (const uint64_t *)scr + p * RADIX, ctx->d_status,
-                           counter, epoch, ctx->d_err);
+        if (ctx->lds_atomic_ordered)
+            hipLaunchKernelGGL((onesweep_pass<NT, SI, EARLY, V, false, true>), dim3((uint32_t)n_tiles), dim3(NT), 0,
+                               ctx->stream, kb[cur], kb[cur ^ 1], vb[cur], vb[cur ^ 1], n, sh[p], bi[p],
+                               (const uint64_t *)scr + p * RADIX, ctx->d_status, counter, epoch, ctx->d_err, nullptr);
+        else
+            hipLaunchKernelGGL((onesweep_pass<NT, SI, EARLY, V>), dim3((uint32_t)n_tiles), dim3(NT), 0, ctx->stream,
+                               kb[cur], kb[cur ^ 1], vb[cur], vb[cur ^ 1], n, sh[p], bi[p],
+                               (const uint64_t *)scr + p * RADIX, ctx->d_status, counter, epoch, ctx->d_err, nullptr);
         HIP_TRY(ctx, hipGetLastError());
         cur ^= 1;
     }
@@ -299,6 +441,14 @@ int dispatch_vals(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, void *v0, void *v1,
 }
 
 }  // namespace
+
+#if defined(KMAN_ABL) && (KMAN_ABL & 4)
+// diagnostic builds only (not part of include/kman.h)
+extern "C" int kman_debug_set(kman_ctx *ctx, void *dptr) {
+    HIP_TRY(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_dbg), &dptr, sizeof(dptr)));
+    return KMAN_OK;
+}
+#endif
 
 extern "C" int kman_sort_plan(uint32_t key_bits, uint32_t *npass, uint32_t *shift, uint32_t *bits) {
     if (!npass || !shift || !bits || key_bits == 0 || key_bits > 64) return KMAN_EINVAL;
@@ -376,9 +526,14 @@ int launch_partition(kman_ctx *ctx, const uint64_t *kin, uint64_t *kout, const V
     uint32_t epoch, *counter;
     KMAN_TRY(kman_lookback_begin(ctx, n_tiles * RADIX, &epoch, &counter));
     KTimer kt_(ctx, "partition");
-    hipLaunchKernelGGL((onesweep_pass<NT, SI, true, V, true>), dim3((uint32_t)n_tiles), dim3(NT), 0, ctx->stream,
-                       kin, kout, vin, vout, n, lut_shift, bits, d_base, ctx->d_status, counter, epoch, ctx->d_err,
-                       lut);
+    if (ctx->lds_atomic_ordered)
+        hipLaunchKernelGGL((onesweep_pass<NT, SI, true, V, true, true>), dim3((uint32_t)n_tiles), dim3(NT), 0,
+                           ctx->stream, kin, kout, vin, vout, n, lut_shift, bits, d_base, ctx->d_status, counter,
+                           epoch, ctx->d_err, lut);
+    else
+        hipLaunchKernelGGL((onesweep_pass<NT, SI, true, V, true>), dim3((uint32_t)n_tiles), dim3(NT), 0, ctx->stream,
+                           kin, kout, vin, vout, n, lut_shift, bits, d_base, ctx->d_status, counter, epoch,
+                           ctx->d_err, lut);
     HIP_TRY(ctx, hipGetLastError());
     return KMAN_OK;
 }
