@@ -13,6 +13,9 @@
  *                      + alphabet check / mkrc            kmermaid/seq.py:279,318,500-509
  *   kman_sort          Batch.sorted (stable, by .seq)     kmermaid/batch.py:156-168
  *                      + BatcherBase.write_all re-sort    kmermaid/batcher.py:133-153,392
+ *   kman_sort_range    the same, by a prefix of the key bits
+ *   kman_finish        Batch.sorted / Crawler.do_batch + join_* over prefix-sorted keys
+ *                                                         batch.py:156-168, join.py:95-130,244-285
  *   kman_rle_count     Crawler.do_batch + join_sequence_count
  *                                                         kmermaid/join.py:95-130,266-285
  *   kman_rle_uniq      Crawler.do_batch + join_unique     kmermaid/join.py:95-130,244-263
@@ -61,6 +64,15 @@ extern "C" {
 #define KMAN_RC 1u          /* also emit reverse complements (kmer -r, seq.py:274-282) */
 #define KMAN_WANT_POS 2u    /* also emit the pos payload (uniq / batch modes) */
 #define KMAN_CANONICAL 4u   /* emit min(fwd, rc) instead (not in the reference) */
+/* kman_extract: accumulate d_hist for the passes over bits [b, 2k) only
+ * (the prefix passes of kman_split_bits); default b = 0, every bit */
+#define KMAN_HIST_LO(b) (((uint32_t)(b) & 0x7fu) << 8)
+#define KMAN_HIST_LO_OF(flags) (((flags) >> 8) & 0x7fu)
+
+/* kman_finish modes */
+#define KMAN_FINISH_SORT 0  /* full stable sort, in place          (batch.py:156-168) */
+#define KMAN_FINISH_COUNT 1 /* (key, group size) per distinct key  (join.py:266-285) */
+#define KMAN_FINISH_UNIQ 2  /* keys occurring once + payload       (join.py:244-263) */
 
 typedef struct kman_ctx kman_ctx;
 
@@ -138,6 +150,31 @@ int kman_sort_plan(uint32_t key_bits, uint32_t *npass, uint32_t *shift, uint32_t
 int kman_sort(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, void *d_vals, void *d_vals_alt,
               uint32_t val_bytes, uint64_t n, uint32_t key_bits, const uint64_t *d_hist,
               int *result_in_alt);
+
+/* The same sort restricted to bits [lo_bit, hi_bit): a stable sort by those
+ * bits only.  d_hist: NULL or kman_extract's with KMAN_HIST_LO(lo_bit). */
+int kman_sort_plan_range(uint32_t lo_bit, uint32_t hi_bit, uint32_t *npass, uint32_t *shift,
+                         uint32_t *bits);
+int kman_sort_range(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, void *d_vals, void *d_vals_alt,
+                    uint32_t val_bytes, uint64_t n, uint32_t lo_bit, uint32_t hi_bit, const uint64_t *d_hist,
+                    int *result_in_alt);
+
+/* Prefix-split sort: kman_sort_range over the top bits [lo_bit, key_bits)
+ * (kman_split_bits picks lo_bit so that equal-prefix segments average <= 512
+ * keys), then kman_finish completes the order of every segment in LDS and
+ * emits in the same pass (Batch.sorted + Crawler.do_batch, batch.py:156-168,
+ * join.py:95-130):
+ *   SORT   d_keys / d_vals fully sorted in place (stable); *n_out = n
+ *   COUNT  d_okeys[j], d_ovals[j] = group size (oval_bytes 4 | 8); d_vals unused
+ *   UNIQ   d_okeys[j], d_ovals[j] = payload of keys that occur once
+ *          (oval_bytes == val_bytes)
+ * Input: keys stably sorted by bits [lo_bit, key_bits).  In COUNT / UNIQ mode
+ * the input arrays are scratch afterwards (segments longer than a chunk's
+ * staging area are sorted in place through d_*_alt-free temporary buffers). */
+int kman_split_bits(uint64_t n, uint32_t key_bits, uint32_t *lo_bit);
+int kman_finish(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, void *d_vals, void *d_vals_alt,
+                uint32_t val_bytes, uint64_t n, uint32_t key_bits, uint32_t lo_bit, int mode,
+                uint64_t *d_okeys, void *d_ovals, uint32_t oval_bytes, uint64_t *n_out);
 
 /* Run-length count of sorted keys (join.py:95-130 + 266-285):
  * d_ukeys[j], d_counts[j] (u32 if count_bytes == 4 else u64). */

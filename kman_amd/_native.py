@@ -31,6 +31,13 @@ KMAN_ECAP = -7
 KMAN_RC = 1
 KMAN_WANT_POS = 2
 KMAN_CANONICAL = 4
+KMAN_FINISH_SORT = 0
+KMAN_FINISH_COUNT = 1
+KMAN_FINISH_UNIQ = 2
+
+
+def KMAN_HIST_LO(b: int) -> int:
+    return (int(b) & 0x7F) << 8
 
 
 class ParseInfo(ctypes.Structure):
@@ -68,6 +75,19 @@ SIGNATURES = {
     "kman_sort": (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, POINTER(c_int)],
+    ),
+    "kman_sort_plan_range": (
+        c_int, [c_uint32, c_uint32, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]),
+    "kman_sort_range": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_uint32, c_void_p,
+         POINTER(c_int)],
+    ),
+    "kman_split_bits": (c_int, [c_uint64, c_uint32, POINTER(c_uint32)]),
+    "kman_finish": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_uint32, c_int,
+         c_void_p, c_void_p, c_uint32, POINTER(c_uint64)],
     ),
     "kman_rle_count": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, POINTER(c_uint64)]),
     "kman_rle_uniq": (

@@ -32,6 +32,9 @@ struct kman_ctx {
     // generic device scratch
     void *d_scratch = nullptr;
     size_t scratch_bytes = 0;
+    // second scratch for callers that hold a region across calls that use d_scratch
+    void *d_aux = nullptr;
+    size_t aux_bytes = 0;
     // optional launch timing (kman_timing_*)
     bool timing = false;
     struct TimedLaunch {
@@ -62,6 +65,7 @@ int kman_hip_fail(kman_ctx *ctx, hipError_t e, const char *what);
 // counter for dynamic tile ids of that epoch.
 int kman_lookback_begin(kman_ctx *ctx, size_t words, uint32_t *epoch, uint32_t **counter);
 int kman_scratch(kman_ctx *ctx, size_t bytes, void **p);
+int kman_aux(kman_ctx *ctx, size_t bytes, void **p);
 int kman_check_device_error(kman_ctx *ctx);
 // synchronises; reads the inclusive value of the last tile of the most recent
 // look-back launch (checks its epoch) and the device error word.

@@ -276,7 +276,11 @@ extern "C" int kman_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_ba
     }
     Plan plan{};
     uint32_t np, sh[MAXPASS], bi[MAXPASS];
-    KMAN_TRY(kman_sort_plan(2 * k, &np, sh, bi));
+    // histograms for the passes over bits [lo, 2k) (kman_split_bits), all
+    // bits when the caller passes no KMAN_HIST_LO
+    const uint32_t hist_lo = KMAN_HIST_LO_OF(flags);
+    if (hist_lo > 2 * k) return kman_fail(ctx, KMAN_EINVAL, "histogram low bit %u > 2k", hist_lo);
+    KMAN_TRY(kman_sort_plan_range(hist_lo, 2 * k, &np, sh, bi));
     plan.npass = (int)np;
     for (uint32_t i = 0; i < np; i++) {
         plan.shift[i] = (uint8_t)sh[i];

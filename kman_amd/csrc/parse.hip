@@ -142,7 +142,9 @@ KMAN_DEV void load_chunk(const uint8_t *text, uint64_t n, uint64_t pos, Chunk &c
             ch.w[q] = v;
         }
     }
-    const uint32_t prev = pos ? text[pos - 1] : '\n';  // position 0 starts a line
+    // position 0 starts a line; a chunk wholly past the end reads nothing (its
+    // byte before may lie past the allocation)
+    const uint32_t prev = pos == 0 ? '\n' : (pos <= n ? text[pos - 1] : 0u);
     uint64_t keep = 0, ls = 0, gt = 0, exo = 0, term = 0, nonws = 0;
     uint32_t pc = prev;
 #pragma unroll

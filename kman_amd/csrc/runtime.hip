@@ -37,6 +37,22 @@ int kman_scratch(kman_ctx *ctx, size_t bytes, void **p) {
     return KMAN_OK;
 }
 
+int kman_aux(kman_ctx *ctx, size_t bytes, void **p) {
+    if (bytes > ctx->aux_bytes) {
+        if (ctx->d_aux) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            HIP_TRY(ctx, hipFree(ctx->d_aux));
+            ctx->d_aux = nullptr;
+            ctx->aux_bytes = 0;
+        }
+        size_t nb = bytes < (1u << 16) ? (1u << 16) : bytes + bytes / 4;
+        HIP_TRY(ctx, hipMalloc(&ctx->d_aux, nb));
+        ctx->aux_bytes = nb;
+    }
+    *p = ctx->d_aux;
+    return KMAN_OK;
+}
+
 int kman_lookback_begin(kman_ctx *ctx, size_t words, uint32_t *epoch, uint32_t **counter) {
     if (words > ctx->status_words) {
         if (ctx->d_status) {
@@ -227,6 +243,7 @@ void kman_destroy(kman_ctx *ctx) {
     for (auto e : ctx->event_pool) (void)hipEventDestroy(e);
     if (ctx->d_status) (void)hipFree(ctx->d_status);
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
+    if (ctx->d_aux) (void)hipFree(ctx->d_aux);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->h_small) (void)hipHostFree(ctx->h_small);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);

@@ -172,8 +172,8 @@ KMAN_DEV uint64_t group_lookback(uint64_t *st, int64_t tile, uint64_t agg, uint3
 
 // One LSD digit pass over a tile of NT*SI keys.  With LUT the digit is
 // lut[key >> shift] (destination rank of a prefix range: kman_partition).
-template <int NT, int SI, bool EARLY, typename V, bool LUT = false, bool ATOMIC = false>
-__global__ __launch_bounds__(NT) void onesweep_pass(const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
+template <int NT, int SI, bool EARLY, typename V, bool LUT = false, bool ATOMIC = false, int MINW = 1>
+__global__ __launch_bounds__(NT, MINW) void onesweep_pass(const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
                                                     const V *__restrict__ vin, V *__restrict__ vout, uint64_t n,
                                                     uint32_t shift, uint32_t bits,
                                                     const uint64_t *__restrict__ bucket_base,
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256) void histogram_kernel(const uint64_t *__restri
     }
 }
 
-template <int NT, int SI, bool EARLY, typename V>
+template <int NT, int SI, bool EARLY, typename V, int MINW>
 int run_passes(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, V *v0, V *v1, uint64_t n, uint32_t np, const uint32_t *sh,
                const uint32_t *bi, const uint64_t *h_hist, int *result_in_alt) {
     // bucket bases per pass (host: 256 x npass), skipping single-bucket passes
@@ -415,11 +415,11 @@ int run_passes(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, V *v0, V *v1, uint64_t
         KMAN_TRY(kman_lookback_begin(ctx, n_tiles * RADIX, &epoch, &counter));
         KTimer kt_(ctx, "sort_pass");
         if (ctx->lds_atomic_ordered)
-            hipLaunchKernelGGL((onesweep_pass<NT, SI, EARLY, V, false, true>), dim3((uint32_t)n_tiles), dim3(NT), 0,
+            hipLaunchKernelGGL((onesweep_pass<NT, SI, EARLY, V, false, true, MINW>), dim3((uint32_t)n_tiles), dim3(NT), 0,
                                ctx->stream, kb[cur], kb[cur ^ 1], vb[cur], vb[cur ^ 1], n, sh[p], bi[p],
                                (const uint64_t *)scr + p * RADIX, ctx->d_status, counter, epoch, ctx->d_err, nullptr);
         else
-            hipLaunchKernelGGL((onesweep_pass<NT, SI, EARLY, V>), dim3((uint32_t)n_tiles), dim3(NT), 0, ctx->stream,
+            hipLaunchKernelGGL((onesweep_pass<NT, SI, EARLY, V, false, false, MINW>), dim3((uint32_t)n_tiles), dim3(NT), 0, ctx->stream,
                                kb[cur], kb[cur ^ 1], vb[cur], vb[cur ^ 1], n, sh[p], bi[p],
                                (const uint64_t *)scr + p * RADIX, ctx->d_status, counter, epoch, ctx->d_err, nullptr);
         HIP_TRY(ctx, hipGetLastError());
@@ -429,14 +429,14 @@ int run_passes(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, V *v0, V *v1, uint64_t
     return KMAN_OK;
 }
 
-template <int NT, int SI, bool EARLY = true>
+template <int NT, int SI, bool EARLY = true, int MINW = 1>
 int dispatch_vals(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, void *v0, void *v1, uint32_t vb, uint64_t n, uint32_t np,
                   const uint32_t *sh, const uint32_t *bi, const uint64_t *h_hist, int *res) {
-    if (vb == 0) return run_passes<NT, SI, EARLY, NoVal>(ctx, k0, k1, nullptr, nullptr, n, np, sh, bi, h_hist, res);
+    if (vb == 0) return run_passes<NT, SI, EARLY, NoVal, MINW>(ctx, k0, k1, nullptr, nullptr, n, np, sh, bi, h_hist, res);
     if (vb == 4)
-        return run_passes<NT, SI, EARLY, uint32_t>(ctx, k0, k1, (uint32_t *)v0, (uint32_t *)v1, n, np, sh, bi, h_hist,
+        return run_passes<NT, SI, EARLY, uint32_t, MINW>(ctx, k0, k1, (uint32_t *)v0, (uint32_t *)v1, n, np, sh, bi, h_hist,
                                                    res);
-    return run_passes<NT, SI, EARLY, uint64_t>(ctx, k0, k1, (uint64_t *)v0, (uint64_t *)v1, n, np, sh, bi, h_hist,
+    return run_passes<NT, SI, EARLY, uint64_t, MINW>(ctx, k0, k1, (uint64_t *)v0, (uint64_t *)v1, n, np, sh, bi, h_hist,
                                                res);
 }
 
@@ -450,13 +450,16 @@ extern "C" int kman_debug_set(kman_ctx *ctx, void *dptr) {
 }
 #endif
 
-extern "C" int kman_sort_plan(uint32_t key_bits, uint32_t *npass, uint32_t *shift, uint32_t *bits) {
-    if (!npass || !shift || !bits || key_bits == 0 || key_bits > 64) return KMAN_EINVAL;
-    // as few passes of <= 8 bits as possible, bits spread evenly (k=21: 6 x 7)
-    const uint32_t np = (key_bits + 7) / 8;
-    uint32_t at = 0;
+// as few passes of <= 8 bits as possible over bits [lo, hi), bits spread
+// evenly (k=21 full sort: 6 x 7; the prefix [21, 42) of kman_split_bits: 3 x 7)
+extern "C" int kman_sort_plan_range(uint32_t lo_bit, uint32_t hi_bit, uint32_t *npass, uint32_t *shift,
+                                    uint32_t *bits) {
+    if (!npass || !shift || !bits || hi_bit > 64 || lo_bit > hi_bit) return KMAN_EINVAL;
+    const uint32_t nb = hi_bit - lo_bit;
+    const uint32_t np = (nb + 7) / 8;
+    uint32_t at = lo_bit;
     for (uint32_t p = 0; p < np; p++) {
-        const uint32_t b = (key_bits - at + (np - p) - 1) / (np - p);
+        const uint32_t b = (hi_bit - at + (np - p) - 1) / (np - p);
         shift[p] = at;
         bits[p] = b;
         at += b;
@@ -465,9 +468,14 @@ extern "C" int kman_sort_plan(uint32_t key_bits, uint32_t *npass, uint32_t *shif
     return KMAN_OK;
 }
 
-extern "C" int kman_sort(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, void *d_vals, void *d_vals_alt,
-                         uint32_t val_bytes, uint64_t n, uint32_t key_bits, const uint64_t *d_hist,
-                         int *result_in_alt) {
+extern "C" int kman_sort_plan(uint32_t key_bits, uint32_t *npass, uint32_t *shift, uint32_t *bits) {
+    if (key_bits == 0) return KMAN_EINVAL;
+    return kman_sort_plan_range(0, key_bits, npass, shift, bits);
+}
+
+extern "C" int kman_sort_range(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, void *d_vals,
+                               void *d_vals_alt, uint32_t val_bytes, uint64_t n, uint32_t lo_bit, uint32_t hi_bit,
+                               const uint64_t *d_hist, int *result_in_alt) {
     if (!ctx || !result_in_alt) return KMAN_EINVAL;
     if (val_bytes != 0 && val_bytes != 4 && val_bytes != 8)
         return kman_fail(ctx, KMAN_EINVAL, "val_bytes must be 0, 4 or 8");
@@ -477,7 +485,9 @@ extern "C" int kman_sort(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, 
         return kman_fail(ctx, KMAN_EINVAL, "null buffer");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     uint32_t np, sh[MAXPASS], bi[MAXPASS];
-    KMAN_TRY(kman_sort_plan(key_bits, &np, sh, bi));
+    if (kman_sort_plan_range(lo_bit, hi_bit, &np, sh, bi) != KMAN_OK)
+        return kman_fail(ctx, KMAN_EINVAL, "bad bit range [%u, %u)", lo_bit, hi_bit);
+    if (np == 0) return KMAN_OK;
     // histograms of every pass (device), then to the host for the bucket bases
     unsigned long long *hist;
     void *scr;
@@ -505,16 +515,24 @@ extern "C" int kman_sort(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, 
         return e ? atoi(e) : 0;
     }();
     switch (cfg) {
-        case 1: KMAN_TRY((dispatch_vals<512, 16>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
+        case 1: KMAN_TRY((dispatch_vals<512, 12>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
         case 2: KMAN_TRY((dispatch_vals<256, 24>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
         case 3: KMAN_TRY((dispatch_vals<1024, 8>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
         case 4: KMAN_TRY((dispatch_vals<256, 16>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
         case 6: KMAN_TRY((dispatch_vals<256, 16, false>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
         case 7: KMAN_TRY((dispatch_vals<512, 12, false>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
         case 5: KMAN_TRY((dispatch_vals<256, 8>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
-        default: KMAN_TRY((dispatch_vals<512, 12>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
+        default: KMAN_TRY((dispatch_vals<512, 16>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
     }
     return kman_check_device_error(ctx);
+}
+
+extern "C" int kman_sort(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, void *d_vals, void *d_vals_alt,
+                         uint32_t val_bytes, uint64_t n, uint32_t key_bits, const uint64_t *d_hist,
+                         int *result_in_alt) {
+    if (key_bits == 0 || key_bits > 64) return ctx ? kman_fail(ctx, KMAN_EINVAL, "key_bits must be 1..64") : KMAN_EINVAL;
+    return kman_sort_range(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, 0, key_bits, d_hist,
+                           result_in_alt);
 }
 
 namespace {

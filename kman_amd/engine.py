@@ -237,6 +237,10 @@ class Kmers:
     k: int
     hist: DeviceBuffer
     sorted: bool = False
+    # histogram plan of kman_extract: bits [lo_bit, 2k) (kman_split_bits);
+    # hist_valid False = no usable histogram (sort computes its own)
+    lo_bit: int = 0
+    hist_valid: bool = False
 
     def free(self) -> None:
         for b in (self.keys, self.alt, self.pos, self.pos_alt, self.hist):
@@ -278,25 +282,57 @@ def extract(p: Parsed, k: int, rc: bool, want_pos: bool, canonical: bool = False
     hist = dev.alloc(8 * 256 * 8)
     dev.memset(hist, 0, 8 * 256 * 8)
     out = c_uint64(0)
-    rc_ = L.kman_extract(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k, flags_for(rc, want_pos, canonical),
+    lo = split_bits(bound, 2 * k)
+    rc_ = L.kman_extract(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
+                         flags_for(rc, want_pos, canonical) | N.KMAN_HIST_LO(lo),
                          c_void_p(keys.ptr), c_void_p(pos.ptr if pos else None), pos_bytes, bound,
                          c_void_p(hist.ptr), byref(out))
     N.check(dev.ctx, rc_, "kman_extract")
-    return Kmers(keys, alt, pos, pos_alt, pos_bytes if want_pos else 0, int(out.value), k, hist)
+    return Kmers(keys, alt, pos, pos_alt, pos_bytes if want_pos else 0, int(out.value), k, hist, lo_bit=lo,
+                 hist_valid=True)
 
 
-def sort(km: Kmers, dev: Device) -> None:
-    """kman_sort (stable LSD radix) in place: afterwards km.keys/km.pos are sorted."""
-    if km.sorted:
-        return
+def split_bits(n: int, key_bits: int) -> int:
+    """kman_split_bits: low bit of the prefix the global passes sort by."""
+    lo = ctypes.c_uint32(0)
+    if N.lib().kman_split_bits(max(int(n), 0), key_bits, byref(lo)) != N.KMAN_OK:
+        raise ValueError("bad key_bits %d" % key_bits)
+    return int(lo.value)
+
+
+def _sort_prefix(km: Kmers, dev: Device, key_bits: int) -> None:
+    """kman_sort_range over bits [km.lo_bit, key_bits): a stable sort by the
+    prefix; km.keys / km.pos then hold the prefix-sorted data."""
     res = c_int(0)
-    rc = N.lib().kman_sort(dev.ctx, c_void_p(km.keys.ptr), c_void_p(km.alt.ptr),
-                           c_void_p(km.pos.ptr if km.pos else None), c_void_p(km.pos_alt.ptr if km.pos_alt else None),
-                           km.pos_bytes, km.n, 2 * km.k, c_void_p(km.hist.ptr), byref(res))
-    N.check(dev.ctx, rc, "kman_sort")
+    hist = c_void_p(km.hist.ptr) if km.hist_valid and km.hist is not None else c_void_p(None)
+    rc = N.lib().kman_sort_range(dev.ctx, c_void_p(km.keys.ptr), c_void_p(km.alt.ptr),
+                                 c_void_p(km.pos.ptr if km.pos else None),
+                                 c_void_p(km.pos_alt.ptr if km.pos_alt else None), km.pos_bytes, km.n, km.lo_bit,
+                                 key_bits, hist, byref(res))
+    N.check(dev.ctx, rc, "kman_sort_range")
     if res.value:
         km.keys, km.alt = km.alt, km.keys
         km.pos, km.pos_alt = km.pos_alt, km.pos
+
+
+def _finish(km: Kmers, dev: Device, key_bits: int, mode: int, okeys=None, ovals=None, ob: int = 0) -> int:
+    out = c_uint64(0)
+    N.check(dev.ctx, N.lib().kman_finish(dev.ctx, c_void_p(km.keys.ptr), c_void_p(km.alt.ptr),
+                                         c_void_p(km.pos.ptr if km.pos else None),
+                                         c_void_p(km.pos_alt.ptr if km.pos_alt else None), km.pos_bytes, km.n,
+                                         key_bits, km.lo_bit, mode, c_void_p(okeys.ptr if okeys else None),
+                                         c_void_p(ovals.ptr if ovals else None), ob, byref(out)), "kman_finish")
+    return int(out.value)
+
+
+def sort(km: Kmers, dev: Device) -> None:
+    """Stable sort of km.keys (+ km.pos) by key, Batch.sorted (batch.py:156-168):
+    kman_sort_range over the prefix bits, then kman_finish(SORT) in LDS."""
+    if km.sorted:
+        return
+    if km.n > 1:
+        _sort_prefix(km, dev, 2 * km.k)
+        _finish(km, dev, 2 * km.k, N.KMAN_FINISH_SORT)
     km.sorted = True
 
 
@@ -310,9 +346,15 @@ class CountResult:
 
 
 def rle_count(km: Kmers, dev: Device) -> CountResult:
+    """(key, group size) per distinct key.  Sorted input: kman_rle_count;
+    unsorted: the prefix sort + kman_finish(COUNT) (km is consumed)."""
     cb = 4 if km.n <= 0xFFFFFFFF else 8
     ukeys = dev.alloc(8 * max(km.n, 1))
     counts = dev.alloc(cb * max(km.n, 1))
+    if not km.sorted:
+        _sort_prefix(km, dev, 2 * km.k)
+        n = _finish(km, dev, 2 * km.k, N.KMAN_FINISH_COUNT, ukeys, counts, cb)
+        return CountResult(ukeys, counts, cb, n, km.k)
     out = c_uint64(0)
     N.check(dev.ctx, N.lib().kman_rle_count(dev.ctx, c_void_p(km.keys.ptr), km.n, c_void_p(ukeys.ptr),
                                              c_void_p(counts.ptr), cb, byref(out)), "kman_rle_count")
@@ -333,6 +375,10 @@ def rle_uniq(km: Kmers, dev: Device) -> UniqResult:
         raise ValueError("uniq needs the pos payload (extract with want_pos=True)")
     okeys = dev.alloc(8 * max(km.n, 1))
     opos = dev.alloc(km.pos_bytes * max(km.n, 1))
+    if not km.sorted:
+        _sort_prefix(km, dev, 2 * km.k)
+        n = _finish(km, dev, 2 * km.k, N.KMAN_FINISH_UNIQ, okeys, opos, km.pos_bytes)
+        return UniqResult(okeys, opos, km.pos_bytes, n, km.k)
     out = c_uint64(0)
     N.check(dev.ctx, N.lib().kman_rle_uniq(dev.ctx, c_void_p(km.keys.ptr), c_void_p(km.pos.ptr), km.pos_bytes,
                                             km.n, c_void_p(okeys.ptr), c_void_p(opos.ptr), byref(out)),
@@ -450,7 +496,6 @@ def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = No
         try:
             if km.n == 0:
                 return b""
-            sort(km, dev)
             r = rle_count(km, dev)
             try:
                 ukeys, counts = download_count(dev, r)
@@ -475,7 +520,6 @@ def uniq_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = Non
         try:
             if km.n == 0:
                 return b""
-            sort(km, dev)
             r = rle_uniq(km, dev)
             try:
                 keys, pos = download_uniq(dev, r)
@@ -498,10 +542,15 @@ class ResidentPipeline:
     the result device-resident (what bench.py times)."""
 
     def __init__(self, dev: Device, text: bytes, k: int, mode: str = "uniq", rc: bool = False,
-                 pos_bytes: Optional[int] = None):
+                 pos_bytes: Optional[int] = None, path: str = "split"):
         _check_k(k)
         if mode not in ("count", "uniq"):
             raise ValueError(mode)
+        if path not in ("split", "full"):
+            raise ValueError(path)
+        # split: prefix passes + kman_finish (default); full: every bit in
+        # global passes + kman_rle_* (the previous engine, kept for A/B runs)
+        self.path = path
         self.dev, self.k, self.mode, self.rc = dev, k, mode, rc
         n = len(text)
         self.n_bytes = n
@@ -522,7 +571,8 @@ class ResidentPipeline:
         self.out_keys = dev.alloc(8 * self.bound)
         self.count_bytes = 4 if self.bound <= 0xFFFFFFFF else 8
         self.out_vals = dev.alloc((self.pos_bytes if want_pos else self.count_bytes) * self.bound)
-        self.flags = flags_for(rc, want_pos)
+        self.lo_bit = split_bits(self.bound, 2 * k) if path == "split" else 0
+        self.flags = flags_for(rc, want_pos) | N.KMAN_HIST_LO(self.lo_bit)
         self.n_kmers = 0
         self.n_out = 0
         self.n_bases = 0
@@ -559,14 +609,25 @@ class ResidentPipeline:
                                     c_void_p(self.hist.ptr), byref(n)), "kman_extract")
         self.n_kmers = int(n.value)
         res = c_int(0)
-        N.check(ctx, L.kman_sort(ctx, c_void_p(self.keys.ptr), c_void_p(self.alt.ptr), pos,
-                                 c_void_p(self.pos_alt.ptr if self.pos_alt else None),
-                                 self.pos_bytes if self.pos else 0, self.n_kmers, 2 * self.k,
-                                 c_void_p(self.hist.ptr), byref(res)), "kman_sort")
+        vb = self.pos_bytes if self.pos else 0
+        pos_alt = c_void_p(self.pos_alt.ptr if self.pos_alt else None)
+        N.check(ctx, L.kman_sort_range(ctx, c_void_p(self.keys.ptr), c_void_p(self.alt.ptr), pos, pos_alt, vb,
+                                       self.n_kmers, self.lo_bit, 2 * self.k, c_void_p(self.hist.ptr), byref(res)),
+                "kman_sort_range")
         self.sorted_in_alt = bool(res.value)
         skeys = self.alt if res.value else self.keys
         out = c_uint64(0)
-        if self.mode == "count":
+        if self.path == "split":
+            spos = self.pos_alt if res.value else self.pos
+            other = self.keys if res.value else self.alt
+            opos = self.pos if res.value else self.pos_alt
+            mode = N.KMAN_FINISH_COUNT if self.mode == "count" else N.KMAN_FINISH_UNIQ
+            ob = self.count_bytes if self.mode == "count" else self.pos_bytes
+            N.check(ctx, L.kman_finish(ctx, c_void_p(skeys.ptr), c_void_p(other.ptr),
+                                       c_void_p(spos.ptr if spos else None), c_void_p(opos.ptr if opos else None), vb,
+                                       self.n_kmers, 2 * self.k, self.lo_bit, mode, c_void_p(self.out_keys.ptr),
+                                       c_void_p(self.out_vals.ptr), ob, byref(out)), "kman_finish")
+        elif self.mode == "count":
             N.check(ctx, L.kman_rle_count(ctx, c_void_p(skeys.ptr), self.n_kmers, c_void_p(self.out_keys.ptr),
                                           c_void_p(self.out_vals.ptr), self.count_bytes, byref(out)),
                     "kman_rle_count")

@@ -101,7 +101,7 @@ def test_extract_matches_oracle(dev, golden_inputs, k, mode):
                 import ctypes
 
                 npass, sh, bi = ctypes.c_uint32(), (ctypes.c_uint32 * 8)(), (ctypes.c_uint32 * 8)()
-                N.lib().kman_sort_plan(2 * k, ctypes.byref(npass), sh, bi)
+                N.lib().kman_sort_plan_range(km.lo_bit, 2 * k, ctypes.byref(npass), sh, bi)
                 for q in range(npass.value):
                     d = (kref >> np.uint64(sh[q])) & np.uint64((1 << bi[q]) - 1)
                     want = np.bincount(d.astype(np.int64), minlength=256)
@@ -194,6 +194,111 @@ def test_rle_count_and_uniq(dev, n, distinct):
     np.testing.assert_array_equal(sk, wk2)
     np.testing.assert_array_equal(sv, wv2)
     km.free()
+
+
+def _keys_of(dist, n, key_bits, rng):
+    top = 2**key_bits if key_bits < 64 else 2**64
+    if dist == "uniform":
+        return rng.integers(0, top, size=n, dtype=np.uint64) if key_bits < 64 else \
+            rng.integers(0, 2**63, size=n, dtype=np.uint64) * np.uint64(2) + rng.integers(0, 2, size=n).astype(np.uint64)
+    if dist == "ties":  # few distinct values spread over the whole key range
+        pool = rng.integers(0, min(top, 2**63), size=37, dtype=np.uint64)
+        return pool[rng.integers(0, len(pool), size=n)]
+    # skew: half the keys are one value, a quarter share one prefix, rest uniform
+    keys = rng.integers(0, min(top, 2**63), size=n, dtype=np.uint64)
+    hot = np.uint64(rng.integers(0, min(top, 2**63)))
+    keys[rng.random(n) < 0.5] = hot
+    sel = rng.random(n) < 0.25
+    low = np.uint64((1 << max(1, key_bits // 3)) - 1)
+    keys[sel] = (hot & ~low) | (keys[sel] & low)
+    return keys
+
+
+def _finish_case(dev, keys, vals, key_bits, lo_bit, mode, ob):
+    """kman_sort_range over [lo_bit, key_bits) + kman_finish on the device."""
+    import ctypes
+    from ctypes import byref, c_void_p
+    from kman_amd import _native as N
+
+    L = N.lib()
+    n = len(keys)
+    vb = vals.dtype.itemsize if vals is not None else 0
+    bufs = [dev.alloc(8 * max(n, 1)), dev.alloc(8 * max(n, 1))]
+    vbufs = [dev.alloc(vb * max(n, 1)), dev.alloc(vb * max(n, 1))] if vb else [None, None]
+    okeys, ovals = dev.alloc(8 * max(n, 1)), dev.alloc(8 * max(n, 1))
+    try:
+        dev.upload(bufs[0], keys)
+        if vb:
+            dev.upload(vbufs[0], vals)
+        res = ctypes.c_int(0)
+        p = lambda b: c_void_p(b.ptr if b is not None else None)  # noqa: E731
+        N.check(dev.ctx, L.kman_sort_range(dev.ctx, p(bufs[0]), p(bufs[1]), p(vbufs[0]), p(vbufs[1]), vb, n, lo_bit,
+                                           key_bits, None, byref(res)), "sort_range")
+        c = res.value
+        if os.environ.get("KMAN_TEST_VERIFY"):
+            got = dev.download(bufs[c], n, np.uint64)
+            order = np.argsort(keys >> np.uint64(lo_bit) if lo_bit < 64 else np.zeros(n, np.uint64), kind="stable")
+            assert np.array_equal(got, keys[order]), "prefix sort wrong: %d mismatches" % int((got != keys[order]).sum())
+        out = ctypes.c_uint64(0)
+        N.check(dev.ctx, L.kman_finish(dev.ctx, p(bufs[c]), p(bufs[c ^ 1]), p(vbufs[c]), p(vbufs[c ^ 1]), vb, n,
+                                       key_bits, lo_bit, mode, p(okeys), p(ovals), ob, byref(out)), "finish")
+        m = int(out.value)
+        dev.sync()
+        if mode == N.KMAN_FINISH_SORT:
+            assert m == n
+            return dev.download(bufs[c], n, np.uint64), (dev.download(vbufs[c], n, vals.dtype) if vb else None)
+        return dev.download(okeys, m, np.uint64), dev.download(ovals, m, np.uint32 if ob == 4 else np.uint64)
+    finally:
+        for b in bufs + vbufs + [okeys, ovals]:
+            if b is not None:
+                b.free()
+
+
+@pytest.mark.parametrize("n", [1, 2, 1000, 4096, 4097, 100_003, 2_000_001])
+@pytest.mark.parametrize("key_bits", [14, 42, 64])
+@pytest.mark.parametrize("dist", ["uniform", "ties", "skew"])
+@pytest.mark.parametrize("split", ["auto", "coarse"])
+def test_finish_modes(dev, n, key_bits, dist, split):
+    """prefix sort + kman_finish == stable sort / RLE count / uniq of the
+    oracle; 'coarse' prefixes (3 bits) force big segments through the
+    presorted-slice fallback, 'skew' makes groups span many chunks."""
+    import np_oracle
+    from kman_amd import _native as N, engine
+
+    rng = np.random.default_rng(n * 7 + key_bits * 3 + len(dist) + len(split))
+    keys = _keys_of(dist, n, key_bits, rng)
+    lo = engine.split_bits(n, key_bits) if split == "auto" else key_bits - 3
+    vals = np.arange(n, dtype=np.uint32)
+    gk, gv = _finish_case(dev, keys, vals, key_bits, lo, N.KMAN_FINISH_SORT, 0)
+    wk, wv = np_oracle.stable_sort(keys, vals)
+    np.testing.assert_array_equal(gk, wk)
+    np.testing.assert_array_equal(gv, wv)
+    ck, cc = _finish_case(dev, keys, None, key_bits, lo, N.KMAN_FINISH_COUNT, 4 if n % 2 else 8)
+    rk, rcnt = np_oracle.rle_count(wk)
+    np.testing.assert_array_equal(ck, rk)
+    np.testing.assert_array_equal(cc.astype(np.uint64), rcnt)
+    v = rng.integers(0, 2**40, size=n, dtype=np.uint64) if n % 2 else rng.integers(0, 2**31, size=n, dtype=np.uint32)
+    uk, uv = _finish_case(dev, keys, v, key_bits, lo, N.KMAN_FINISH_UNIQ, v.dtype.itemsize)
+    sk, sv = np_oracle.stable_sort(keys, v)
+    qk, qv = np_oracle.rle_uniq(sk, sv)
+    np.testing.assert_array_equal(uk, qk)
+    np.testing.assert_array_equal(uv, qv)
+
+
+def test_finish_single_value(dev):
+    """every key equal: one segment of n keys, one group spanning every chunk."""
+    from kman_amd import _native as N
+
+    n = 300_000
+    keys = np.full(n, 12345, dtype=np.uint64)
+    vals = np.arange(n, dtype=np.uint32)
+    gk, gv = _finish_case(dev, keys, vals, 42, 21, N.KMAN_FINISH_SORT, 0)
+    np.testing.assert_array_equal(gk, keys)
+    np.testing.assert_array_equal(gv, vals)
+    ck, cc = _finish_case(dev, keys, None, 42, 21, N.KMAN_FINISH_COUNT, 4)
+    assert ck.tolist() == [12345] and cc.tolist() == [n]
+    uk, uv = _finish_case(dev, keys, vals, 42, 21, N.KMAN_FINISH_UNIQ, 4)
+    assert len(uk) == 0 and len(uv) == 0
 
 
 def _golden_cases(key):
