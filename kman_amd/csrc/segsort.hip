@@ -37,7 +37,7 @@ namespace {
 
 constexpr int FT = 512;        // threads per chunk
 constexpr int FW = FT / 64;    // waves
-constexpr int FC = 4096;       // chunk: segments that start here are owned
+constexpr int FC = 5120;       // chunk: segments that start here are owned
 constexpr int FR = 6144;       // region capacity: chunk + tail of its last segment
 constexpr int FI = FR / FT;    // items per thread
 constexpr int FRADIX = 128;    // local LSD digit radix
@@ -50,6 +50,7 @@ struct NoV {};
 #if defined(KMAN_ABL) && (KMAN_ABL & 4)
 // diagnostic build only: per-chunk s_memrealtime stamps (100 MHz), thread 0
 __device__ uint64_t *g_fdbg;
+__device__ unsigned long long g_fstat[4];  // wave-path chunks, block-path chunks, segments, sorted keys
 #define FSTAMP(i)                                                                                   \
     do {                                                                                            \
         if (threadIdx.x == 0 && g_fdbg) g_fdbg[(uint64_t)tile * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
@@ -121,7 +122,11 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
     __shared__ uint32_t s_first, s_lastp1, s_end, s_tile, s_flags, s_maxseg;
     __shared__ uint64_t s_out;
 
-    const int64_t tile = grab_tile(counter, &s_tile);
+    // dynamic chunk id (chunks start in id order: every predecessor of a chunk is
+    // resident or done); s_tile is never rewritten, so one barrier suffices
+    if (threadIdx.x == 0) s_tile = atomicAdd(counter, 1u);
+    __syncthreads();
+    const int64_t tile = s_tile;
     FSTAMP(0);
     const uint64_t base = (uint64_t)tile * FC;
     const uint32_t cnt = (uint32_t)(n - base < (uint64_t)FC ? n - base : (uint64_t)FC);
@@ -156,19 +161,21 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
     const uint32_t last = s_lastp1 - 1;
     // listed big segments: the leading one (started before the chunk) and the
     // last one starting here are processed as presorted slices
-    if (t == 0 && n_ov) {
-        uint32_t f = 0;
-        if (first > 0 && base > 0) {
-            const int64_t i = find_big(ov, n_ov, base);
-            if (i >= 0 && ov[2 * i + 1] > base) f |= 1;
+    if (n_ov) {
+        if (t == 0) {
+            uint32_t f = 0;
+            if (first > 0 && base > 0) {
+                const int64_t i = find_big(ov, n_ov, base);
+                if (i >= 0 && ov[2 * i + 1] > base) f |= 1;
+            }
+            if (has_start) {
+                const int64_t i = find_big(ov, n_ov, base + last);
+                if (i >= 0 && ov[2 * i] == base + last) f |= 2;
+            }
+            s_flags = f;
         }
-        if (has_start) {
-            const int64_t i = find_big(ov, n_ov, base + last);
-            if (i >= 0 && ov[2 * i] == base + last) f |= 2;
-        }
-        s_flags = f;
+        __syncthreads();
     }
-    __syncthreads();
     const bool lead_pre = s_flags & 1;
     const bool last_pre = s_flags & 2;
     FSTAMP(1);
@@ -243,7 +250,7 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
         nsegs += 1;  // segment 0 starts at q = 0
         const uint32_t s0 = lead_pre ? 1u : 0u, s1 = nsegs - (trail_pre ? 1u : 0u);
         const uint32_t low_bits = lo_bit >= 64 ? 64u : lo_bit;
-        bool wave_path = nsegs <= (uint32_t)MAXSEG;
+        bool wave_path = nsegs <= (uint32_t)MAXSEG && low_bits <= 51;
         if (wave_path) {
 #pragma unroll
             for (int i = 0; i < FI; i++) {
@@ -259,30 +266,47 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
                     if (sz > (uint32_t)(WI * 64)) atomicMax(&s_maxseg, sz);
                 }
             }
+            // identity positions for the presorted slices and single-key segments
+            // (the sorted segments write theirs in the last pass)
             for (uint32_t q = t; q < m; q += FT) spk[lo + q] = lo + q;
             __syncthreads();
             wave_path = s_maxseg == 0;
         }
+#if defined(KMAN_ABL) && (KMAN_ABL & 4)
+        if (t == 0) {
+            atomicAdd(&g_fstat[wave_path ? 0 : 1], 1ull);
+            atomicAdd(&g_fstat[2], (unsigned long long)nsegs);
+            atomicAdd(&g_fstat[3], (unsigned long long)m);
+        }
+#endif
         if (wave_path) {
             // one wave per segment: stable LSD over the low bits with the
-            // wave's own counters; no block barrier until every segment is done
+            // wave's own counters; no block barrier until every segment is done.
+            // Items travel packed as (low bits << 13 | position): one 8-byte LDS
+            // store and load per item per pass; the prefix is the segment's.
             const uint32_t npl = (low_bits + FBITS - 1) / FBITS;
+            const uint64_t lmask = low_bits >= 64 ? ~0ull : ((1ull << low_bits) - 1);
+#if defined(KMAN_ABL) && (KMAN_ABL & 8)
+            // ablation build only: no segment sort (wrong order, measures the rest)
+            for (uint32_t sg = s1; sg < s1; sg += FW) {
+#else
             for (uint32_t sg = s0 + w; sg < s1; sg += FW) {
+#endif
                 const uint32_t sa = lo + segstart[sg];
                 const uint32_t sz = lo + segstart[sg + 1] - sa;
                 if (sz < 2) continue;
-                uint64_t wk[WI];
-                uint32_t wp[WI];
+                const uint64_t pfx_hi = skey[sa] & ~lmask;
+                uint64_t pw[WI];
 #pragma unroll
                 for (int i = 0; i < WI; i++) {
+                    if ((uint32_t)(i * 64) >= sz) break;
                     const uint32_t p = (uint32_t)(i * 64 + lane);
-                    wk[i] = p < sz ? skey[sa + p] : 0;
-                    wp[i] = sa + p;
+                    pw[i] = p < sz ? ((skey[sa + p] & lmask) << 13) | (sa + p) : 0;
                 }
                 uint32_t at = 0;
                 for (uint32_t pp = 0; pp < npl; pp++) {
                     const uint32_t bw = (low_bits - at + (npl - pp) - 1) / (npl - pp);
-                    const uint32_t sh = at, dm = (1u << bw) - 1;
+                    const uint32_t sh = at + 13, dm = (1u << bw) - 1;
                     at += bw;
                     whist[w][lane] = 0;
                     whist[w][lane + 64] = 0;
@@ -290,8 +314,9 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
                     uint32_t r[WI], d[WI];
 #pragma unroll
                     for (int i = 0; i < WI; i++) {
+                        if ((uint32_t)(i * 64) >= sz) break;
                         const uint32_t p = (uint32_t)(i * 64 + lane);
-                        d[i] = (uint32_t)(wk[i] >> sh) & dm;
+                        d[i] = (uint32_t)(pw[i] >> sh) & dm;
                         if (ATOMIC) {
                             r[i] = p < sz ? atomicAdd(&whist[w][d[i]], 1u) : 0u;
                         } else {
@@ -316,24 +341,28 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
                     whist[w][2 * lane] = inc - c0 - c1;
                     whist[w][2 * lane + 1] = inc - c1;
                     __builtin_amdgcn_wave_barrier();
+                    const bool last_pass = pp + 1 == npl;
 #pragma unroll
                     for (int i = 0; i < WI; i++) {
+                        if ((uint32_t)(i * 64) >= sz) break;
                         const uint32_t p = (uint32_t)(i * 64 + lane);
                         if (p < sz) {
                             const uint32_t dst = sa + whist[w][d[i]] + r[i];
-                            skey[dst] = wk[i];
-                            spk[dst] = wp[i];
+                            if (last_pass) {
+                                skey[dst] = pfx_hi | (pw[i] >> 13);
+                                spk[dst] = (uint32_t)(pw[i] & 8191u);
+                            } else {
+                                skey[dst] = pw[i];
+                            }
                         }
                     }
                     __builtin_amdgcn_wave_barrier();
-                    if (pp + 1 < npl) {
+                    if (!last_pass) {
 #pragma unroll
                         for (int i = 0; i < WI; i++) {
+                            if ((uint32_t)(i * 64) >= sz) break;
                             const uint32_t p = (uint32_t)(i * 64 + lane);
-                            if (p < sz) {
-                                wk[i] = skey[sa + p];
-                                wp[i] = spk[sa + p];
-                            }
+                            if (p < sz) pw[i] = skey[sa + p];
                         }
                         __builtin_amdgcn_wave_barrier();
                     }
@@ -770,6 +799,12 @@ int finish_typed(kman_ctx *ctx, uint64_t *keys, uint64_t *keys_alt, V *vals, V *
 #if defined(KMAN_ABL) && (KMAN_ABL & 4)
 extern "C" int kman_debug_set_finish(kman_ctx *ctx, void *dptr) {
     HIP_TRY(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_fdbg), &dptr, sizeof(dptr)));
+    unsigned long long z[4] = {0, 0, 0, 0};
+    HIP_TRY(ctx, hipMemcpyToSymbol(HIP_SYMBOL(g_fstat), z, sizeof(z)));
+    return KMAN_OK;
+}
+extern "C" int kman_debug_finish_stats(kman_ctx *ctx, unsigned long long *out4) {
+    HIP_TRY(ctx, hipMemcpyFromSymbol(out4, HIP_SYMBOL(g_fstat), 4 * sizeof(unsigned long long)));
     return KMAN_OK;
 }
 #endif

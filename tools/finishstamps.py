@@ -53,5 +53,8 @@ for i, nm in enumerate(names):
     print("%-20s p10 %7.0f  p50 %7.0f  p90 %7.0f  p99 %8.0f ns" % (nm, *q))
 tot = (s[:, 6] - s[:, 0]) * 10.0
 print("%-20s p10 %7.0f  p50 %7.0f  p90 %7.0f  p99 %8.0f ns" % ("chunk total", *np.percentile(tot, [10, 50, 90, 99])))
+st = (ctypes.c_ulonglong * 4)()
+L.kman_debug_finish_stats(dev.ctx, st)
+print("wave-path chunks %d, block-path chunks %d, segments %d, sorted keys %d" % tuple(st))
 mid = (s[:, 0].min() + s[:, 6].max()) // 2
 print("chunks in flight at mid-kernel: %d" % int(((s[:, 0] <= mid) & (s[:, 6] >= mid)).sum()))
