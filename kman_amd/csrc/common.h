@@ -147,53 +147,34 @@ KMAN_DEV T shfl_any(T v, int src) {
     return r;
 }
 
-// DPP move of a 4- or 8-byte value; lanes without a source (or in rows outside
-// row_mask) read `fill`
+// DPP move of a value made of 32-bit words; lanes without a source (or in
+// rows outside row_mask) read `fill`
 template <int CTRL, int ROWMASK, typename T>
 KMAN_DEV T dpp_move(T v, T fill) {
-    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "32/64-bit");
-    if constexpr (sizeof(T) == 4) {
-        int x, f;
-        memcpy(&x, &v, 4);
-        memcpy(&f, &fill, 4);
-        const int r = __builtin_amdgcn_update_dpp(f, x, CTRL, ROWMASK, 0xf, false);
-        T o;
-        memcpy(&o, &r, 4);
-        return o;
-    } else {
-        int x[2], f[2], r[2];
-        memcpy(x, &v, 8);
-        memcpy(f, &fill, 8);
-        r[0] = __builtin_amdgcn_update_dpp(f[0], x[0], CTRL, ROWMASK, 0xf, false);
-        r[1] = __builtin_amdgcn_update_dpp(f[1], x[1], CTRL, ROWMASK, 0xf, false);
-        T o;
-        memcpy(&o, r, 8);
-        return o;
-    }
+    static_assert(sizeof(T) % 4 == 0, "32-bit granular");
+    constexpr int W = sizeof(T) / 4;
+    int x[W], f[W], r[W];
+    memcpy(x, &v, sizeof(T));
+    memcpy(f, &fill, sizeof(T));
+#pragma unroll
+    for (int i = 0; i < W; i++) r[i] = __builtin_amdgcn_update_dpp(f[i], x[i], CTRL, ROWMASK, 0xf, false);
+    T o;
+    memcpy(&o, r, sizeof(T));
+    return o;
 }
 
 // Inclusive scan across the 64 lanes; op(a, b) with a the earlier element,
-// `identity` its identity.  4/8-byte values scan with DPP alone (row_shr
-// 1/2/4/8, row_bcast 15/31: no LDS traffic); larger ones with shuffles.
+// `identity` its identity (op need not commute).  DPP only: row_shr 1/2/4/8
+// inside rows of 16, then row_bcast 15 / 31 across rows; no LDS traffic.
 template <typename T, typename Op>
 KMAN_DEV T wave_inclusive_scan(T v, Op op, T identity) {
-    if constexpr (sizeof(T) == 4 || sizeof(T) == 8) {
-        v = op(dpp_move<0x111, 0xf>(v, identity), v);
-        v = op(dpp_move<0x112, 0xf>(v, identity), v);
-        v = op(dpp_move<0x114, 0xf>(v, identity), v);
-        v = op(dpp_move<0x118, 0xf>(v, identity), v);
-        v = op(dpp_move<0x142, 0xa>(v, identity), v);
-        v = op(dpp_move<0x143, 0xc>(v, identity), v);
-        return v;
-    } else {
-        const int lane = lane_id();
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            T o = shfl_up_any(v, d);
-            if (lane >= d) v = op(o, v);
-        }
-        return v;
-    }
+    v = op(dpp_move<0x111, 0xf>(v, identity), v);
+    v = op(dpp_move<0x112, 0xf>(v, identity), v);
+    v = op(dpp_move<0x114, 0xf>(v, identity), v);
+    v = op(dpp_move<0x118, 0xf>(v, identity), v);
+    v = op(dpp_move<0x142, 0xa>(v, identity), v);
+    v = op(dpp_move<0x143, 0xc>(v, identity), v);
+    return v;
 }
 
 template <typename T, typename Op>
@@ -204,12 +185,7 @@ KMAN_DEV T wave_inclusive_scan(T v, Op op) {
 // the previous lane's value (lane 0: fill), DPP wave_shr:1
 template <typename T>
 KMAN_DEV T wave_shr1(T v, T fill) {
-    if constexpr (sizeof(T) == 4 || sizeof(T) == 8) {
-        return dpp_move<0x138, 0xf>(v, fill);
-    } else {
-        T o = shfl_up_any(v, 1);
-        return lane_id() ? o : fill;
-    }
+    return dpp_move<0x138, 0xf>(v, fill);
 }
 
 // Exclusive block scan for NT threads (NT multiple of 64, <= 1024).

@@ -119,10 +119,18 @@ __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__
         const uint32_t cnt = __popc(valid) * (RC && !CANON ? 2 : 1);
         uint32_t total;
         const uint32_t loff = block_exclusive_scan<ET>(cnt, SumU32(), 0u, lds_scan, &total);
+#if defined(KMAN_ABL) && (KMAN_ABL & 32)
+        // ablation build only: no look-back (wrong offsets, measures the rest)
+        if (threadIdx.x == 0) {
+            lds_base = tb;
+            st_store(&status[tile], st_make(ST_INCL, epoch, tb + total));
+        }
+#else
         if (threadIdx.x < 64) {
             const uint64_t b = wave_lookback<0>(status, tile, total, epoch, err);
             if (threadIdx.x == 0) lds_base = b;
         }
+#endif
         // stage keys at compacted offsets
         {
             uint32_t o = loff;
@@ -139,7 +147,11 @@ __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__
         for (uint32_t q = threadIdx.x; q < total; q += ET) {
             const uint64_t key = skeys[q];
             keys[base + q] = key;
+#if defined(KMAN_ABL) && (KMAN_ABL & 64)
+            if (false) {
+#else
             if (hist) {
+#endif
                 for (int p = 0; p < plan.npass; p++) {
                     const uint32_t d = (uint32_t)(key >> plan.shift[p]) & ((1u << plan.bits[p]) - 1);
                     atomicAdd(&lhist[p][d], 1u);

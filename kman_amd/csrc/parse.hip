@@ -17,7 +17,7 @@
 //   PRE (no header seen yet) / HDR (inside a header line) / SEQ (sequence line)
 // whose per-chunk summary is a transformer "incoming state -> (outgoing state,
 // kept chars)"; transformers compose associatively, so the whole file is
-// parsed with a reduce -> scan -> downsweep over 16 KiB tiles.  (b) is resolved
+// parsed with a reduce -> two-level scan -> downsweep over 16 KiB tiles.  (b) is resolved
 // right-to-left inside each thread's 64-byte chunk plus, only when a chunk
 // ends inside a whitespace run, a forward probe past the chunk.
 //
@@ -30,7 +30,7 @@ namespace {
 constexpr int PT = 256;           // threads per tile
 constexpr int PB = 64;            // bytes per thread
 constexpr int PTILE = PT * PB;    // 16 KiB per tile
-constexpr int SCAN_T = 1024;      // threads of the single-block tile scan
+constexpr int SCAN_T = 1024;      // tiles per block of the two-level tile scan
 constexpr uint32_t XF_ID_OUTS = 0u | (1u << 2) | (2u << 4);
 
 enum : uint32_t { S_PRE = 0, S_HDR = 1, S_SEQ = 2 };
@@ -50,7 +50,6 @@ struct TileIn {  // concrete state entering a tile
     uint64_t kept;
     uint64_t nhdr;
     uint32_t state;
-    uint32_t pad;
 };
 
 KMAN_DEV uint32_t xf_out(uint32_t outs, uint32_t s) { return (outs >> (2 * s)) & 3u; }
@@ -93,15 +92,6 @@ KMAN_DEV bool is_term(uint32_t c) { return c == '\n' || c == '\r'; }
 KMAN_DEV bool py_space(uint32_t c) { return c == ' ' || (c >= 9 && c <= 13) || (c >= 0x1c && c <= 0x1f); }
 // whitespace that is kept unless it is trailing (terminators and ' ' never kept)
 KMAN_DEV bool exotic_ws(uint32_t c) { return c == 9 || c == 11 || c == 12 || (c >= 0x1c && c <= 0x1f); }
-KMAN_DEV uint8_t base_code(uint32_t c) {
-    switch (c | 0x20u) {  // case-insensitive for letters
-        case 'a': return 0;
-        case 'c': return 1;
-        case 'g': return 2;
-        case 't': return 3;
-        default: return 4;
-    }
-}
 
 // A thread's 64-byte chunk of the text, reduced to bit masks (bit i = byte i).
 // Bytes are kept in 16 registers and only ever indexed at compile time.
@@ -115,6 +105,24 @@ struct Chunk {
 };
 
 KMAN_DEV uint32_t byte_at(const uint32_t (&w)[PB / 4], int i) { return (w[i >> 2] >> (8 * (i & 3))) & 0xffu; }
+
+// SWAR byte tests on 4 packed bytes: 0x80 in every byte equal to zero
+KMAN_DEV uint32_t zero_bytes(uint32_t t) { return ~(((t & 0x7f7f7f7fu) + 0x7f7f7f7fu) | t | 0x7f7f7f7fu); }
+KMAN_DEV uint32_t eq_bytes(uint32_t w, uint32_t c) { return zero_bytes(w ^ (c * 0x01010101u)); }
+// the 0x80 bits of four bytes -> a 4-bit mask
+KMAN_DEV uint32_t hibits4(uint32_t m) {
+    m >>= 7;
+    return (m | (m >> 7) | (m >> 14) | (m >> 21)) & 0xfu;
+}
+// base codes of four bytes (A/a 0, C/c 1, G/g 2, T/t 3, else 4): (c >> 1) & 3
+// maps A C T G to 0 1 2 3, x ^ (x >> 1) swaps the last two
+KMAN_DEV uint32_t codes4(uint32_t w) {
+    const uint32_t x = (w >> 1) & 0x03030303u;
+    const uint32_t code = x ^ ((x >> 1) & 0x01010101u);
+    const uint32_t y = w | 0x20202020u;
+    const uint32_t ok = eq_bytes(y, 'a') | eq_bytes(y, 'c') | eq_bytes(y, 'g') | eq_bytes(y, 't');
+    return (code & ((ok >> 7) * 3u)) | ((~ok & 0x80808080u) >> 5);
+}
 KMAN_DEV uint64_t bits_from(int i) { return i >= 64 ? 0ull : (~0ull << i); }
 KMAN_DEV uint64_t bits_below(int i) { return i >= 64 ? ~0ull : ((1ull << i) - 1); }
 
@@ -145,6 +153,28 @@ KMAN_DEV void load_chunk(const uint8_t *text, uint64_t n, uint64_t pos, Chunk &c
     // position 0 starts a line; a chunk wholly past the end reads nothing (its
     // byte before may lie past the allocation)
     const uint32_t prev = pos == 0 ? '\n' : (pos <= n ? text[pos - 1] : 0u);
+    if (ch.cnt == PB) {
+        // fast path (plain sequence text): no byte below 0x21 except '\n' and
+        // no '>'; then only newlines matter and every other byte is content
+        uint32_t spec = 0;
+        uint64_t nl = 0;
+#pragma unroll
+        for (int v = 0; v < PB / 4; v++) {
+            const uint32_t w = ch.w[v];
+            const uint32_t znl = eq_bytes(w, '\n');
+            const uint32_t lt21 = ~((w & 0x7f7f7f7fu) + 0x5f5f5f5fu) & ~w & 0x80808080u;
+            spec |= (lt21 & ~znl) | eq_bytes(w, '>');
+            nl |= (uint64_t)hibits4(znl) << (4 * v);
+        }
+        if (!spec) {
+            const uint64_t ls0 = (prev == '\n' || (prev == '\r' && !(nl & 1ull))) ? 1ull : 0ull;
+            ch.ls = (nl << 1) | ls0;
+            ch.hls = 0;
+            ch.keep = ~nl;
+            ch.hdr = 0;
+            return;
+        }
+    }
     uint64_t keep = 0, ls = 0, gt = 0, exo = 0, term = 0, nonws = 0;
     uint32_t pc = prev;
 #pragma unroll
@@ -262,49 +292,57 @@ __global__ __launch_bounds__(PT) void parse_reduce(const uint8_t *__restrict__ t
     }
 }
 
-// Single block: turn per-tile transformers into concrete incoming states.
-__global__ __launch_bounds__(SCAN_T) void parse_scan(const Xf64 *__restrict__ tiles, uint64_t T,
-                                                     TileIn *__restrict__ tin, uint64_t *__restrict__ info) {
-    __shared__ Xf64 lds[SCAN_T / 64];
-    const uint64_t chunk = (T + SCAN_T - 1) / SCAN_T;
-    const uint64_t b = threadIdx.x * chunk;
-    const uint64_t e = b + chunk < T ? b + chunk : T;
+KMAN_DEV Xf64 xf64_id() {
     Xf64 id;
     id.outs = XF_ID_OUTS;
     id.pad = 0;
     id.kept[0] = id.kept[1] = id.kept[2] = 0;
     id.nhdr = 0;
-    Xf64 acc = id;
-    ComposeXf64 op;
-    for (uint64_t t = b; t < e; t++) acc = op(acc, tiles[t]);
+    return id;
+}
+
+// Tile scan, level 1: SCAN_T tiles per block -> each tile's exclusive prefix
+// inside its block, and the block's total.
+__global__ __launch_bounds__(SCAN_T) void parse_scan_blocks(const Xf64 *__restrict__ tiles, uint64_t T,
+                                                            Xf64 *__restrict__ local, Xf64 *__restrict__ btot) {
+    __shared__ Xf64 lds[SCAN_T / 64];
+    const uint64_t t = (uint64_t)blockIdx.x * SCAN_T + threadIdx.x;
+    const Xf64 id = xf64_id();
+    const Xf64 x = t < T ? tiles[t] : id;
     Xf64 tot;
-    Xf64 pre = block_exclusive_scan<SCAN_T>(acc, op, id, lds, &tot);
-    uint32_t s = xf_out(pre.outs, S_PRE);
-    uint64_t kept = pre.kept[S_PRE];
-    uint64_t nh = pre.nhdr;
-    for (uint64_t t = b; t < e; t++) {
-        TileIn ti;
-        ti.kept = kept;
-        ti.nhdr = nh;
-        ti.state = s;
-        ti.pad = 0;
-        tin[t] = ti;
-        const Xf64 x = tiles[t];
-        kept += s == 0 ? x.kept[0] : (s == 1 ? x.kept[1] : x.kept[2]);
-        nh += x.nhdr;
-        s = xf_out(x.outs, s);
+    const Xf64 ex = block_exclusive_scan<SCAN_T>(x, ComposeXf64(), id, lds, &tot);
+    if (t < T) local[t] = ex;
+    if (threadIdx.x == 0) btot[blockIdx.x] = tot;
+}
+
+// Level 2 (one block): exclusive prefixes of the block totals, and the file
+// totals (n_bases, n_records).
+__global__ __launch_bounds__(SCAN_T) void parse_scan_top(const Xf64 *__restrict__ btot, uint64_t NB,
+                                                         Xf64 *__restrict__ bpre, uint64_t *__restrict__ info) {
+    __shared__ Xf64 lds[SCAN_T / 64];
+    const Xf64 id = xf64_id();
+    ComposeXf64 op;
+    Xf64 carry = id;
+    for (uint64_t b0 = 0; b0 < NB; b0 += SCAN_T) {
+        const uint64_t b = b0 + threadIdx.x;
+        const Xf64 x = b < NB ? btot[b] : id;
+        Xf64 tot;
+        const Xf64 ex = block_exclusive_scan<SCAN_T>(x, op, id, lds, &tot);
+        if (b < NB) bpre[b] = op(carry, ex);
+        carry = op(carry, tot);
     }
     if (threadIdx.x == 0) {
-        info[0] = tot.kept[S_PRE];  // n_bases
-        info[1] = tot.nhdr;         // n_records
+        info[0] = carry.kept[S_PRE];  // n_bases
+        info[1] = carry.nhdr;         // n_records
     }
 }
 
 __global__ __launch_bounds__(PT) void parse_emit(const uint8_t *__restrict__ text, uint64_t n,
-                                                 const TileIn *__restrict__ tin, uint8_t *__restrict__ codes,
+                                                 const Xf64 *__restrict__ local, const Xf64 *__restrict__ bpre,
+                                                 uint8_t *__restrict__ codes,
                                                  uint64_t *__restrict__ rec_hdr, uint64_t *__restrict__ rec_seq) {
     __shared__ Xf lds[PT / 64];
-    __shared__ uint8_t stage[PTILE];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[PTILE + 32];
     const uint64_t pos = (uint64_t)blockIdx.x * PTILE + (uint64_t)threadIdx.x * PB;
     Chunk ch;
     load_chunk(text, n, pos, ch);
@@ -315,7 +353,14 @@ __global__ __launch_bounds__(PT) void parse_emit(const uint8_t *__restrict__ tex
     id.nhdr = 0;
     Xf tot;
     const Xf pre = block_exclusive_scan<PT>(x, ComposeXf(), id, lds, &tot);
-    const TileIn ti = tin[blockIdx.x];
+    // the concrete state entering this tile: the file prefix applied to PRE
+    TileIn ti;
+    {
+        const Xf64 p = ComposeXf64()(bpre[blockIdx.x / SCAN_T], local[blockIdx.x]);
+        ti.state = xf_out(p.outs, S_PRE);
+        ti.kept = p.kept[S_PRE];
+        ti.nhdr = p.nhdr;
+    }
     const uint32_t s = xf_out(pre.outs, ti.state);  // state entering this thread's chunk
     const uint32_t lk0 = ti.state == 0 ? pre.kept[0] : (ti.state == 1 ? pre.kept[1] : pre.kept[2]);        // tile-local kept offset of this thread
     const uint64_t nh0 = ti.nhdr + pre.nhdr;
@@ -331,14 +376,36 @@ __global__ __launch_bounds__(PT) void parse_emit(const uint8_t *__restrict__ tex
             nh++;
         }
     }
-    uint32_t lk = lk0;
+    // codes staged at the tile's output alignment, so LDS and HBM agree mod 16
+    const uint32_t al = (uint32_t)(ti.kept & 15u);
+    uint32_t cw[PB / 4];
 #pragma unroll
-    for (int i = 0; i < PB; i++) {
-        if ((em >> i) & 1ull) stage[lk++] = base_code(byte_at(ch.w, i));
+    for (int v = 0; v < PB / 4; v++) cw[v] = codes4(ch.w[v]);
+    uint32_t lk = al + lk0;
+    if (em == ~0ull) {
+#pragma unroll
+        for (int i = 0; i < PB; i++) stage[lk + i] = (uint8_t)byte_at(cw, i);
+    } else {
+#pragma unroll
+        for (int i = 0; i < PB; i++) {
+            if ((em >> i) & 1ull) stage[lk++] = (uint8_t)byte_at(cw, i);
+        }
     }
     __syncthreads();
-    uint8_t *dst = codes + ti.kept;
-    for (uint32_t q = threadIdx.x; q < tile_kept; q += PT) dst[q] = stage[q];
+    // [al, al + tile_kept) of stage -> codes + ti.kept: whole 16-byte words as
+    // vectors, the two partial end words (shared with the neighbour tiles) bytewise
+    uint8_t *dst = codes + (ti.kept - al);
+    const uint32_t end = al + tile_kept;
+    const uint32_t nwords = (end + 15) / 16;
+    for (uint32_t q = threadIdx.x; q < nwords; q += PT) {
+        const uint32_t b0 = q * 16;
+        if (b0 >= al && b0 + 16 <= end) {
+            *reinterpret_cast<uint4 *>(dst + b0) = *reinterpret_cast<const uint4 *>(stage + b0);
+        } else {
+            for (uint32_t b = b0; b < b0 + 16; b++)
+                if (b >= al && b < end) dst[b] = stage[b];
+        }
+    }
 }
 
 // bit 3 on the first code of every non-empty record
@@ -362,17 +429,22 @@ extern "C" int kman_parse_fasta(kman_ctx *ctx, const uint8_t *d_text, uint64_t n
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const uint64_t T = n_bytes ? ceil_div(n_bytes, PTILE) : 0;
     if (T == 0) return kman_fail(ctx, KMAN_EFORMAT, "premature end of file or empty file");
-    // scratch: tiles (Xf64) + tile-in + info
+    // scratch: tile transformers, their in-block prefixes, block totals and
+    // prefixes (Xf64 each), info
+    const uint64_t NB = ceil_div(T, (uint64_t)SCAN_T);
     const size_t xf_bytes = ((T * sizeof(Xf64)) + 255) & ~size_t(255);
-    const size_t ti_bytes = ((T * sizeof(TileIn)) + 255) & ~size_t(255);
+    const size_t nb_bytes = ((NB * sizeof(Xf64)) + 255) & ~size_t(255);
     void *scr;
-    KMAN_TRY(kman_scratch(ctx, xf_bytes + ti_bytes + 256, &scr));
+    KMAN_TRY(kman_scratch(ctx, 2 * xf_bytes + 2 * nb_bytes + 256, &scr));
     Xf64 *d_xf = (Xf64 *)scr;
-    TileIn *d_ti = (TileIn *)((char *)scr + xf_bytes);
-    uint64_t *d_info = (uint64_t *)((char *)scr + xf_bytes + ti_bytes);
+    Xf64 *d_local = (Xf64 *)((char *)scr + xf_bytes);
+    Xf64 *d_btot = (Xf64 *)((char *)scr + 2 * xf_bytes);
+    Xf64 *d_bpre = (Xf64 *)((char *)scr + 2 * xf_bytes + nb_bytes);
+    uint64_t *d_info = (uint64_t *)((char *)scr + 2 * xf_bytes + 2 * nb_bytes);
     { KTimer kt_(ctx, "parse");
     hipLaunchKernelGGL(parse_reduce, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf);
-    hipLaunchKernelGGL(parse_scan, dim3(1), dim3(SCAN_T), 0, ctx->stream, d_xf, T, d_ti, d_info); }
+    hipLaunchKernelGGL(parse_scan_blocks, dim3((uint32_t)NB), dim3(SCAN_T), 0, ctx->stream, d_xf, T, d_local, d_btot);
+    hipLaunchKernelGGL(parse_scan_top, dim3(1), dim3(SCAN_T), 0, ctx->stream, d_btot, NB, d_bpre, d_info); }
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small, d_info, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -383,7 +455,7 @@ extern "C" int kman_parse_fasta(kman_ctx *ctx, const uint8_t *d_text, uint64_t n
         return kman_fail(ctx, KMAN_ECAP, "record capacity %llu < %llu", (unsigned long long)rec_cap,
                          (unsigned long long)info->n_records);
     { KTimer kt_(ctx, "parse");
-    hipLaunchKernelGGL(parse_emit, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_ti, d_codes,
+    hipLaunchKernelGGL(parse_emit, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_local, d_bpre, d_codes,
                        d_rec_hdr, d_rec_seq);
     const uint64_t R = info->n_records;
     hipLaunchKernelGGL(mark_records, dim3((uint32_t)ceil_div(R, 256)), dim3(256), 0, ctx->stream, d_codes,

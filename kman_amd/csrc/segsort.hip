@@ -101,6 +101,104 @@ KMAN_DEV uint64_t run_end(const uint64_t *keys, uint64_t n, uint64_t from, uint6
     return lo;
 }
 
+// One wave sorts segments sg0, sg0 + FW, ... < sg1 of the staged range by their
+// low bits (stable LSD, 7-bit digits, the wave's own 128 counters).  Items travel
+// packed: IT = u32 holds (low bits << 10 | offset in the segment) when the low
+// bits fit in 22 (passes bounce through spk), IT = u64 holds (low bits << 13 |
+// position) (passes bounce through skey).  The last pass writes the full key to
+// skey and its original position to spk.
+template <typename IT, bool ATOMIC>
+KMAN_DEV void wave_sort_segments(uint64_t *skey, uint32_t *spk, uint32_t *wh, const uint32_t *segstart, uint32_t sg0,
+                                 uint32_t sg1, uint32_t lo, uint32_t low_bits) {
+    constexpr bool SMALL = sizeof(IT) == 4;
+    constexpr uint32_t PS = SMALL ? 10 : 13;  // position bits
+    const int lane = lane_id();
+    const uint32_t npl = (low_bits + FBITS - 1) / FBITS;
+    const uint64_t lmask = low_bits >= 64 ? ~0ull : ((1ull << low_bits) - 1);
+    for (uint32_t sg = sg0; sg < sg1; sg += FW) {
+        const uint32_t sa = lo + segstart[sg];
+        const uint32_t sz = lo + segstart[sg + 1] - sa;
+        if (sz < 2) continue;
+        const uint64_t pfx_hi = skey[sa] & ~lmask;
+        IT pw[WI];
+#pragma unroll
+        for (int i = 0; i < WI; i++) {
+            if ((uint32_t)(i * 64) >= sz) break;
+            const uint32_t p = (uint32_t)(i * 64 + lane);
+            pw[i] = p < sz ? (IT)(((skey[sa + p] & lmask) << PS) | (SMALL ? p : sa + p)) : (IT)0;
+        }
+        uint32_t at = 0;
+        for (uint32_t pp = 0; pp < npl; pp++) {
+            const uint32_t bw = (low_bits - at + (npl - pp) - 1) / (npl - pp);
+            const uint32_t sh = at + PS, dm = (1u << bw) - 1;
+            at += bw;
+            wh[lane] = 0;
+            wh[lane + 64] = 0;
+            __builtin_amdgcn_wave_barrier();
+            uint32_t r[WI], d[WI];
+#pragma unroll
+            for (int i = 0; i < WI; i++) {
+                if ((uint32_t)(i * 64) >= sz) break;
+                const uint32_t p = (uint32_t)(i * 64 + lane);
+                d[i] = (uint32_t)(pw[i] >> sh) & dm;
+                if (ATOMIC) {
+                    r[i] = p < sz ? atomicAdd(&wh[d[i]], 1u) : 0u;
+                } else {
+                    const bool valid = p < sz;
+                    uint64_t peers = __ballot(valid);
+                    for (uint32_t bb = 0; bb < bw; bb++) {
+                        const bool set = (d[i] >> bb) & 1u;
+                        const uint64_t mm = __ballot(set);
+                        peers &= set ? mm : ~mm;
+                    }
+                    uint32_t before = 0;
+                    if (valid) before = wh[d[i]];
+                    r[i] = before + (uint32_t)__popcll(peers & lanemask_lt());
+                    const int leader = __ffsll((unsigned long long)peers) - 1;
+                    if (valid && lane == leader) wh[d[i]] = before + (uint32_t)__popcll(peers);
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t c0 = wh[2 * lane], c1 = wh[2 * lane + 1];
+            const uint32_t inc = wave_inclusive_scan(c0 + c1, SumU32());
+            wh[2 * lane] = inc - c0 - c1;
+            wh[2 * lane + 1] = inc - c1;
+            __builtin_amdgcn_wave_barrier();
+            const bool last_pass = pp + 1 == npl;
+#pragma unroll
+            for (int i = 0; i < WI; i++) {
+                if ((uint32_t)(i * 64) >= sz) break;
+                const uint32_t p = (uint32_t)(i * 64 + lane);
+                if (p < sz) {
+                    const uint32_t dst = sa + wh[d[i]] + r[i];
+                    if (last_pass) {
+                        skey[dst] = pfx_hi | (uint64_t)(pw[i] >> PS);
+                        spk[dst] = SMALL ? sa + (uint32_t)(pw[i] & 1023u) : (uint32_t)(pw[i] & 8191u);
+                    } else if constexpr (SMALL) {
+                        spk[dst] = (uint32_t)pw[i];
+                    } else {
+                        skey[dst] = (uint64_t)pw[i];
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (!last_pass) {
+#pragma unroll
+                for (int i = 0; i < WI; i++) {
+                    if ((uint32_t)(i * 64) >= sz) break;
+                    const uint32_t p = (uint32_t)(i * 64 + lane);
+                    if (p < sz) {
+                        if constexpr (SMALL) pw[i] = (IT)spk[sa + p];
+                        else pw[i] = (IT)skey[sa + p];
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+    }
+}
+
 enum { M_SORT = 0, M_COUNT = 1, M_UNIQ = 2 };
 
 template <int MODE, typename V, typename O, bool ATOMIC>
@@ -272,7 +370,7 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
             __syncthreads();
             wave_path = s_maxseg == 0;
         }
-#if defined(KMAN_ABL) && (KMAN_ABL & 4)
+#if defined(KMAN_ABL) && (KMAN_ABL & 16)
         if (t == 0) {
             atomicAdd(&g_fstat[wave_path ? 0 : 1], 1ull);
             atomicAdd(&g_fstat[2], (unsigned long long)nsegs);
@@ -281,92 +379,16 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
 #endif
         if (wave_path) {
             // one wave per segment: stable LSD over the low bits with the
-            // wave's own counters; no block barrier until every segment is done.
-            // Items travel packed as (low bits << 13 | position): one 8-byte LDS
-            // store and load per item per pass; the prefix is the segment's.
-            const uint32_t npl = (low_bits + FBITS - 1) / FBITS;
-            const uint64_t lmask = low_bits >= 64 ? ~0ull : ((1ull << low_bits) - 1);
+            // wave's own counters; no block barrier until every segment is done
 #if defined(KMAN_ABL) && (KMAN_ABL & 8)
             // ablation build only: no segment sort (wrong order, measures the rest)
-            for (uint32_t sg = s1; sg < s1; sg += FW) {
-#else
-            for (uint32_t sg = s0 + w; sg < s1; sg += FW) {
+            if (false)
 #endif
-                const uint32_t sa = lo + segstart[sg];
-                const uint32_t sz = lo + segstart[sg + 1] - sa;
-                if (sz < 2) continue;
-                const uint64_t pfx_hi = skey[sa] & ~lmask;
-                uint64_t pw[WI];
-#pragma unroll
-                for (int i = 0; i < WI; i++) {
-                    if ((uint32_t)(i * 64) >= sz) break;
-                    const uint32_t p = (uint32_t)(i * 64 + lane);
-                    pw[i] = p < sz ? ((skey[sa + p] & lmask) << 13) | (sa + p) : 0;
-                }
-                uint32_t at = 0;
-                for (uint32_t pp = 0; pp < npl; pp++) {
-                    const uint32_t bw = (low_bits - at + (npl - pp) - 1) / (npl - pp);
-                    const uint32_t sh = at + 13, dm = (1u << bw) - 1;
-                    at += bw;
-                    whist[w][lane] = 0;
-                    whist[w][lane + 64] = 0;
-                    __builtin_amdgcn_wave_barrier();
-                    uint32_t r[WI], d[WI];
-#pragma unroll
-                    for (int i = 0; i < WI; i++) {
-                        if ((uint32_t)(i * 64) >= sz) break;
-                        const uint32_t p = (uint32_t)(i * 64 + lane);
-                        d[i] = (uint32_t)(pw[i] >> sh) & dm;
-                        if (ATOMIC) {
-                            r[i] = p < sz ? atomicAdd(&whist[w][d[i]], 1u) : 0u;
-                        } else {
-                            const bool valid = p < sz;
-                            uint64_t peers = __ballot(valid);
-                            for (uint32_t bb = 0; bb < bw; bb++) {
-                                const bool set = (d[i] >> bb) & 1u;
-                                const uint64_t mm = __ballot(set);
-                                peers &= set ? mm : ~mm;
-                            }
-                            uint32_t before = 0;
-                            if (valid) before = whist[w][d[i]];
-                            r[i] = before + (uint32_t)__popcll(peers & lanemask_lt());
-                            const int leader = __ffsll((unsigned long long)peers) - 1;
-                            if (valid && lane == leader) whist[w][d[i]] = before + (uint32_t)__popcll(peers);
-                            __builtin_amdgcn_wave_barrier();
-                        }
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    const uint32_t c0 = whist[w][2 * lane], c1 = whist[w][2 * lane + 1];
-                    const uint32_t inc = wave_inclusive_scan(c0 + c1, SumU32());
-                    whist[w][2 * lane] = inc - c0 - c1;
-                    whist[w][2 * lane + 1] = inc - c1;
-                    __builtin_amdgcn_wave_barrier();
-                    const bool last_pass = pp + 1 == npl;
-#pragma unroll
-                    for (int i = 0; i < WI; i++) {
-                        if ((uint32_t)(i * 64) >= sz) break;
-                        const uint32_t p = (uint32_t)(i * 64 + lane);
-                        if (p < sz) {
-                            const uint32_t dst = sa + whist[w][d[i]] + r[i];
-                            if (last_pass) {
-                                skey[dst] = pfx_hi | (pw[i] >> 13);
-                                spk[dst] = (uint32_t)(pw[i] & 8191u);
-                            } else {
-                                skey[dst] = pw[i];
-                            }
-                        }
-                    }
-                    __builtin_amdgcn_wave_barrier();
-                    if (!last_pass) {
-#pragma unroll
-                        for (int i = 0; i < WI; i++) {
-                            if ((uint32_t)(i * 64) >= sz) break;
-                            const uint32_t p = (uint32_t)(i * 64 + lane);
-                            if (p < sz) pw[i] = skey[sa + p];
-                        }
-                        __builtin_amdgcn_wave_barrier();
-                    }
-                }
+            {
+                if (low_bits <= 22)
+                    wave_sort_segments<uint32_t, ATOMIC>(skey, spk, whist[w], segstart, s0 + w, s1, lo, low_bits);
+                else
+                    wave_sort_segments<uint64_t, ATOMIC>(skey, spk, whist[w], segstart, s0 + w, s1, lo, low_bits);
             }
             __syncthreads();
         } else {

@@ -11,7 +11,8 @@ then:
                                                   (kman_partition, 1 onesweep pass)
 5. exchanges per-destination counts and then the keys (+ pos)
                                                   (kman_allgather_u64 + kman_alltoallv)
-6. sorts what it received and run-length groups it (kman_sort + kman_rle_*).
+6. sorts what it received by prefix and finishes it in LDS with the count / uniq
+   output (kman_sort_range + kman_finish).
 
 Rank r then holds the complete count/uniq result for its prefix range; the
 ranges are in rank order, so concatenating the ranks' outputs is the global
@@ -151,23 +152,21 @@ class DistPipeline:
                                            c_void_p(self.recv_pos.ptr), _u64p(recv), _u64p(recv_off), 8),
                     "alltoallv")
         self.n_recv = nrecv
-        # 6. local sort + RLE
+        # 6. local prefix sort + finish (segments sorted in LDS, count | uniq)
         res = c_int(0)
-        N.check(ctx, L.kman_sort(ctx, c_void_p(self.recv_keys.ptr), c_void_p(self.recv_alt.ptr),
-                                 c_void_p(self.recv_pos.ptr if vb else None),
-                                 c_void_p(self.recv_pos_alt.ptr if vb else None), vb, nrecv, 2 * self.k, None,
-                                 byref(res)), "kman_sort")
+        lo = engine.split_bits(nrecv, 2 * self.k)
+        rp = c_void_p(self.recv_pos.ptr if vb else None)
+        rpa = c_void_p(self.recv_pos_alt.ptr if vb else None)
+        N.check(ctx, L.kman_sort_range(ctx, c_void_p(self.recv_keys.ptr), c_void_p(self.recv_alt.ptr), rp, rpa, vb,
+                                       nrecv, lo, 2 * self.k, None, byref(res)), "kman_sort_range")
         self.sorted_in_alt = bool(res.value)
-        skeys = self.recv_alt if res.value else self.recv_keys
+        skeys, okeys = (self.recv_alt, self.recv_keys) if res.value else (self.recv_keys, self.recv_alt)
+        spos, opos = (rpa, rp) if res.value else (rp, rpa)
         out = c_uint64(0)
-        if self.mode == "count":
-            N.check(ctx, L.kman_rle_count(ctx, c_void_p(skeys.ptr), nrecv, c_void_p(self.out_keys.ptr),
-                                          c_void_p(self.out_vals.ptr), 8, byref(out)), "rle_count")
-        else:
-            spos = self.recv_pos_alt if res.value else self.recv_pos
-            N.check(ctx, L.kman_rle_uniq(ctx, c_void_p(skeys.ptr), c_void_p(spos.ptr), 8, nrecv,
-                                         c_void_p(self.out_keys.ptr), c_void_p(self.out_vals.ptr), byref(out)),
-                    "rle_uniq")
+        mode = N.KMAN_FINISH_COUNT if self.mode == "count" else N.KMAN_FINISH_UNIQ
+        N.check(ctx, L.kman_finish(ctx, c_void_p(skeys.ptr), c_void_p(okeys.ptr), spos, opos, vb, nrecv, 2 * self.k,
+                                   lo, mode, c_void_p(self.out_keys.ptr), c_void_p(self.out_vals.ptr), 8, byref(out)),
+                "kman_finish")
         self.n_out = int(out.value)
         return n
 
