@@ -6,8 +6,9 @@ Workload (BASELINE.json configs[1]): 1 GB synthetic FASTA (numpy PCG64 seed
 syn<i>), k=21, extract + radix sort + uniq (``kmer uniq``: keys and their
 pos payload) as one device batch.  A "step" is one full pass of the hot path
 over the FASTA bytes that are already resident in HBM:
-    parse -> extract -> prefix sort (3 onesweep digit passes over the top 21
-    key bits) -> finish (segments sorted in LDS + uniq, one pass)
+    parse -> k-mer digit histograms -> extraction fused with the first prefix
+    pass -> 2 more onesweep digit passes over the top 21 key bits -> finish
+    (segments sorted in LDS + uniq, one pass)
 leaving the (k-mer, header pos) result device-resident.  Text formatting and
 the file write are not part of the step (reported separately by the CLI).
 
@@ -138,8 +139,8 @@ def main() -> None:
     # live roofline of the dominant kernel (sort pass), from HIP events
     n_pass, pass_ms = pipe.timed("sort_pass")
     stages = {}
-    for tag in ("parse", "extract", "prefix_hist", "partition", "sort_hist", "sort_pass", "finish", "rle_count",
-                "rle_uniq"):
+    for tag in ("parse", "kmer_hist", "extract_pass", "extract", "prefix_hist", "partition", "sort_hist", "sort_pass",
+                "finish", "rle_count", "rle_uniq"):
         c, ms = pipe.timed(tag)
         if c:
             stages[tag] = round(ms / args.steps, 3)

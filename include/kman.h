@@ -172,6 +172,15 @@ int kman_sort_range(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, void 
  * the input arrays are scratch afterwards (segments longer than a chunk's
  * staging area are sorted in place through d_*_alt-free temporary buffers). */
 int kman_split_bits(uint64_t n, uint32_t key_bits, uint32_t *lo_bit);
+
+/* kman_extract + kman_sort_range(lo_bit, 2k) in one call: the first prefix
+ * pass is fused into the extraction (a histogram pre-pass over the codes, then
+ * one kernel that rolls the windows and scatters them by digit 0), so the
+ * keys are never written in stream order.  Same result as the two calls;
+ * flags as kman_extract's (KMAN_CANONICAL, k > 25 or u64 pos run the two calls). */
+int kman_extract_sorted(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                        uint32_t lo_bit, uint64_t *d_keys, uint64_t *d_keys_alt, void *d_pos, void *d_pos_alt,
+                        uint32_t pos_bytes, uint64_t cap, uint64_t *n_kmers, int *result_in_alt);
 int kman_finish(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, void *d_vals, void *d_vals_alt,
                 uint32_t val_bytes, uint64_t n, uint32_t key_bits, uint32_t lo_bit, int mode,
                 uint64_t *d_okeys, void *d_ovals, uint32_t oval_bytes, uint64_t *n_out);

@@ -84,6 +84,11 @@ SIGNATURES = {
          POINTER(c_int)],
     ),
     "kman_split_bits": (c_int, [c_uint64, c_uint32, POINTER(c_uint32)]),
+    "kman_extract_sorted": (
+        c_int,
+        [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
+         c_uint32, c_uint64, POINTER(c_uint64), POINTER(c_int)],
+    ),
     "kman_finish": (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_uint32, c_int,

@@ -22,6 +22,7 @@
 //
 // Algorithmic bytes: 1 B code read + 8 B key write (+ 4/8 B pos) per k-mer.
 #include "common.h"
+#include "kmer.h"
 
 namespace {
 
@@ -35,55 +36,6 @@ struct Plan {
 };
 
 struct NoPos {};
-
-template <int EI>
-KMAN_DEV void stage_codes(const uint8_t *__restrict__ codes, uint64_t n_bases, uint64_t tb, uint8_t *s) {
-    constexpr int BYTES = ET * EI + 64;
-    const uint64_t limit = n_bases + 64;  // padded region is valid memory, value 4
-    for (int v = threadIdx.x; v < BYTES / 16; v += ET) {
-        const uint64_t off = tb + (uint64_t)v * 16;
-        if (off + 16 <= limit) {
-            *reinterpret_cast<uint4 *>(s + v * 16) = *reinterpret_cast<const uint4 *>(codes + off);
-        } else {
-#pragma unroll
-            for (int b = 0; b < 16; b++) s[v * 16 + b] = (off + b < limit) ? codes[off + b] : 4;
-        }
-    }
-}
-
-// Roll the EI windows starting at s[base .. base+EI) (k from LDS bytes).
-template <int EI, bool CANON>
-KMAN_DEV uint32_t roll(const uint8_t *s, int base, int k, uint64_t mask, uint64_t p0, uint64_t n_bases,
-                       uint64_t (&kf)[EI], uint64_t (&kr)[EI]) {
-    uint64_t f = 0, r = 0;
-    uint32_t run = 0;
-    const int rsh = 2 * k - 2;
-    for (int q = 0; q < k - 1; q++) {
-        const uint32_t c = s[base + q];
-        run = (c & 8) ? 0 : run;
-        run = (c & 4) ? 0 : run + 1;
-        f = (f << 2) | (c & 3);
-        r = (r >> 2) | ((uint64_t)(3 - (c & 3)) << rsh);
-    }
-    uint32_t valid = 0;
-#pragma unroll
-    for (int j = 0; j < EI; j++) {
-        const uint32_t c = s[base + k - 1 + j];
-        run = (c & 8) ? 0 : run;
-        run = (c & 4) ? 0 : run + 1;
-        f = (f << 2) | (c & 3);
-        r = (r >> 2) | ((uint64_t)(3 - (c & 3)) << rsh);
-        const uint64_t fm = f & mask;
-        if (CANON) {
-            kf[j] = fm < r ? fm : r;
-        } else {
-            kf[j] = fm;
-            kr[j] = r;
-        }
-        valid |= (uint32_t)(run >= (uint32_t)k && p0 + j < n_bases) << j;
-    }
-    return valid;
-}
 
 template <int EI, bool RC, bool CANON, typename P>
 __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__ codes, uint64_t n_bases,
@@ -111,7 +63,7 @@ __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__
         const int64_t tile = grab_tile(counter, &lds_tile);
         if ((uint64_t)tile >= n_tiles) break;
         const uint64_t tb = (uint64_t)tile * TILE;
-        stage_codes<EI>(codes, n_bases, tb, scodes);
+        stage_codes<ET, EI>(codes, n_bases, tb, scodes);
         __syncthreads();
         uint64_t kf[EI], kr[EI];
         const uint64_t p0 = tb + (uint64_t)threadIdx.x * EI;
@@ -195,7 +147,7 @@ __global__ __launch_bounds__(ET) void count_kernel(const uint8_t *__restrict__ c
     uint64_t acc = 0;
     for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const uint64_t tb = tile * TILE;
-        stage_codes<EI>(codes, n_bases, tb, scodes);
+        stage_codes<ET, EI>(codes, n_bases, tb, scodes);
         __syncthreads();
         uint64_t kf[EI], kr[EI];
         const uint64_t p0 = tb + (uint64_t)threadIdx.x * EI;
@@ -205,6 +157,49 @@ __global__ __launch_bounds__(ET) void count_kernel(const uint8_t *__restrict__ c
     uint32_t tot;
     block_exclusive_scan<ET>((uint32_t)acc, SumU32(), 0u, lds_scan, &tot);
     if (threadIdx.x == 0 && tot) atomicAdd(out, (unsigned long long)tot);
+}
+
+// valid-window count and the radix-digit histograms of every pass of `plan`,
+// no keys written: the pre-pass of the fused extract + first sort pass
+// (kman_extract_sorted needs the global digit-0 counts before any key moves)
+template <int EI, bool RC>
+__global__ __launch_bounds__(ET) void kmer_hist_kernel(const uint8_t *__restrict__ codes, uint64_t n_bases,
+                                                       uint64_t n_tiles, int k, unsigned long long *__restrict__ count,
+                                                       uint64_t *__restrict__ hist, Plan plan) {
+    constexpr int TILE = ET * EI;
+    __shared__ __attribute__((aligned(16))) uint8_t scodes[TILE + 64];
+    __shared__ uint32_t lhist[MAXPASS][256];
+    __shared__ uint32_t lds_scan[ET / 64];
+    const uint64_t mask = k == 32 ? ~0ull : ((1ull << (2 * k)) - 1);
+    for (int i = threadIdx.x; i < MAXPASS * 256; i += ET) (&lhist[0][0])[i] = 0;
+    uint64_t acc = 0;
+    for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const uint64_t tb = tile * TILE;
+        stage_codes<ET, EI>(codes, n_bases, tb, scodes);
+        __syncthreads();
+        uint64_t kf[EI], kr[EI];
+        const uint64_t p0 = tb + (uint64_t)threadIdx.x * EI;
+        const uint32_t valid = roll<EI, false>(scodes, threadIdx.x * EI, k, mask, p0, n_bases, kf, kr);
+        acc += __popc(valid) * (RC ? 2 : 1);
+#pragma unroll
+        for (int j = 0; j < EI; j++) {
+            if ((valid >> j) & 1u) {
+                for (int p = 0; p < plan.npass; p++) {
+                    const uint32_t dm = (1u << plan.bits[p]) - 1;
+                    atomicAdd(&lhist[p][(uint32_t)(kf[j] >> plan.shift[p]) & dm], 1u);
+                    if (RC) atomicAdd(&lhist[p][(uint32_t)(kr[j] >> plan.shift[p]) & dm], 1u);
+                }
+            }
+        }
+        __syncthreads();
+    }
+    uint32_t tot;
+    block_exclusive_scan<ET>((uint32_t)acc, SumU32(), 0u, lds_scan, &tot);
+    if (threadIdx.x == 0 && tot) atomicAdd(count, (unsigned long long)tot);
+    for (int p = 0; p < plan.npass; p++) {
+        const uint32_t c = lhist[p][threadIdx.x];
+        if (c) atomicAdd((unsigned long long *)&hist[p * 256 + threadIdx.x], (unsigned long long)c);
+    }
 }
 
 int persistent_grid(kman_ctx *ctx, const void *fn, int threads, uint64_t n_tiles) {
@@ -310,4 +305,37 @@ extern "C" int kman_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_ba
     // the last tile's inclusive prefix is the number of k-mers written
     const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * ((flags & KMAN_RC) && !(flags & KMAN_CANONICAL) ? 8 : 16));
     return kman_lookback_total(ctx, n_tiles, n_kmers);
+}
+
+// pre-pass of kman_extract_sorted: n_kmers and d_hist (zeroed here) for the
+// passes over bits [lo_bit, 2k); flags: KMAN_RC only
+int kman_kmer_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                   uint32_t lo_bit, uint64_t *d_hist, uint64_t *n_kmers) {
+    Plan plan{};
+    uint32_t np, sh[MAXPASS], bi[MAXPASS];
+    KMAN_TRY(kman_sort_plan_range(lo_bit, 2 * k, &np, sh, bi));
+    plan.npass = (int)np;
+    for (uint32_t i = 0; i < np; i++) {
+        plan.shift[i] = (uint8_t)sh[i];
+        plan.bits[i] = (uint8_t)bi[i];
+    }
+    void *scr;
+    KMAN_TRY(kman_scratch(ctx, 256, &scr));
+    HIP_TRY(ctx, hipMemsetAsync(scr, 0, 8, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(d_hist, 0, MAXPASS * 256 * 8, ctx->stream));
+    const bool rc = flags & KMAN_RC;
+    const int EI = 16;
+    const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * EI);
+    auto fn = rc ? kmer_hist_kernel<16, true> : kmer_hist_kernel<16, false>;
+    const int grid = persistent_grid(ctx, (const void *)fn, ET, n_tiles);
+    {
+        KTimer kt_(ctx, "kmer_hist");
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(ET), 0, ctx->stream, d_codes, n_bases, n_tiles, (int)k,
+                           (unsigned long long *)scr, d_hist, plan);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small, scr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    *n_kmers = ctx->h_small[0];
+    return KMAN_OK;
 }

@@ -21,6 +21,7 @@
 // one histogram pass, so a pass reads and writes every key exactly once:
 // 16 B/key (+ 2x payload bytes) — the figure the roofline is quoted against.
 #include "common.h"
+#include "kmer.h"
 
 namespace {
 
@@ -363,6 +364,180 @@ __global__ __launch_bounds__(NT, MINW) void onesweep_pass(const uint64_t *__rest
     STAMP(5);
 }
 
+
+// ---------------------------------------------------------------------------
+// Fused k-mer extraction + first prefix pass (kman_extract_sorted).
+// A tile of NT*EI window starts is rolled into keys exactly like extract.hip
+// (stream order: window, then '+' before '-' with -r), the valid keys are
+// compacted into LDS in stream order with their tile-local (window << 1 |
+// strand) packed above the 2k key bits, and the tile then runs the onesweep
+// body on digit 0: stable rank, early digit counts, grouped look-back,
+// LDS-staged coalesced scatter.  The keys never exist in stream order in HBM:
+// 1 B code read + the pass's 8 B key + payload writes per k-mer.
+constexpr int XT = 512;
+
+template <int EI, bool RC, typename V, bool ATOMIC>
+__global__ __launch_bounds__(XT) void extract_pass(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
+                                                   uint64_t *__restrict__ kout, V *__restrict__ vout, uint32_t shift,
+                                                   uint32_t bits, const uint64_t *__restrict__ bucket_base,
+                                                   uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
+                                                   uint32_t epoch, uint32_t *__restrict__ err) {
+    constexpr int NT = XT;
+    constexpr int NWAVE = NT / 64;
+    constexpr int WIN = NT * EI;          // window starts per tile
+    constexpr int TILE = WIN * (RC ? 2 : 1);  // keys per tile, at most
+    constexpr int SI = TILE / NT;
+    constexpr bool HAS_V = !std::is_same<V, NoVal>::value;
+    static_assert(WIN + 64 <= TILE * 8, "codes fit in the key staging area");
+    __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
+    __shared__ uint32_t whist[NWAVE][RADIX];
+    __shared__ uint32_t thist[RADIX];
+    __shared__ uint32_t lstart[RADIX];
+    __shared__ uint64_t gstart[RADIX];
+    __shared__ uint32_t lds_scan[NWAVE];
+    __shared__ uint32_t lds_tile;
+
+    const int64_t tile = grab_tile(counter, &lds_tile);
+    const int lane = lane_id();
+    const int w = threadIdx.x >> 6;
+    const uint32_t radix = 1u << bits;
+    const uint32_t dmask = radix - 1;
+    const uint32_t kb = 2u * (uint32_t)k;
+    const uint64_t keymask = kb >= 64 ? ~0ull : ((1ull << kb) - 1);
+    const uint64_t wb = (uint64_t)tile * WIN;
+    uint8_t *scodes = reinterpret_cast<uint8_t *>(skeys);
+    stage_codes<NT, EI>(codes, n_bases, wb, scodes);
+    for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&whist[0][0])[i] = 0;
+    if (threadIdx.x < RADIX) thist[threadIdx.x] = 0;
+    __syncthreads();
+
+    // roll this thread's EI windows; compact the valid keys in stream order
+    uint64_t kf[EI], kr[EI];
+    const uint32_t w0 = threadIdx.x * EI;
+    const uint32_t valid = roll<EI, false>(scodes, w0, k, keymask, wb + w0, n_bases, kf, kr);
+    uint32_t tcnt;
+    const uint32_t off = block_exclusive_scan<NT>((uint32_t)__popc(valid) * (RC ? 2u : 1u), SumU32(), 0u, lds_scan,
+                                                  &tcnt);
+    {
+        // (the scan's barriers ordered every read of the codes before this)
+        uint32_t o = off;
+#pragma unroll
+        for (int j = 0; j < EI; j++) {
+            if ((valid >> j) & 1u) {
+                const uint64_t tag = (uint64_t)((w0 + j) << 1) << kb;
+                skeys[o++] = kf[j] | tag;
+                if (RC) skeys[o++] = kr[j] | tag | (1ull << kb);
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- the onesweep body on digit 0 (items wave-striped, stream order)
+    const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
+    uint64_t key[SI];
+    uint32_t rank[SI];
+#pragma unroll
+    for (int i = 0; i < SI; i++) key[i] = ib + i * 64 < tcnt ? skeys[ib + i * 64] : 0;
+#define XDIGIT(x) ((uint32_t)((x) >> shift) & dmask)
+    if (ATOMIC) {
+#pragma unroll
+        for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&whist[w][XDIGIT(key[i])], 1u) : 0u;
+        __syncthreads();
+        if (threadIdx.x < radix) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int ww = 0; ww < NWAVE; ww++) c += whist[ww][threadIdx.x];
+            thist[threadIdx.x] = c;
+            digit_publish(status + threadIdx.x, tile, c, epoch);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < SI; i++)
+            if (ib + i * 64 < tcnt) atomicAdd(&thist[XDIGIT(key[i])], 1u);
+        __syncthreads();
+        if (threadIdx.x < radix) digit_publish(status + threadIdx.x, tile, thist[threadIdx.x], epoch);
+#pragma unroll
+        for (int i = 0; i < SI; i++) {
+            const bool valid_i = ib + i * 64 < tcnt;
+            const uint32_t d = XDIGIT(key[i]);
+            uint64_t peers = __ballot(valid_i);
+            for (uint32_t b = 0; b < bits; b++) {
+                const bool set = (d >> b) & 1u;
+                const uint64_t m = __ballot(set);
+                peers &= set ? m : ~m;
+            }
+            uint32_t before = 0;
+            if (valid_i) before = whist[w][d];
+            rank[i] = before + (uint32_t)__popcll(peers & lanemask_lt());
+            const int leader = __ffsll((unsigned long long)peers) - 1;
+            if (valid_i && lane == leader) whist[w][d] = before + (uint32_t)__popcll(peers);
+        }
+    }
+    __syncthreads();
+    const uint32_t d0 = threadIdx.x;
+    uint32_t tot = 0;
+    if (d0 < RADIX) {
+#pragma unroll
+        for (int ww = 0; ww < NWAVE; ww++) {
+            const uint32_t c = whist[ww][d0];
+            whist[ww][d0] = tot;
+            tot += c;
+        }
+    }
+    const uint32_t ls = block_exclusive_scan<NT>(tot, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
+    if (d0 < RADIX) lstart[d0] = ls;
+    __syncthreads();
+    {
+        const uint32_t tpd = NT / radix >= 4 ? 4 : (NT / radix >= 2 ? 2 : 1);
+        if (threadIdx.x < radix * tpd) {
+            const uint32_t d = threadIdx.x / tpd;
+            uint64_t excl;
+            if (tpd == 4) excl = group_lookback<4>(status + d, tile, thist[d], epoch, err);
+            else if (tpd == 2) excl = group_lookback<2>(status + d, tile, thist[d], epoch, err);
+            else excl = group_lookback<1>(status + d, tile, thist[d], epoch, err);
+            if (threadIdx.x % tpd == 0) gstart[d] = bucket_base[d] + excl - lstart[d];
+        }
+    }
+    __syncthreads();
+    uint32_t lp[SI];
+#pragma unroll
+    for (int i = 0; i < SI; i++) {
+        const bool valid_i = ib + i * 64 < tcnt;
+        const uint32_t d = XDIGIT(key[i]);
+        lp[i] = valid_i ? lstart[d] + whist[w][d] + rank[i] : 0xffffffffu;
+        if (valid_i) skeys[lp[i]] = key[i];
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < tcnt; q += NT) {
+        const uint64_t kk = skeys[q];
+        kout[gstart[XDIGIT(kk)] + q] = kk & keymask;
+    }
+    if constexpr (HAS_V) {
+        uint8_t dq[(TILE + NT - 1) / NT];
+#pragma unroll
+        for (int r = 0; r < (TILE + NT - 1) / NT; r++) {
+            const uint32_t q = threadIdx.x + r * NT;
+            dq[r] = q < tcnt ? (uint8_t)XDIGIT(skeys[q]) : 0;
+        }
+        __syncthreads();
+        V *sval = reinterpret_cast<V *>(skeys);
+#pragma unroll
+        for (int i = 0; i < SI; i++) {
+            if (lp[i] != 0xffffffffu) {
+                const uint64_t f = key[i] >> kb;  // (window << 1 | strand)
+                sval[lp[i]] = (V)(((wb + (f >> 1)) << 1) | (f & 1u));
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < (TILE + NT - 1) / NT; r++) {
+            const uint32_t q = threadIdx.x + r * NT;
+            if (q < tcnt) vout[gstart[dq[r]] + q] = sval[q];
+        }
+    }
+#undef XDIGIT
+}
+
 __global__ __launch_bounds__(256) void histogram_kernel(const uint64_t *__restrict__ keys, uint64_t n, int npass,
                                                         const uint32_t *__restrict__ shift_bits,
                                                         unsigned long long *__restrict__ hist) {
@@ -588,5 +763,99 @@ extern "C" int kman_partition(kman_ctx *ctx, const uint64_t *d_keys, uint64_t *d
         KMAN_TRY(launch_partition<uint64_t>(ctx, d_keys, d_keys_out, (const uint64_t *)d_vals, (uint64_t *)d_vals_out,
                                             n, d_lut, lut_shift, bits, d_base));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return kman_check_device_error(ctx);
+}
+
+namespace {
+template <int EI, bool RC, typename V>
+int launch_extract_pass(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, uint32_t k, uint64_t *kout, V *vout,
+                        uint32_t shift, uint32_t bits, const uint64_t *d_base) {
+    const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)XT * EI);
+    uint32_t epoch, *counter;
+    KMAN_TRY(kman_lookback_begin(ctx, n_tiles * RADIX, &epoch, &counter));
+    KTimer kt_(ctx, "extract_pass");
+    if (ctx->lds_atomic_ordered)
+        hipLaunchKernelGGL((extract_pass<EI, RC, V, true>), dim3((uint32_t)n_tiles), dim3(XT), 0, ctx->stream, codes,
+                           n_bases, (int)k, kout, vout, shift, bits, d_base, ctx->d_status, counter, epoch, ctx->d_err);
+    else
+        hipLaunchKernelGGL((extract_pass<EI, RC, V, false>), dim3((uint32_t)n_tiles), dim3(XT), 0, ctx->stream, codes,
+                           n_bases, (int)k, kout, vout, shift, bits, d_base, ctx->d_status, counter, epoch, ctx->d_err);
+    HIP_TRY(ctx, hipGetLastError());
+    return KMAN_OK;
+}
+}  // namespace
+
+extern "C" int kman_extract_sorted(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                                   uint32_t lo_bit, uint64_t *d_keys, uint64_t *d_keys_alt, void *d_pos,
+                                   void *d_pos_alt, uint32_t pos_bytes, uint64_t cap, uint64_t *n_kmers,
+                                   int *result_in_alt) {
+    if (!ctx || !n_kmers || !result_in_alt) return KMAN_EINVAL;
+    *n_kmers = 0;
+    *result_in_alt = 0;
+    if (k < 2 || k > 32) return kman_fail(ctx, KMAN_EINVAL, "k must be in [2, 32] on the GPU path, got %u", k);
+    if (lo_bit > 2 * k) return kman_fail(ctx, KMAN_EINVAL, "low bit %u > 2k", lo_bit);
+    const bool want_pos = flags & KMAN_WANT_POS;
+    if (want_pos && pos_bytes != 4 && pos_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "pos_bytes must be 4 or 8");
+    if (want_pos && pos_bytes == 4 && (n_bases << 1) > 0xffffffffull)
+        return kman_fail(ctx, KMAN_EINVAL, "u32 pos payload cannot address %llu bases", (unsigned long long)n_bases);
+    if (!d_keys || !d_keys_alt || (want_pos && (!d_pos || !d_pos_alt)))
+        return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (n_bases == 0) return KMAN_OK;
+    const uint32_t vb = want_pos ? pos_bytes : 0;
+    uint64_t *d_hist;
+    KMAN_TRY(kman_aux(ctx, MAXPASS * RADIX * 8, (void **)&d_hist));
+    // the fused path: forward / -r keys of k <= 25 (the tile-local window index
+    // rides in the 14 bits above the key), u32 or no payload
+    const bool fused = !(flags & KMAN_CANONICAL) && k <= 25 && lo_bit < 2 * k && vb != 8;
+    if (!fused) {
+        HIP_TRY(ctx, hipMemsetAsync(d_hist, 0, MAXPASS * RADIX * 8, ctx->stream));
+        uint64_t n;
+        KMAN_TRY(kman_extract(ctx, d_codes, n_bases, k, flags | KMAN_HIST_LO(lo_bit), d_keys, d_pos, pos_bytes, cap,
+                              d_hist, &n));
+        *n_kmers = n;
+        return kman_sort_range(ctx, d_keys, d_keys_alt, d_pos, d_pos_alt, vb, n, lo_bit, 2 * k, d_hist,
+                               result_in_alt);
+    }
+    const bool rc = flags & KMAN_RC;
+    uint64_t n;
+    KMAN_TRY(kman_kmer_hist(ctx, d_codes, n_bases, k, rc ? KMAN_RC : 0u, lo_bit, d_hist, &n));
+    if (n > cap)
+        return kman_fail(ctx, KMAN_ECAP, "key capacity %llu < %llu", (unsigned long long)cap, (unsigned long long)n);
+    *n_kmers = n;
+    if (n == 0) return KMAN_OK;
+    uint32_t np, sh[MAXPASS], bi[MAXPASS];
+    KMAN_TRY(kman_sort_plan_range(lo_bit, 2 * k, &np, sh, bi));
+    static thread_local uint64_t h_hist[MAXPASS * RADIX];
+    static thread_local uint64_t h_base[RADIX];
+    HIP_TRY(ctx, hipMemcpyAsync(h_hist, d_hist, np * RADIX * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    uint64_t acc = 0;
+    for (int d = 0; d < RADIX; d++) {
+        h_base[d] = acc;
+        acc += h_hist[d];
+    }
+    if (acc != n) return kman_fail(ctx, KMAN_EINVAL, "digit histogram sums to %llu, expected %llu",
+                                   (unsigned long long)acc, (unsigned long long)n);
+    void *scr;
+    KMAN_TRY(kman_scratch(ctx, RADIX * 8, &scr));
+    HIP_TRY(ctx, hipMemcpyAsync(scr, h_base, RADIX * 8, hipMemcpyHostToDevice, ctx->stream));
+    if (rc) {
+        if (vb) KMAN_TRY((launch_extract_pass<8, true, uint32_t>(ctx, d_codes, n_bases, k, d_keys, (uint32_t *)d_pos,
+                                                                sh[0], bi[0], (const uint64_t *)scr)));
+        else KMAN_TRY((launch_extract_pass<8, true, NoVal>(ctx, d_codes, n_bases, k, d_keys, nullptr, sh[0], bi[0],
+                                                           (const uint64_t *)scr)));
+    } else {
+        if (vb) KMAN_TRY((launch_extract_pass<16, false, uint32_t>(ctx, d_codes, n_bases, k, d_keys,
+                                                                  (uint32_t *)d_pos, sh[0], bi[0],
+                                                                  (const uint64_t *)scr)));
+        else KMAN_TRY((launch_extract_pass<16, false, NoVal>(ctx, d_codes, n_bases, k, d_keys, nullptr, sh[0], bi[0],
+                                                             (const uint64_t *)scr)));
+    }
+    // the remaining prefix passes, ping-ponging from the pass-0 output
+    if (np > 1) {
+        KMAN_TRY((dispatch_vals<512, 16>(ctx, d_keys, d_keys_alt, d_pos, d_pos_alt, vb, n, np - 1, sh + 1, bi + 1,
+                                         h_hist + RADIX, result_in_alt)));
+    }
     return kman_check_device_error(ctx);
 }

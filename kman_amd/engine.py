@@ -241,6 +241,7 @@ class Kmers:
     # hist_valid False = no usable histogram (sort computes its own)
     lo_bit: int = 0
     hist_valid: bool = False
+    prefix_sorted: bool = False  # keys stably sorted by bits [lo_bit, 2k) (kman_extract_sorted)
 
     def free(self) -> None:
         for b in (self.keys, self.alt, self.pos, self.pos_alt, self.hist):
@@ -292,6 +293,31 @@ def extract(p: Parsed, k: int, rc: bool, want_pos: bool, canonical: bool = False
                  hist_valid=True)
 
 
+def extract_sorted(p: Parsed, k: int, rc: bool, want_pos: bool) -> Kmers:
+    """kman_extract_sorted: the k-mers already stably sorted by their prefix
+    bits [lo, 2k) (first prefix pass fused into the extraction)."""
+    _check_k(k)
+    dev = p.dev
+    L = N.lib()
+    bound = p.n_bases * (2 if rc else 1)
+    n = max(bound, 1)
+    pos_bytes = 4 if 2 * p.n_bases <= 0xFFFFFFFF else 8
+    keys, alt = dev.alloc(8 * n), dev.alloc(8 * n)
+    pos = dev.alloc(pos_bytes * n) if want_pos else None
+    pos_alt = dev.alloc(pos_bytes * n) if want_pos else None
+    lo = split_bits(bound, 2 * k)
+    out, res = c_uint64(0), c_int(0)
+    N.check(dev.ctx, L.kman_extract_sorted(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k, flags_for(rc, want_pos), lo,
+                                           c_void_p(keys.ptr), c_void_p(alt.ptr),
+                                           c_void_p(pos.ptr if pos else None), c_void_p(pos_alt.ptr if pos else None),
+                                           pos_bytes, bound, byref(out), byref(res)), "kman_extract_sorted")
+    if res.value:
+        keys, alt = alt, keys
+        pos, pos_alt = pos_alt, pos
+    return Kmers(keys, alt, pos, pos_alt, pos_bytes if want_pos else 0, int(out.value), k, dev.alloc(8), lo_bit=lo,
+                 prefix_sorted=True)
+
+
 def split_bits(n: int, key_bits: int) -> int:
     """kman_split_bits: low bit of the prefix the global passes sort by."""
     lo = ctypes.c_uint32(0)
@@ -303,6 +329,8 @@ def split_bits(n: int, key_bits: int) -> int:
 def _sort_prefix(km: Kmers, dev: Device, key_bits: int) -> None:
     """kman_sort_range over bits [km.lo_bit, key_bits): a stable sort by the
     prefix; km.keys / km.pos then hold the prefix-sorted data."""
+    if km.prefix_sorted:
+        return
     res = c_int(0)
     hist = c_void_p(km.hist.ptr) if km.hist_valid and km.hist is not None else c_void_p(None)
     rc = N.lib().kman_sort_range(dev.ctx, c_void_p(km.keys.ptr), c_void_p(km.alt.ptr),
@@ -313,6 +341,7 @@ def _sort_prefix(km: Kmers, dev: Device, key_bits: int) -> None:
     if res.value:
         km.keys, km.alt = km.alt, km.keys
         km.pos, km.pos_alt = km.pos_alt, km.pos
+    km.prefix_sorted = True
 
 
 def _finish(km: Kmers, dev: Device, key_bits: int, mode: int, okeys=None, ovals=None, ob: int = 0) -> int:
@@ -492,7 +521,7 @@ def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = No
     p = parse(dev, text)
     try:
         check_empty_names(p, k)
-        km = extract(p, k, rc, want_pos=False)
+        km = extract_sorted(p, k, rc, want_pos=False)
         try:
             if km.n == 0:
                 return b""
@@ -516,7 +545,7 @@ def uniq_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = Non
     p = parse(dev, text)
     try:
         check_empty_names(p, k)
-        km = extract(p, k, rc, want_pos=True)
+        km = extract_sorted(p, k, rc, want_pos=True)
         try:
             if km.n == 0:
                 return b""
@@ -601,19 +630,26 @@ class ResidentPipeline:
                                         c_void_p(self.rec_hdr.ptr), c_void_p(self.rec_seq.ptr), self.rec_cap,
                                         byref(info)), "kman_parse_fasta")
         self.n_bases = int(info.n_bases)
-        N.check(ctx, L.kman_memset(ctx, c_void_p(self.hist.ptr), 0, 8 * 256 * 8), "memset")
         n = c_uint64(0)
-        pos = c_void_p(self.pos.ptr) if self.pos else c_void_p(None)
-        N.check(ctx, L.kman_extract(ctx, c_void_p(self.codes.ptr), self.n_bases, self.k, self.flags,
-                                    c_void_p(self.keys.ptr), pos, self.pos_bytes, self.bound,
-                                    c_void_p(self.hist.ptr), byref(n)), "kman_extract")
-        self.n_kmers = int(n.value)
         res = c_int(0)
+        pos = c_void_p(self.pos.ptr) if self.pos else c_void_p(None)
         vb = self.pos_bytes if self.pos else 0
         pos_alt = c_void_p(self.pos_alt.ptr if self.pos_alt else None)
-        N.check(ctx, L.kman_sort_range(ctx, c_void_p(self.keys.ptr), c_void_p(self.alt.ptr), pos, pos_alt, vb,
-                                       self.n_kmers, self.lo_bit, 2 * self.k, c_void_p(self.hist.ptr), byref(res)),
-                "kman_sort_range")
+        if self.path == "split":
+            # extraction fused with the first prefix pass, then the other prefix passes
+            N.check(ctx, L.kman_extract_sorted(ctx, c_void_p(self.codes.ptr), self.n_bases, self.k,
+                                               self.flags & 0xff, self.lo_bit, c_void_p(self.keys.ptr),
+                                               c_void_p(self.alt.ptr), pos, pos_alt, self.pos_bytes, self.bound,
+                                               byref(n), byref(res)), "kman_extract_sorted")
+            self.n_kmers = int(n.value)
+        else:
+            N.check(ctx, L.kman_memset(ctx, c_void_p(self.hist.ptr), 0, 8 * 256 * 8), "memset")
+            N.check(ctx, L.kman_extract(ctx, c_void_p(self.codes.ptr), self.n_bases, self.k, self.flags,
+                                        c_void_p(self.keys.ptr), pos, self.pos_bytes, self.bound,
+                                        c_void_p(self.hist.ptr), byref(n)), "kman_extract")
+            self.n_kmers = int(n.value)
+            N.check(ctx, L.kman_sort(ctx, c_void_p(self.keys.ptr), c_void_p(self.alt.ptr), pos, pos_alt, vb,
+                                     self.n_kmers, 2 * self.k, c_void_p(self.hist.ptr), byref(res)), "kman_sort")
         self.sorted_in_alt = bool(res.value)
         skeys = self.alt if res.value else self.keys
         out = c_uint64(0)

@@ -112,6 +112,52 @@ def test_extract_matches_oracle(dev, golden_inputs, k, mode):
             p.free()
 
 
+@pytest.mark.parametrize("k", [2, 5, 13, 21, 25, 31])
+@pytest.mark.parametrize("rc", [False, True])
+@pytest.mark.parametrize("want_pos", [True, False])
+def test_extract_sorted_matches_oracle(dev, golden_inputs, k, rc, want_pos):
+    """kman_extract_sorted (histogram pre-pass + fused extract/first pass +
+    remaining prefix passes; k > 25 runs extract + sort_range) == the stream
+    k-mers stably sorted by their top bits [lo, 2k)."""
+    import ctypes
+    from ctypes import byref, c_void_p
+    import np_oracle
+    from kman_amd import _native as N, engine
+
+    L = N.lib()
+    for text in (_read(golden_inputs["messy1"]), _messy(7), WEIRD[5], b">x\n" + b"ACGT" * 40000 + b"\n"):
+        recs = np_oracle.parse_fasta(text)
+        kref, pref = np_oracle.stream_kmers(recs, k, rc=rc)
+        p = engine.parse(dev, text)
+        try:
+            nb = max(p.n_bases * (2 if rc else 1), 1)
+            for lo in sorted({engine.split_bits(nb, 2 * k), max(0, 2 * k - 7), 0}):
+                bufs = [dev.alloc(8 * nb) for _ in range(2)]
+                pbufs = [dev.alloc(4 * nb) for _ in range(2)] if want_pos else [None, None]
+                try:
+                    n, res = ctypes.c_uint64(0), ctypes.c_int(0)
+                    P = lambda b: c_void_p(b.ptr if b is not None else None)  # noqa: E731
+                    flags = (N.KMAN_RC if rc else 0) | (N.KMAN_WANT_POS if want_pos else 0)
+                    N.check(dev.ctx, L.kman_extract_sorted(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k, flags, lo,
+                                                           P(bufs[0]), P(bufs[1]), P(pbufs[0]), P(pbufs[1]), 4, nb,
+                                                           byref(n), byref(res)), "extract_sorted")
+                    assert n.value == len(kref)
+                    c = res.value
+                    order = np.argsort(kref >> np.uint64(lo) if lo < 64 else np.zeros(len(kref), np.uint64),
+                                       kind="stable")
+                    got = dev.download(bufs[c], n.value, np.uint64)
+                    np.testing.assert_array_equal(got, kref[order])
+                    if want_pos:
+                        gp = dev.download(pbufs[c], n.value, np.uint32).astype(np.uint64)
+                        np.testing.assert_array_equal(gp, pref[order])
+                finally:
+                    for b in bufs + pbufs:
+                        if b is not None:
+                            b.free()
+        finally:
+            p.free()
+
+
 def _sort_case(dev, keys, vals, key_bits):
     from kman_amd import engine
 
