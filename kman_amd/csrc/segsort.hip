@@ -37,8 +37,12 @@ namespace {
 
 constexpr int FT = 512;        // threads per chunk
 constexpr int FW = FT / 64;    // waves
-constexpr int FC = 5120;       // chunk: segments that start here are owned
-constexpr int FR = 6144;       // region capacity: chunk + tail of its last segment
+#ifndef KMAN_FC
+#define KMAN_FC 5120
+#define KMAN_FR 6144
+#endif
+constexpr int FC = KMAN_FC;    // chunk: segments that start here are owned
+constexpr int FR = KMAN_FR;    // region capacity: chunk + tail of its last segment
 constexpr int FI = FR / FT;    // items per thread
 constexpr int FRADIX = 128;    // local LSD digit radix
 constexpr int FBITS = 7;

@@ -293,13 +293,23 @@ __global__ __launch_bounds__(NT, MINW) void onesweep_pass(const uint64_t *__rest
     uint32_t tile_total;
     const uint32_t ls = block_exclusive_scan<NT>(tot, SumU32(), 0u, lds_scan, &tile_total);
     if (d0 < RADIX) lstart[d0] = ls;
+    __syncthreads();
+    // scatter into LDS in tile order: tile-local offsets only, so the LDS
+    // stores are in flight while the look-back below waits on other tiles
+    uint32_t lp[SI];
+#pragma unroll
+    for (int i = 0; i < SI; i++) {
+        const bool valid = ib + (uint64_t)i * 64 < n;
+        const uint32_t d = DIGIT(key[i]);
+        lp[i] = valid ? lstart[d] + whist[w][d] + rank[i] : 0xffffffffu;
+        if (valid) skeys[lp[i]] = key[i];
+    }
 #if defined(KMAN_ABL) && (KMAN_ABL & 1)
     // ablation build only: no look-back (wrong offsets, measures the rest)
     if (d0 < radix) gstart[d0] = bucket_base[d0] + (uint64_t)tile * TILE / radix - ls;
 #else
     if constexpr (EARLY) {
         // several lanes per digit walk the chain (see group_lookback)
-        __syncthreads();
         const uint32_t tpd = NT / radix >= 4 ? 4 : (NT / radix >= 2 ? 2 : 1);
         if (threadIdx.x < radix * tpd) {
             const uint32_t d = threadIdx.x / tpd;
@@ -316,39 +326,26 @@ __global__ __launch_bounds__(NT, MINW) void onesweep_pass(const uint64_t *__rest
 #endif
     __syncthreads();
     STAMP(3);
-
-    // scatter into LDS in tile order
-    uint32_t lp[SI];
-#pragma unroll
-    for (int i = 0; i < SI; i++) {
-        const bool valid = ib + (uint64_t)i * 64 < n;
-        const uint32_t d = DIGIT(key[i]);
-        lp[i] = valid ? lstart[d] + whist[w][d] + rank[i] : 0xffffffffu;
-        if (valid) skeys[lp[i]] = key[i];
-    }
-    __syncthreads();
     const uint32_t cnt = (uint32_t)(n - tb < (uint64_t)TILE ? n - tb : (uint64_t)TILE);
+    constexpr int RQ = (TILE + NT - 1) / NT;
+    uint8_t dq[HAS_V ? RQ : 1];  // digits of the tile-ordered keys, for the payload
+#pragma unroll
+    for (int r = 0; r < RQ; r++) {
+        const uint32_t q = threadIdx.x + r * NT;
+        if (q < cnt) {
+            const uint64_t kk = skeys[q];
+            const uint32_t d = DIGIT(kk);
 #if defined(KMAN_ABL) && (KMAN_ABL & 2)
-    // ablation build only: contiguous writes instead of the digit scatter
-    for (uint32_t q = threadIdx.x; q < cnt; q += NT) {
-        const uint64_t kk = skeys[q];
-        kout[tb + q] = kk + gstart[DIGIT(kk)];
-    }
+            // ablation build only: contiguous writes instead of the digit scatter
+            kout[tb + q] = kk + gstart[d];
 #else
-    for (uint32_t q = threadIdx.x; q < cnt; q += NT) {
-        const uint64_t kk = skeys[q];
-        kout[gstart[DIGIT(kk)] + q] = kk;
-    }
+            kout[gstart[d] + q] = kk;
 #endif
+            if constexpr (HAS_V) dq[r] = (uint8_t)d;
+        }
+    }
     STAMP(4);
     if constexpr (HAS_V) {
-        // digits of the tile-ordered keys, before skeys is reused for values
-        uint8_t dq[(TILE + NT - 1) / NT];
-#pragma unroll
-        for (int r = 0; r < (TILE + NT - 1) / NT; r++) {
-            const uint32_t q = threadIdx.x + r * NT;
-            dq[r] = q < cnt ? (uint8_t)DIGIT(skeys[q]) : 0;
-        }
         __syncthreads();
         V *sval = reinterpret_cast<V *>(skeys);
 #pragma unroll
@@ -356,7 +353,7 @@ __global__ __launch_bounds__(NT, MINW) void onesweep_pass(const uint64_t *__rest
             if (lp[i] != 0xffffffffu) sval[lp[i]] = val[i];
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < (TILE + NT - 1) / NT; r++) {
+        for (int r = 0; r < RQ; r++) {
             const uint32_t q = threadIdx.x + r * NT;
             if (q < cnt) vout[gstart[dq[r]] + q] = sval[q];
         }
@@ -487,6 +484,15 @@ __global__ __launch_bounds__(XT) void extract_pass(const uint8_t *__restrict__ c
     const uint32_t ls = block_exclusive_scan<NT>(tot, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
     if (d0 < RADIX) lstart[d0] = ls;
     __syncthreads();
+    // tile-order scatter into LDS first: in flight while the look-back waits
+    uint32_t lp[SI];
+#pragma unroll
+    for (int i = 0; i < SI; i++) {
+        const bool valid_i = ib + i * 64 < tcnt;
+        const uint32_t d = XDIGIT(key[i]);
+        lp[i] = valid_i ? lstart[d] + whist[w][d] + rank[i] : 0xffffffffu;
+        if (valid_i) skeys[lp[i]] = key[i];
+    }
     {
         const uint32_t tpd = NT / radix >= 4 ? 4 : (NT / radix >= 2 ? 2 : 1);
         if (threadIdx.x < radix * tpd) {
@@ -499,26 +505,19 @@ __global__ __launch_bounds__(XT) void extract_pass(const uint8_t *__restrict__ c
         }
     }
     __syncthreads();
-    uint32_t lp[SI];
+    constexpr int RQ = (TILE + NT - 1) / NT;
+    uint8_t dq[HAS_V ? RQ : 1];
 #pragma unroll
-    for (int i = 0; i < SI; i++) {
-        const bool valid_i = ib + i * 64 < tcnt;
-        const uint32_t d = XDIGIT(key[i]);
-        lp[i] = valid_i ? lstart[d] + whist[w][d] + rank[i] : 0xffffffffu;
-        if (valid_i) skeys[lp[i]] = key[i];
-    }
-    __syncthreads();
-    for (uint32_t q = threadIdx.x; q < tcnt; q += NT) {
-        const uint64_t kk = skeys[q];
-        kout[gstart[XDIGIT(kk)] + q] = kk & keymask;
+    for (int r = 0; r < RQ; r++) {
+        const uint32_t q = threadIdx.x + r * NT;
+        if (q < tcnt) {
+            const uint64_t kk = skeys[q];
+            const uint32_t d = XDIGIT(kk);
+            kout[gstart[d] + q] = kk & keymask;
+            if constexpr (HAS_V) dq[r] = (uint8_t)d;
+        }
     }
     if constexpr (HAS_V) {
-        uint8_t dq[(TILE + NT - 1) / NT];
-#pragma unroll
-        for (int r = 0; r < (TILE + NT - 1) / NT; r++) {
-            const uint32_t q = threadIdx.x + r * NT;
-            dq[r] = q < tcnt ? (uint8_t)XDIGIT(skeys[q]) : 0;
-        }
         __syncthreads();
         V *sval = reinterpret_cast<V *>(skeys);
 #pragma unroll
@@ -530,7 +529,7 @@ __global__ __launch_bounds__(XT) void extract_pass(const uint8_t *__restrict__ c
         }
         __syncthreads();
 #pragma unroll
-        for (int r = 0; r < (TILE + NT - 1) / NT; r++) {
+        for (int r = 0; r < RQ; r++) {
             const uint32_t q = threadIdx.x + r * NT;
             if (q < tcnt) vout[gstart[dq[r]] + q] = sval[q];
         }
