@@ -67,6 +67,8 @@ int kman_lookback_begin(kman_ctx *ctx, size_t words, uint32_t *epoch, uint32_t *
 int kman_scratch(kman_ctx *ctx, size_t bytes, void **p);
 int kman_aux(kman_ctx *ctx, size_t bytes, void **p);
 int kman_check_device_error(kman_ctx *ctx);
+// blocks of `fn` resident at once on the device (occupancy x CUs), capped at n_tiles
+int kman_persistent_grid(kman_ctx *ctx, const void *fn, int threads, uint64_t n_tiles);
 // internal (not in kman.h): the histogram pre-pass of kman_extract_sorted
 int kman_kmer_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
                    uint32_t lo_bit, uint64_t *d_hist, uint64_t *n_kmers);

@@ -202,15 +202,6 @@ __global__ __launch_bounds__(ET) void kmer_hist_kernel(const uint8_t *__restrict
     }
 }
 
-int persistent_grid(kman_ctx *ctx, const void *fn, int threads, uint64_t n_tiles) {
-    int per_cu = 1, cus = 256;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0);
-    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
-    uint64_t g = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
-    if (g > n_tiles) g = n_tiles;
-    return (int)(g ? g : 1);
-}
-
 template <int EI, bool RC, bool CANON, typename P>
 int launch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k, uint64_t *keys, P *pos,
                    uint64_t *hist, const Plan &plan) {
@@ -218,7 +209,7 @@ int launch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k,
     uint32_t epoch, *counter;
     KMAN_TRY(kman_lookback_begin(ctx, n_tiles, &epoch, &counter));
     auto fn = extract_kernel<EI, RC, CANON, P>;
-    const int grid = persistent_grid(ctx, (const void *)fn, ET, n_tiles);
+    const int grid = kman_persistent_grid(ctx, (const void *)fn, ET, n_tiles);
     KTimer kt_(ctx, "extract");
     hipLaunchKernelGGL(fn, dim3(grid), dim3(ET), 0, ctx->stream, codes, n_bases, n_tiles, k, keys, pos,
                        ctx->d_status, counter, epoch, ctx->d_err, hist, plan);
@@ -327,7 +318,7 @@ int kman_kmer_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint
     const int EI = 16;
     const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * EI);
     auto fn = rc ? kmer_hist_kernel<16, true> : kmer_hist_kernel<16, false>;
-    const int grid = persistent_grid(ctx, (const void *)fn, ET, n_tiles);
+    const int grid = kman_persistent_grid(ctx, (const void *)fn, ET, n_tiles);
     {
         KTimer kt_(ctx, "kmer_hist");
         hipLaunchKernelGGL(fn, dim3(grid), dim3(ET), 0, ctx->stream, d_codes, n_bases, n_tiles, (int)k,

@@ -37,6 +37,15 @@ int kman_scratch(kman_ctx *ctx, size_t bytes, void **p) {
     return KMAN_OK;
 }
 
+int kman_persistent_grid(kman_ctx *ctx, const void *fn, int threads, uint64_t n_tiles) {
+    int per_cu = 1, cus = 256;
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
+    uint64_t g = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
+    if (g > n_tiles) g = n_tiles;
+    return (int)(g ? g : 1);
+}
+
 int kman_aux(kman_ctx *ctx, size_t bytes, void **p) {
     if (bytes > ctx->aux_bytes) {
         if (ctx->d_aux) {

@@ -35,19 +35,25 @@
 
 namespace {
 
-constexpr int FT = 512;        // threads per chunk
-constexpr int FW = FT / 64;    // waves
+#ifndef KMAN_FT
+#define KMAN_FT 512
+#endif
 #ifndef KMAN_FC
 #define KMAN_FC 5120
 #define KMAN_FR 6144
 #endif
+constexpr int FT = KMAN_FT;    // threads per chunk
+constexpr int FW = FT / 64;    // waves
 constexpr int FC = KMAN_FC;    // chunk: segments that start here are owned
 constexpr int FR = KMAN_FR;    // region capacity: chunk + tail of its last segment
 constexpr int FI = FR / FT;    // items per thread
+constexpr int PI = FC / FT + 1;  // rounds loaded up front: the chunk and the next FT keys
+constexpr int NWORD = FR / 64;   // segment-start mask words
 constexpr int FRADIX = 128;    // local LSD digit radix
 constexpr int FBITS = 7;
-constexpr int MAXSEG = 256;    // wave-per-segment path: segments per range
-constexpr int WI = 12;         // ... and items per lane (segments <= 768 keys)
+constexpr int WI = 12;         // wave-per-segment path: items per lane (segments <= 768 keys)
+static_assert(FC % FT == 0 && FR % FT == 0 && FR >= FC + FT && FT % 64 == 0, "chunk geometry");
+static_assert(NWORD <= 128, "mask words: two per lane");
 
 struct NoV {};
 
@@ -105,24 +111,21 @@ KMAN_DEV uint64_t run_end(const uint64_t *keys, uint64_t n, uint64_t from, uint6
     return lo;
 }
 
-// One wave sorts segments sg0, sg0 + FW, ... < sg1 of the staged range by their
-// low bits (stable LSD, 7-bit digits, the wave's own 128 counters).  Items travel
+// One wave sorts the staged segment [sa, sa + sz) by its low bits (stable LSD,
+// 7-bit digits, the wave's own 128 counters).  Items travel
 // packed: IT = u32 holds (low bits << 10 | offset in the segment) when the low
 // bits fit in 22 (passes bounce through spk), IT = u64 holds (low bits << 13 |
 // position) (passes bounce through skey).  The last pass writes the full key to
 // skey and its original position to spk.
 template <typename IT, bool ATOMIC>
-KMAN_DEV void wave_sort_segments(uint64_t *skey, uint32_t *spk, uint32_t *wh, const uint32_t *segstart, uint32_t sg0,
-                                 uint32_t sg1, uint32_t lo, uint32_t low_bits) {
+KMAN_DEV void wave_sort_segment(uint64_t *skey, uint32_t *spk, uint32_t *wh, uint32_t sa, uint32_t sz,
+                                uint32_t low_bits) {
     constexpr bool SMALL = sizeof(IT) == 4;
     constexpr uint32_t PS = SMALL ? 10 : 13;  // position bits
     const int lane = lane_id();
     const uint32_t npl = (low_bits + FBITS - 1) / FBITS;
     const uint64_t lmask = low_bits >= 64 ? ~0ull : ((1ull << low_bits) - 1);
-    for (uint32_t sg = sg0; sg < sg1; sg += FW) {
-        const uint32_t sa = lo + segstart[sg];
-        const uint32_t sz = lo + segstart[sg + 1] - sa;
-        if (sz < 2) continue;
+    {
         const uint64_t pfx_hi = skey[sa] & ~lmask;
         IT pw[WI];
 #pragma unroll
@@ -203,8 +206,49 @@ KMAN_DEV void wave_sort_segments(uint64_t *skey, uint32_t *spk, uint32_t *wh, co
     }
 }
 
+// position of the n-th (0-based) set bit of x; n < popcount(x)
+KMAN_DEV uint32_t nth_bit(uint64_t x, uint32_t n) {
+    uint32_t pos = 0, c;
+    c = (uint32_t)__popc((uint32_t)x);
+    if (n >= c) { n -= c; x >>= 32; pos += 32; }
+    c = (uint32_t)__popc((uint32_t)x & 0xffffu);
+    if (n >= c) { n -= c; x >>= 16; pos += 16; }
+    c = (uint32_t)__popc((uint32_t)x & 0xffu);
+    if (n >= c) { n -= c; x >>= 8; pos += 8; }
+    c = (uint32_t)__popc((uint32_t)x & 0xfu);
+    if (n >= c) { n -= c; x >>= 4; pos += 4; }
+    c = (uint32_t)__popc((uint32_t)x & 0x3u);
+    if (n >= c) { n -= c; x >>= 2; pos += 2; }
+    c = (uint32_t)(x & 1u);
+    if (n >= c) pos += 1;
+    return pos;
+}
+
+// bits of mask word wi (positions 64 wi ..) that lie in [a, b)
+KMAN_DEV uint64_t span_bits(uint32_t wi, uint32_t a, uint32_t b) {
+    auto below = [wi](uint32_t lim) -> uint64_t {
+        const int32_t d = (int32_t)lim - (int32_t)(wi * 64);
+        return d <= 0 ? 0ull : d >= 64 ? ~0ull : ((1ull << d) - 1);
+    };
+    return below(b) & ~below(a);
+}
+
+KMAN_DEV uint32_t wave_min_u32(uint32_t v) {
+    v = wave_inclusive_scan(v, [](uint32_t a, uint32_t b) { return a < b ? a : b; }, 0xffffffffu);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+KMAN_DEV uint32_t wave_max_u32(uint32_t v) {
+    v = wave_inclusive_scan(v, [](uint32_t a, uint32_t b) { return a > b ? a : b; }, 0u);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 enum { M_SORT = 0, M_COUNT = 1, M_UNIQ = 2 };
 
+// One chunk per block.  Segment starts are found while the chunk loads (the
+// previous key of each lane comes over DPP) and kept as a bit mask in LDS;
+// every wave then derives the same plan from the mask (owned range, tail end,
+// segment bounds and the longest segment) without further block barriers, and
+// sorts its share of the segments (round robin) alone.
 template <int MODE, typename V, typename O, bool ATOMIC>
 __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys, V *__restrict__ vals, uint64_t n,
                                                     uint32_t lo_bit, const uint64_t *__restrict__ ov, uint32_t n_ov,
@@ -214,14 +258,16 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
                                                     uint32_t *__restrict__ counter, uint32_t epoch,
                                                     uint32_t *__restrict__ err) {
     constexpr bool HAS_V = !std::is_same<V, NoV>::value;
+    constexpr bool V32 = HAS_V && sizeof(V) == 4 && MODE != M_COUNT;  // u32 payload staged through LDS
+    constexpr uint32_t NONE = 0xffffffffu;
     __shared__ __attribute__((aligned(16))) uint64_t skey[FR];
     __shared__ uint32_t spk[FR];  // (segment index << 16) | position in the chunk
+    __shared__ uint64_t smask[NWORD];  // bit p: a segment starts at position p
     __shared__ uint32_t whist[FW][FRADIX];
     __shared__ uint32_t lstart[FRADIX];
     __shared__ uint32_t lds_scan[FW];
     __shared__ uint64_t lds_scan64[FW];
-    __shared__ uint32_t segstart[MAXSEG + 2];
-    __shared__ uint32_t s_first, s_lastp1, s_end, s_tile, s_flags, s_maxseg;
+    __shared__ uint32_t s_end, s_tile, s_flags;
     __shared__ uint64_t s_out;
 
     // dynamic chunk id (chunks start in id order: every predecessor of a chunk is
@@ -236,31 +282,68 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
     const int w = threadIdx.x >> 6;
     const int t = threadIdx.x;
     if (t == 0) {
-        s_first = FC;
-        s_lastp1 = 0;
         s_end = FR + 1;
         s_flags = 0;
-        s_maxseg = 0;
     }
-    for (uint32_t i = t; i < cnt; i += FT) skey[i] = keys[base + i];
-    // the first FT keys past the chunk come with it: the last segment's tail
-    // usually ends there (~half a segment), saving a dependent round trip
-    if (cnt == (uint32_t)FC && base + FC + t < n) skey[FC + t] = keys[base + FC + t];
-    const uint64_t prevk = base ? keys[base - 1] : 0;
-    __syncthreads();
 
-    // ---- segment starts in the chunk
-    for (uint32_t i = t; i < cnt; i += FT) {
-        const uint64_t pk = i ? skey[i - 1] : prevk;
-        if (base + i == 0 || pre_of(skey[i], lo_bit) != pre_of(pk, lo_bit)) {
-            atomicMin(&s_first, i);
-            atomicMax(&s_lastp1, i + 1);
-        }
+    // ---- load the chunk and the next FT keys; mark segment starts.  Every
+    // load is issued before the first is consumed (one round trip, not PI)
+    const uint64_t prevk = base ? keys[base - 1] : 0;
+    uint64_t kk[PI], k0[PI];
+#pragma unroll
+    for (int r = 0; r < PI; r++) {
+        const uint64_t g = base + (uint64_t)(r * FT + t);
+        kk[r] = g < n ? keys[g] : 0;
     }
+    // lane 0's previous key belongs to another wave
+#pragma unroll
+    for (int r = 0; r < PI; r++) {
+        const uint32_t p = (uint32_t)(r * FT + t);
+        const uint64_t g = base + p;
+        k0[r] = (lane == 0 && p > 0 && g <= n) ? keys[g - 1] : prevk;
+    }
+#pragma unroll
+    for (int r = 0; r < PI; r++) {
+        const uint32_t p = (uint32_t)(r * FT + t);
+        const uint64_t g = base + p;
+        const bool in = g < n;
+        const uint64_t k = kk[r];
+        uint64_t kp = wave_shr1(k, (uint64_t)0);
+        if (lane == 0) kp = k0[r];
+        const bool st = in && (g == 0 || pre_of(k, lo_bit) != pre_of(kp, lo_bit));
+        const uint64_t mk = __ballot(st);
+        if (in) skey[p] = k;
+        if (lane == 0) smask[p >> 6] = mk;
+    }
+    for (int wi = PI * FT / 64 + t; wi < NWORD; wi += FT) smask[wi] = 0;
     __syncthreads();
-    const uint32_t first = s_first;
-    const bool has_start = first < (uint32_t)FC;
-    const uint32_t last = s_lastp1 - 1;
+    FSTAMP(1);
+
+    // ---- the plan, computed by every wave from the mask (lane l: words l, l + 64)
+    const uint32_t wia = (uint32_t)lane, wib = (uint32_t)lane + 64;
+    const uint64_t ma = wia < (uint32_t)NWORD ? smask[wia] : 0ull;
+    const uint64_t mb = wib < (uint32_t)NWORD ? smask[wib] : 0ull;
+    uint32_t first, lastp1, endp;
+    {
+        const uint64_t ia = ma & span_bits(wia, 0, cnt), ib = mb & span_bits(wib, 0, cnt);
+        const uint64_t oa = ma & ~span_bits(wia, 0, cnt), ob = mb & ~span_bits(wib, 0, cnt);
+        uint32_t f = NONE, l = 0, e = NONE;
+        if (ia) {
+            f = wia * 64 + (uint32_t)__ffsll((unsigned long long)ia) - 1;
+            l = wia * 64 + 64 - (uint32_t)__clzll(ia);
+        }
+        if (ib) {
+            f = f < NONE ? f : wib * 64 + (uint32_t)__ffsll((unsigned long long)ib) - 1;
+            l = wib * 64 + 64 - (uint32_t)__clzll(ib);
+        }
+        if (oa) e = wia * 64 + (uint32_t)__ffsll((unsigned long long)oa) - 1;
+        else if (ob) e = wib * 64 + (uint32_t)__ffsll((unsigned long long)ob) - 1;
+        first = wave_min_u32(f);
+        lastp1 = wave_max_u32(l);
+        endp = wave_min_u32(e);
+    }
+    const bool has_start = first < cnt;
+    const uint32_t last = lastp1 - 1;
     // listed big segments: the leading one (started before the chunk) and the
     // last one starting here are processed as presorted slices
     if (n_ov) {
@@ -280,123 +363,156 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
     }
     const bool lead_pre = s_flags & 1;
     const bool last_pre = s_flags & 2;
-    FSTAMP(1);
 
-    // ---- end of the last owned segment (tail keys are staged behind the chunk)
+    // ---- end of the last owned segment
     uint32_t hi = cnt;
     bool trail_pre = last_pre;  // the last segment is a presorted (or unstaged big) slice
     if (has_start && !last_pre && base + cnt < n) {
-        const uint64_t lp = pre_of(skey[last], lo_bit);
-        for (uint32_t r0 = FC; r0 < (uint32_t)FR; r0 += FT) {
-            const uint32_t rel = r0 + t;
-            const uint64_t g = base + rel;
-            if (g < n) {
-                uint64_t kk;
-                if (r0 == (uint32_t)FC) {
-                    kk = skey[rel];  // prefetched with the chunk
-                } else {
-                    kk = keys[g];
+        if (endp != NONE) {
+            hi = endp;  // a start among the keys loaded with the chunk
+        } else if (n - base <= (uint64_t)(PI * FT)) {
+            hi = (uint32_t)(n - base);  // the array ends there
+        } else {
+            // longer tail: load further rounds until the prefix changes
+            const uint64_t lp = pre_of(skey[last], lo_bit);
+            for (uint32_t r0 = PI * FT; r0 < (uint32_t)FR; r0 += FT) {
+                const uint32_t rel = r0 + t;
+                const uint64_t g = base + rel;
+                if (g < n) {
+                    const uint64_t kk = keys[g];
                     skey[rel] = kk;
+                    if (pre_of(kk, lo_bit) != lp) atomicMin(&s_end, rel);
+                } else if (g == n) {
+                    atomicMin(&s_end, rel);
                 }
-                if (pre_of(kk, lo_bit) != lp) atomicMin(&s_end, rel);
-            } else if (g == n) {
-                atomicMin(&s_end, rel);
+                __syncthreads();
+                if (s_end < r0 + FT) break;
             }
-            __syncthreads();
-            if (s_end < r0 + FT) break;
-        }
-        hi = s_end;
-        if (hi > (uint32_t)FR) {
-            trail_pre = true;
-            // a big segment nobody listed (first run): record it; this run's
-            // output is discarded by the host
-            if (t == 0) {
-                const uint32_t slot = atomicAdd(n_big, 1u);
-                if (slot < big_cap) big[slot] = base + last;
+            hi = s_end;
+            if (hi > (uint32_t)FR) {
+                trail_pre = true;
+                // a big segment nobody listed (first run): record it; this run's
+                // output is discarded by the host
+                if (t == 0) {
+                    const uint32_t slot = atomicAdd(n_big, 1u);
+                    if (slot < big_cap) big[slot] = base + last;
+                }
+                hi = cnt;
             }
-            hi = cnt;
         }
     }
     const uint32_t lo = lead_pre ? 0u : (has_start ? first : cnt);
     if (!has_start && !lead_pre) hi = lo;
     const uint32_t m = hi - lo;
     const bool need_sort = has_start && m > 1;
+    // the u32 payload of positions t + r FT in [lo, hi): in flight during the sort
+    uint32_t cv[V32 ? FI : 1];
+    if constexpr (V32) {
+#pragma unroll
+        for (int r = 0; r < FI; r++) {
+            const uint32_t p = (uint32_t)(t + r * FT);
+            cv[r] = (p >= lo && p < hi) ? (uint32_t)vals[base + p] : 0u;
+        }
+    }
 
     FSTAMP(2);
     // ---- stable LDS sort of [lo, hi): every owned segment by its low bits
     if (need_sort) {
-        // segment index of every item (starts inside the range, in order)
-        uint64_t key[FI];
-        uint32_t pk[FI];
-        uint32_t run = 0, stm = 0;
-#pragma unroll
-        for (int i = 0; i < FI; i++) {
-            const uint32_t q = (uint32_t)(w * FI * 64 + i * 64 + lane);
-            const bool valid = q < m;
-            key[i] = valid ? skey[lo + q] : 0;
-            const bool st = valid && q > 0 && pre_of(key[i], lo_bit) != pre_of(skey[lo + q - 1], lo_bit);
-            stm |= (uint32_t)st << i;
-            const uint64_t msk = __ballot(st);
-            pk[i] = run + (uint32_t)__popcll(msk & (lanemask_lt() | (1ull << lane)));
-            run += (uint32_t)__popcll(msk);
-        }
-        if (lane == 0) lds_scan[w] = run;
-        __syncthreads();
-        uint32_t woff = 0, nsegs = 0;
-#pragma unroll
-        for (int ww = 0; ww < FW; ww++) {
-            const uint32_t c = lds_scan[ww];
-            woff += ww < w ? c : 0;
-            nsegs += c;
-        }
-        nsegs += 1;  // segment 0 starts at q = 0
-        const uint32_t s0 = lead_pre ? 1u : 0u, s1 = nsegs - (trail_pre ? 1u : 0u);
         const uint32_t low_bits = lo_bit >= 64 ? 64u : lo_bit;
-        bool wave_path = nsegs <= (uint32_t)MAXSEG && low_bits <= 51;
-        if (wave_path) {
-#pragma unroll
-            for (int i = 0; i < FI; i++) {
-                const uint32_t q = (uint32_t)(w * FI * 64 + i * 64 + lane);
-                if (q == 0) segstart[0] = 0;
-                else if ((stm >> i) & 1u) segstart[pk[i] + woff] = q;
+        // segment starts after lo (the range's first segment starts at lo)
+        const uint64_t xa = ma & span_bits(wia, lo + 1, hi), xb = mb & span_bits(wib, lo + 1, hi);
+        const uint32_t ca = (uint32_t)__popcll(xa), cb = (uint32_t)__popcll(xb);
+        const uint32_t inca = wave_inclusive_scan(ca, SumU32()), incb = wave_inclusive_scan(cb, SumU32());
+        const uint32_t tota = (uint32_t)__builtin_amdgcn_readlane((int)inca, 63);
+        const uint32_t nsegs = 1 + tota + (uint32_t)__builtin_amdgcn_readlane((int)incb, 63);
+        const uint32_t prea = inca - ca, preb = tota + incb - cb;
+        // longest segment: gaps between consecutive starts (lo and hi included)
+        uint32_t maxlen;
+        {
+            auto mx = [](uint32_t a, uint32_t b) { return a > b ? a : b; };
+            const uint32_t la = xa ? wia * 64 + 63 - (uint32_t)__clzll(xa) : 0u;
+            const uint32_t lb = xb ? wib * 64 + 63 - (uint32_t)__clzll(xb) : 0u;
+            // last start before each word (in word order a[0..63], b[0..31])
+            const uint32_t pa = wave_shr1(wave_inclusive_scan(la, mx), 0u);
+            const uint32_t lasta = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_scan(la, mx), 63);
+            const uint32_t pb = mx(wave_shr1(wave_inclusive_scan(lb, mx), 0u), lasta);
+            uint32_t g = 0;
+            uint64_t x = xa;
+            uint32_t prv = mx(pa, lo);
+            while (x) {
+                const uint32_t q = wia * 64 + (uint32_t)__ffsll((unsigned long long)x) - 1;
+                g = mx(g, q - prv);
+                prv = q;
+                x &= x - 1;
             }
-            if (t == 0) segstart[nsegs] = m;
-            __syncthreads();
-            if ((uint32_t)t + s0 < s1) {
-                for (uint32_t sg = s0 + t; sg < s1; sg += FT) {
-                    const uint32_t sz = segstart[sg + 1] - segstart[sg];
-                    if (sz > (uint32_t)(WI * 64)) atomicMax(&s_maxseg, sz);
-                }
+            x = xb;
+            prv = mx(pb, lo);
+            while (x) {
+                const uint32_t q = wib * 64 + (uint32_t)__ffsll((unsigned long long)x) - 1;
+                g = mx(g, q - prv);
+                prv = q;
+                x &= x - 1;
             }
-            // identity positions for the presorted slices and single-key segments
-            // (the sorted segments write theirs in the last pass)
-            for (uint32_t q = t; q < m; q += FT) spk[lo + q] = lo + q;
-            __syncthreads();
-            wave_path = s_maxseg == 0;
+            const uint32_t lastall = mx(mx(lasta, (uint32_t)__builtin_amdgcn_readlane(
+                                                         (int)wave_inclusive_scan(lb, mx), 63)), lo);
+            maxlen = mx(wave_max_u32(g), hi - lastall);
         }
-#if defined(KMAN_ABL) && (KMAN_ABL & 16)
-        if (t == 0) {
-            atomicAdd(&g_fstat[wave_path ? 0 : 1], 1ull);
-            atomicAdd(&g_fstat[2], (unsigned long long)nsegs);
-            atomicAdd(&g_fstat[3], (unsigned long long)m);
-        }
-#endif
+        const bool wave_path = maxlen <= (uint32_t)(WI * 64) && low_bits <= 51;
         if (wave_path) {
-            // one wave per segment: stable LSD over the low bits with the
-            // wave's own counters; no block barrier until every segment is done
+            // start of segment j (j >= 1): the (j-1)-th set bit after lo
+            auto seg_start = [&](uint32_t j) -> uint32_t {
+                if (j == 0) return lo;
+                if (j >= nsegs) return hi;
+                const uint32_t nb = j - 1;
+                const uint64_t ba = __ballot(ca && nb >= prea && nb < prea + ca);
+                const uint64_t bb = __ballot(cb && nb >= preb && nb < preb + cb);
+                const bool inb = ba == 0;
+                const int src = __ffsll((unsigned long long)(inb ? bb : ba)) - 1;
+                const uint32_t pos = inb ? wib * 64 + nth_bit(xb, nb - preb) : wia * 64 + nth_bit(xa, nb - prea);
+                return (uint32_t)__builtin_amdgcn_readlane((int)pos, src);
+            };
+            if (lead_pre || trail_pre) {
+                // identity positions for the presorted slices
+                for (uint32_t q = t; q < m; q += FT) spk[lo + q] = lo + q;
+                __syncthreads();
+            }
+            const uint32_t s0 = lead_pre ? 1u : 0u, s1 = nsegs - (trail_pre ? 1u : 0u);
 #if defined(KMAN_ABL) && (KMAN_ABL & 8)
             // ablation build only: no segment sort (wrong order, measures the rest)
             if (false)
 #endif
-            {
+            for (uint32_t j = s0 + (uint32_t)w; j < s1; j += FW) {
+                const uint32_t sa = seg_start(j), sb = seg_start(j + 1);
+                if (sb - sa < 2) {
+                    if (lane == 0) spk[sa] = sa;
+                    continue;
+                }
                 if (low_bits <= 22)
-                    wave_sort_segments<uint32_t, ATOMIC>(skey, spk, whist[w], segstart, s0 + w, s1, lo, low_bits);
+                    wave_sort_segment<uint32_t, ATOMIC>(skey, spk, whist[w], sa, sb - sa, low_bits);
                 else
-                    wave_sort_segments<uint64_t, ATOMIC>(skey, spk, whist[w], segstart, s0 + w, s1, lo, low_bits);
+                    wave_sort_segment<uint64_t, ATOMIC>(skey, spk, whist[w], sa, sb - sa, low_bits);
             }
             __syncthreads();
         } else {
             // many or long segments: block-wide LSD on (segment index, low bits)
+            uint64_t key[FI];
+            uint32_t pk[FI];
+            uint32_t run = 0;
+#pragma unroll
+            for (int i = 0; i < FI; i++) {
+                const uint32_t q = (uint32_t)(w * FI * 64 + i * 64 + lane);
+                const bool valid = q < m;
+                key[i] = valid ? skey[lo + q] : 0;
+                const bool st = valid && q > 0 && ((smask[(lo + q) >> 6] >> ((lo + q) & 63)) & 1ull);
+                const uint64_t msk = __ballot(st);
+                pk[i] = run + (uint32_t)__popcll(msk & (lanemask_lt() | (1ull << lane)));
+                run += (uint32_t)__popcll(msk);
+            }
+            if (lane == 0) lds_scan[w] = run;
+            __syncthreads();
+            uint32_t woff = 0;
+#pragma unroll
+            for (int ww = 0; ww < FW; ww++) woff += ww < w ? lds_scan[ww] : 0u;
 #pragma unroll
             for (int i = 0; i < FI; i++) {
                 const uint32_t q = (uint32_t)(w * FI * 64 + i * 64 + lane);
@@ -484,29 +600,26 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
     if constexpr (MODE == M_SORT) {
         if (!need_sort) return;
         for (uint32_t q = t; q < m; q += FT) keys[base + lo + q] = skey[lo + q];
-        if constexpr (HAS_V && sizeof(V) == 4) {
-            // u32 payload: read the range coalesced into LDS (over spk, once every
-            // sorted position has been read), then permute it from there
+        if constexpr (V32) {
+            // u32 payload: staged in LDS by position (over spk, once every sorted
+            // position has been read) and permuted from there
             uint32_t ixr[FI];
-            V vl[FI];
 #pragma unroll
             for (int r = 0; r < FI; r++) {
                 const uint32_t q = t + r * FT;
-                ixr[r] = q < m ? (spk[lo + q] & 0xffffu) - lo : 0;
-                vl[r] = q < m ? vals[base + lo + q] : (V)0;
+                ixr[r] = q < m ? spk[lo + q] & 0xffffu : 0;
             }
             __syncthreads();
-            V *sv = reinterpret_cast<V *>(spk);
 #pragma unroll
             for (int r = 0; r < FI; r++) {
-                const uint32_t q = t + r * FT;
-                if (q < m) sv[q] = vl[r];
+                const uint32_t p = (uint32_t)(t + r * FT);
+                if (p >= lo && p < hi) spk[p] = cv[r];
             }
             __syncthreads();
 #pragma unroll
             for (int r = 0; r < FI; r++) {
                 const uint32_t q = t + r * FT;
-                if (q < m) vals[base + lo + q] = sv[ixr[r]];
+                if (q < m) vals[base + lo + q] = (V)spk[ixr[r]];
             }
         } else if constexpr (HAS_V) {
             // gather the payload in sorted order; staging it in LDS makes every
@@ -533,14 +646,16 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
         const bool has_prev_g = base + lo > 0;
         const uint64_t prev_g = lo ? skey[lo - 1] : prevk;  // [0, lo) is untouched by the sort
         const bool has_next_g = base + hi < n;
-        const uint64_t next_g = has_next_g ? keys[base + hi] : 0;
+        // the first key past the range (another segment) was staged by the chunk
+        // load or the tail rounds
+        const uint64_t next_g = has_next_g ? skey[hi] : 0;
         uint64_t k[FI];
-        uint32_t ix[FI];  // UNIQ: each item's position in the range, for its payload
+        uint32_t ix[FI];  // UNIQ: each item's position in the chunk, for its payload
         const uint32_t q0 = (uint32_t)t * FI;
 #pragma unroll
         for (int j = 0; j < FI; j++) {
             k[j] = q0 + j < m ? skey[lo + q0 + j] : 0;
-            ix[j] = (MODE == M_UNIQ && q0 + j < m) ? (spk[lo + q0 + j] & 0xffffu) - lo : 0;
+            ix[j] = (MODE == M_UNIQ && q0 + j < m) ? spk[lo + q0 + j] & 0xffffu : 0;
         }
         uint32_t heads = 0, tails = 0;
 #pragma unroll
@@ -591,16 +706,7 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
         FSTAMP(7);
         // (the scan's barriers ordered every read of skey / spk above before the
         // writes below)
-        constexpr bool LDS_V = MODE == M_UNIQ && sizeof(V) == 4;
-        V vl[LDS_V ? FI : 1];
-        if constexpr (LDS_V) {
-            // the range's payload, coalesced; in flight during the look-back
-#pragma unroll
-            for (int r = 0; r < FI; r++) {
-                const uint32_t q = t + r * FT;
-                vl[r] = q < m ? vals[base + lo + q] : (V)0;
-            }
-        }
+        constexpr bool LDS_V = MODE == M_UNIQ && V32;
         if (w == 0) {
             const uint64_t b = wave_lookback<0>(status, tile, total, epoch, err);
             if (lane == 0) s_out = b;
@@ -609,17 +715,17 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
         if constexpr (MODE == M_UNIQ && !LDS_V) {
 #pragma unroll
             for (int j = 0; j < FI; j++)
-                ov_[j] = ((emit >> j) & 1u) ? (O)vals[base + lo + ix[j]] : (O)0;
+                ov_[j] = ((emit >> j) & 1u) ? (O)vals[base + ix[j]] : (O)0;
         } else if constexpr (MODE == M_COUNT) {
 #pragma unroll
             for (int j = 0; j < FI; j++) ov_[j] = (O)cval[j];
         }
         if constexpr (LDS_V) {
-            V *sv = reinterpret_cast<V *>(spk);
+            // the range's payload by position
 #pragma unroll
             for (int r = 0; r < FI; r++) {
-                const uint32_t q = t + r * FT;
-                if (q < m) sv[q] = vl[r];
+                const uint32_t p = (uint32_t)(t + r * FT);
+                if (p >= lo && p < hi) spk[p] = cv[r];
             }
         }
         FSTAMP(4);
@@ -630,9 +736,8 @@ __global__ __launch_bounds__(FT) void segfin_kernel(uint64_t *__restrict__ keys,
             if ((emit >> j) & 1u) skey[o++] = k[j];
         __syncthreads();
         if constexpr (LDS_V) {
-            const V *sv = reinterpret_cast<const V *>(spk);
 #pragma unroll
-            for (int j = 0; j < FI; j++) ov_[j] = ((emit >> j) & 1u) ? (O)sv[ix[j]] : (O)0;
+            for (int j = 0; j < FI; j++) ov_[j] = ((emit >> j) & 1u) ? (O)spk[ix[j]] : (O)0;
         }
         const uint64_t ob = s_out;
         FSTAMP(5);
