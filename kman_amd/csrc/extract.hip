@@ -162,32 +162,50 @@ __global__ __launch_bounds__(ET) void count_kernel(const uint8_t *__restrict__ c
 // valid-window count and the radix-digit histograms of every pass of `plan`,
 // no keys written: the pre-pass of the fused extract + first sort pass
 // (kman_extract_sorted needs the global digit-0 counts before any key moves)
+#ifndef KMAN_KH_C
+#define KMAN_KH_C 2
+#endif
+// Counters are spread over KH_C copies (lane & (KH_C - 1)) interleaved per bin,
+// so same-digit lanes of one wave update different words.
+constexpr int KH_C = KMAN_KH_C;
+
 template <int EI, bool RC>
 __global__ __launch_bounds__(ET) void kmer_hist_kernel(const uint8_t *__restrict__ codes, uint64_t n_bases,
                                                        uint64_t n_tiles, int k, unsigned long long *__restrict__ count,
                                                        uint64_t *__restrict__ hist, Plan plan) {
     constexpr int TILE = ET * EI;
     __shared__ __attribute__((aligned(16))) uint8_t scodes[TILE + 64];
-    __shared__ uint32_t lhist[MAXPASS][256];
+    __shared__ uint32_t lhist[MAXPASS * 256 * KH_C];
     __shared__ uint32_t lds_scan[ET / 64];
     const uint64_t mask = k == 32 ? ~0ull : ((1ull << (2 * k)) - 1);
-    for (int i = threadIdx.x; i < MAXPASS * 256; i += ET) (&lhist[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < plan.npass * 256 * KH_C; i += ET) lhist[i] = 0;
+    const uint32_t copy = (uint32_t)lane_id() & (KH_C - 1);
     uint64_t acc = 0;
+    // the next tile's codes are loaded into registers while this one counts
+    CodeVecs<ET, EI> cv;
+    if ((uint64_t)blockIdx.x < n_tiles) load_codes<ET, EI>(codes, n_bases, (uint64_t)blockIdx.x * TILE, cv);
     for (uint64_t tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
         const uint64_t tb = tile * TILE;
-        stage_codes<ET, EI>(codes, n_bases, tb, scodes);
+        store_codes<ET, EI>(cv, codes, n_bases, tb, scodes);
         __syncthreads();
+        if (tile + gridDim.x < n_tiles) load_codes<ET, EI>(codes, n_bases, (tile + gridDim.x) * TILE, cv);
         uint64_t kf[EI], kr[EI];
         const uint64_t p0 = tb + (uint64_t)threadIdx.x * EI;
         const uint32_t valid = roll<EI, false>(scodes, threadIdx.x * EI, k, mask, p0, n_bases, kf, kr);
         acc += __popc(valid) * (RC ? 2 : 1);
+#if defined(KMAN_ABL) && (KMAN_ABL & 128)
+        // ablation build only: no histogram atomics
+        if (valid == 0x12345) acc += kf[3] ^ kr[5];
+        else continue;
+#endif
 #pragma unroll
         for (int j = 0; j < EI; j++) {
             if ((valid >> j) & 1u) {
                 for (int p = 0; p < plan.npass; p++) {
                     const uint32_t dm = (1u << plan.bits[p]) - 1;
-                    atomicAdd(&lhist[p][(uint32_t)(kf[j] >> plan.shift[p]) & dm], 1u);
-                    if (RC) atomicAdd(&lhist[p][(uint32_t)(kr[j] >> plan.shift[p]) & dm], 1u);
+                    uint32_t *h = lhist + p * 256 * KH_C + copy;
+                    atomicAdd(&h[((uint32_t)(kf[j] >> plan.shift[p]) & dm) * KH_C], 1u);
+                    if (RC) atomicAdd(&h[((uint32_t)(kr[j] >> plan.shift[p]) & dm) * KH_C], 1u);
                 }
             }
         }
@@ -197,7 +215,9 @@ __global__ __launch_bounds__(ET) void kmer_hist_kernel(const uint8_t *__restrict
     block_exclusive_scan<ET>((uint32_t)acc, SumU32(), 0u, lds_scan, &tot);
     if (threadIdx.x == 0 && tot) atomicAdd(count, (unsigned long long)tot);
     for (int p = 0; p < plan.npass; p++) {
-        const uint32_t c = lhist[p][threadIdx.x];
+        uint32_t c = 0;
+#pragma unroll
+        for (int cc = 0; cc < KH_C; cc++) c += lhist[(p * 256 + threadIdx.x) * KH_C + cc];
         if (c) atomicAdd((unsigned long long *)&hist[p * 256 + threadIdx.x], (unsigned long long)c);
     }
 }
@@ -329,4 +349,11 @@ int kman_kmer_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     *n_kmers = ctx->h_small[0];
     return KMAN_OK;
+}
+
+// diagnostic entry (not in kman.h): the histogram pre-pass alone, for timing
+extern "C" int kman_debug_kmer_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k,
+                                    uint32_t flags, uint32_t lo_bit, uint64_t *d_hist, uint64_t *n_kmers) {
+    if (!ctx || !n_kmers) return KMAN_EINVAL;
+    return kman_kmer_hist(ctx, d_codes, n_bases, k, flags, lo_bit, d_hist, n_kmers);
 }

@@ -7,21 +7,61 @@
 
 namespace {
 
-// the codes of windows [tb, tb + NT*EI) plus a 64-byte halo into LDS (16-byte
-// loads; past the padded end, code 4 = not ACGT)
+// The codes of windows [tb, tb + NT*EI) plus a 64-byte halo, in 16-byte
+// vectors (past the padded end, code 4 = not ACGT).  load_codes issues every
+// load of a thread (no wait); store_codes puts them into LDS.
+template <int NT, int EI>
+struct CodeVecs {
+    static constexpr int NV = (NT * EI + 64) / 16;  // 16-byte vectors
+    static constexpr int R = (NV + NT - 1) / NT;    // per thread
+    uint4 v[R];
+    bool full[R];
+};
+
+template <int NT, int EI>
+KMAN_DEV void load_codes(const uint8_t *__restrict__ codes, uint64_t n_bases, uint64_t tb, CodeVecs<NT, EI> &cv) {
+    using C = CodeVecs<NT, EI>;
+    const uint64_t limit = n_bases + 64;  // padded region is valid memory, value 4
+#pragma unroll
+    for (int i = 0; i < C::R; i++) {
+        const int vi = threadIdx.x + i * NT;
+        const uint64_t off = tb + (uint64_t)vi * 16;
+        cv.full[i] = vi < C::NV && off + 16 <= limit;
+        // unconditional (a safe address when not full); volatile keeps the
+        // compiler from sinking a load into its store's branch
+        const volatile uint4 *src = reinterpret_cast<const volatile uint4 *>(codes + (cv.full[i] ? off : 0));
+        cv.v[i].x = src->x;
+        cv.v[i].y = src->y;
+        cv.v[i].z = src->z;
+        cv.v[i].w = src->w;
+    }
+}
+
+template <int NT, int EI>
+KMAN_DEV void store_codes(const CodeVecs<NT, EI> &cv, const uint8_t *__restrict__ codes, uint64_t n_bases,
+                          uint64_t tb, uint8_t *s) {
+    using C = CodeVecs<NT, EI>;
+    const uint64_t limit = n_bases + 64;
+#pragma unroll
+    for (int i = 0; i < C::R; i++) {
+        const int vi = threadIdx.x + i * NT;
+        if (vi < C::NV) *reinterpret_cast<uint4 *>(s + vi * 16) = cv.v[i];
+    }
+    // the vectors that cross the padded end, byte by byte (last tile only)
+#pragma unroll
+    for (int i = 0; i < C::R; i++) {
+        const int vi = threadIdx.x + i * NT;
+        const uint64_t off = tb + (uint64_t)vi * 16;
+        if (vi < C::NV && !cv.full[i])
+            for (int b = 0; b < 16; b++) s[vi * 16 + b] = (off + b < limit) ? codes[off + b] : 4;
+    }
+}
+
 template <int NT, int EI>
 KMAN_DEV void stage_codes(const uint8_t *__restrict__ codes, uint64_t n_bases, uint64_t tb, uint8_t *s) {
-    constexpr int BYTES = NT * EI + 64;
-    const uint64_t limit = n_bases + 64;  // padded region is valid memory, value 4
-    for (int v = threadIdx.x; v < BYTES / 16; v += NT) {
-        const uint64_t off = tb + (uint64_t)v * 16;
-        if (off + 16 <= limit) {
-            *reinterpret_cast<uint4 *>(s + v * 16) = *reinterpret_cast<const uint4 *>(codes + off);
-        } else {
-#pragma unroll
-            for (int b = 0; b < 16; b++) s[v * 16 + b] = (off + b < limit) ? codes[off + b] : 4;
-        }
-    }
+    CodeVecs<NT, EI> cv;
+    load_codes<NT, EI>(codes, n_bases, tb, cv);
+    store_codes<NT, EI>(cv, codes, n_bases, tb, s);
 }
 
 // Roll the EI windows starting at s[base .. base+EI) (k from LDS bytes).
