@@ -68,10 +68,13 @@ int kman_scratch(kman_ctx *ctx, size_t bytes, void **p);
 int kman_aux(kman_ctx *ctx, size_t bytes, void **p);
 int kman_check_device_error(kman_ctx *ctx);
 // blocks of `fn` resident at once on the device (occupancy x CUs), capped at n_tiles
-int kman_persistent_grid(kman_ctx *ctx, const void *fn, int threads, uint64_t n_tiles);
+int kman_persistent_grid(kman_ctx *ctx, const void *fn, int threads, uint64_t n_tiles, size_t dyn_lds = 0);
 // internal (not in kman.h): the histogram pre-pass of kman_extract_sorted
 int kman_kmer_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
-                   uint32_t lo_bit, uint64_t *d_hist, uint64_t *n_kmers);
+                   uint32_t lo_bit, uint32_t nseg, uint64_t seg_w, uint64_t *d_seg, uint64_t *n_kmers);
+// the most segments (<= want) whose per-pass digit tables [pass][seg][bin] x copies
+// fit `lds_bytes`; radix of each pass from bits[]
+uint32_t kman_seg_fit(uint32_t np, const uint32_t *bits, uint32_t want, uint32_t copies, size_t lds_bytes);
 // synchronises; reads the inclusive value of the last tile of the most recent
 // look-back launch (checks its epoch) and the device error word.
 int kman_lookback_total(kman_ctx *ctx, uint64_t n_tiles, uint64_t *total);

@@ -33,6 +33,7 @@ struct Plan {
     int npass;
     uint8_t shift[MAXPASS];
     uint8_t bits[MAXPASS];
+    uint32_t off[MAXPASS];  // kmer_hist: first counter of each pass's [seg][bin] table
 };
 
 struct NoPos {};
@@ -172,13 +173,18 @@ constexpr int KH_C = KMAN_KH_C;
 template <int EI, bool RC>
 __global__ __launch_bounds__(ET) void kmer_hist_kernel(const uint8_t *__restrict__ codes, uint64_t n_bases,
                                                        uint64_t n_tiles, int k, unsigned long long *__restrict__ count,
-                                                       uint64_t *__restrict__ hist, Plan plan) {
+                                                       unsigned long long *__restrict__ seg_hist, Plan plan,
+                                                       uint32_t nseg, uint64_t seg_w) {
     constexpr int TILE = ET * EI;
     __shared__ __attribute__((aligned(16))) uint8_t scodes[TILE + 64];
-    __shared__ uint32_t lhist[MAXPASS * 256 * KH_C];
     __shared__ uint32_t lds_scan[ET / 64];
+    // counters [pass][seg][bin][copy]: pass p at plan.off[p]; segment of pass 0
+    // = window range (seg_w windows), of pass p >= 1 = group of digit p - 1
+    // ((d * nseg) >> bits): the input segments of the segmented passes
+    extern __shared__ uint32_t lhist[];
+    const uint32_t ncnt = plan.off[plan.npass - 1] + ((nseg << plan.bits[plan.npass - 1]) * KH_C);
     const uint64_t mask = k == 32 ? ~0ull : ((1ull << (2 * k)) - 1);
-    for (int i = threadIdx.x; i < plan.npass * 256 * KH_C; i += ET) lhist[i] = 0;
+    for (uint32_t i = threadIdx.x; i < ncnt; i += ET) lhist[i] = 0;
     const uint32_t copy = (uint32_t)lane_id() & (KH_C - 1);
     uint64_t acc = 0;
     // the next tile's codes are loaded into registers while this one counts
@@ -193,19 +199,28 @@ __global__ __launch_bounds__(ET) void kmer_hist_kernel(const uint8_t *__restrict
         const uint64_t p0 = tb + (uint64_t)threadIdx.x * EI;
         const uint32_t valid = roll<EI, false>(scodes, threadIdx.x * EI, k, mask, p0, n_bases, kf, kr);
         acc += __popc(valid) * (RC ? 2 : 1);
+        // EI windows of a thread never straddle a window segment (seg_w % EI == 0)
+        const uint32_t wseg = (uint32_t)(p0 / seg_w);
 #if defined(KMAN_ABL) && (KMAN_ABL & 128)
         // ablation build only: no histogram atomics
-        if (valid == 0x12345) acc += kf[3] ^ kr[5];
+        if (valid == 0x12345) acc += kf[3] ^ kr[5] ^ wseg;
         else continue;
 #endif
 #pragma unroll
         for (int j = 0; j < EI; j++) {
             if ((valid >> j) & 1u) {
+                uint32_t sf = wseg, sr = wseg;
                 for (int p = 0; p < plan.npass; p++) {
-                    const uint32_t dm = (1u << plan.bits[p]) - 1;
-                    uint32_t *h = lhist + p * 256 * KH_C + copy;
-                    atomicAdd(&h[((uint32_t)(kf[j] >> plan.shift[p]) & dm) * KH_C], 1u);
-                    if (RC) atomicAdd(&h[((uint32_t)(kr[j] >> plan.shift[p]) & dm) * KH_C], 1u);
+                    const uint32_t b = plan.bits[p], dm = (1u << b) - 1;
+                    uint32_t *h = lhist + plan.off[p] + copy;
+                    const uint32_t df = (uint32_t)(kf[j] >> plan.shift[p]) & dm;
+                    atomicAdd(&h[((sf << b) | df) * KH_C], 1u);
+                    sf = (df * nseg) >> b;
+                    if (RC) {
+                        const uint32_t dr = (uint32_t)(kr[j] >> plan.shift[p]) & dm;
+                        atomicAdd(&h[((sr << b) | dr) * KH_C], 1u);
+                        sr = (dr * nseg) >> b;
+                    }
                 }
             }
         }
@@ -215,10 +230,15 @@ __global__ __launch_bounds__(ET) void kmer_hist_kernel(const uint8_t *__restrict
     block_exclusive_scan<ET>((uint32_t)acc, SumU32(), 0u, lds_scan, &tot);
     if (threadIdx.x == 0 && tot) atomicAdd(count, (unsigned long long)tot);
     for (int p = 0; p < plan.npass; p++) {
-        uint32_t c = 0;
+        const uint32_t b = plan.bits[p];
+        for (uint32_t i = threadIdx.x; i < (nseg << b); i += ET) {
+            uint32_t c = 0;
 #pragma unroll
-        for (int cc = 0; cc < KH_C; cc++) c += lhist[(p * 256 + threadIdx.x) * KH_C + cc];
-        if (c) atomicAdd((unsigned long long *)&hist[p * 256 + threadIdx.x], (unsigned long long)c);
+            for (int cc = 0; cc < KH_C; cc++) c += lhist[plan.off[p] + i * KH_C + cc];
+            // output [pass][seg][256]
+            if (c) atomicAdd(&seg_hist[((uint64_t)p * nseg + (i >> b)) * 256 + (i & ((1u << b) - 1))],
+                             (unsigned long long)c);
+        }
     }
 }
 
@@ -321,28 +341,36 @@ extern "C" int kman_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_ba
 // pre-pass of kman_extract_sorted: n_kmers and d_hist (zeroed here) for the
 // passes over bits [lo_bit, 2k); flags: KMAN_RC only
 int kman_kmer_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
-                   uint32_t lo_bit, uint64_t *d_hist, uint64_t *n_kmers) {
+                   uint32_t lo_bit, uint32_t nseg, uint64_t seg_w, uint64_t *d_seg, uint64_t *n_kmers) {
     Plan plan{};
     uint32_t np, sh[MAXPASS], bi[MAXPASS];
     KMAN_TRY(kman_sort_plan_range(lo_bit, 2 * k, &np, sh, bi));
+    if (np == 0) return kman_fail(ctx, KMAN_EINVAL, "empty digit plan");
+    if (nseg < 1 || seg_w == 0 || seg_w % 16) return kman_fail(ctx, KMAN_EINVAL, "bad segments %u / %llu", nseg,
+                                                                (unsigned long long)seg_w);
     plan.npass = (int)np;
+    uint32_t ncnt = 0;
     for (uint32_t i = 0; i < np; i++) {
         plan.shift[i] = (uint8_t)sh[i];
         plan.bits[i] = (uint8_t)bi[i];
+        plan.off[i] = ncnt;
+        ncnt += (nseg << bi[i]) * KH_C;
     }
+    const size_t lds = (size_t)ncnt * 4;
+    if (lds > 64 * 1024) return kman_fail(ctx, KMAN_EINVAL, "histogram tables need %zu B of LDS", lds);
     void *scr;
     KMAN_TRY(kman_scratch(ctx, 256, &scr));
     HIP_TRY(ctx, hipMemsetAsync(scr, 0, 8, ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(d_hist, 0, MAXPASS * 256 * 8, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(d_seg, 0, (size_t)np * nseg * 256 * 8, ctx->stream));
     const bool rc = flags & KMAN_RC;
     const int EI = 16;
     const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * EI);
     auto fn = rc ? kmer_hist_kernel<16, true> : kmer_hist_kernel<16, false>;
-    const int grid = kman_persistent_grid(ctx, (const void *)fn, ET, n_tiles);
+    const int grid = kman_persistent_grid(ctx, (const void *)fn, ET, n_tiles, lds);
     {
         KTimer kt_(ctx, "kmer_hist");
-        hipLaunchKernelGGL(fn, dim3(grid), dim3(ET), 0, ctx->stream, d_codes, n_bases, n_tiles, (int)k,
-                           (unsigned long long *)scr, d_hist, plan);
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(ET), lds, ctx->stream, d_codes, n_bases, n_tiles, (int)k,
+                           (unsigned long long *)scr, (unsigned long long *)d_seg, plan, nseg, seg_w);
         HIP_TRY(ctx, hipGetLastError());
     }
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small, scr, 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -352,8 +380,9 @@ int kman_kmer_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint
 }
 
 // diagnostic entry (not in kman.h): the histogram pre-pass alone, for timing
+// (one segment; d_hist [pass][256])
 extern "C" int kman_debug_kmer_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k,
                                     uint32_t flags, uint32_t lo_bit, uint64_t *d_hist, uint64_t *n_kmers) {
     if (!ctx || !n_kmers) return KMAN_EINVAL;
-    return kman_kmer_hist(ctx, d_codes, n_bases, k, flags, lo_bit, d_hist, n_kmers);
+    return kman_kmer_hist(ctx, d_codes, n_bases, k, flags, lo_bit, 1, 1ull << 62, d_hist, n_kmers);
 }

@@ -37,9 +37,18 @@ int kman_scratch(kman_ctx *ctx, size_t bytes, void **p) {
     return KMAN_OK;
 }
 
-int kman_persistent_grid(kman_ctx *ctx, const void *fn, int threads, uint64_t n_tiles) {
+uint32_t kman_seg_fit(uint32_t np, const uint32_t *bits, uint32_t want, uint32_t copies, size_t lds_bytes) {
+    for (uint32_t s = want; s > 1; s--) {
+        size_t c = 0;
+        for (uint32_t p = 0; p < np; p++) c += (size_t)s << bits[p];
+        if (c * copies * 4 <= lds_bytes) return s;
+    }
+    return 1;
+}
+
+int kman_persistent_grid(kman_ctx *ctx, const void *fn, int threads, uint64_t n_tiles, size_t dyn_lds) {
     int per_cu = 1, cus = 256;
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, threads, dyn_lds);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
     uint64_t g = (uint64_t)(per_cu > 0 ? per_cu : 1) * (uint64_t)(cus > 0 ? cus : 1);
     if (g > n_tiles) g = n_tiles;

@@ -34,6 +34,20 @@ constexpr int LB = KMAN_LB;  // predecessor status words fetched per look-back r
 
 struct NoVal {};
 
+// A pass's input is cut into NSEG segments of contiguous tiles, each with its
+// own look-back chain; tile ids are handed out round robin over the segments
+// so the chains advance side by side.  A segment's bucket bases include the
+// digit counts of the segments before it (known before the pass), so no chain
+// ever waits on another.  With one chain, every tile in flight lies on it and
+// the inclusive-prefix frontier (TPD x LB tiles per look-back round) bounds
+// the pass.
+constexpr int NSEG = 8;
+struct SegDesc {
+    uint64_t start, end;  // input range (keys; windows for the extraction pass)
+    uint32_t tile0;       // status index of the segment's first tile
+    uint32_t ntiles;
+};
+
 #if defined(KMAN_ABL) && (KMAN_ABL & 4)
 // diagnostic build only: per-tile s_memrealtime stamps (100 MHz) at phase
 // boundaries, thread 0, into a buffer set with kman_debug_set
@@ -51,25 +65,26 @@ __device__ uint64_t *g_dbg;
 // One thread per digit walks back along that digit's tile chain, LB
 // predecessors per round (independent sc1 loads in flight), summing AGG
 // counts until it meets an INCL prefix.
-KMAN_DEV void digit_publish(uint64_t *st, int64_t tile, uint64_t agg, uint32_t epoch) {
-    st_store(&st[(uint64_t)tile * RADIX], st_make(tile == 0 ? ST_INCL : ST_AGG, epoch, agg));
+KMAN_DEV void digit_publish(uint64_t *st, int64_t tile, int64_t first, uint64_t agg, uint32_t epoch) {
+    st_store(&st[(uint64_t)tile * RADIX], st_make(tile == first ? ST_INCL : ST_AGG, epoch, agg));
 }
 
 template <bool PUBLISHED>
-KMAN_DEV uint64_t digit_lookback(uint64_t *st, int64_t tile, uint64_t agg, uint32_t epoch, uint32_t *err) {
-    if (tile == 0) {
-        if (!PUBLISHED) st_store(&st[0], st_make(ST_INCL, epoch, agg));
+KMAN_DEV uint64_t digit_lookback(uint64_t *st, int64_t tile, int64_t first, uint64_t agg, uint32_t epoch,
+                                uint32_t *err) {
+    if (tile == first) {
+        if (!PUBLISHED) st_store(&st[(uint64_t)tile * RADIX], st_make(ST_INCL, epoch, agg));
         return 0;
     }
     if (!PUBLISHED) st_store(&st[(uint64_t)tile * RADIX], st_make(ST_AGG, epoch, agg));
     uint64_t excl = 0;
     int64_t j = tile - 1;
     uint32_t spins = 0;
-    while (j >= 0) {
+    while (j >= first) {
         uint64_t w[LB];
 #pragma unroll
         for (int q = 0; q < LB; q++)
-            w[q] = (j - q >= 0) ? st_load(&st[(uint64_t)(j - q) * RADIX]) : st_make(ST_INCL, epoch, 0);
+            w[q] = (j - q >= first) ? st_load(&st[(uint64_t)(j - q) * RADIX]) : st_make(ST_INCL, epoch, 0);
         bool done = false, stall = false;
         int used = 0;
 #pragma unroll
@@ -102,18 +117,19 @@ KMAN_DEV uint64_t digit_lookback(uint64_t *st, int64_t tile, uint64_t agg, uint3
 // (predecessors per round) / (round latency) tiles per unit time: widening the
 // round is what raises it.  The aggregate has been published already (EARLY).
 template <int TPD>
-KMAN_DEV uint64_t group_lookback(uint64_t *st, int64_t tile, uint64_t agg, uint32_t epoch, uint32_t *err) {
+KMAN_DEV uint64_t group_lookback(uint64_t *st, int64_t tile, int64_t first, uint64_t agg, uint32_t epoch,
+                                uint32_t *err) {
     const int lane = lane_id();
     const int sub = lane % TPD;
     const int g0 = lane - sub;
-    if (tile == 0) return 0;  // tile 0 published its inclusive count with the aggregate
+    if (tile == first) return 0;  // a chain's first tile published its inclusive count with the aggregate
     uint64_t excl = 0;
     int64_t base = tile - 1;
     uint32_t spins = 0;
 #if defined(KMAN_ABL) && (KMAN_ABL & 4)
     uint64_t rounds_dbg = 0;
 #endif
-    while (base >= 0) {
+    while (base >= first) {
 #if defined(KMAN_ABL) && (KMAN_ABL & 4)
         rounds_dbg++;
 #endif
@@ -121,7 +137,7 @@ KMAN_DEV uint64_t group_lookback(uint64_t *st, int64_t tile, uint64_t agg, uint3
 #pragma unroll
         for (int q = 0; q < LB; q++) {
             const int64_t j = base - (int64_t)sub * LB - q;
-            w[q] = j >= 0 ? st_load(&st[(uint64_t)j * RADIX]) : st_make(ST_INCL, epoch, 0);
+            w[q] = j >= first ? st_load(&st[(uint64_t)j * RADIX]) : st_make(ST_INCL, epoch, 0);
         }
         // this lane's segment, in distance order: 0 all AGG, 1 met INCL, 2 stalled
         uint32_t state = 0, used = 0;
@@ -175,7 +191,8 @@ KMAN_DEV uint64_t group_lookback(uint64_t *st, int64_t tile, uint64_t agg, uint3
 // lut[key >> shift] (destination rank of a prefix range: kman_partition).
 template <int NT, int SI, bool EARLY, typename V, bool LUT = false, bool ATOMIC = false, int MINW = 1>
 __global__ __launch_bounds__(NT, MINW) void onesweep_pass(const uint64_t *__restrict__ kin, uint64_t *__restrict__ kout,
-                                                    const V *__restrict__ vin, V *__restrict__ vout, uint64_t n,
+                                                    const V *__restrict__ vin, V *__restrict__ vout,
+                                                    const SegDesc *__restrict__ segs, uint32_t nseg,
                                                     uint32_t shift, uint32_t bits,
                                                     const uint64_t *__restrict__ bucket_base,
                                                     uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
@@ -194,7 +211,15 @@ __global__ __launch_bounds__(NT, MINW) void onesweep_pass(const uint64_t *__rest
     __shared__ uint32_t lds_scan[NT / 64];
     __shared__ uint32_t lds_tile;
 
-    const int64_t tile = grab_tile(counter, &lds_tile);
+    // round-robin over the segments: id c -> tile c / nseg of segment c % nseg
+    const uint32_t cid = (uint32_t)grab_tile(counter, &lds_tile);
+    const uint32_t sgi = cid % nseg, jj = cid / nseg;
+    const SegDesc sd = segs[sgi];
+    if (jj >= sd.ntiles) return;  // (block-uniform) past a shorter segment's end
+    const int64_t tile = (int64_t)sd.tile0 + jj;  // status index
+    const int64_t first = sd.tile0;
+    const uint64_t n = sd.end;  // this segment's end bounds the tile
+    const uint64_t *__restrict__ bb = bucket_base + (uint64_t)sgi * RADIX;
     STAMP(0);
     const int lane = lane_id();
     const int w = threadIdx.x >> 6;
@@ -203,7 +228,7 @@ __global__ __launch_bounds__(NT, MINW) void onesweep_pass(const uint64_t *__rest
     for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&whist[0][0])[i] = 0;
     if (EARLY && threadIdx.x < RADIX) thist[threadIdx.x] = 0;
 
-    const uint64_t tb = (uint64_t)tile * TILE;
+    const uint64_t tb = sd.start + (uint64_t)jj * TILE;
     const uint64_t ib = tb + (uint64_t)w * (SI * 64) + lane;
     uint64_t key[SI];
     uint32_t rank[SI];
@@ -245,7 +270,7 @@ __global__ __launch_bounds__(NT, MINW) void onesweep_pass(const uint64_t *__rest
 #pragma unroll
             for (int ww = 0; ww < NWAVE; ww++) c += whist[ww][threadIdx.x];
             thist[threadIdx.x] = c;
-            digit_publish(status + threadIdx.x, tile, c, epoch);
+            digit_publish(status + threadIdx.x, tile, first, c, epoch);
         }
     } else {
         if (EARLY) {
@@ -255,7 +280,7 @@ __global__ __launch_bounds__(NT, MINW) void onesweep_pass(const uint64_t *__rest
             for (int i = 0; i < SI; i++)
                 if (ib + (uint64_t)i * 64 < n) atomicAdd(&thist[DIGIT(key[i])], 1u);
             __syncthreads();
-            if (threadIdx.x < radix) digit_publish(status + threadIdx.x, tile, thist[threadIdx.x], epoch);
+            if (threadIdx.x < radix) digit_publish(status + threadIdx.x, tile, first, thist[threadIdx.x], epoch);
         }
 
         // stable in-wave ranking: items in order, lanes in order (ballot match-any)
@@ -306,7 +331,7 @@ __global__ __launch_bounds__(NT, MINW) void onesweep_pass(const uint64_t *__rest
     }
 #if defined(KMAN_ABL) && (KMAN_ABL & 1)
     // ablation build only: no look-back (wrong offsets, measures the rest)
-    if (d0 < radix) gstart[d0] = bucket_base[d0] + (uint64_t)tile * TILE / radix - ls;
+    if (d0 < radix) gstart[d0] = bb[d0] + (uint64_t)jj * TILE / radix - ls;
 #else
     if constexpr (EARLY) {
         // several lanes per digit walk the chain (see group_lookback)
@@ -314,14 +339,14 @@ __global__ __launch_bounds__(NT, MINW) void onesweep_pass(const uint64_t *__rest
         if (threadIdx.x < radix * tpd) {
             const uint32_t d = threadIdx.x / tpd;
             uint64_t excl;
-            if (tpd == 4) excl = group_lookback<4>(status + d, tile, thist[d], epoch, err);
-            else if (tpd == 2) excl = group_lookback<2>(status + d, tile, thist[d], epoch, err);
-            else excl = group_lookback<1>(status + d, tile, thist[d], epoch, err);
-            if (threadIdx.x % tpd == 0) gstart[d] = bucket_base[d] + excl - lstart[d];
+            if (tpd == 4) excl = group_lookback<4>(status + d, tile, first, thist[d], epoch, err);
+            else if (tpd == 2) excl = group_lookback<2>(status + d, tile, first, thist[d], epoch, err);
+            else excl = group_lookback<1>(status + d, tile, first, thist[d], epoch, err);
+            if (threadIdx.x % tpd == 0) gstart[d] = bb[d] + excl - lstart[d];
         }
     } else if (d0 < radix) {
-        const uint64_t excl = digit_lookback<EARLY>(status + d0, tile, tot, epoch, err);
-        gstart[d0] = bucket_base[d0] + excl - ls;
+        const uint64_t excl = digit_lookback<EARLY>(status + d0, tile, first, tot, epoch, err);
+        gstart[d0] = bb[d0] + excl - ls;
     }
 #endif
     __syncthreads();
@@ -375,7 +400,8 @@ constexpr int XT = 512;
 
 template <int EI, bool RC, typename V, bool ATOMIC>
 __global__ __launch_bounds__(XT) void extract_pass(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
-                                                   uint64_t *__restrict__ kout, V *__restrict__ vout, uint32_t shift,
+                                                   uint64_t *__restrict__ kout, V *__restrict__ vout,
+                                                   const SegDesc *__restrict__ segs, uint32_t nseg, uint32_t shift,
                                                    uint32_t bits, const uint64_t *__restrict__ bucket_base,
                                                    uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
                                                    uint32_t epoch, uint32_t *__restrict__ err) {
@@ -394,14 +420,22 @@ __global__ __launch_bounds__(XT) void extract_pass(const uint8_t *__restrict__ c
     __shared__ uint32_t lds_scan[NWAVE];
     __shared__ uint32_t lds_tile;
 
-    const int64_t tile = grab_tile(counter, &lds_tile);
+    // round-robin over the window segments (see SegDesc)
+    const uint32_t cid = (uint32_t)grab_tile(counter, &lds_tile);
+    const uint32_t sgi = cid % nseg, jj = cid / nseg;
+    const SegDesc sd = segs[sgi];
+    if (jj >= sd.ntiles) return;
+    const int64_t tile = (int64_t)sd.tile0 + jj;
+    const int64_t first = sd.tile0;
+    const uint64_t *__restrict__ bb = bucket_base + (uint64_t)sgi * RADIX;
     const int lane = lane_id();
     const int w = threadIdx.x >> 6;
     const uint32_t radix = 1u << bits;
     const uint32_t dmask = radix - 1;
     const uint32_t kb = 2u * (uint32_t)k;
     const uint64_t keymask = kb >= 64 ? ~0ull : ((1ull << kb) - 1);
-    const uint64_t wb = (uint64_t)tile * WIN;
+    const uint64_t wb = sd.start + (uint64_t)jj * WIN;
+    // segments end on tile boundaries, except the last at n_bases
     uint8_t *scodes = reinterpret_cast<uint8_t *>(skeys);
     stage_codes<NT, EI>(codes, n_bases, wb, scodes);
     for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&whist[0][0])[i] = 0;
@@ -445,14 +479,14 @@ __global__ __launch_bounds__(XT) void extract_pass(const uint8_t *__restrict__ c
 #pragma unroll
             for (int ww = 0; ww < NWAVE; ww++) c += whist[ww][threadIdx.x];
             thist[threadIdx.x] = c;
-            digit_publish(status + threadIdx.x, tile, c, epoch);
+            digit_publish(status + threadIdx.x, tile, first, c, epoch);
         }
     } else {
 #pragma unroll
         for (int i = 0; i < SI; i++)
             if (ib + i * 64 < tcnt) atomicAdd(&thist[XDIGIT(key[i])], 1u);
         __syncthreads();
-        if (threadIdx.x < radix) digit_publish(status + threadIdx.x, tile, thist[threadIdx.x], epoch);
+        if (threadIdx.x < radix) digit_publish(status + threadIdx.x, tile, first, thist[threadIdx.x], epoch);
 #pragma unroll
         for (int i = 0; i < SI; i++) {
             const bool valid_i = ib + i * 64 < tcnt;
@@ -498,10 +532,10 @@ __global__ __launch_bounds__(XT) void extract_pass(const uint8_t *__restrict__ c
         if (threadIdx.x < radix * tpd) {
             const uint32_t d = threadIdx.x / tpd;
             uint64_t excl;
-            if (tpd == 4) excl = group_lookback<4>(status + d, tile, thist[d], epoch, err);
-            else if (tpd == 2) excl = group_lookback<2>(status + d, tile, thist[d], epoch, err);
-            else excl = group_lookback<1>(status + d, tile, thist[d], epoch, err);
-            if (threadIdx.x % tpd == 0) gstart[d] = bucket_base[d] + excl - lstart[d];
+            if (tpd == 4) excl = group_lookback<4>(status + d, tile, first, thist[d], epoch, err);
+            else if (tpd == 2) excl = group_lookback<2>(status + d, tile, first, thist[d], epoch, err);
+            else excl = group_lookback<1>(status + d, tile, first, thist[d], epoch, err);
+            if (threadIdx.x % tpd == 0) gstart[d] = bb[d] + excl - lstart[d];
         }
     }
     __syncthreads();
@@ -537,65 +571,157 @@ __global__ __launch_bounds__(XT) void extract_pass(const uint8_t *__restrict__ c
 #undef XDIGIT
 }
 
-__global__ __launch_bounds__(256) void histogram_kernel(const uint64_t *__restrict__ keys, uint64_t n, int npass,
-                                                        const uint32_t *__restrict__ shift_bits,
+// digit tables [pass][seg][256] of every pass: the segment of pass 0 is the
+// position range (seg_len keys), of pass p >= 1 the group of digit p - 1
+// ((d * nseg) >> bits, see SegDesc); counters in dynamic LDS at off[p]
+struct HistPlan {
+    uint32_t np, nseg;
+    uint64_t seg_len;
+    uint8_t shift[MAXPASS], bits[MAXPASS];
+    uint32_t off[MAXPASS];
+};
+
+__global__ __launch_bounds__(256) void histogram_kernel(const uint64_t *__restrict__ keys, uint64_t n, HistPlan hp,
                                                         unsigned long long *__restrict__ hist) {
-    __shared__ uint32_t lh[MAXPASS][RADIX];
-    for (int i = threadIdx.x; i < MAXPASS * RADIX; i += 256) (&lh[0][0])[i] = 0;
+    extern __shared__ uint32_t lh[];
+    const uint32_t ncnt = hp.off[hp.np - 1] + (hp.nseg << hp.bits[hp.np - 1]);
+    for (uint32_t i = threadIdx.x; i < ncnt; i += 256) lh[i] = 0;
     __syncthreads();
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         const uint64_t k = keys[i];
-        for (int p = 0; p < npass; p++) {
-            const uint32_t sh = shift_bits[p] & 0xff, b = shift_bits[p] >> 8;
-            atomicAdd(&lh[p][(uint32_t)(k >> sh) & ((1u << b) - 1)], 1u);
+        uint32_t sg = (uint32_t)(i / hp.seg_len);
+        for (uint32_t p = 0; p < hp.np; p++) {
+            const uint32_t b = hp.bits[p];
+            const uint32_t d = (uint32_t)(k >> hp.shift[p]) & ((1u << b) - 1);
+            atomicAdd(&lh[hp.off[p] + ((sg << b) | d)], 1u);
+            sg = (d * hp.nseg) >> b;
         }
     }
     __syncthreads();
-    for (int p = 0; p < npass; p++) {
-        const uint32_t c = lh[p][threadIdx.x];
-        if (c) atomicAdd(&hist[p * RADIX + threadIdx.x], (unsigned long long)c);
+    for (uint32_t p = 0; p < hp.np; p++) {
+        const uint32_t b = hp.bits[p];
+        for (uint32_t i = threadIdx.x; i < (hp.nseg << b); i += 256) {
+            const uint32_t c = lh[hp.off[p] + i];
+            if (c) atomicAdd(&hist[((uint64_t)p * hp.nseg + (i >> b)) * RADIX + (i & ((1u << b) - 1))],
+                             (unsigned long long)c);
+        }
     }
 }
 
+// Segments of one pass over n keys in tiles of TILE: cut at `cut` (nseg + 1
+// positions), bucket bases per segment from the global digit counts g and the
+// segment tables t ([nseg][RADIX], null: one segment).  Checks every segment's
+// table against its length.
+int plan_pass(kman_ctx *ctx, uint64_t n, uint64_t tile, uint32_t nseg, const uint64_t *cut, const uint64_t *g,
+              const uint64_t *t, SegDesc *segs, uint64_t *bases, uint32_t *tiles_total, uint32_t *max_tiles) {
+    uint64_t run[RADIX];
+    uint64_t acc = 0;
+    for (int d = 0; d < RADIX; d++) {
+        run[d] = acc;
+        acc += g[d];
+    }
+    if (acc != n)
+        return kman_fail(ctx, KMAN_EINVAL, "digit histogram sums to %llu, expected %llu", (unsigned long long)acc,
+                         (unsigned long long)n);
+    uint32_t t0 = 0, mx = 0;
+    for (uint32_t sg = 0; sg < nseg; sg++) {
+        const uint64_t len = cut[sg + 1] - cut[sg];
+        if (t) {
+            uint64_t sum = 0;
+            for (int d = 0; d < RADIX; d++) sum += t[(uint64_t)sg * RADIX + d];
+            if (sum != len)
+                return kman_fail(ctx, KMAN_EINVAL, "segment %u table sums to %llu, length %llu", sg,
+                                 (unsigned long long)sum, (unsigned long long)len);
+        }
+        for (int d = 0; d < RADIX; d++) {
+            bases[(uint64_t)sg * RADIX + d] = run[d];
+            run[d] += t ? t[(uint64_t)sg * RADIX + d] : g[d];
+        }
+        const uint32_t nt = (uint32_t)ceil_div(len, tile);
+        segs[sg] = SegDesc{cut[sg], cut[sg + 1], t0, nt};
+        t0 += nt;
+        mx = nt > mx ? nt : mx;
+    }
+    *tiles_total = t0;
+    *max_tiles = mx;
+    return KMAN_OK;
+}
+
+// cut points of pass p's input: equal tile-aligned ranges (by_pos), or the
+// groups of the previous pass's digit (global counts prev, bits pbits)
+void pass_cuts(uint64_t n, uint64_t tile, uint32_t nseg, bool by_pos, const uint64_t *prev, uint32_t pbits,
+               uint64_t *cut) {
+    if (by_pos) {
+        const uint64_t len = ceil_div(ceil_div(n, tile), nseg) * tile;
+        for (uint32_t sg = 0; sg <= nseg; sg++) cut[sg] = sg * len < n ? sg * len : n;
+        return;
+    }
+    const uint32_t r = 1u << pbits;
+    uint64_t acc = 0;
+    uint32_t d = 0;
+    for (uint32_t sg = 0; sg <= nseg; sg++) {
+        const uint32_t lim = (uint32_t)ceil_div((uint64_t)sg * r, nseg);  // first digit of group sg
+        while (d < lim && d < r) acc += prev[d++];
+        cut[sg] = sg == nseg ? n : acc;
+    }
+}
+
+// The onesweep passes of a plan.  h_hist: global digit counts [pass][RADIX];
+// h_seg: segment tables [pass][nseg][RADIX] (null: one chain per pass).  The
+// first pass's input is cut by position (prev null) or by the groups of the
+// previous pass's digit (prev: its global counts, pbits: its width).
 template <int NT, int SI, bool EARLY, typename V, int MINW>
 int run_passes(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, V *v0, V *v1, uint64_t n, uint32_t np, const uint32_t *sh,
-               const uint32_t *bi, const uint64_t *h_hist, int *result_in_alt) {
-    // bucket bases per pass (host: 256 x npass), skipping single-bucket passes
-    uint64_t bases[MAXPASS][RADIX];
+               const uint32_t *bi, const uint64_t *h_hist, const uint64_t *h_seg, uint32_t nseg, const uint64_t *prev,
+               uint32_t pbits, int *result_in_alt) {
+    constexpr uint64_t TILE = (uint64_t)NT * SI;
+    if (!h_seg) nseg = 1;
+    // per pass: the segment descriptors, then the bases [nseg][RADIX]
+    constexpr size_t PER_PASS = NSEG * sizeof(SegDesc) + NSEG * RADIX * 8;
+    static thread_local unsigned char tab[MAXPASS * PER_PASS];
+    uint32_t tiles[MAXPASS], maxt[MAXPASS];
     bool skip[MAXPASS];
     for (uint32_t p = 0; p < np; p++) {
-        uint64_t acc = 0;
+        const uint64_t *g = h_hist + (uint64_t)p * RADIX;
         skip[p] = false;
-        for (int d = 0; d < RADIX; d++) {
-            bases[p][d] = acc;
-            const uint64_t c = h_hist[p * RADIX + d];
-            if (c == n) skip[p] = true;
-            acc += c;
+        for (int d = 0; d < RADIX; d++) skip[p] |= g[d] == n;
+        uint64_t cut[NSEG + 1];
+        if (nseg == 1) {
+            cut[0] = 0;
+            cut[1] = n;
+        } else if (p == 0) {
+            pass_cuts(n, TILE, nseg, prev == nullptr, prev, pbits, cut);
+        } else {
+            pass_cuts(n, TILE, nseg, false, h_hist + (uint64_t)(p - 1) * RADIX, bi[p - 1], cut);
         }
-        if (acc != n)
-            return kman_fail(ctx, KMAN_EINVAL, "histogram of pass %u sums to %llu, expected %llu", p,
-                             (unsigned long long)acc, (unsigned long long)n);
+        SegDesc *segs = reinterpret_cast<SegDesc *>(tab + p * PER_PASS);
+        uint64_t *bases = reinterpret_cast<uint64_t *>(tab + p * PER_PASS + NSEG * sizeof(SegDesc));
+        KMAN_TRY(plan_pass(ctx, n, TILE, nseg, cut, g, h_seg ? h_seg + (uint64_t)p * nseg * RADIX : nullptr, segs,
+                           bases, &tiles[p], &maxt[p]));
     }
     void *scr;
-    KMAN_TRY(kman_scratch(ctx, sizeof(bases), &scr));
-    HIP_TRY(ctx, hipMemcpyAsync(scr, bases, sizeof(bases), hipMemcpyHostToDevice, ctx->stream));
-    const uint64_t n_tiles = ceil_div(n, (uint64_t)NT * SI);
+    KMAN_TRY(kman_scratch(ctx, np * PER_PASS, &scr));
+    HIP_TRY(ctx, hipMemcpyAsync(scr, tab, np * PER_PASS, hipMemcpyHostToDevice, ctx->stream));
     int cur = 0;
     uint64_t *kb[2] = {k0, k1};
     V *vb[2] = {v0, v1};
     for (uint32_t p = 0; p < np; p++) {
         if (skip[p]) continue;
+        const SegDesc *d_segs = reinterpret_cast<const SegDesc *>((const unsigned char *)scr + p * PER_PASS);
+        const uint64_t *d_bases =
+            reinterpret_cast<const uint64_t *>((const unsigned char *)scr + p * PER_PASS + NSEG * sizeof(SegDesc));
         uint32_t epoch, *counter;
-        KMAN_TRY(kman_lookback_begin(ctx, n_tiles * RADIX, &epoch, &counter));
+        KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)tiles[p] * RADIX, &epoch, &counter));
+        const uint32_t grid = nseg * maxt[p];
         KTimer kt_(ctx, "sort_pass");
         if (ctx->lds_atomic_ordered)
-            hipLaunchKernelGGL((onesweep_pass<NT, SI, EARLY, V, false, true, MINW>), dim3((uint32_t)n_tiles), dim3(NT), 0,
-                               ctx->stream, kb[cur], kb[cur ^ 1], vb[cur], vb[cur ^ 1], n, sh[p], bi[p],
-                               (const uint64_t *)scr + p * RADIX, ctx->d_status, counter, epoch, ctx->d_err, nullptr);
+            hipLaunchKernelGGL((onesweep_pass<NT, SI, EARLY, V, false, true, MINW>), dim3(grid), dim3(NT), 0,
+                               ctx->stream, kb[cur], kb[cur ^ 1], vb[cur], vb[cur ^ 1], d_segs, nseg, sh[p], bi[p],
+                               d_bases, ctx->d_status, counter, epoch, ctx->d_err, nullptr);
         else
-            hipLaunchKernelGGL((onesweep_pass<NT, SI, EARLY, V, false, false, MINW>), dim3((uint32_t)n_tiles), dim3(NT), 0, ctx->stream,
-                               kb[cur], kb[cur ^ 1], vb[cur], vb[cur ^ 1], n, sh[p], bi[p],
-                               (const uint64_t *)scr + p * RADIX, ctx->d_status, counter, epoch, ctx->d_err, nullptr);
+            hipLaunchKernelGGL((onesweep_pass<NT, SI, EARLY, V, false, false, MINW>), dim3(grid), dim3(NT), 0,
+                               ctx->stream, kb[cur], kb[cur ^ 1], vb[cur], vb[cur ^ 1], d_segs, nseg, sh[p], bi[p],
+                               d_bases, ctx->d_status, counter, epoch, ctx->d_err, nullptr);
         HIP_TRY(ctx, hipGetLastError());
         cur ^= 1;
     }
@@ -605,13 +731,16 @@ int run_passes(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, V *v0, V *v1, uint64_t
 
 template <int NT, int SI, bool EARLY = true, int MINW = 1>
 int dispatch_vals(kman_ctx *ctx, uint64_t *k0, uint64_t *k1, void *v0, void *v1, uint32_t vb, uint64_t n, uint32_t np,
-                  const uint32_t *sh, const uint32_t *bi, const uint64_t *h_hist, int *res) {
-    if (vb == 0) return run_passes<NT, SI, EARLY, NoVal, MINW>(ctx, k0, k1, nullptr, nullptr, n, np, sh, bi, h_hist, res);
+                  const uint32_t *sh, const uint32_t *bi, const uint64_t *h_hist, const uint64_t *h_seg, uint32_t nseg,
+                  const uint64_t *prev, uint32_t pbits, int *res) {
+    if (vb == 0)
+        return run_passes<NT, SI, EARLY, NoVal, MINW>(ctx, k0, k1, nullptr, nullptr, n, np, sh, bi, h_hist, h_seg,
+                                                      nseg, prev, pbits, res);
     if (vb == 4)
-        return run_passes<NT, SI, EARLY, uint32_t, MINW>(ctx, k0, k1, (uint32_t *)v0, (uint32_t *)v1, n, np, sh, bi, h_hist,
-                                                   res);
-    return run_passes<NT, SI, EARLY, uint64_t, MINW>(ctx, k0, k1, (uint64_t *)v0, (uint64_t *)v1, n, np, sh, bi, h_hist,
-                                               res);
+        return run_passes<NT, SI, EARLY, uint32_t, MINW>(ctx, k0, k1, (uint32_t *)v0, (uint32_t *)v1, n, np, sh, bi,
+                                                         h_hist, h_seg, nseg, prev, pbits, res);
+    return run_passes<NT, SI, EARLY, uint64_t, MINW>(ctx, k0, k1, (uint64_t *)v0, (uint64_t *)v1, n, np, sh, bi,
+                                                     h_hist, h_seg, nseg, prev, pbits, res);
 }
 
 }  // namespace
@@ -662,42 +791,69 @@ extern "C" int kman_sort_range(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys
     if (kman_sort_plan_range(lo_bit, hi_bit, &np, sh, bi) != KMAN_OK)
         return kman_fail(ctx, KMAN_EINVAL, "bad bit range [%u, %u)", lo_bit, hi_bit);
     if (np == 0) return KMAN_OK;
-    // histograms of every pass (device), then to the host for the bucket bases
-    unsigned long long *hist;
-    void *scr;
-    KMAN_TRY(kman_scratch(ctx, MAXPASS * RADIX * 8 + 256, &scr));
-    hist = (unsigned long long *)scr;
+    // digit tables of every pass (device), then to the host for the bucket bases:
+    // per segment when computed here, global only when the caller gives them
+    constexpr uint64_t TILE = 512 * 16;
+    uint32_t nseg = d_hist ? 1u : kman_seg_fit(np, bi, NSEG, 1, 48 * 1024);
+    unsigned long long *hist = nullptr;
+    void *scr = nullptr;
+    const size_t hbytes = (size_t)np * nseg * RADIX * 8;
+    // (in scratch, not aux: kman_finish holds its big-segment list in aux across
+    // the nested full sort; run_passes reuses scratch only after the download)
+    if (!d_hist) KMAN_TRY(kman_scratch(ctx, hbytes, (void **)&hist));
+    static thread_local uint64_t h_hist[MAXPASS * RADIX];
+    static thread_local uint64_t h_seg[MAXPASS * NSEG * RADIX];
     if (d_hist) {
-        HIP_TRY(ctx, hipMemcpyAsync(hist, d_hist, np * RADIX * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        HIP_TRY(ctx, hipMemcpyAsync(h_hist, d_hist, np * RADIX * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     } else {
-        uint32_t *d_sb = (uint32_t *)((char *)scr + MAXPASS * RADIX * 8);
-        uint32_t sb[MAXPASS];
-        for (uint32_t p = 0; p < np; p++) sb[p] = sh[p] | (bi[p] << 8);
-        HIP_TRY(ctx, hipMemsetAsync(hist, 0, np * RADIX * 8, ctx->stream));
-        HIP_TRY(ctx, hipMemcpyAsync(d_sb, sb, sizeof(sb), hipMemcpyHostToDevice, ctx->stream));
+        HistPlan hp{};
+        hp.np = np;
+        hp.nseg = nseg;
+        hp.seg_len = ceil_div(ceil_div(n, TILE), nseg) * TILE;
+        uint32_t ncnt = 0;
+        for (uint32_t p = 0; p < np; p++) {
+            hp.shift[p] = (uint8_t)sh[p];
+            hp.bits[p] = (uint8_t)bi[p];
+            hp.off[p] = ncnt;
+            ncnt += nseg << bi[p];
+        }
+        HIP_TRY(ctx, hipMemsetAsync(hist, 0, hbytes, ctx->stream));
         const uint64_t blocks = ceil_div(n, 256 * 16);
         KTimer kt_(ctx, "sort_hist");
-        hipLaunchKernelGGL(histogram_kernel, dim3((uint32_t)(blocks < 2048 ? blocks : 2048)), dim3(256), 0,
-                           ctx->stream, d_keys, n, (int)np, d_sb, hist);
+        hipLaunchKernelGGL(histogram_kernel, dim3((uint32_t)(blocks < 2048 ? blocks : 2048)), dim3(256),
+                           (size_t)ncnt * 4, ctx->stream, d_keys, n, hp, hist);
         HIP_TRY(ctx, hipGetLastError());
+        HIP_TRY(ctx, hipMemcpyAsync(h_seg, hist, hbytes, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        for (uint32_t p = 0; p < np; p++)
+            for (int d = 0; d < RADIX; d++) {
+                uint64_t c = 0;
+                for (uint32_t sg = 0; sg < nseg; sg++) c += h_seg[((uint64_t)p * nseg + sg) * RADIX + d];
+                h_hist[p * RADIX + d] = c;
+            }
     }
-    static thread_local uint64_t h_hist[MAXPASS * RADIX];
-    HIP_TRY(ctx, hipMemcpyAsync(h_hist, hist, np * RADIX * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    (void)scr;
+    const uint64_t *hs = d_hist ? nullptr : h_seg;
     static const int cfg = [] {
         const char *e = getenv("KMAN_SORT_CFG");  // tuning experiments only
         return e ? atoi(e) : 0;
     }();
+    if (cfg) nseg = 1, hs = nullptr;  // (tile-size experiments: one chain, global bases)
+#define KMAN_DV(NT_, SI_, ...)                                                                                     \
+    KMAN_TRY((dispatch_vals<NT_, SI_, ##__VA_ARGS__>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, \
+                                                      sh, bi, h_hist, hs, nseg, nullptr, 0, result_in_alt)))
     switch (cfg) {
-        case 1: KMAN_TRY((dispatch_vals<512, 12>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
-        case 2: KMAN_TRY((dispatch_vals<256, 24>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
-        case 3: KMAN_TRY((dispatch_vals<1024, 8>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
-        case 4: KMAN_TRY((dispatch_vals<256, 16>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
-        case 6: KMAN_TRY((dispatch_vals<256, 16, false>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
-        case 7: KMAN_TRY((dispatch_vals<512, 12, false>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
-        case 5: KMAN_TRY((dispatch_vals<256, 8>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
-        default: KMAN_TRY((dispatch_vals<512, 16>(ctx, d_keys, d_keys_alt, d_vals, d_vals_alt, val_bytes, n, np, sh, bi, h_hist, result_in_alt))); break;
+        case 1: KMAN_DV(512, 12); break;
+        case 2: KMAN_DV(256, 24); break;
+        case 3: KMAN_DV(1024, 8); break;
+        case 4: KMAN_DV(256, 16); break;
+        case 6: KMAN_DV(256, 16, false); break;
+        case 7: KMAN_DV(512, 12, false); break;
+        case 5: KMAN_DV(256, 8); break;
+        default: KMAN_DV(512, 16); break;
     }
+#undef KMAN_DV
     return kman_check_device_error(ctx);
 }
 
@@ -717,14 +873,16 @@ int launch_partition(kman_ctx *ctx, const uint64_t *kin, uint64_t *kout, const V
     const uint64_t n_tiles = ceil_div(n, (uint64_t)NT * SI);
     uint32_t epoch, *counter;
     KMAN_TRY(kman_lookback_begin(ctx, n_tiles * RADIX, &epoch, &counter));
+    // one chain: the segment descriptor rides behind the bases in scratch
+    const SegDesc *d_seg = reinterpret_cast<const SegDesc *>(d_base + RADIX);
     KTimer kt_(ctx, "partition");
     if (ctx->lds_atomic_ordered)
         hipLaunchKernelGGL((onesweep_pass<NT, SI, true, V, true, true>), dim3((uint32_t)n_tiles), dim3(NT), 0,
-                           ctx->stream, kin, kout, vin, vout, n, lut_shift, bits, d_base, ctx->d_status, counter,
-                           epoch, ctx->d_err, lut);
+                           ctx->stream, kin, kout, vin, vout, d_seg, 1u, lut_shift, bits, d_base, ctx->d_status,
+                           counter, epoch, ctx->d_err, lut);
     else
         hipLaunchKernelGGL((onesweep_pass<NT, SI, true, V, true>), dim3((uint32_t)n_tiles), dim3(NT), 0, ctx->stream,
-                           kin, kout, vin, vout, n, lut_shift, bits, d_base, ctx->d_status, counter, epoch,
+                           kin, kout, vin, vout, d_seg, 1u, lut_shift, bits, d_base, ctx->d_status, counter, epoch,
                            ctx->d_err, lut);
     HIP_TRY(ctx, hipGetLastError());
     return KMAN_OK;
@@ -749,9 +907,16 @@ extern "C" int kman_partition(kman_ctx *ctx, const uint64_t *d_keys, uint64_t *d
                          (unsigned long long)n);
     uint32_t bits = 1;
     while ((1u << bits) < nbuckets) bits++;
+    struct {
+        uint64_t base[RADIX];
+        SegDesc seg;
+    } tab;
+    memcpy(tab.base, base, sizeof(base));
+    tab.seg = SegDesc{0, n, 0, (uint32_t)ceil_div(n, 512 * 12)};
     void *scr;
-    KMAN_TRY(kman_scratch(ctx, sizeof(base), &scr));
-    HIP_TRY(ctx, hipMemcpyAsync(scr, base, sizeof(base), hipMemcpyHostToDevice, ctx->stream));
+    KMAN_TRY(kman_scratch(ctx, sizeof(tab), &scr));
+    HIP_TRY(ctx, hipMemcpyAsync(scr, &tab, sizeof(tab), hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     const uint64_t *d_base = (const uint64_t *)scr;
     if (val_bytes == 0)
         KMAN_TRY(launch_partition<NoVal>(ctx, d_keys, d_keys_out, nullptr, nullptr, n, d_lut, lut_shift, bits, d_base));
@@ -768,17 +933,20 @@ extern "C" int kman_partition(kman_ctx *ctx, const uint64_t *d_keys, uint64_t *d
 namespace {
 template <int EI, bool RC, typename V>
 int launch_extract_pass(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, uint32_t k, uint64_t *kout, V *vout,
-                        uint32_t shift, uint32_t bits, const uint64_t *d_base) {
-    const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)XT * EI);
+                        uint32_t shift, uint32_t bits, const SegDesc *d_segs, uint32_t nseg, uint32_t n_tiles,
+                        uint32_t max_tiles, const uint64_t *d_base) {
     uint32_t epoch, *counter;
-    KMAN_TRY(kman_lookback_begin(ctx, n_tiles * RADIX, &epoch, &counter));
+    KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)n_tiles * RADIX, &epoch, &counter));
     KTimer kt_(ctx, "extract_pass");
+    const uint32_t grid = nseg * max_tiles;
     if (ctx->lds_atomic_ordered)
-        hipLaunchKernelGGL((extract_pass<EI, RC, V, true>), dim3((uint32_t)n_tiles), dim3(XT), 0, ctx->stream, codes,
-                           n_bases, (int)k, kout, vout, shift, bits, d_base, ctx->d_status, counter, epoch, ctx->d_err);
+        hipLaunchKernelGGL((extract_pass<EI, RC, V, true>), dim3(grid), dim3(XT), 0, ctx->stream, codes, n_bases,
+                           (int)k, kout, vout, d_segs, nseg, shift, bits, d_base, ctx->d_status, counter, epoch,
+                           ctx->d_err);
     else
-        hipLaunchKernelGGL((extract_pass<EI, RC, V, false>), dim3((uint32_t)n_tiles), dim3(XT), 0, ctx->stream, codes,
-                           n_bases, (int)k, kout, vout, shift, bits, d_base, ctx->d_status, counter, epoch, ctx->d_err);
+        hipLaunchKernelGGL((extract_pass<EI, RC, V, false>), dim3(grid), dim3(XT), 0, ctx->stream, codes, n_bases,
+                           (int)k, kout, vout, d_segs, nseg, shift, bits, d_base, ctx->d_status, counter, epoch,
+                           ctx->d_err);
     HIP_TRY(ctx, hipGetLastError());
     return KMAN_OK;
 }
@@ -817,44 +985,80 @@ extern "C" int kman_extract_sorted(kman_ctx *ctx, const uint8_t *d_codes, uint64
                                result_in_alt);
     }
     const bool rc = flags & KMAN_RC;
+    uint32_t np, sh[MAXPASS], bi[MAXPASS];
+    KMAN_TRY(kman_sort_plan_range(lo_bit, 2 * k, &np, sh, bi));
+    // window segments of the extraction pass: whole tiles, equal counts
+    const uint64_t WIN = (uint64_t)XT * (rc ? 8 : 16);
+    const uint32_t nseg = kman_seg_fit(np, bi, NSEG, 2, 48 * 1024);
+    const uint64_t xtiles = ceil_div(n_bases, WIN);
+    const uint64_t tps = ceil_div(xtiles, nseg);
+    uint64_t *d_seg;
+    KMAN_TRY(kman_aux(ctx, (size_t)np * nseg * RADIX * 8, (void **)&d_seg));
     uint64_t n;
-    KMAN_TRY(kman_kmer_hist(ctx, d_codes, n_bases, k, rc ? KMAN_RC : 0u, lo_bit, d_hist, &n));
+    KMAN_TRY(kman_kmer_hist(ctx, d_codes, n_bases, k, rc ? KMAN_RC : 0u, lo_bit, nseg, tps * WIN, d_seg, &n));
     if (n > cap)
         return kman_fail(ctx, KMAN_ECAP, "key capacity %llu < %llu", (unsigned long long)cap, (unsigned long long)n);
     *n_kmers = n;
     if (n == 0) return KMAN_OK;
-    uint32_t np, sh[MAXPASS], bi[MAXPASS];
-    KMAN_TRY(kman_sort_plan_range(lo_bit, 2 * k, &np, sh, bi));
+    static thread_local uint64_t h_seg[MAXPASS * NSEG * RADIX];
     static thread_local uint64_t h_hist[MAXPASS * RADIX];
-    static thread_local uint64_t h_base[RADIX];
-    HIP_TRY(ctx, hipMemcpyAsync(h_hist, d_hist, np * RADIX * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(h_seg, d_seg, (size_t)np * nseg * RADIX * 8, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    uint64_t acc = 0;
-    for (int d = 0; d < RADIX; d++) {
-        h_base[d] = acc;
-        acc += h_hist[d];
+    for (uint32_t p = 0; p < np; p++)
+        for (int d = 0; d < RADIX; d++) {
+            uint64_t c = 0;
+            for (uint32_t sg = 0; sg < nseg; sg++) c += h_seg[((uint64_t)p * nseg + sg) * RADIX + d];
+            h_hist[p * RADIX + d] = c;
+        }
+    // pass 0 tables: segment descriptors over windows, bases per segment
+    struct {
+        SegDesc segs[NSEG];
+        uint64_t base[NSEG][RADIX];
+    } tab;
+    {
+        uint64_t run[RADIX], acc = 0;
+        for (int d = 0; d < RADIX; d++) {
+            run[d] = acc;
+            acc += h_hist[d];
+        }
+        if (acc != n)
+            return kman_fail(ctx, KMAN_EINVAL, "digit histogram sums to %llu, expected %llu", (unsigned long long)acc,
+                             (unsigned long long)n);
+        for (uint32_t sg = 0; sg < nseg; sg++) {
+            for (int d = 0; d < RADIX; d++) {
+                tab.base[sg][d] = run[d];
+                run[d] += h_seg[(uint64_t)sg * RADIX + d];
+            }
+            const uint64_t t0 = sg * tps < xtiles ? sg * tps : xtiles;
+            const uint64_t t1 = (sg + 1) * tps < xtiles ? (sg + 1) * tps : xtiles;
+            tab.segs[sg] = SegDesc{t0 * WIN, t1 * WIN < n_bases ? t1 * WIN : n_bases, (uint32_t)t0,
+                                   (uint32_t)(t1 - t0)};
+        }
     }
-    if (acc != n) return kman_fail(ctx, KMAN_EINVAL, "digit histogram sums to %llu, expected %llu",
-                                   (unsigned long long)acc, (unsigned long long)n);
     void *scr;
-    KMAN_TRY(kman_scratch(ctx, RADIX * 8, &scr));
-    HIP_TRY(ctx, hipMemcpyAsync(scr, h_base, RADIX * 8, hipMemcpyHostToDevice, ctx->stream));
+    KMAN_TRY(kman_scratch(ctx, sizeof(tab), &scr));
+    HIP_TRY(ctx, hipMemcpyAsync(scr, &tab, sizeof(tab), hipMemcpyHostToDevice, ctx->stream));
+    const SegDesc *d_segs = (const SegDesc *)scr;
+    const uint64_t *d_base = (const uint64_t *)((const char *)scr + sizeof(tab.segs));
+    const uint32_t nt = (uint32_t)xtiles, mt = (uint32_t)tps;
     if (rc) {
         if (vb) KMAN_TRY((launch_extract_pass<8, true, uint32_t>(ctx, d_codes, n_bases, k, d_keys, (uint32_t *)d_pos,
-                                                                sh[0], bi[0], (const uint64_t *)scr)));
+                                                                sh[0], bi[0], d_segs, nseg, nt, mt, d_base)));
         else KMAN_TRY((launch_extract_pass<8, true, NoVal>(ctx, d_codes, n_bases, k, d_keys, nullptr, sh[0], bi[0],
-                                                           (const uint64_t *)scr)));
+                                                           d_segs, nseg, nt, mt, d_base)));
     } else {
         if (vb) KMAN_TRY((launch_extract_pass<16, false, uint32_t>(ctx, d_codes, n_bases, k, d_keys,
-                                                                  (uint32_t *)d_pos, sh[0], bi[0],
-                                                                  (const uint64_t *)scr)));
+                                                                  (uint32_t *)d_pos, sh[0], bi[0], d_segs, nseg, nt,
+                                                                  mt, d_base)));
         else KMAN_TRY((launch_extract_pass<16, false, NoVal>(ctx, d_codes, n_bases, k, d_keys, nullptr, sh[0], bi[0],
-                                                             (const uint64_t *)scr)));
+                                                             d_segs, nseg, nt, mt, d_base)));
     }
-    // the remaining prefix passes, ping-ponging from the pass-0 output
+    // the remaining prefix passes, ping-ponging from the pass-0 output; their
+    // input segments are the groups of the previous digit
     if (np > 1) {
         KMAN_TRY((dispatch_vals<512, 16>(ctx, d_keys, d_keys_alt, d_pos, d_pos_alt, vb, n, np - 1, sh + 1, bi + 1,
-                                         h_hist + RADIX, result_in_alt)));
+                                         h_hist + RADIX, h_seg + (uint64_t)nseg * RADIX, nseg, h_hist, bi[0],
+                                         result_in_alt)));
     }
     return kman_check_device_error(ctx);
 }
