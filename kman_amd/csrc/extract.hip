@@ -170,7 +170,7 @@ __global__ __launch_bounds__(ET) void count_kernel(const uint8_t *__restrict__ c
 // so same-digit lanes of one wave update different words.
 constexpr int KH_C = KMAN_KH_C;
 
-template <int EI, bool RC>
+template <int EI, bool RC, int NP>
 __global__ __launch_bounds__(ET) void kmer_hist_kernel(const uint8_t *__restrict__ codes, uint64_t n_bases,
                                                        uint64_t n_tiles, int k, unsigned long long *__restrict__ count,
                                                        unsigned long long *__restrict__ seg_hist, Plan plan,
@@ -182,7 +182,7 @@ __global__ __launch_bounds__(ET) void kmer_hist_kernel(const uint8_t *__restrict
     // = window range (seg_w windows), of pass p >= 1 = group of digit p - 1
     // ((d * nseg) >> bits): the input segments of the segmented passes
     extern __shared__ uint32_t lhist[];
-    const uint32_t ncnt = plan.off[plan.npass - 1] + ((nseg << plan.bits[plan.npass - 1]) * KH_C);
+    const uint32_t ncnt = plan.off[NP - 1] + ((nseg << plan.bits[NP - 1]) * KH_C);
     const uint64_t mask = k == 32 ? ~0ull : ((1ull << (2 * k)) - 1);
     for (uint32_t i = threadIdx.x; i < ncnt; i += ET) lhist[i] = 0;
     const uint32_t copy = (uint32_t)lane_id() & (KH_C - 1);
@@ -210,7 +210,9 @@ __global__ __launch_bounds__(ET) void kmer_hist_kernel(const uint8_t *__restrict
         for (int j = 0; j < EI; j++) {
             if ((valid >> j) & 1u) {
                 uint32_t sf = wseg, sr = wseg;
-                for (int p = 0; p < plan.npass; p++) {
+                // NP passes unrolled: the plan sits in scalar registers
+#pragma unroll
+                for (int p = 0; p < NP; p++) {
                     const uint32_t b = plan.bits[p], dm = (1u << b) - 1;
                     uint32_t *h = lhist + plan.off[p] + copy;
                     const uint32_t df = (uint32_t)(kf[j] >> plan.shift[p]) & dm;
@@ -365,7 +367,15 @@ int kman_kmer_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint
     const bool rc = flags & KMAN_RC;
     const int EI = 16;
     const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * EI);
-    auto fn = rc ? kmer_hist_kernel<16, true> : kmer_hist_kernel<16, false>;
+    if (np > 4) return kman_fail(ctx, KMAN_EINVAL, "histogram pre-pass plans at most 4 passes, got %u", np);
+    using KFn = void (*)(const uint8_t *, uint64_t, uint64_t, int, unsigned long long *, unsigned long long *, Plan,
+                         uint32_t, uint64_t);
+    static const KFn fns[2][4] = {
+        {kmer_hist_kernel<16, false, 1>, kmer_hist_kernel<16, false, 2>, kmer_hist_kernel<16, false, 3>,
+         kmer_hist_kernel<16, false, 4>},
+        {kmer_hist_kernel<16, true, 1>, kmer_hist_kernel<16, true, 2>, kmer_hist_kernel<16, true, 3>,
+         kmer_hist_kernel<16, true, 4>}};
+    const KFn fn = fns[rc ? 1 : 0][np - 1];
     const int grid = kman_persistent_grid(ctx, (const void *)fn, ET, n_tiles, lds);
     {
         KTimer kt_(ctx, "kmer_hist");

@@ -974,7 +974,10 @@ extern "C" int kman_extract_sorted(kman_ctx *ctx, const uint8_t *d_codes, uint64
     KMAN_TRY(kman_aux(ctx, MAXPASS * RADIX * 8, (void **)&d_hist));
     // the fused path: forward / -r keys of k <= 25 (the tile-local window index
     // rides in the 14 bits above the key), u32 or no payload
-    const bool fused = !(flags & KMAN_CANONICAL) && k <= 25 && lo_bit < 2 * k && vb != 8;
+    // (and at most 4 prefix passes: the histogram pre-pass's unrolled plans)
+    uint32_t np0, sh0[MAXPASS], bi0[MAXPASS];
+    KMAN_TRY(kman_sort_plan_range(lo_bit, 2 * k, &np0, sh0, bi0));
+    const bool fused = !(flags & KMAN_CANONICAL) && k <= 25 && lo_bit < 2 * k && vb != 8 && np0 <= 4;
     if (!fused) {
         HIP_TRY(ctx, hipMemsetAsync(d_hist, 0, MAXPASS * RADIX * 8, ctx->stream));
         uint64_t n;
