@@ -81,6 +81,8 @@ def main() -> None:
     ap.add_argument("--mode", choices=["uniq", "count"], default="uniq")
     ap.add_argument("--bases", type=int, default=1_000_000_000, help="synthetic bases per GPU (1 GB FASTA)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--path", choices=["region", "split", "full"], default="region",
+                    help="single-GPU engine path (region falls back to split outside its domain)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -107,7 +109,7 @@ def main() -> None:
         dist.broadcast_object_list(uid, src=0)
         pipe = kd.DistPipeline(dev, text, args.k, args.mode, world, rank, uid[0])
     else:
-        pipe = engine.ResidentPipeline(dev, text, args.k, mode=args.mode)
+        pipe = engine.ResidentPipeline(dev, text, args.k, mode=args.mode, path=args.path)
     fasta_bytes = len(text)
     del text
 
@@ -136,23 +138,28 @@ def main() -> None:
     else:
         total_kmers = float(kmers)
 
-    # live roofline of the dominant kernel (sort pass), from HIP events
-    n_pass, pass_ms = pipe.timed("sort_pass")
+    # live roofline of the dominant kernel (the digit pass), from HIP events
+    # recorded on the engine's own stream around every launch
+    region = getattr(pipe, "path", "split") == "region"
+    n_pass, pass_ms = pipe.timed("region_pass" if region else "sort_pass")
     stages = {}
-    for tag in ("parse", "kmer_hist", "extract_pass", "extract", "prefix_hist", "partition", "sort_hist", "sort_pass",
-                "finish", "rle_count", "rle_uniq"):
+    for tag in ("parse", "region_extract", "region_pass", "region_finish", "kmer_hist", "extract_pass", "extract",
+                "prefix_hist", "partition", "sort_hist", "sort_pass", "finish", "rle_count", "rle_uniq"):
         c, ms = pipe.timed(tag)
         if c:
             stages[tag] = round(ms / args.steps, 3)
     avg_pass_s = pass_ms / n_pass / 1e3
-    bytes_per_key = 16 + (2 * pipe.pos_bytes if args.mode == "uniq" else 0)
+    # region path: one packed u64 item read + written per k-mer; LSD path: the
+    # key read + written, plus the pos payload read + written (uniq)
+    bytes_per_key = 16 if region else 16 + (2 * pipe.pos_bytes if args.mode == "uniq" else 0)
     achieved = bytes_per_key * pipe.n_sorted / avg_pass_s / 1e9
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_sort_pass.json")
     if os.path.isfile(pmc):
         with open(pmc) as fh:
             p = json.load(fh)
-        if p.get("mode") == args.mode and p.get("k") == args.k and p.get("bases") == args.bases:
+        if (p.get("mode") == args.mode and p.get("k") == args.k and p.get("bases") == args.bases
+                and p.get("kernel", "onesweep_pass") == ("rg_pass" if region else "onesweep_pass")):
             traffic = p.get("hbm_bytes_per_launch")
 
     if rank != 0:
@@ -180,10 +187,12 @@ def main() -> None:
             "k": args.k,
             "mode": args.mode,
             "parallelism": "dp%d: prefix-range partition + RCCL all-to-all" % world if world > 1 else "single",
+            "path": getattr(pipe, "path", "dist"),
             "stages_ms_per_step": stages,
         },
         "roofline": {
-            "kernel": "onesweep_pass (LSD digit pass, %d per step)" % (n_pass // args.steps),
+            "kernel": ("rg_pass (per-bucket MSD digit pass over packed u64 items, %d per step)" if region else
+                       "onesweep_pass (LSD digit pass, %d per step)") % (n_pass // args.steps),
             "bound": "hbm",
             "achieved": achieved,
             "peak": HBM_PEAK_GBS,

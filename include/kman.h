@@ -16,6 +16,10 @@
  *   kman_sort_range    the same, by a prefix of the key bits
  *   kman_finish        Batch.sorted / Crawler.do_batch + join_* over prefix-sorted keys
  *                                                         batch.py:156-168, join.py:95-130,244-285
+ *   kman_groups        the whole count / uniq chain of one stream:
+ *                      yield_kmers -> Batch.sorted -> Crawler -> join_*
+ *                                                         seq.py:285-328, batch.py:156-168,
+ *                                                         join.py:63-130,244-285
  *   kman_rle_count     Crawler.do_batch + join_sequence_count
  *                                                         kmermaid/join.py:95-130,266-285
  *   kman_rle_uniq      Crawler.do_batch + join_unique     kmermaid/join.py:95-130,244-263
@@ -59,6 +63,7 @@ extern "C" {
 #define KMAN_ETIMEOUT (-5) /* a device-side wait exceeded its bound (engine bug) */
 #define KMAN_ECOMM (-6)    /* RCCL error */
 #define KMAN_ECAP (-7)     /* output capacity too small; *needed reports the size */
+#define KMAN_EFALLBACK (-8) /* kman_groups: input outside the region path; use the general path */
 
 /* kman_extract flags */
 #define KMAN_RC 1u          /* also emit reverse complements (kmer -r, seq.py:274-282) */
@@ -184,6 +189,28 @@ int kman_extract_sorted(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases,
 int kman_finish(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, void *d_vals, void *d_vals_alt,
                 uint32_t val_bytes, uint64_t n, uint32_t key_bits, uint32_t lo_bit, int mode,
                 uint64_t *d_okeys, void *d_ovals, uint32_t oval_bytes, uint64_t *n_out);
+
+/* Count / uniq of one k-mer stream straight from the base codes, through
+ * padded regions of packed items (region.hip): extraction scattered by the
+ * top 8 key bits, one pass per 8-bit bucket by the next bits, then one LDS
+ * block per region sorts, groups and emits.  Replaces the chain
+ * Sequence.yield_kmers -> Batch.sorted -> Crawler.do_records/do_batch ->
+ * KJoiner.join_sequence_count | join_unique (seq.py:285-328,
+ * batch.py:156-168, join.py:63-130,244-285) for one batch stream; same output
+ * arrays as kman_extract_sorted + kman_finish(COUNT | UNIQ):
+ *   COUNT  d_okeys[j], d_ovals[j] = group size (oval_bytes 4 | 8)
+ *   UNIQ   d_okeys[j], d_ovals[j] = pos of the keys that occur once
+ * in ascending key order; *n_kmers = k-mers extracted, *n_out = rows.
+ * kman_groups_plan gives the work-area size, or KMAN_EFALLBACK when the input
+ * is outside the path (canonical, k > 25, too many k-mers for the region
+ * capacities).  kman_groups returns KMAN_EFALLBACK also when a region
+ * overflowed (a strongly skewed prefix distribution); the outputs are then
+ * undefined and the caller runs the general path.  d_okeys / d_ovals hold
+ * up to n_bases x (RC ? 2 : 1) entries. */
+int kman_groups_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, uint64_t *work_bytes);
+int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags, int mode,
+                void *d_work, uint64_t work_bytes, uint64_t *d_okeys, void *d_ovals, uint32_t oval_bytes,
+                uint64_t *n_kmers, uint64_t *n_out);
 
 /* Run-length count of sorted keys (join.py:95-130 + 266-285):
  * d_ukeys[j], d_counts[j] (u32 if count_bytes == 4 else u64). */

@@ -27,6 +27,7 @@ KMAN_EFORMAT = -4
 KMAN_ETIMEOUT = -5
 KMAN_ECOMM = -6
 KMAN_ECAP = -7
+KMAN_EFALLBACK = -8
 
 KMAN_RC = 1
 KMAN_WANT_POS = 2
@@ -93,6 +94,12 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_uint32, c_int,
          c_void_p, c_void_p, c_uint32, POINTER(c_uint64)],
+    ),
+    "kman_groups_plan": (c_int, [c_uint64, c_uint32, c_uint32, c_int, POINTER(c_uint64)]),
+    "kman_groups": (
+        c_int,
+        [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_int, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32,
+         POINTER(c_uint64), POINTER(c_uint64)],
     ),
     "kman_rle_count": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, POINTER(c_uint64)]),
     "kman_rle_uniq": (

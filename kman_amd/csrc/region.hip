@@ -1,0 +1,738 @@
+// region.hip — `kmer count` / `kmer uniq` of one FASTA stream in three
+// kernels, through padded regions of packed items (kman_groups).
+//
+// Replaces, for one device-resident batch stream, the whole chain
+//   Sequence.yield_kmers (kmermaid/seq.py:285-328) -> Batch.sorted
+//   (batch.py:156-168, forced by batcher.py:392) -> Crawler.do_records /
+//   do_batch (join.py:63-130) -> join_sequence_count / join_unique
+//   (join.py:244-285)
+// for the inputs whose shape allows it (uniform-ish prefix distribution, k <=
+// 25; anything else returns KMAN_EFALLBACK and the caller runs
+// kman_extract_sorted + kman_finish, which handle every input).
+//
+// MSD instead of the LSD prefix passes of sort.hip:
+//   pass 0 (rg_extract)  rolls the windows of a tile and scatters them by the
+//                        top 8 key bits b into region (b, s) of capacity C0,
+//                        s = one of RS position segments (own look-back
+//                        chains).  b is implied by the region from here on, so
+//                        an item is ONE u64: (key minus its top 8 bits) << Q |
+//                        window index (Q bits; Q = 0 in count mode).
+//   pass 1 (rg_pass)     per bucket b (its own chain over the regions (b, *)):
+//                        scatter by the next B2 key bits d into region
+//                        r = (b << B2 | d) of capacity C1 <= FCAP.
+//   finish (rg_finish)   one 1024-thread block per region r: load it (<= FCAP
+//                        items, 144 KiB of LDS), LSD-sort the remaining key
+//                        bits in LDS, run-length pass, emit (key, count) or the
+//                        keys that occur once with their pos, compacted by one
+//                        look-back over the regions in key order.
+// No digit histogram is computed before any pass: every region has a fixed
+// capacity (1.5x its expected fill), the passes publish their final region
+// counts themselves, and a region that would overflow raises a device flag
+// (nothing is written past a capacity) that turns the call into
+// KMAN_EFALLBACK.  Algorithmic HBM bytes per k-mer: 1 code read + 8 (pass 0)
+// + 16 (pass 1) + 8 (finish read) + the output, against 13 + 2 x 24 + 12 for
+// the LSD pipeline of the same workload.
+#include "common.h"
+#include "kmer.h"
+#include "onesweep.h"
+
+#include <cstdlib>
+
+namespace {
+
+constexpr int RT = 512;           // threads of passes 0 and 1
+constexpr int RS = 64;            // position segments of pass 0 (one wave of counts)
+constexpr int RSI = 16;           // items per thread, pass 1
+constexpr uint64_t T1 = (uint64_t)RT * RSI;  // pass-1 tile
+constexpr int FT = 1024;          // finish threads
+constexpr int FW = FT / 64;
+constexpr int FIPT = 17;          // finish items per thread
+constexpr int FCAP = FT * FIPT;   // 17408 items = 136 KiB: largest region
+constexpr int FBITS = 9;          // finish LSD digit (26 bits: 3 passes)
+constexpr int FRAD = 1 << FBITS;
+constexpr int FWORD = FRAD / 2;   // per-wave counters: two u16 per word
+constexpr uint32_t ERR_REGION = 1u << 8;  // a region would overflow (not an engine fault)
+constexpr uint32_t B1 = 8;        // pass-0 digit = top 8 key bits
+
+KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t bits) {
+    // stable in-wave rank among equal digits (ballot match-any), lane order
+    const int lane = lane_id();
+    uint64_t peers = __ballot(valid);
+    for (uint32_t b = 0; b < bits; b++) {
+        const bool set = (d >> b) & 1u;
+        const uint64_t m = __ballot(set);
+        peers &= set ? m : ~m;
+    }
+    uint32_t before = 0;
+    if (valid) before = hist[d];
+    const uint32_t r = before + (uint32_t)__popcll(peers & lanemask_lt());
+    const int leader = __ffsll((unsigned long long)peers) - 1;
+    if (valid && lane == leader) hist[d] = before + (uint32_t)__popcll(peers);
+    return r;
+}
+
+// ---------------------------------------------------------------- pass 0
+// A tile of RT*EI window starts: windows rolled from LDS-staged codes, the
+// valid ones compacted in stream order (tile-local window << 1 | strand
+// packed above the 2k key bits), ranked by the top 8 key bits, digit counts
+// published early, grouped look-back per digit along the segment's chain,
+// LDS-staged coalesced scatter into region (b, s).
+template <int EI, bool RC, bool ATOMIC>
+__global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
+                                                 uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
+                                                 uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ cnt0,
+                                                 uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
+                                                 uint32_t epoch, uint32_t *__restrict__ err) {
+    constexpr int NT = RT;
+    constexpr int NWAVE = NT / 64;
+    constexpr int WIN = NT * EI;
+    constexpr int TILE = WIN * (RC ? 2 : 1);
+    constexpr int SI = TILE / NT;
+    static_assert(WIN + 64 <= TILE * 8, "codes fit in the key staging area");
+    __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
+    __shared__ uint32_t whist[NWAVE][RADIX];
+    __shared__ uint32_t thist[RADIX];
+    __shared__ uint32_t lstart[RADIX];
+    __shared__ uint64_t gexcl[RADIX];
+    __shared__ uint32_t lds_scan[NWAVE];
+    __shared__ uint32_t lds_tile;
+
+    const uint32_t cid = (uint32_t)grab_tile(counter, &lds_tile);
+    const uint32_t sgi = cid % RS, jj = cid / RS;
+    const uint32_t t0 = sgi * seg_tiles;
+    const uint32_t t1 = t0 + seg_tiles < n_tiles ? t0 + seg_tiles : n_tiles;
+    if (t0 + jj >= t1) return;  // (block-uniform) past a segment's end
+    const int64_t tile = (int64_t)t0 + jj;
+    const int64_t first = t0;
+    const int lane = lane_id();
+    const int w = threadIdx.x >> 6;
+    const uint32_t kb = 2u * (uint32_t)k;
+    const uint32_t shift = kb - B1;
+    const uint64_t keymask = kb >= 64 ? ~0ull : ((1ull << kb) - 1);
+    const uint64_t restmask = (1ull << shift) - 1;
+    const uint64_t wb = (uint64_t)tile * WIN;
+    uint8_t *scodes = reinterpret_cast<uint8_t *>(skeys);
+    stage_codes<NT, EI>(codes, n_bases, wb, scodes);
+    for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&whist[0][0])[i] = 0;
+    if (threadIdx.x < RADIX) thist[threadIdx.x] = 0;
+    __syncthreads();
+
+    uint64_t kf[EI], kr[EI];
+    const uint32_t w0 = threadIdx.x * EI;
+    const uint32_t valid = roll<EI, false>(scodes, w0, k, keymask, wb + w0, n_bases, kf, kr);
+    uint32_t tcnt;
+    const uint32_t off = block_exclusive_scan<NT>((uint32_t)__popc(valid) * (RC ? 2u : 1u), SumU32(), 0u, lds_scan,
+                                                  &tcnt);
+    {
+        uint32_t o = off;
+#pragma unroll
+        for (int j = 0; j < EI; j++) {
+            if ((valid >> j) & 1u) {
+                const uint64_t tag = (uint64_t)((w0 + j) << 1) << kb;
+                skeys[o++] = kf[j] | tag;
+                if (RC) skeys[o++] = kr[j] | tag | (1ull << kb);
+            }
+        }
+    }
+    __syncthreads();
+
+    const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
+    uint64_t key[SI];
+    uint32_t rank[SI];
+#pragma unroll
+    for (int i = 0; i < SI; i++) key[i] = ib + i * 64 < tcnt ? skeys[ib + i * 64] : 0;
+#define XDIGIT(x) ((uint32_t)(((x) & keymask) >> shift))
+    if (ATOMIC) {
+#pragma unroll
+        for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&whist[w][XDIGIT(key[i])], 1u) : 0u;
+        __syncthreads();
+        if (threadIdx.x < RADIX) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int ww = 0; ww < NWAVE; ww++) c += whist[ww][threadIdx.x];
+            thist[threadIdx.x] = c;
+            digit_publish(status + threadIdx.x, tile, first, c, epoch);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < SI; i++)
+            if (ib + i * 64 < tcnt) atomicAdd(&thist[XDIGIT(key[i])], 1u);
+        __syncthreads();
+        if (threadIdx.x < RADIX) digit_publish(status + threadIdx.x, tile, first, thist[threadIdx.x], epoch);
+#pragma unroll
+        for (int i = 0; i < SI; i++) rank[i] = ballot_rank(whist[w], XDIGIT(key[i]), ib + i * 64 < tcnt, B1);
+    }
+    __syncthreads();
+    const uint32_t d0 = threadIdx.x;
+    uint32_t tot = 0;
+    if (d0 < RADIX) {
+#pragma unroll
+        for (int ww = 0; ww < NWAVE; ww++) {
+            const uint32_t c = whist[ww][d0];
+            whist[ww][d0] = tot;
+            tot += c;
+        }
+    }
+    const uint32_t ls = block_exclusive_scan<NT>(tot, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
+    if (d0 < RADIX) lstart[d0] = ls;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < SI; i++) {
+        if (ib + i * 64 < tcnt) {
+            const uint32_t d = XDIGIT(key[i]);
+            skeys[lstart[d] + whist[w][d] + rank[i]] = key[i];
+        }
+    }
+    {
+        constexpr uint32_t TPD = NT / RADIX >= 4 ? 4 : (NT / RADIX >= 2 ? 2 : 1);
+        if (threadIdx.x < RADIX * TPD) {
+            const uint32_t d = threadIdx.x / TPD;
+            const uint64_t excl = group_lookback<TPD>(status + d, tile, first, thist[d], epoch, err);
+            if (threadIdx.x % TPD == 0) {
+                gexcl[d] = excl;
+                const uint64_t incl = excl + thist[d];
+                if (incl > C0) atomicOr(err, ERR_REGION);
+                if (tile == (int64_t)t1 - 1) cnt0[d * RS + sgi] = (uint32_t)(incl < C0 ? incl : C0);
+            }
+        }
+    }
+    __syncthreads();
+    constexpr int RQ = (TILE + NT - 1) / NT;
+#pragma unroll
+    for (int r = 0; r < RQ; r++) {
+        const uint32_t q = threadIdx.x + r * NT;
+        if (q < tcnt) {
+            const uint64_t kk = skeys[q];
+            const uint32_t d = XDIGIT(kk);
+            const uint64_t at = gexcl[d] + (q - lstart[d]);
+            if (at < C0) {
+                const uint64_t f = kk >> kb;  // tile-local (window << 1 | strand)
+                const uint64_t win = wb + (f >> 1);
+                const uint64_t idx = RC ? ((win << 1) | (f & 1u)) : win;
+                out[((uint64_t)d * RS + sgi) * C0 + at] = Q ? (((kk & restmask) << Q) | idx) : (kk & restmask);
+            }
+        }
+    }
+#undef XDIGIT
+}
+
+// ---------------------------------------------------------------- pass 1
+// One tile of the regions (b, 0..RS-1) of bucket b (cid round robin over the
+// buckets; tile r of a bucket numbers its regions' tiles in region order), so
+// each bucket is its own look-back chain.  Digit = item bits [shift, shift +
+// bits); output region (b << bits | d) of capacity C1.  The bucket's last tile
+// writes the final region counts.
+template <bool ATOMIC>
+__global__ __launch_bounds__(RT, 4) void rg_pass(const uint64_t *__restrict__ in, uint64_t C0,
+                                              const uint32_t *__restrict__ cnt0, const uint32_t *__restrict__ lim_p,
+                                              uint32_t maxt, uint32_t shift, uint32_t bits,
+                                              uint64_t *__restrict__ out, uint64_t C1, uint32_t *__restrict__ cnt1,
+                                              uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
+                                              uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg) {
+    constexpr int NT = RT, SI = RSI, TILE = NT * SI, NWAVE = NT / 64;
+    __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
+    __shared__ uint32_t whist[NWAVE][RADIX];
+    __shared__ uint32_t thist[RADIX];
+    __shared__ uint32_t lstart[RADIX];
+    __shared__ uint64_t gexcl[RADIX];
+    __shared__ uint32_t lds_scan[NWAVE];
+    __shared__ uint32_t spre[RS + 1];
+    __shared__ uint32_t lds_tile;
+    static_assert(RS <= 64 && (RS & (RS - 1)) == 0, "region prefixes: one wave, binary search");
+
+    // persistent: tile ids until the bucket-major limit (rg_tiles); a block
+    // finishes its tile before taking the next, so every predecessor of a
+    // tile is taken and in progress (forward progress of the look-back)
+    const uint32_t lim = *lim_p;
+    for (;;) {
+    const uint32_t cid = (uint32_t)grab_tile(counter, &lds_tile);
+    if (cid >= lim) break;
+    const uint32_t b = cid % RADIX, r = cid / RADIX;
+    // the bucket's RS regions read as one concatenated sequence of items
+    if (threadIdx.x < 64) {
+        const uint32_t c = threadIdx.x < RS ? cnt0[b * RS + threadIdx.x] : 0u;
+        const uint32_t inc = wave_inclusive_scan(c, SumU32());
+        if (threadIdx.x < RS) spre[threadIdx.x + 1] = inc;
+        if (threadIdx.x == 0) spre[0] = 0;
+    }
+    __syncthreads();
+    const uint32_t items = spre[RS];
+    const uint32_t total = (items + TILE - 1) / TILE;
+    if (r >= total) continue;  // (block-uniform) past the bucket's tiles
+    const int64_t tile = (int64_t)b * maxt + r;
+    const int64_t first = (int64_t)b * maxt;
+    const uint32_t t0 = r * TILE;
+    const uint32_t n = items - t0 < (uint32_t)TILE ? items - t0 : (uint32_t)TILE;
+    const uint64_t *bin = in + (uint64_t)b * RS * C0;
+    const int lane = lane_id();
+    const int w = threadIdx.x >> 6;
+    const uint32_t radix = 1u << bits, dmask = radix - 1;
+    for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&whist[0][0])[i] = 0;
+    if (threadIdx.x < RADIX) thist[threadIdx.x] = 0;
+
+    const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
+    uint64_t key[SI];
+    uint32_t rank[SI];
+#pragma unroll
+    for (int i = 0; i < SI; i++) {
+        // logical item -> (region s, offset): binary search of the prefixes
+        const uint32_t li = t0 + ib + i * 64;
+        uint32_t sg = 0;
+#pragma unroll
+        for (int step = RS / 2; step; step >>= 1)
+            if (spre[sg + step] <= li) sg += step;
+        key[i] = ib + i * 64 < n ? bin[(uint64_t)sg * C0 + (li - spre[sg])] : 0;
+    }
+    __syncthreads();
+#define PDIGIT(x) ((uint32_t)((x) >> shift) & dmask)
+    if (ATOMIC) {
+#pragma unroll
+        for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < n ? atomicAdd(&whist[w][PDIGIT(key[i])], 1u) : 0u;
+        __syncthreads();
+        if (threadIdx.x < radix) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int ww = 0; ww < NWAVE; ww++) c += whist[ww][threadIdx.x];
+            thist[threadIdx.x] = c;
+            digit_publish(status + threadIdx.x, tile, first, c, epoch);
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < SI; i++)
+            if (ib + i * 64 < n) atomicAdd(&thist[PDIGIT(key[i])], 1u);
+        __syncthreads();
+        if (threadIdx.x < radix) digit_publish(status + threadIdx.x, tile, first, thist[threadIdx.x], epoch);
+#pragma unroll
+        for (int i = 0; i < SI; i++) rank[i] = ballot_rank(whist[w], PDIGIT(key[i]), ib + i * 64 < n, bits);
+    }
+    __syncthreads();
+    const uint32_t d0 = threadIdx.x;
+    uint32_t tot = 0;
+    if (d0 < RADIX) {
+#pragma unroll
+        for (int ww = 0; ww < NWAVE; ww++) {
+            const uint32_t c = whist[ww][d0];
+            whist[ww][d0] = tot;
+            tot += c;
+        }
+    }
+    const uint32_t ls = block_exclusive_scan<NT>(tot, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
+    if (d0 < RADIX) lstart[d0] = ls;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < SI; i++) {
+        if (ib + i * 64 < n) {
+            const uint32_t d = PDIGIT(key[i]);
+            skeys[lstart[d] + whist[w][d] + rank[i]] = key[i];
+        }
+    }
+    {
+        const uint32_t tpd = NT / radix >= 4 ? 4 : (NT / radix >= 2 ? 2 : 1);
+        if (threadIdx.x < radix * tpd) {
+            const uint32_t d = threadIdx.x / tpd;
+            uint64_t excl;
+            // a bucket's chain has ~2 tiles in flight: the predecessor is
+            // usually done, so rounds of 2 status loads per lane
+            if (dbg & 1) excl = 0;  // timing ablation only: no look-back (wrong offsets)
+            else if (tpd == 4) excl = group_lookback<4, 2>(status + d, tile, first, thist[d], epoch, err);
+            else if (tpd == 2) excl = group_lookback<2, 2>(status + d, tile, first, thist[d], epoch, err);
+            else excl = group_lookback<1, 2>(status + d, tile, first, thist[d], epoch, err);
+            if (threadIdx.x % tpd == 0) {
+                gexcl[d] = excl;
+                const uint64_t incl = excl + thist[d];
+                if (incl > C1) atomicOr(err, ERR_REGION);
+                if (r + 1 == total) cnt1[(b << bits) | d] = (uint32_t)(incl < C1 ? incl : C1);
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int rr = 0; rr < SI; rr++) {
+        const uint32_t q = threadIdx.x + rr * NT;
+        if (q < n) {
+            const uint64_t kk = skeys[q];
+            const uint32_t d = PDIGIT(kk);
+            const uint64_t at = gexcl[d] + (q - lstart[d]);
+            if (at < C1) out[((uint64_t)((b << bits) | d)) * C1 + at] = kk;
+        }
+    }
+    }
+#undef PDIGIT
+}
+
+// tiles of every bucket of pass 1 (from the region counts of pass 0) -> the
+// tile-id limit of the persistent rg_pass: max over buckets x RADIX
+__global__ __launch_bounds__(RADIX) void rg_tiles(const uint32_t *__restrict__ cnt0, uint32_t *__restrict__ lim) {
+    __shared__ uint32_t sc[RADIX / 64];
+    uint32_t items = 0;
+    for (int s = 0; s < RS; s++) items += cnt0[threadIdx.x * RS + s];
+    const uint32_t t = (items + (uint32_t)T1 - 1) / (uint32_t)T1;
+    const uint32_t m = wave_inclusive_scan(t, [](uint32_t a, uint32_t b) { return a > b ? a : b; }, 0u);
+    if (lane_id() == 63) sc[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t mx = 0;
+        for (int w = 0; w < RADIX / 64; w++) mx = sc[w] > mx ? sc[w] : mx;
+        *lim = mx * RADIX;
+    }
+}
+
+// ---------------------------------------------------------------- finish
+// One block per region r (regions in key order = grab order): LSD sort of the
+// item bits [Q, Q + rest) in LDS (7-bit digits, per-wave counters, stable),
+// run-length pass, output compacted through one look-back over the regions.
+// COUNT: okeys[j], ovals[j] = group size; UNIQ: keys of groups of one and
+// their pos ((window << 1) | strand).
+enum { RG_COUNT = 1, RG_UNIQ = 2 };
+
+template <int MODE, typename O, bool ATOMIC>
+__global__ __launch_bounds__(FT) void rg_finish(const uint64_t *__restrict__ in, uint64_t C1,
+                                                const uint32_t *__restrict__ cnt1, uint32_t Q, uint32_t rest,
+                                                uint32_t rc, uint64_t *__restrict__ okeys, O *__restrict__ ovals,
+                                                uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
+                                                uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg) {
+    __shared__ __attribute__((aligned(16))) uint64_t s[FCAP];
+    __shared__ uint32_t wh[FW][FWORD];  // per-wave digit counters, u16 pairs
+    __shared__ uint32_t dstart[FRAD];
+    __shared__ uint32_t lds_scan[FW];
+    __shared__ uint32_t s_tile;
+    __shared__ uint64_t s_out;
+
+    if (threadIdx.x == 0) s_tile = atomicAdd(counter, 1u);
+    __syncthreads();
+    const uint32_t r = s_tile;
+    const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
+    const uint32_t m = cnt1[r];
+    const uint64_t *src = in + (uint64_t)r * C1;
+    const uint64_t rmask = (1ull << rest) - 1;
+    const uint32_t pw = (uint32_t)w * (FIPT * 64) + (uint32_t)lane;  // wave-striped positions
+    uint64_t x[FIPT];
+#pragma unroll
+    for (int i = 0; i < FIPT; i++) x[i] = pw + i * 64 < m ? src[pw + i * 64] : 0;
+
+    // stable LSD passes of <= 9 bits.  Ranks: per-wave u16 counters packed two
+    // to a word (a wave ranks <= 64 * FIPT items), same-word LDS atomics of one
+    // wave return in lane order (probed: ATOMIC), else ballot match-any.
+    // (dbg & 1: timing ablation only, no sort passes)
+    const uint32_t np = (dbg & 1) ? 0u : (rest + FBITS - 1) / FBITS;
+    uint32_t at = 0;
+    for (uint32_t p = 0; p < np; p++) {
+        const uint32_t bw = (rest - at + (np - p) - 1) / (np - p);
+        const uint32_t sh = Q + at, dm = (1u << bw) - 1;
+        at += bw;
+#pragma unroll
+        for (int q = 0; q < FWORD / 64; q++) wh[w][lane + 64 * q] = 0;
+        __builtin_amdgcn_wave_barrier();
+        uint32_t rk[FIPT];
+#pragma unroll
+        for (int i = 0; i < FIPT; i++) {
+            const bool valid = pw + i * 64 < m;
+            const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
+            const uint32_t hs = (d & 1u) * 16u;
+            if (ATOMIC) {
+                rk[i] = valid ? (atomicAdd(&wh[w][d >> 1], 1u << hs) >> hs) & 0xffffu : 0u;
+            } else {
+                uint64_t peers = __ballot(valid);
+                for (uint32_t bb = 0; bb < bw; bb++) {
+                    const bool set = (d >> bb) & 1u;
+                    const uint64_t mm = __ballot(set);
+                    peers &= set ? mm : ~mm;
+                }
+                const uint32_t before = valid ? (wh[w][d >> 1] >> hs) & 0xffffu : 0u;
+                rk[i] = before + (uint32_t)__popcll(peers & lanemask_lt());
+                __builtin_amdgcn_wave_barrier();
+                const int leader = __ffsll((unsigned long long)peers) - 1;
+                if (valid && lane == leader) atomicAdd(&wh[w][d >> 1], (uint32_t)__popcll(peers) << hs);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        __syncthreads();
+        // thread t < FWORD: digits 2t, 2t+1 -> per-wave exclusive offsets (in
+        // place) and their totals; block scan of the totals -> digit starts
+        uint32_t tlo = 0, thi = 0;
+        if (t < FWORD) {
+#pragma unroll
+            for (int ww = 0; ww < FW; ww++) {
+                const uint32_t c = wh[ww][t];
+                wh[ww][t] = tlo | (thi << 16);
+                tlo += c & 0xffffu;
+                thi += c >> 16;
+            }
+        }
+        const uint32_t ls = block_exclusive_scan<FT>(tlo + thi, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
+        if (t < FWORD) {
+            dstart[2 * t] = ls;
+            dstart[2 * t + 1] = ls + tlo;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < FIPT; i++) {
+            if (pw + i * 64 < m) {
+                const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
+                s[dstart[d] + ((wh[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rk[i]] = x[i];
+            }
+        }
+        __syncthreads();
+        if (p + 1 < np) {
+#pragma unroll
+            for (int i = 0; i < FIPT; i++)
+                if (pw + i * 64 < m) x[i] = s[pw + i * 64];
+        }
+    }
+    if (np == 0) {
+#pragma unroll
+        for (int i = 0; i < FIPT; i++)
+            if (pw + i * 64 < m) s[pw + i * 64] = x[i];
+        __syncthreads();
+    }
+
+    // ---- run-length pass (thread t: sorted positions t*FIPT ..)
+    const uint32_t q0 = (uint32_t)t * FIPT;
+    uint64_t kv[FIPT];
+    uint32_t heads = 0, tails = 0;
+#pragma unroll
+    for (int j = 0; j < FIPT; j++) kv[j] = q0 + j < m ? s[q0 + j] : 0;
+#define RKEY(v) (((v) >> Q) & rmask)
+#pragma unroll
+    for (int j = 0; j < FIPT; j++) {
+        const uint32_t q = q0 + j;
+        if (q < m) {
+            const uint64_t kq = RKEY(kv[j]);
+            const bool h = q == 0 || kq != RKEY(j ? kv[j - 1] : s[q - 1]);
+            const bool e = q + 1 == m || kq != RKEY(j + 1 < FIPT ? kv[j + 1] : s[q + 1]);
+            heads |= (uint32_t)h << j;
+            tails |= (uint32_t)e << j;
+        }
+    }
+    uint32_t emit = 0;
+    uint32_t cval[FIPT];
+    if constexpr (MODE == RG_UNIQ) {
+        emit = heads & tails;
+    } else {
+        const uint32_t lh = heads ? q0 + (31 - __clz(heads)) + 1 : 0u;
+        const uint32_t lh_before = block_exclusive_scan<FT>(
+            lh, [](uint32_t a, uint32_t b) { return a > b ? a : b; }, 0u, lds_scan, (uint32_t *)nullptr);
+        uint32_t cur = lh_before;  // head position + 1 of the open group
+#pragma unroll
+        for (int j = 0; j < FIPT; j++) {
+            const uint32_t q = q0 + j;
+            cval[j] = 0;
+            if (q >= m) continue;
+            if ((heads >> j) & 1u) cur = q + 1;
+            if ((tails >> j) & 1u) {
+                emit |= 1u << j;
+                cval[j] = q + 2 - cur;
+            }
+        }
+    }
+    const uint32_t ne = (uint32_t)__popc(emit);
+    uint32_t total;
+    const uint32_t off = block_exclusive_scan<FT>(ne, SumU32(), 0u, lds_scan, &total);
+    // (the scan's barriers ordered every read of s above before the writes below)
+    if (w == 0) {
+        const uint64_t ob = wave_lookback<0>(status, r, total, epoch, err);
+        if (lane == 0) s_out = ob;
+    }
+    O ov[FIPT];
+    const uint64_t qmask = Q ? ((1ull << Q) - 1) : 0ull;
+    uint32_t o = off;
+#pragma unroll
+    for (int j = 0; j < FIPT; j++) {
+        if ((emit >> j) & 1u) {
+            if constexpr (MODE == RG_UNIQ) {
+                const uint64_t idx = kv[j] & qmask;
+                ov[j] = (O)(rc ? idx : (idx << 1));
+            } else {
+                ov[j] = (O)cval[j];
+            }
+            s[o++] = ((uint64_t)r << rest) | RKEY(kv[j]);
+        }
+    }
+#undef RKEY
+    __syncthreads();
+    const uint64_t ob = s_out;
+    if (dbg & 2) return;  // timing ablation only: no output writes
+    for (uint32_t q = t; q < total; q += FT) okeys[ob + q] = s[q];
+    __syncthreads();
+    O *so = reinterpret_cast<O *>(s);
+    o = off;
+#pragma unroll
+    for (int j = 0; j < FIPT; j++)
+        if ((emit >> j) & 1u) so[o++] = ov[j];
+    __syncthreads();
+    for (uint32_t q = t; q < total; q += FT) ovals[ob + q] = so[q];
+}
+
+struct RegionPlan {
+    uint32_t K, Q, B2, rest;
+    bool rc;
+    uint64_t W;          // windows (x2 with rc): bound on the k-mers
+    uint64_t C0, C1;     // region capacities (items)
+    uint32_t n_tiles0, seg_tiles, maxt1;
+    uint32_t ei;         // windows per thread of pass 0
+    uint64_t off_r1, off_c0, off_c1, off_lim, bytes;
+};
+
+uint32_t bitlen(uint64_t x) { return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u; }
+
+int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan *pl) {
+    if (mode != KMAN_FINISH_COUNT && mode != KMAN_FINISH_UNIQ) return KMAN_EINVAL;
+    if (k < 2 || k > 32) return KMAN_EINVAL;
+    if (getenv("KMAN_NO_REGION")) return KMAN_EFALLBACK;
+    // k <= 25: the tile-local window index rides above the key bits in pass 0
+    if ((flags & KMAN_CANONICAL) || k > 25 || n_bases == 0) return KMAN_EFALLBACK;
+    RegionPlan p{};
+    p.rc = flags & KMAN_RC;
+    p.K = 2 * k;
+    p.W = n_bases * (p.rc ? 2 : 1);
+    p.Q = mode == KMAN_FINISH_UNIQ ? (bitlen(p.W - 1) ? bitlen(p.W - 1) : 1u) : 0u;
+    if (p.K - B1 + p.Q > 64) return KMAN_EFALLBACK;
+    // B2: fewest bits with an expected region fill <= 12288 (at most 8)
+    uint32_t b2 = 1;
+    while (b2 < 8 && (p.W >> (B1 + b2)) > 12288) b2++;
+    if ((p.W >> (B1 + b2)) > 16000) return KMAN_EFALLBACK;
+    if (p.K < B1 + b2 + 1) return KMAN_EFALLBACK;
+    p.B2 = b2;
+    p.rest = p.K - B1 - b2;
+    p.ei = p.rc ? 8 : 16;
+    const uint64_t win = (uint64_t)RT * p.ei;
+    p.n_tiles0 = (uint32_t)ceil_div(n_bases, win);
+    p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, RS);
+    const uint64_t e0 = p.W / ((uint64_t)RADIX * RS);
+    p.C0 = ceil_div(e0 + e0 / 2 + 256, 64) * 64;
+    const uint64_t e1 = p.W >> (B1 + b2);
+    uint64_t c1 = ceil_div(e1 + e1 / 2 + 512, 64) * 64;
+    p.C1 = c1 < (uint64_t)FCAP ? c1 : (uint64_t)FCAP;
+    p.maxt1 = (uint32_t)ceil_div((uint64_t)RS * p.C0, T1);
+    const uint64_t nreg = 1ull << (B1 + b2);
+    p.off_r1 = (uint64_t)RADIX * RS * p.C0 * 8;
+    p.off_c0 = p.off_r1 + nreg * p.C1 * 8;
+    p.off_c1 = p.off_c0 + (uint64_t)RADIX * RS * 4;
+    p.off_lim = p.off_c1 + nreg * 4;
+    p.bytes = p.off_lim + 64;
+    *pl = p;
+    return KMAN_OK;
+}
+
+template <int MODE, typename O>
+void launch_finish(kman_ctx *ctx, const RegionPlan &p, const uint64_t *r1, const uint32_t *c1, uint64_t *okeys,
+                   void *ovals, uint32_t nreg, uint32_t epoch, uint32_t *counter, uint32_t dbg) {
+    if (ctx->lds_atomic_ordered)
+        hipLaunchKernelGGL((rg_finish<MODE, O, true>), dim3(nreg), dim3(FT), 0, ctx->stream, r1, p.C1, c1, p.Q,
+                           p.rest, (uint32_t)p.rc, okeys, (O *)ovals, ctx->d_status, counter, epoch, ctx->d_err, dbg);
+    else
+        hipLaunchKernelGGL((rg_finish<MODE, O, false>), dim3(nreg), dim3(FT), 0, ctx->stream, r1, p.C1, c1, p.Q,
+                           p.rest, (uint32_t)p.rc, okeys, (O *)ovals, ctx->d_status, counter, epoch, ctx->d_err, dbg);
+}
+
+template <int EI, bool RC>
+void launch_extract(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
+                    uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter) {
+    const uint32_t grid = RS * p.seg_tiles;
+    if (ctx->lds_atomic_ordered)
+        hipLaunchKernelGGL((rg_extract<EI, RC, true>), dim3(grid), dim3(RT), 0, ctx->stream, codes, n_bases, (int)k,
+                           p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch, ctx->d_err);
+    else
+        hipLaunchKernelGGL((rg_extract<EI, RC, false>), dim3(grid), dim3(RT), 0, ctx->stream, codes, n_bases, (int)k,
+                           p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch, ctx->d_err);
+}
+
+}  // namespace
+
+extern "C" int kman_groups_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, uint64_t *work_bytes) {
+    if (!work_bytes) return KMAN_EINVAL;
+    RegionPlan p;
+    const int rc = make_plan(n_bases, k, flags, mode, &p);
+    *work_bytes = rc == KMAN_OK ? p.bytes : 0;
+    return rc;
+}
+
+extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                           int mode, void *d_work, uint64_t work_bytes, uint64_t *d_okeys, void *d_ovals,
+                           uint32_t oval_bytes, uint64_t *n_kmers, uint64_t *n_out) {
+    if (!ctx || !n_kmers || !n_out) return KMAN_EINVAL;
+    *n_kmers = 0;
+    *n_out = 0;
+    RegionPlan p;
+    const int prc = make_plan(n_bases, k, flags, mode, &p);
+    if (prc == KMAN_EINVAL) return kman_fail(ctx, KMAN_EINVAL, "kman_groups: bad mode or k");
+    if (prc != KMAN_OK) return prc;
+    if (!d_codes || !d_work || !d_okeys || !d_ovals) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    if (work_bytes < p.bytes)
+        return kman_fail(ctx, KMAN_ECAP, "work area %llu < %llu bytes", (unsigned long long)work_bytes,
+                         (unsigned long long)p.bytes);
+    if (oval_bytes != 4 && oval_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "oval_bytes must be 4 or 8");
+    if (oval_bytes == 4 && mode == KMAN_FINISH_UNIQ && (p.rc ? p.W : 2 * p.W) - 1 > 0xffffffffull)
+        return kman_fail(ctx, KMAN_EINVAL, "u32 pos cannot address %llu bases", (unsigned long long)n_bases);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const char *dbg_env = getenv("KMAN_RG_DBG");  // timing ablations (tools/regionbench.py)
+    const uint32_t dbg = dbg_env ? (uint32_t)atoi(dbg_env) : 0u;
+    uint64_t *r0 = (uint64_t *)d_work;
+    uint64_t *r1 = (uint64_t *)((char *)d_work + p.off_r1);
+    uint32_t *c0 = (uint32_t *)((char *)d_work + p.off_c0);
+    uint32_t *c1 = (uint32_t *)((char *)d_work + p.off_c1);
+    uint32_t *lim = (uint32_t *)((char *)d_work + p.off_lim);
+    const uint32_t nreg = 1u << (B1 + p.B2);
+    HIP_TRY(ctx, hipMemsetAsync(c0, 0, p.bytes - p.off_c0, ctx->stream));
+    uint32_t epoch, *counter;
+    // pass 0: extraction by the top 8 bits
+    KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
+    {
+        KTimer kt_(ctx, "region_extract");
+        if (p.rc) launch_extract<8, true>(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter);
+        else launch_extract<16, false>(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    // pass 1: per bucket, by the next B2 bits
+    KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)RADIX * p.maxt1 * RADIX, &epoch, &counter));
+    {
+        hipLaunchKernelGGL(rg_tiles, dim3(1), dim3(RADIX), 0, ctx->stream, c0, lim);
+        KTimer kt_(ctx, "region_pass");
+        const uint32_t sh = p.Q + p.rest;
+        const void *fn = ctx->lds_atomic_ordered ? (const void *)rg_pass<true> : (const void *)rg_pass<false>;
+        const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, RT, (uint64_t)RADIX * p.maxt1);
+        if (ctx->lds_atomic_ordered)
+            hipLaunchKernelGGL((rg_pass<true>), dim3(grid), dim3(RT), 0, ctx->stream, r0, p.C0, c0, lim, p.maxt1, sh,
+                               p.B2, r1, p.C1, c1, ctx->d_status, counter, epoch, ctx->d_err, dbg >> 4);
+        else
+            hipLaunchKernelGGL((rg_pass<false>), dim3(grid), dim3(RT), 0, ctx->stream, r0, p.C0, c0, lim, p.maxt1,
+                               sh, p.B2, r1, p.C1, c1, ctx->d_status, counter, epoch, ctx->d_err, dbg >> 4);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    // finish: one block per region
+    KMAN_TRY(kman_lookback_begin(ctx, nreg, &epoch, &counter));
+    {
+        KTimer kt_(ctx, "region_finish");
+        if (mode == KMAN_FINISH_UNIQ) {
+            if (oval_bytes == 4) launch_finish<RG_UNIQ, uint32_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15);
+            else launch_finish<RG_UNIQ, uint64_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15);
+        } else {
+            if (oval_bytes == 4) launch_finish<RG_COUNT, uint32_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15);
+            else launch_finish<RG_COUNT, uint64_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15);
+        }
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    // results: output count (last region's inclusive), region-0 counts (k-mers), error word
+    uint64_t *h = ctx->h_small;
+    HIP_TRY(ctx, hipMemcpyAsync(h + 4, ctx->d_status + (nreg - 1), 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(h + 8, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    std::vector<uint32_t> hc(RADIX * RS);
+    HIP_TRY(ctx, hipMemcpyAsync(hc.data(), c0, hc.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    uint32_t e;
+    memcpy(&e, h + 8, 4);
+    if (e) {
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(uint32_t), ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if (e == ERR_REGION) return KMAN_EFALLBACK;  // a region overflowed: outputs invalid
+        return kman_fail(ctx, KMAN_ETIMEOUT, "device look-back wait exceeded its bound (code %u)", e);
+    }
+    const uint64_t wd = h[4];
+    if (((wd >> 56) & 63u) != epoch || (wd >> 62) != ST_INCL)
+        return kman_fail(ctx, KMAN_EHIP, "region output total not published");
+    uint64_t nk = 0;
+    for (uint32_t v : hc) nk += v;
+    *n_kmers = nk;
+    *n_out = wd & ST_VMASK;
+    return KMAN_OK;
+}

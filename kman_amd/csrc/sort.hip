@@ -22,16 +22,11 @@
 // 16 B/key (+ 2x payload bytes) — the figure the roofline is quoted against.
 #include "common.h"
 #include "kmer.h"
+#include "onesweep.h"
 
 namespace {
 
-constexpr int RADIX = 256;
 constexpr int MAXPASS = 8;
-#ifndef KMAN_LB
-#define KMAN_LB 8
-#endif
-constexpr int LB = KMAN_LB;  // predecessor status words fetched per look-back round
-
 struct NoVal {};
 
 // A pass's input is cut into NSEG segments of contiguous tiles, each with its
@@ -62,13 +57,9 @@ __device__ uint64_t *g_dbg;
     } while (0)
 #endif
 
-// One thread per digit walks back along that digit's tile chain, LB
+// one thread per digit walks back along that digit's tile chain, LB
 // predecessors per round (independent sc1 loads in flight), summing AGG
-// counts until it meets an INCL prefix.
-KMAN_DEV void digit_publish(uint64_t *st, int64_t tile, int64_t first, uint64_t agg, uint32_t epoch) {
-    st_store(&st[(uint64_t)tile * RADIX], st_make(tile == first ? ST_INCL : ST_AGG, epoch, agg));
-}
-
+// counts until it meets an INCL prefix
 template <bool PUBLISHED>
 KMAN_DEV uint64_t digit_lookback(uint64_t *st, int64_t tile, int64_t first, uint64_t agg, uint32_t epoch,
                                 uint32_t *err) {
@@ -107,83 +98,6 @@ KMAN_DEV uint64_t digit_lookback(uint64_t *st, int64_t tile, int64_t first, uint
         }
     }
     st_store(&st[(uint64_t)tile * RADIX], st_make(ST_INCL, epoch, excl + agg));
-    return excl;
-}
-
-// TPD adjacent lanes walk one digit's chain together: lane `sub` of the group
-// loads predecessors base - sub*LB - q (q < LB), so one round covers TPD*LB
-// tiles.  With many tiles in flight the inclusive-prefix frontier lags by
-// (look-back time / tile start interval) tiles, so the pass runs at about
-// (predecessors per round) / (round latency) tiles per unit time: widening the
-// round is what raises it.  The aggregate has been published already (EARLY).
-template <int TPD>
-KMAN_DEV uint64_t group_lookback(uint64_t *st, int64_t tile, int64_t first, uint64_t agg, uint32_t epoch,
-                                uint32_t *err) {
-    const int lane = lane_id();
-    const int sub = lane % TPD;
-    const int g0 = lane - sub;
-    if (tile == first) return 0;  // a chain's first tile published its inclusive count with the aggregate
-    uint64_t excl = 0;
-    int64_t base = tile - 1;
-    uint32_t spins = 0;
-#if defined(KMAN_ABL) && (KMAN_ABL & 4)
-    uint64_t rounds_dbg = 0;
-#endif
-    while (base >= first) {
-#if defined(KMAN_ABL) && (KMAN_ABL & 4)
-        rounds_dbg++;
-#endif
-        uint64_t w[LB];
-#pragma unroll
-        for (int q = 0; q < LB; q++) {
-            const int64_t j = base - (int64_t)sub * LB - q;
-            w[q] = j >= first ? st_load(&st[(uint64_t)j * RADIX]) : st_make(ST_INCL, epoch, 0);
-        }
-        // this lane's segment, in distance order: 0 all AGG, 1 met INCL, 2 stalled
-        uint32_t state = 0, used = 0;
-        uint64_t sum = 0;
-#pragma unroll
-        for (int q = 0; q < LB; q++) {
-            if (state) continue;
-            const uint64_t f = st_flag(w[q], epoch);
-            if (f == 0) {
-                state = 2;
-                continue;
-            }
-            sum += w[q] & ST_VMASK;
-            used++;
-            if (f == ST_INCL) state = 1;
-        }
-        // combine the group's segments in distance order
-        const uint64_t m = (__ballot(state != 0) >> g0) & ((1ull << TPD) - 1);
-        const int first = m ? __ffsll((unsigned long long)m) - 1 : TPD;
-        uint64_t tot = 0;
-        int64_t adv = 0;
-#pragma unroll
-        for (int s = 0; s < TPD; s++) {
-            const uint64_t ss = shfl_any(sum, g0 + s);
-            const uint32_t su = (uint32_t)__shfl((int)used, g0 + s, 64);
-            if (s <= first) {
-                tot += ss;
-                adv += su;
-            }
-        }
-        const uint32_t fstate = first < TPD ? (uint32_t)__shfl((int)state, g0 + first, 64) : 0;
-        excl += tot;
-        if (fstate == 1) break;
-        base -= first < TPD ? adv : (int64_t)TPD * LB;
-        if (fstate == 2) {
-            if (spin_give_up(spins, err, 2u)) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    if (sub == 0) st_store(&st[(uint64_t)tile * RADIX], st_make(ST_INCL, epoch, excl + agg));
-#if defined(KMAN_ABL) && (KMAN_ABL & 4)
-    if (threadIdx.x == 0 && g_dbg) {
-        g_dbg[(uint64_t)tile * 8 + 6] = rounds_dbg;
-        g_dbg[(uint64_t)tile * 8 + 7] = spins;
-    }
-#endif
     return excl;
 }
 

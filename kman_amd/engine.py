@@ -415,6 +415,40 @@ def rle_uniq(km: Kmers, dev: Device) -> UniqResult:
     return UniqResult(okeys, opos, km.pos_bytes, int(out.value), km.k)
 
 
+def groups(p: Parsed, k: int, rc: bool, mode: str):
+    """kman_groups: count / uniq of the whole stream straight from the codes
+    (region.hip).  Returns a CountResult / UniqResult, or None when the input
+    is outside the region path (kman_groups_plan / a region overflow said
+    KMAN_EFALLBACK): the caller then runs extract_sorted + rle_*."""
+    L, dev = N.lib(), p.dev
+    m = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
+    flags = flags_for(rc, mode == "uniq")
+    wb = c_uint64(0)
+    rc_ = L.kman_groups_plan(p.n_bases, k, flags, m, byref(wb))
+    if rc_ == N.KMAN_EFALLBACK:
+        return None
+    N.check(dev.ctx, rc_, "kman_groups_plan")
+    cap = max(1, p.n_bases * (2 if rc else 1))
+    vb = (4 if 2 * p.n_bases <= 0xFFFFFFFF else 8) if mode == "uniq" else (4 if cap <= 0xFFFFFFFF else 8)
+    work = dev.alloc(int(wb.value))
+    okeys = dev.alloc(8 * cap)
+    ovals = dev.alloc(vb * cap)
+    nk, no = c_uint64(0), c_uint64(0)
+    try:
+        rc_ = L.kman_groups(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k, flags, m, c_void_p(work.ptr), wb.value,
+                            c_void_p(okeys.ptr), c_void_p(ovals.ptr), vb, byref(nk), byref(no))
+    finally:
+        work.free()
+    if rc_ == N.KMAN_EFALLBACK:
+        okeys.free()
+        ovals.free()
+        return None
+    N.check(dev.ctx, rc_, "kman_groups")
+    if mode == "uniq":
+        return UniqResult(okeys, ovals, vb, int(no.value), k)
+    return CountResult(okeys, ovals, vb, int(no.value), k)
+
+
 # ------------------------------------------------------------------ formatting
 
 
@@ -521,18 +555,20 @@ def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = No
     p = parse(dev, text)
     try:
         check_empty_names(p, k)
-        km = extract_sorted(p, k, rc, want_pos=False)
-        try:
-            if km.n == 0:
-                return b""
-            r = rle_count(km, dev)
+        r = groups(p, k, rc, "count")
+        if r is None:
+            km = extract_sorted(p, k, rc, want_pos=False)
             try:
-                ukeys, counts = download_count(dev, r)
+                if km.n == 0:
+                    return b""
+                r = rle_count(km, dev)
             finally:
-                r.ukeys.free()
-                r.counts.free()
+                km.free()
+        try:
+            ukeys, counts = download_count(dev, r)
         finally:
-            km.free()
+            r.ukeys.free()
+            r.counts.free()
         return format_count(ukeys, counts, k)
     finally:
         p.free()
@@ -545,18 +581,20 @@ def uniq_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = Non
     p = parse(dev, text)
     try:
         check_empty_names(p, k)
-        km = extract_sorted(p, k, rc, want_pos=True)
-        try:
-            if km.n == 0:
-                return b""
-            r = rle_uniq(km, dev)
+        r = groups(p, k, rc, "uniq")
+        if r is None:
+            km = extract_sorted(p, k, rc, want_pos=True)
             try:
-                keys, pos = download_uniq(dev, r)
+                if km.n == 0:
+                    return b""
+                r = rle_uniq(km, dev)
             finally:
-                r.keys.free()
-                r.pos.free()
+                km.free()
+        try:
+            keys, pos = download_uniq(dev, r)
         finally:
-            km.free()
+            r.keys.free()
+            r.pos.free()
         return format_fasta(keys, pos, k, p)
     finally:
         p.free()
@@ -571,15 +609,17 @@ class ResidentPipeline:
     the result device-resident (what bench.py times)."""
 
     def __init__(self, dev: Device, text: bytes, k: int, mode: str = "uniq", rc: bool = False,
-                 pos_bytes: Optional[int] = None, path: str = "split"):
+                 pos_bytes: Optional[int] = None, path: str = "region"):
         _check_k(k)
         if mode not in ("count", "uniq"):
             raise ValueError(mode)
-        if path not in ("split", "full"):
+        if path not in ("region", "split", "full"):
             raise ValueError(path)
-        # split: prefix passes + kman_finish (default); full: every bit in
-        # global passes + kman_rle_* (the previous engine, kept for A/B runs)
+        # region: kman_groups (default; falls back to split when the input is
+        # outside the region path); split: prefix passes + kman_finish; full:
+        # every bit in global passes + kman_rle_* (kept for A/B runs)
         self.path = path
+        self.work = None
         self.dev, self.k, self.mode, self.rc = dev, k, mode, rc
         n = len(text)
         self.n_bytes = n
@@ -606,6 +646,25 @@ class ResidentPipeline:
         self.n_out = 0
         self.n_bases = 0
         self.sorted_in_alt = False
+        if self.path == "region":
+            self._parse()
+            wb = c_uint64(0)
+            m = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
+            r = N.lib().kman_groups_plan(self.n_bases, k, flags_for(rc, want_pos), m, byref(wb))
+            if r == N.KMAN_EFALLBACK:
+                self.path = "split"
+            else:
+                N.check(dev.ctx, r, "kman_groups_plan")
+                self.work = dev.alloc(int(wb.value))
+                self.work_bytes = int(wb.value)
+
+    def _parse(self) -> None:
+        info = N.ParseInfo()
+        N.check(self.dev.ctx, N.lib().kman_parse_fasta(self.dev.ctx, c_void_p(self.text.ptr), self.n_bytes,
+                                                        c_void_p(self.codes.ptr), c_void_p(self.rec_hdr.ptr),
+                                                        c_void_p(self.rec_seq.ptr), self.rec_cap, byref(info)),
+                "kman_parse_fasta")
+        self.n_bases = int(info.n_bases)
 
     def extract_only(self) -> int:
         """parse + extract (stream-order keys / pos in self.keys / self.pos)."""
@@ -625,11 +684,22 @@ class ResidentPipeline:
 
     def step(self) -> int:
         L, ctx = N.lib(), self.dev.ctx
-        info = N.ParseInfo()
-        N.check(ctx, L.kman_parse_fasta(ctx, c_void_p(self.text.ptr), self.n_bytes, c_void_p(self.codes.ptr),
-                                        c_void_p(self.rec_hdr.ptr), c_void_p(self.rec_seq.ptr), self.rec_cap,
-                                        byref(info)), "kman_parse_fasta")
-        self.n_bases = int(info.n_bases)
+        self._parse()
+        if self.path == "region":
+            m = N.KMAN_FINISH_UNIQ if self.mode == "uniq" else N.KMAN_FINISH_COUNT
+            ob = self.count_bytes if self.mode == "count" else self.pos_bytes
+            nk, no = c_uint64(0), c_uint64(0)
+            r = L.kman_groups(ctx, c_void_p(self.codes.ptr), self.n_bases, self.k, self.flags & 0xff, m,
+                              c_void_p(self.work.ptr), self.work_bytes, c_void_p(self.out_keys.ptr),
+                              c_void_p(self.out_vals.ptr), ob, byref(nk), byref(no))
+            if r != N.KMAN_EFALLBACK:
+                N.check(ctx, r, "kman_groups")
+                self.n_kmers, self.n_out = int(nk.value), int(no.value)
+                return self.n_kmers
+            # a region overflowed (skewed input): the general path from here on
+            self.path = "split"
+            self.work.free()
+            self.work = None
         n = c_uint64(0)
         res = c_int(0)
         pos = c_void_p(self.pos.ptr) if self.pos else c_void_p(None)
@@ -689,6 +759,6 @@ class ResidentPipeline:
 
     def free(self) -> None:
         for b in (self.text, self.codes, self.rec_hdr, self.rec_seq, self.keys, self.alt, self.pos, self.pos_alt,
-                  self.hist, self.out_keys, self.out_vals):
+                  self.hist, self.out_keys, self.out_vals, self.work):
             if b is not None:
                 b.free()

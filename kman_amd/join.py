@@ -45,6 +45,22 @@ def _entries(batches: List[Batch]):
     return out
 
 
+def _whole_stream(entries):
+    """The FastaSource whose whole k-mer stream the entries cover exactly once
+    (any batch order), else None."""
+    from .source import FastaSource
+
+    src = entries[0][0]
+    if not isinstance(src, FastaSource) or any(s is not src for s, _, _ in entries):
+        return None
+    at = 0
+    for _, s, e in sorted(entries, key=lambda x: x[1]):
+        if s != at:
+            return None
+        at = e
+    return src if at == src.n_kmers else None
+
+
 class Crawler:
     """Merged crawl over batches (join.py:36-130)."""
 
@@ -178,6 +194,22 @@ def join_bytes(batches: List[Batch], count: bool) -> bytes:
         return b""
     from .source import gather_sorted
 
+    whole = _whole_stream(entries)
+    if whole is not None:
+        # the batches are one FASTA stream, each k-mer once: count / uniq do
+        # not depend on the batch cut, so the region path takes
+        # the stream straight from the codes
+        r = engine.groups(whole.parsed, whole.k, whole.rc, "count" if count else "uniq")
+        if r is not None:
+            try:
+                if count:
+                    ukeys, counts = engine.download_count(whole.dev, r)
+                    return engine.format_count(ukeys, counts, whole.k)
+                keys, pos = engine.download_uniq(whole.dev, r)
+                return whole.format_fasta(keys, pos)
+            finally:
+                for b in ((r.ukeys, r.counts) if count else (r.keys, r.pos)):
+                    b.free()
     km, srcs, tagged = gather_sorted(entries, want_pos=not count)
     dev = srcs[0].dev
     k = srcs[0].k

@@ -1,0 +1,199 @@
+"""GPU parity of the region path (kman_groups, kman_amd/csrc/region.hip):
+count / uniq of a whole stream straight from the codes.
+
+Bar: bit-exact against the numpy restatement of the reference's path
+(np_oracle: stream_kmers -> stable sort -> run-length count / uniq, which
+restates seq.py:285-328, batch.py:156-168 and join.py:95-130,244-285), and
+identical to the general (prefix-split) GPU path on the same input.  Full
+size (BASELINE config 2: 1 GB FASTA, k=21) is checked through
+size-independent properties and against the general path's count output."""
+
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_uint64
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from kman_amd import engine
+
+    return engine.default_device()
+
+
+def _texts(golden_inputs):
+    import inputs
+
+    from kman_amd.engine import read_input
+
+    return [
+        read_input(golden_inputs["messy1"]),
+        inputs.messy_records(11, n_records=60, max_len=20000),
+        inputs.syn_numpy(100_000, 5),
+        inputs.syn_numpy(3_000_000, 6, record_len=1 << 20),
+    ]
+
+
+def _oracle(text, k, rc, mode):
+    import np_oracle
+
+    recs = np_oracle.parse_fasta(text)
+    keys, pos = np_oracle.stream_kmers(recs, k, rc=rc)
+    sk, sp = np_oracle.stable_sort(keys, pos)
+    if mode == "count":
+        return np_oracle.rle_count(sk)
+    return np_oracle.rle_uniq(sk, sp)
+
+
+def _groups(dev, text, k, rc, mode):
+    from kman_amd import engine
+
+    p = engine.parse(dev, text)
+    try:
+        r = engine.groups(p, k, rc, mode)
+        if r is None:
+            return None
+        try:
+            if mode == "count":
+                return engine.download_count(dev, r)
+            return engine.download_uniq(dev, r)
+        finally:
+            for b in ((r.ukeys, r.counts) if mode == "count" else (r.keys, r.pos)):
+                b.free()
+    finally:
+        p.free()
+
+
+@pytest.mark.parametrize("k", [5, 9, 13, 21, 25])
+@pytest.mark.parametrize("rc", [False, True])
+@pytest.mark.parametrize("mode", ["count", "uniq"])
+def test_groups_matches_oracle(dev, golden_inputs, k, rc, mode):
+    from kman_amd import _native as N
+
+    for text in _texts(golden_inputs):
+        n_bases = sum(len(s) for _, s in __import__("np_oracle").parse_fasta(text))
+        m = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
+        flags = (N.KMAN_RC if rc else 0) | (N.KMAN_WANT_POS if mode == "uniq" else 0)
+        wb = c_uint64(0)
+        inside = N.lib().kman_groups_plan(n_bases, k, flags, m, byref(wb)) == N.KMAN_OK
+        # outside: 2k - 8 key bits + the pos bits exceed one u64 item
+        q = max(1, int(n_bases * (2 if rc else 1) - 1).bit_length()) if mode == "uniq" else 0
+        assert inside == (2 * k - 8 + q <= 64)
+        got = _groups(dev, text, k, rc, mode)
+        if not inside:
+            assert got is None
+            continue
+        assert got is not None, "input inside the region path fell back"
+        want = _oracle(text, k, rc, mode)
+        np.testing.assert_array_equal(got[0], want[0])
+        np.testing.assert_array_equal(got[1].astype(np.uint64), want[1])
+
+
+def test_groups_plan_domain():
+    """kman_groups_plan: KMAN_EFALLBACK outside the path, a size inside it."""
+    from kman_amd import _native as N
+
+    L = N.lib()
+    wb = c_uint64(0)
+    U, C = N.KMAN_FINISH_UNIQ, N.KMAN_FINISH_COUNT
+    assert L.kman_groups_plan(1_000_000_000, 21, N.KMAN_WANT_POS, U, byref(wb)) == N.KMAN_OK and wb.value > 0
+    assert L.kman_groups_plan(1_000_000_000, 21, 0, C, byref(wb)) == N.KMAN_OK
+    assert L.kman_groups_plan(1000, 31, 0, C, byref(wb)) == N.KMAN_EFALLBACK  # k > 25
+    assert L.kman_groups_plan(1000, 21, N.KMAN_CANONICAL, C, byref(wb)) == N.KMAN_EFALLBACK
+    assert L.kman_groups_plan(1000, 4, 0, C, byref(wb)) == N.KMAN_EFALLBACK  # too few key bits
+    assert L.kman_groups_plan(4_000_000_000, 21, 0, C, byref(wb)) == N.KMAN_EFALLBACK  # regions too full
+    assert L.kman_groups_plan(1000, 21, 0, 0, byref(wb)) == N.KMAN_EINVAL  # SORT is not a groups mode
+
+
+@pytest.mark.parametrize("mode", ["count", "uniq"])
+def test_groups_overflow_falls_back(dev, mode):
+    """A skewed stream (one k-mer repeated) overflows a region: kman_groups
+    says KMAN_EFALLBACK and the command output still matches the oracle
+    through the general path."""
+    from kman_amd import engine
+
+    text = b">a\n" + b"A" * 300_000 + b"\n>b\n" + b"ACGT" * 1000 + b"\n"
+    assert _groups(dev, text, 21, False, mode) is None
+    fn = engine.count_text if mode == "count" else engine.uniq_text
+    got = fn(text, 21, dev=dev)
+    want = _oracle(text, 21, False, mode)
+    if mode == "count":
+        lines = got.decode().splitlines()
+        assert len(lines) == len(want[0])
+        assert [int(x.split("\t")[1]) for x in lines] == want[1].tolist()
+    else:
+        assert got.count(b">") == len(want[0])
+
+
+@pytest.mark.parametrize("mode", ["count", "uniq"])
+@pytest.mark.parametrize("rc", [False, True])
+def test_pipeline_region_equals_split(dev, mode, rc):
+    """ResidentPipeline: region path == prefix-split path, 60 Mbase input."""
+    import inputs
+    from kman_amd import engine
+
+    text = inputs.syn_numpy(60_000_000, 9)
+    outs = []
+    for path in ("region", "split"):
+        pipe = engine.ResidentPipeline(dev, text, 21, mode=mode, rc=rc, path=path)
+        try:
+            assert pipe.path == path
+            n = pipe.step()
+            n2 = pipe.step()  # a second step over the same resident input
+            assert n == n2
+            vt = np.uint32 if (pipe.count_bytes if mode == "count" else pipe.pos_bytes) == 4 else np.uint64
+            outs.append((n, pipe.n_out, dev.download(pipe.out_keys, pipe.n_out, np.uint64),
+                         dev.download(pipe.out_vals, pipe.n_out, vt)))
+        finally:
+            pipe.free()
+    assert outs[0][0] == outs[1][0] and outs[0][1] == outs[1][1]
+    np.testing.assert_array_equal(outs[0][2], outs[1][2])
+    np.testing.assert_array_equal(outs[0][3], outs[1][3])
+
+
+def test_full_size_region(dev):
+    """BASELINE config 2 (1 GB synthetic FASTA, k=21) on the region path:
+    uniq keys are exactly the count-1 keys of the count run, counts sum to
+    the k-mer count, keys strictly increase, the key checksum of the stream
+    is preserved, and every uniq pos decodes (from the codes) to its key."""
+    import inputs
+    from kman_amd import engine
+
+    text = inputs.syn_numpy(1_000_000_000, 1)
+    pu = engine.ResidentPipeline(dev, text, 21, mode="uniq")
+    assert pu.path == "region"
+    n = pu.step()
+    assert n == 1_000_000_000 - 4 * 20
+    assert pu.path == "region"
+    uk = dev.download(pu.out_keys, pu.n_out, np.uint64)
+    up = dev.download(pu.out_vals, pu.n_out, np.uint32)
+    codes = dev.download(pu.codes, pu.n_bases, np.uint8)
+    pu.free()
+    assert (uk[1:] > uk[:-1]).all()
+    rng = np.random.default_rng(0)
+    for j in rng.integers(0, len(uk), 2000):
+        b = int(up[j]) >> 1
+        w = codes[b : b + 21] & 3
+        key = 0
+        for c in w.tolist():
+            key = (key << 2) | c
+        assert key == int(uk[j])
+    del codes
+    pc = engine.ResidentPipeline(dev, text, 21, mode="count")
+    del text
+    assert pc.step() == n and pc.path == "region"
+    ck = dev.download(pc.out_keys, pc.n_out, np.uint64)
+    cc = dev.download(pc.out_vals, pc.n_out, np.uint32)
+    pc.extract_only()
+    keys = dev.download(pc.keys, n, np.uint64)
+    pc.free()
+    assert int(cc.sum()) == n
+    assert (ck[1:] > ck[:-1]).all()
+    assert int(np.sum(ck * cc.astype(np.uint64), dtype=np.uint64)) == int(np.sum(keys, dtype=np.uint64))
+    del keys
+    np.testing.assert_array_equal(ck[cc == 1], uk)

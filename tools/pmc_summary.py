@@ -42,9 +42,13 @@ for k, v in out.items():
     print("%-60s %3d  fetch %12.0f KiB  write %12.0f KiB  hbm/launch %8.3f GB" % (
         k[:60], v["launches"], v["fetch_kib"], v["write_kib"], v["hbm_bytes_per_launch"] / 1e9))
 if len(sys.argv) > 6:
-    sp = [v for k, v in out.items() if k.startswith("void onesweep_pass") or "onesweep_pass" in k]
-    if sp:
-        best = max(sp, key=lambda v: v["launches"])
-        with open(os.path.join(ROOT, "profiles", "pmc_sort_pass.json"), "w") as fh:
-            json.dump({"mode": sys.argv[4], "k": int(sys.argv[5]), "bases": int(sys.argv[6]), "tag": tag,
-                       "hbm_bytes_per_launch": best["hbm_bytes_per_launch"]}, fh, indent=1)
+    # the bench's roofline kernel: the region path's digit pass (rg_pass), else
+    # the LSD onesweep pass
+    for name in ("rg_pass", "onesweep_pass"):
+        sp = [v for k, v in out.items() if name in k]
+        if sp:
+            best = max(sp, key=lambda v: v["launches"])
+            with open(os.path.join(ROOT, "profiles", "pmc_sort_pass.json"), "w") as fh:
+                json.dump({"mode": sys.argv[4], "k": int(sys.argv[5]), "bases": int(sys.argv[6]), "tag": tag,
+                           "kernel": name, "hbm_bytes_per_launch": best["hbm_bytes_per_launch"]}, fh, indent=1)
+            break

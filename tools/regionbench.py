@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Stage timings of the region path (kman_groups) with timing ablations
+(KMAN_RG_DBG, region.hip): 1 = finish without its LDS sort passes, 2 = finish
+without output writes, 16 = rg_pass without look-back.  Results of ablated
+runs are wrong by construction; only their timings are read."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+
+import inputs  # noqa: E402
+from kman_amd import engine  # noqa: E402
+
+mode = sys.argv[1] if len(sys.argv) > 1 else "uniq"
+text = inputs.syn_numpy(1_000_000_000, 1)
+dev = engine.Device(0)
+pipe = engine.ResidentPipeline(dev, text, 21, mode=mode)
+del text
+for dbg in ["0", "1", "2", "3", "16", "0"]:
+    os.environ["KMAN_RG_DBG"] = dbg
+    pipe.step()
+    pipe.timing(True)
+    steps = 4
+    for _ in range(steps):
+        pipe.step()
+    row = {}
+    for tag in ("parse", "region_extract", "region_pass", "region_finish"):
+        c, ms = pipe.timed(tag)
+        row[tag] = round(ms / max(c, 1), 3)
+    pipe.timing(False)
+    print("dbg=%-3s %s" % (dbg, row), flush=True)
