@@ -14,8 +14,9 @@ constexpr int LB = KMAN_LB;  // predecessor status words fetched per look-back r
 
 
 // publish a tile's digit count: inclusive for a chain's first tile
+template <int STRIDE = RADIX>
 KMAN_DEV void digit_publish(uint64_t *st, int64_t tile, int64_t first, uint64_t agg, uint32_t epoch) {
-    st_store(&st[(uint64_t)tile * RADIX], st_make(tile == first ? ST_INCL : ST_AGG, epoch, agg));
+    st_store(&st[(uint64_t)tile * STRIDE], st_make(tile == first ? ST_INCL : ST_AGG, epoch, agg));
 }
 
 // TPD adjacent lanes walk one digit's chain together: lane `sub` of the group
@@ -26,7 +27,7 @@ KMAN_DEV void digit_publish(uint64_t *st, int64_t tile, int64_t first, uint64_t 
 // round is what raises it.  The aggregate has been published already (EARLY).
 // LBN: predecessors per lane per round (short chains whose predecessors are
 // usually done: 1 or 2, so one round costs few status loads)
-template <int TPD, int LBN = LB>
+template <int TPD, int LBN = LB, int STRIDE = RADIX>
 KMAN_DEV uint64_t group_lookback(uint64_t *st, int64_t tile, int64_t first, uint64_t agg, uint32_t epoch,
                                 uint32_t *err) {
     const int lane = lane_id();
@@ -41,7 +42,7 @@ KMAN_DEV uint64_t group_lookback(uint64_t *st, int64_t tile, int64_t first, uint
 #pragma unroll
         for (int q = 0; q < LBN; q++) {
             const int64_t j = base - (int64_t)sub * LBN - q;
-            w[q] = j >= first ? st_load(&st[(uint64_t)j * RADIX]) : st_make(ST_INCL, epoch, 0);
+            w[q] = j >= first ? st_load(&st[(uint64_t)j * STRIDE]) : st_make(ST_INCL, epoch, 0);
         }
         // this lane's segment, in distance order: 0 all AGG, 1 met INCL, 2 stalled
         uint32_t state = 0, used = 0;
@@ -81,7 +82,7 @@ KMAN_DEV uint64_t group_lookback(uint64_t *st, int64_t tile, int64_t first, uint
             __builtin_amdgcn_s_sleep(1);
         }
     }
-    if (sub == 0) st_store(&st[(uint64_t)tile * RADIX], st_make(ST_INCL, epoch, excl + agg));
+    if (sub == 0) st_store(&st[(uint64_t)tile * STRIDE], st_make(ST_INCL, epoch, excl + agg));
     return excl;
 }
 

@@ -20,8 +20,8 @@
 //   pass 1 (rg_pass)     per bucket b (its own chain over the regions (b, *)):
 //                        scatter by the next B2 key bits d into region
 //                        r = (b << B2 | d) of capacity C1 <= FCAP.
-//   finish (rg_finish)   one 1024-thread block per region r: load it (<= FCAP
-//                        items, 144 KiB of LDS), LSD-sort the remaining key
+//   finish (rg_finish)   one 512-thread block per region r: load it (<= FCAP
+//                        items, 68 KiB of LDS), LSD-sort the remaining key
 //                        bits in LDS, run-length pass, emit (key, count) or the
 //                        keys that occur once with their pos, compacted by one
 //                        look-back over the regions in key order.
@@ -36,6 +36,7 @@
 #include "kmer.h"
 #include "onesweep.h"
 
+#include <cstdio>
 #include <cstdlib>
 
 namespace {
@@ -44,15 +45,30 @@ constexpr int RT = 512;           // threads of passes 0 and 1
 constexpr int RS = 64;            // position segments of pass 0 (one wave of counts)
 constexpr int RSI = 16;           // items per thread, pass 1
 constexpr uint64_t T1 = (uint64_t)RT * RSI;  // pass-1 tile
-constexpr int FT = 1024;          // finish threads
+constexpr int FT = 512;           // finish threads (two blocks per CU)
 constexpr int FW = FT / 64;
 constexpr int FIPT = 17;          // finish items per thread
-constexpr int FCAP = FT * FIPT;   // 17408 items = 136 KiB: largest region
+constexpr int FCAP = FT * FIPT;   // 8704 items = 68 KiB: largest region
 constexpr int FBITS = 9;          // finish LSD digit (26 bits: 3 passes)
 constexpr int FRAD = 1 << FBITS;
 constexpr int FWORD = FRAD / 2;   // per-wave counters: two u16 per word
 constexpr uint32_t ERR_REGION = 1u << 8;  // a region would overflow (not an engine fault)
 constexpr uint32_t B1 = 8;        // pass-0 digit = top 8 key bits
+
+// phase stamps (s_memrealtime, 100 MHz) per tile, thread 0, into `stp`: only
+// in diagnostic builds (make EXTRA=-DKMAN_RG_STAMPS OUT=../lib_stamps,
+// tools/regionstamps.py); `stp` is null otherwise
+#ifdef KMAN_RG_STAMPS
+#define RSTAMP(id, i)                                                                                 \
+    do {                                                                                              \
+        if (stp && threadIdx.x == 0) stp[(uint64_t)(id) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define RSTAMP(id, i) \
+    do {              \
+        (void)stp;    \
+    } while (0)
+#endif
 
 KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t bits) {
     // stable in-wave rank among equal digits (ballot match-any), lane order
@@ -82,7 +98,8 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
                                                  uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
                                                  uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ cnt0,
                                                  uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
-                                                 uint32_t epoch, uint32_t *__restrict__ err) {
+                                                 uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg,
+                                                 uint64_t *__restrict__ stp) {
     constexpr int NT = RT;
     constexpr int NWAVE = NT / 64;
     constexpr int WIN = NT * EI;
@@ -104,6 +121,7 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
     if (t0 + jj >= t1) return;  // (block-uniform) past a segment's end
     const int64_t tile = (int64_t)t0 + jj;
     const int64_t first = t0;
+    RSTAMP(tile, 0);
     const int lane = lane_id();
     const int w = threadIdx.x >> 6;
     const uint32_t kb = 2u * (uint32_t)k;
@@ -116,6 +134,7 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
     for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&whist[0][0])[i] = 0;
     if (threadIdx.x < RADIX) thist[threadIdx.x] = 0;
     __syncthreads();
+    RSTAMP(tile, 1);
 
     uint64_t kf[EI], kr[EI];
     const uint32_t w0 = threadIdx.x * EI;
@@ -135,6 +154,7 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
         }
     }
     __syncthreads();
+    RSTAMP(tile, 2);
 
     const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
     uint64_t key[SI];
@@ -163,6 +183,7 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
         for (int i = 0; i < SI; i++) rank[i] = ballot_rank(whist[w], XDIGIT(key[i]), ib + i * 64 < tcnt, B1);
     }
     __syncthreads();
+    RSTAMP(tile, 3);
     const uint32_t d0 = threadIdx.x;
     uint32_t tot = 0;
     if (d0 < RADIX) {
@@ -187,7 +208,9 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
         constexpr uint32_t TPD = NT / RADIX >= 4 ? 4 : (NT / RADIX >= 2 ? 2 : 1);
         if (threadIdx.x < RADIX * TPD) {
             const uint32_t d = threadIdx.x / TPD;
-            const uint64_t excl = group_lookback<TPD>(status + d, tile, first, thist[d], epoch, err);
+            const uint64_t excl =
+                (dbg & 1) ? 0ull  // timing ablation only: no look-back (wrong offsets)
+                          : group_lookback<TPD>(status + d, tile, first, thist[d], epoch, err);
             if (threadIdx.x % TPD == 0) {
                 gexcl[d] = excl;
                 const uint64_t incl = excl + thist[d];
@@ -197,6 +220,7 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
         }
     }
     __syncthreads();
+    RSTAMP(tile, 4);
     constexpr int RQ = (TILE + NT - 1) / NT;
 #pragma unroll
     for (int r = 0; r < RQ; r++) {
@@ -213,28 +237,35 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
             }
         }
     }
+    RSTAMP(tile, 5);
 #undef XDIGIT
 }
 
 // ---------------------------------------------------------------- pass 1
-// One tile of the regions (b, 0..RS-1) of bucket b (cid round robin over the
-// buckets; tile r of a bucket numbers its regions' tiles in region order), so
-// each bucket is its own look-back chain.  Digit = item bits [shift, shift +
-// bits); output region (b << bits | d) of capacity C1.  The bucket's last tile
-// writes the final region counts.
+// One tile of bucket b's items (cid round robin over the buckets; the RS
+// regions (b, *) read as one concatenated sequence, so each bucket is its own
+// look-back chain with no partial tiles but its last).  Digit = item bits
+// [shift, shift + bits), bits <= 9; output region (b << bits | d) of capacity
+// C1.  Per-wave digit counters are u16 pairs (a wave ranks <= 1024 items), so
+// radix 512 keeps the block at 78 KiB of LDS: two blocks per CU.  The
+// bucket's last tile writes the final region counts.
+constexpr int R1 = 512;  // pass-1 radix bound
 template <bool ATOMIC>
 __global__ __launch_bounds__(RT, 4) void rg_pass(const uint64_t *__restrict__ in, uint64_t C0,
-                                              const uint32_t *__restrict__ cnt0, const uint32_t *__restrict__ lim_p,
-                                              uint32_t maxt, uint32_t shift, uint32_t bits,
-                                              uint64_t *__restrict__ out, uint64_t C1, uint32_t *__restrict__ cnt1,
-                                              uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
-                                              uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg) {
+                                                 const uint32_t *__restrict__ cnt0,
+                                                 const uint32_t *__restrict__ lim_p, uint32_t maxt, uint32_t shift,
+                                                 uint32_t bits, uint64_t *__restrict__ out, uint64_t C1,
+                                                 uint32_t *__restrict__ cnt1, uint64_t *__restrict__ status,
+                                                 uint32_t *__restrict__ counter, uint32_t epoch,
+                                                 uint32_t *__restrict__ err, uint32_t dbg,
+                                                 uint64_t *__restrict__ stp) {
     constexpr int NT = RT, SI = RSI, TILE = NT * SI, NWAVE = NT / 64;
+    static_assert(NT == R1, "one thread per digit");
     __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
-    __shared__ uint32_t whist[NWAVE][RADIX];
-    __shared__ uint32_t thist[RADIX];
-    __shared__ uint32_t lstart[RADIX];
-    __shared__ uint64_t gexcl[RADIX];
+    __shared__ uint32_t whist[NWAVE][R1 / 2];
+    __shared__ uint32_t thist[R1];
+    __shared__ uint32_t lstart[R1];
+    __shared__ uint32_t gexcl[R1];
     __shared__ uint32_t lds_scan[NWAVE];
     __shared__ uint32_t spre[RS + 1];
     __shared__ uint32_t lds_tile;
@@ -244,120 +275,158 @@ __global__ __launch_bounds__(RT, 4) void rg_pass(const uint64_t *__restrict__ in
     // finishes its tile before taking the next, so every predecessor of a
     // tile is taken and in progress (forward progress of the look-back)
     const uint32_t lim = *lim_p;
-    for (;;) {
-    const uint32_t cid = (uint32_t)grab_tile(counter, &lds_tile);
-    if (cid >= lim) break;
-    const uint32_t b = cid % RADIX, r = cid / RADIX;
-    // the bucket's RS regions read as one concatenated sequence of items
-    if (threadIdx.x < 64) {
-        const uint32_t c = threadIdx.x < RS ? cnt0[b * RS + threadIdx.x] : 0u;
-        const uint32_t inc = wave_inclusive_scan(c, SumU32());
-        if (threadIdx.x < RS) spre[threadIdx.x + 1] = inc;
-        if (threadIdx.x == 0) spre[0] = 0;
-    }
-    __syncthreads();
-    const uint32_t items = spre[RS];
-    const uint32_t total = (items + TILE - 1) / TILE;
-    if (r >= total) continue;  // (block-uniform) past the bucket's tiles
-    const int64_t tile = (int64_t)b * maxt + r;
-    const int64_t first = (int64_t)b * maxt;
-    const uint32_t t0 = r * TILE;
-    const uint32_t n = items - t0 < (uint32_t)TILE ? items - t0 : (uint32_t)TILE;
-    const uint64_t *bin = in + (uint64_t)b * RS * C0;
     const int lane = lane_id();
     const int w = threadIdx.x >> 6;
     const uint32_t radix = 1u << bits, dmask = radix - 1;
-    for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&whist[0][0])[i] = 0;
-    if (threadIdx.x < RADIX) thist[threadIdx.x] = 0;
-
-    const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
-    uint64_t key[SI];
-    uint32_t rank[SI];
+    for (;;) {
+        const uint32_t cid = (uint32_t)grab_tile(counter, &lds_tile);
+        if (cid >= lim) break;
+        const uint32_t b = cid % RADIX, r = cid / RADIX;
+        if (threadIdx.x < 64) {
+            const uint32_t c = threadIdx.x < RS ? cnt0[b * RS + threadIdx.x] : 0u;
+            const uint32_t inc = wave_inclusive_scan(c, SumU32());
+            if (threadIdx.x < RS) spre[threadIdx.x + 1] = inc;
+            if (threadIdx.x == 0) spre[0] = 0;
+        }
+        for (int i = threadIdx.x; i < NWAVE * R1 / 2; i += NT) (&whist[0][0])[i] = 0;
+        if (!ATOMIC) thist[threadIdx.x] = 0;
+        __syncthreads();
+        const uint32_t items = spre[RS];
+        const uint32_t total = (items + TILE - 1) / TILE;
+        if (r >= total) continue;  // (block-uniform) past the bucket's tiles
+        const int64_t tile = (int64_t)b * maxt + r;  // status index; a bucket's chain starts at r = 0
+        const uint32_t t0 = r * TILE;
+        const uint32_t n = items - t0 < (uint32_t)TILE ? items - t0 : (uint32_t)TILE;
+        const uint64_t *bin = in + (uint64_t)b * RS * C0;
+        RSTAMP(tile, 0);
+        const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
+        uint64_t key[SI];
+        uint32_t rank[SI];
 #pragma unroll
-    for (int i = 0; i < SI; i++) {
-        // logical item -> (region s, offset): binary search of the prefixes
-        const uint32_t li = t0 + ib + i * 64;
-        uint32_t sg = 0;
+        for (int i = 0; i < SI; i++) {
+            // logical item -> (region s, offset): binary search of the prefixes
+            const uint32_t li = t0 + ib + i * 64;
+            uint32_t sg = 0;
 #pragma unroll
-        for (int step = RS / 2; step; step >>= 1)
-            if (spre[sg + step] <= li) sg += step;
-        key[i] = ib + i * 64 < n ? bin[(uint64_t)sg * C0 + (li - spre[sg])] : 0;
-    }
-    __syncthreads();
+            for (int step = RS / 2; step; step >>= 1)
+                if (spre[sg + step] <= li) sg += step;
+            key[i] = ib + i * 64 < n ? bin[(uint64_t)sg * C0 + (li - spre[sg])] : 0;
+        }
 #define PDIGIT(x) ((uint32_t)((x) >> shift) & dmask)
-    if (ATOMIC) {
+        if (ATOMIC) {
 #pragma unroll
-        for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < n ? atomicAdd(&whist[w][PDIGIT(key[i])], 1u) : 0u;
-        __syncthreads();
-        if (threadIdx.x < radix) {
-            uint32_t c = 0;
+            for (int i = 0; i < SI; i++) {
+                const uint32_t d = PDIGIT(key[i]), hs = (d & 1u) * 16u;
+                rank[i] = ib + i * 64 < n ? (atomicAdd(&whist[w][d >> 1], 1u << hs) >> hs) & 0xffffu : 0u;
+            }
+            __syncthreads();
+            {
+                // every R1 digit (those >= radix count 0): the packed status
+                // words below cover all of them
+                const uint32_t d = threadIdx.x, hs = (d & 1u) * 16u;
+                uint32_t c = 0;
 #pragma unroll
-            for (int ww = 0; ww < NWAVE; ww++) c += whist[ww][threadIdx.x];
-            thist[threadIdx.x] = c;
-            digit_publish(status + threadIdx.x, tile, first, c, epoch);
-        }
-    } else {
+                for (int ww = 0; ww < NWAVE; ww++) c += (whist[ww][d >> 1] >> hs) & 0xffffu;
+                thist[d] = c;
+            }
+        } else {
 #pragma unroll
-        for (int i = 0; i < SI; i++)
-            if (ib + i * 64 < n) atomicAdd(&thist[PDIGIT(key[i])], 1u);
-        __syncthreads();
-        if (threadIdx.x < radix) digit_publish(status + threadIdx.x, tile, first, thist[threadIdx.x], epoch);
+            for (int i = 0; i < SI; i++)
+                if (ib + i * 64 < n) atomicAdd(&thist[PDIGIT(key[i])], 1u);
 #pragma unroll
-        for (int i = 0; i < SI; i++) rank[i] = ballot_rank(whist[w], PDIGIT(key[i]), ib + i * 64 < n, bits);
-    }
-    __syncthreads();
-    const uint32_t d0 = threadIdx.x;
-    uint32_t tot = 0;
-    if (d0 < RADIX) {
-#pragma unroll
-        for (int ww = 0; ww < NWAVE; ww++) {
-            const uint32_t c = whist[ww][d0];
-            whist[ww][d0] = tot;
-            tot += c;
-        }
-    }
-    const uint32_t ls = block_exclusive_scan<NT>(tot, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
-    if (d0 < RADIX) lstart[d0] = ls;
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < SI; i++) {
-        if (ib + i * 64 < n) {
-            const uint32_t d = PDIGIT(key[i]);
-            skeys[lstart[d] + whist[w][d] + rank[i]] = key[i];
-        }
-    }
-    {
-        const uint32_t tpd = NT / radix >= 4 ? 4 : (NT / radix >= 2 ? 2 : 1);
-        if (threadIdx.x < radix * tpd) {
-            const uint32_t d = threadIdx.x / tpd;
-            uint64_t excl;
-            // a bucket's chain has ~2 tiles in flight: the predecessor is
-            // usually done, so rounds of 2 status loads per lane
-            if (dbg & 1) excl = 0;  // timing ablation only: no look-back (wrong offsets)
-            else if (tpd == 4) excl = group_lookback<4, 2>(status + d, tile, first, thist[d], epoch, err);
-            else if (tpd == 2) excl = group_lookback<2, 2>(status + d, tile, first, thist[d], epoch, err);
-            else excl = group_lookback<1, 2>(status + d, tile, first, thist[d], epoch, err);
-            if (threadIdx.x % tpd == 0) {
-                gexcl[d] = excl;
-                const uint64_t incl = excl + thist[d];
-                if (incl > C1) atomicOr(err, ERR_REGION);
-                if (r + 1 == total) cnt1[(b << bits) | d] = (uint32_t)(incl < C1 ? incl : C1);
+            for (int i = 0; i < SI; i++) {
+                const bool valid = ib + i * 64 < n;
+                const uint32_t d = PDIGIT(key[i]), hs = (d & 1u) * 16u;
+                uint64_t peers = __ballot(valid);
+                for (uint32_t bb = 0; bb < bits; bb++) {
+                    const bool set = (d >> bb) & 1u;
+                    const uint64_t mm = __ballot(set);
+                    peers &= set ? mm : ~mm;
+                }
+                const uint32_t before = valid ? (whist[w][d >> 1] >> hs) & 0xffffu : 0u;
+                rank[i] = before + (uint32_t)__popcll(peers & lanemask_lt());
+                __builtin_amdgcn_wave_barrier();
+                const int leader = __ffsll((unsigned long long)peers) - 1;
+                if (valid && lane == leader) atomicAdd(&whist[w][d >> 1], (uint32_t)__popcll(peers) << hs);
+                __builtin_amdgcn_wave_barrier();
             }
         }
-    }
-    __syncthreads();
+        __syncthreads();
+        RSTAMP(tile, 1);
+        // digit pairs (2t, 2t+1), t < R1/2: per-wave exclusive offsets in place,
+        // then the block scan of the digit totals
+        const uint32_t t = threadIdx.x;
+        uint32_t tlo = 0, thi = 0;
+        if (t < R1 / 2) {
 #pragma unroll
-    for (int rr = 0; rr < SI; rr++) {
-        const uint32_t q = threadIdx.x + rr * NT;
-        if (q < n) {
-            const uint64_t kk = skeys[q];
-            const uint32_t d = PDIGIT(kk);
-            const uint64_t at = gexcl[d] + (q - lstart[d]);
-            if (at < C1) out[((uint64_t)((b << bits) | d)) * C1 + at] = kk;
+            for (int ww = 0; ww < NWAVE; ww++) {
+                const uint32_t c = whist[ww][t];
+                whist[ww][t] = tlo | (thi << 16);
+                tlo += c & 0xffffu;
+                thi += c >> 16;
+            }
         }
-    }
-    }
+        const uint32_t ls = block_exclusive_scan<NT>(tlo + thi, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
+        if (t < R1 / 2) {
+            lstart[2 * t] = ls;
+            lstart[2 * t + 1] = ls + tlo;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < SI; i++) {
+            if (ib + i * 64 < n) {
+                const uint32_t d = PDIGIT(key[i]);
+                skeys[lstart[d] + ((whist[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rank[i]] = key[i];
+            }
+        }
+        RSTAMP(tile, 2);
+        if (threadIdx.x < R1 / 4) {
+            // chained scan, four digits per status word: a bucket's chain has
+            // ~2 tiles in flight and the predecessor's inclusive counts are
+            // usually published by now; region counts are < 2^14 (C1 <=
+            // FCAP), so four fit a word's 56 value bits
+            const uint32_t g = threadIdx.x;
+            uint32_t ex[4] = {0, 0, 0, 0};
+            if (r > 0 && !(dbg & 1)) {  // (dbg & 1: timing ablation only, no chain)
+                const uint64_t *pw = status + (uint64_t)(tile - 1) * (R1 / 4) + g;
+                uint32_t spins = 0;
+                uint64_t v;
+                for (;;) {
+                    v = st_load(pw);
+                    if (st_flag(v, epoch) == ST_INCL) break;
+                    if (spin_give_up(spins, err, 2u)) break;
+                    __builtin_amdgcn_s_sleep(1);
+                }
+#pragma unroll
+                for (int q = 0; q < 4; q++) ex[q] = (uint32_t)(v >> (14 * q)) & 0x3fffu;
+            }
+            uint64_t pk = 0;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                const uint32_t d = 4 * g + q;
+                const uint32_t incl = ex[q] + thist[d];
+                if (incl > C1) atomicOr(err, ERR_REGION);
+                pk |= (uint64_t)(incl < 0x3fffu ? incl : 0x3fffu) << (14 * q);
+                gexcl[d] = ex[q];
+                if (r + 1 == total && d < radix) cnt1[(b << bits) | d] = incl < C1 ? incl : (uint32_t)C1;
+            }
+            st_store(status + (uint64_t)tile * (R1 / 4) + g, st_make(ST_INCL, epoch, pk));
+        }
+        __syncthreads();
+        RSTAMP(tile, 3);
+#pragma unroll
+        for (int rr = 0; rr < SI; rr++) {
+            const uint32_t q = threadIdx.x + rr * NT;
+            if (q < n) {
+                const uint64_t kk = skeys[q];
+                const uint32_t d = PDIGIT(kk);
+                const uint64_t at = (uint64_t)gexcl[d] + (q - lstart[d]);
+                if (at < C1) out[((uint64_t)((b << bits) | d)) * C1 + at] = kk;
+            }
+        }
+        RSTAMP(tile, 4);
 #undef PDIGIT
+    }
 }
 
 // tiles of every bucket of pass 1 (from the region counts of pass 0) -> the
@@ -386,11 +455,12 @@ __global__ __launch_bounds__(RADIX) void rg_tiles(const uint32_t *__restrict__ c
 enum { RG_COUNT = 1, RG_UNIQ = 2 };
 
 template <int MODE, typename O, bool ATOMIC>
-__global__ __launch_bounds__(FT) void rg_finish(const uint64_t *__restrict__ in, uint64_t C1,
+__global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ in, uint64_t C1,
                                                 const uint32_t *__restrict__ cnt1, uint32_t Q, uint32_t rest,
                                                 uint32_t rc, uint64_t *__restrict__ okeys, O *__restrict__ ovals,
                                                 uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
-                                                uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg) {
+                                                uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg,
+                                                uint64_t *__restrict__ stp) {
     __shared__ __attribute__((aligned(16))) uint64_t s[FCAP];
     __shared__ uint32_t wh[FW][FWORD];  // per-wave digit counters, u16 pairs
     __shared__ uint32_t dstart[FRAD];
@@ -403,6 +473,7 @@ __global__ __launch_bounds__(FT) void rg_finish(const uint64_t *__restrict__ in,
     const uint32_t r = s_tile;
     const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
     const uint32_t m = cnt1[r];
+    RSTAMP(r, 0);
     const uint64_t *src = in + (uint64_t)r * C1;
     const uint64_t rmask = (1ull << rest) - 1;
     const uint32_t pw = (uint32_t)w * (FIPT * 64) + (uint32_t)lane;  // wave-striped positions
@@ -414,6 +485,7 @@ __global__ __launch_bounds__(FT) void rg_finish(const uint64_t *__restrict__ in,
     // to a word (a wave ranks <= 64 * FIPT items), same-word LDS atomics of one
     // wave return in lane order (probed: ATOMIC), else ballot match-any.
     // (dbg & 1: timing ablation only, no sort passes)
+    RSTAMP(r, 1);
     const uint32_t np = (dbg & 1) ? 0u : (rest + FBITS - 1) / FBITS;
     uint32_t at = 0;
     for (uint32_t p = 0; p < np; p++) {
@@ -486,6 +558,7 @@ __global__ __launch_bounds__(FT) void rg_finish(const uint64_t *__restrict__ in,
         __syncthreads();
     }
 
+    RSTAMP(r, 2);
     // ---- run-length pass (thread t: sorted positions t*FIPT ..)
     const uint32_t q0 = (uint32_t)t * FIPT;
     uint64_t kv[FIPT];
@@ -529,6 +602,7 @@ __global__ __launch_bounds__(FT) void rg_finish(const uint64_t *__restrict__ in,
     uint32_t total;
     const uint32_t off = block_exclusive_scan<FT>(ne, SumU32(), 0u, lds_scan, &total);
     // (the scan's barriers ordered every read of s above before the writes below)
+    RSTAMP(r, 3);
     if (w == 0) {
         const uint64_t ob = wave_lookback<0>(status, r, total, epoch, err);
         if (lane == 0) s_out = ob;
@@ -550,6 +624,7 @@ __global__ __launch_bounds__(FT) void rg_finish(const uint64_t *__restrict__ in,
     }
 #undef RKEY
     __syncthreads();
+    RSTAMP(r, 4);
     const uint64_t ob = s_out;
     if (dbg & 2) return;  // timing ablation only: no output writes
     for (uint32_t q = t; q < total; q += FT) okeys[ob + q] = s[q];
@@ -561,6 +636,7 @@ __global__ __launch_bounds__(FT) void rg_finish(const uint64_t *__restrict__ in,
         if ((emit >> j) & 1u) so[o++] = ov[j];
     __syncthreads();
     for (uint32_t q = t; q < total; q += FT) ovals[ob + q] = so[q];
+    RSTAMP(r, 5);
 }
 
 struct RegionPlan {
@@ -587,10 +663,11 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     p.W = n_bases * (p.rc ? 2 : 1);
     p.Q = mode == KMAN_FINISH_UNIQ ? (bitlen(p.W - 1) ? bitlen(p.W - 1) : 1u) : 0u;
     if (p.K - B1 + p.Q > 64) return KMAN_EFALLBACK;
-    // B2: fewest bits with an expected region fill <= 12288 (at most 8)
+    // B2: fewest bits with an expected region fill <= 6144 (at most 9); up
+    // to 7800 expected keeps > 10 sd (uniform data) below the LDS capacity
     uint32_t b2 = 1;
-    while (b2 < 8 && (p.W >> (B1 + b2)) > 12288) b2++;
-    if ((p.W >> (B1 + b2)) > 16000) return KMAN_EFALLBACK;
+    while (b2 < 9 && (p.W >> (B1 + b2)) > 6144) b2++;
+    if ((p.W >> (B1 + b2)) > 7800) return KMAN_EFALLBACK;
     if (p.K < B1 + b2 + 1) return KMAN_EFALLBACK;
     p.B2 = b2;
     p.rest = p.K - B1 - b2;
@@ -616,25 +693,58 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
 
 template <int MODE, typename O>
 void launch_finish(kman_ctx *ctx, const RegionPlan &p, const uint64_t *r1, const uint32_t *c1, uint64_t *okeys,
-                   void *ovals, uint32_t nreg, uint32_t epoch, uint32_t *counter, uint32_t dbg) {
+                   void *ovals, uint32_t nreg, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     if (ctx->lds_atomic_ordered)
         hipLaunchKernelGGL((rg_finish<MODE, O, true>), dim3(nreg), dim3(FT), 0, ctx->stream, r1, p.C1, c1, p.Q,
-                           p.rest, (uint32_t)p.rc, okeys, (O *)ovals, ctx->d_status, counter, epoch, ctx->d_err, dbg);
+                           p.rest, (uint32_t)p.rc, okeys, (O *)ovals, ctx->d_status, counter, epoch, ctx->d_err, dbg, stp);
     else
         hipLaunchKernelGGL((rg_finish<MODE, O, false>), dim3(nreg), dim3(FT), 0, ctx->stream, r1, p.C1, c1, p.Q,
-                           p.rest, (uint32_t)p.rc, okeys, (O *)ovals, ctx->d_status, counter, epoch, ctx->d_err, dbg);
+                           p.rest, (uint32_t)p.rc, okeys, (O *)ovals, ctx->d_status, counter, epoch, ctx->d_err, dbg, stp);
 }
 
 template <int EI, bool RC>
 void launch_extract(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
-                    uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter) {
+                    uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     const uint32_t grid = RS * p.seg_tiles;
     if (ctx->lds_atomic_ordered)
         hipLaunchKernelGGL((rg_extract<EI, RC, true>), dim3(grid), dim3(RT), 0, ctx->stream, codes, n_bases, (int)k,
-                           p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch, ctx->d_err);
+                           p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch, ctx->d_err, dbg, stp);
     else
         hipLaunchKernelGGL((rg_extract<EI, RC, false>), dim3(grid), dim3(RT), 0, ctx->stream, codes, n_bases, (int)k,
-                           p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch, ctx->d_err);
+                           p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch, ctx->d_err, dbg, stp);
+}
+
+// mean phase durations (us) per kernel from the stamp rows; frees the buffers
+int report_stamps(kman_ctx *ctx, uint64_t **st, const uint64_t *rows) {
+    static const char *names[3] = {"rg_extract", "rg_pass", "rg_finish"};
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (int q = 0; q < 3; q++) {
+        std::vector<uint64_t> h(rows[q] * 8);
+        HIP_TRY(ctx, hipMemcpy(h.data(), st[q], h.size() * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(ctx, hipFree(st[q]));
+        double sum[8] = {0}, tot = 0;
+        uint64_t n[8] = {0}, nt = 0;
+        for (uint64_t r = 0; r < rows[q]; r++) {
+            const uint64_t *x = &h[r * 8];
+            int last = 0;
+            for (int i = 1; i < 8; i++)
+                if (x[i] && x[i - 1]) {
+                    sum[i] += (double)(x[i] - x[i - 1]) / 100.0;
+                    n[i]++;
+                    last = i;
+                }
+            if (x[0] && last) {
+                tot += (double)(x[last] - x[0]) / 100.0;
+                nt++;
+            }
+        }
+        fprintf(stderr, "stamps %-10s tiles %8llu  mean us/tile %.2f  phases:", names[q], (unsigned long long)nt,
+                nt ? tot / nt : 0.0);
+        for (int i = 1; i < 8; i++)
+            if (n[i]) fprintf(stderr, " %d:%.2f", i, sum[i] / n[i]);
+        fprintf(stderr, "\n");
+    }
+    return KMAN_OK;
 }
 
 }  // namespace
@@ -674,17 +784,24 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
     uint32_t *lim = (uint32_t *)((char *)d_work + p.off_lim);
     const uint32_t nreg = 1u << (B1 + p.B2);
     HIP_TRY(ctx, hipMemsetAsync(c0, 0, p.bytes - p.off_c0, ctx->stream));
+    uint64_t *stamps[3] = {nullptr, nullptr, nullptr};
+    const uint64_t stamp_rows[3] = {p.n_tiles0, (uint64_t)RADIX * p.maxt1, nreg};
+    if (getenv("KMAN_RG_STAMPS"))
+        for (int q = 0; q < 3; q++) {
+            HIP_TRY(ctx, hipMalloc((void **)&stamps[q], stamp_rows[q] * 64));
+            HIP_TRY(ctx, hipMemsetAsync(stamps[q], 0, stamp_rows[q] * 64, ctx->stream));
+        }
     uint32_t epoch, *counter;
     // pass 0: extraction by the top 8 bits
     KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
     {
         KTimer kt_(ctx, "region_extract");
-        if (p.rc) launch_extract<8, true>(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter);
-        else launch_extract<16, false>(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter);
+        if (p.rc) launch_extract<8, true>(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter, dbg >> 8, stamps[0]);
+        else launch_extract<16, false>(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter, dbg >> 8, stamps[0]);
         HIP_TRY(ctx, hipGetLastError());
     }
     // pass 1: per bucket, by the next B2 bits
-    KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)RADIX * p.maxt1 * RADIX, &epoch, &counter));
+    KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)RADIX * p.maxt1 * (R1 / 4), &epoch, &counter));
     {
         hipLaunchKernelGGL(rg_tiles, dim3(1), dim3(RADIX), 0, ctx->stream, c0, lim);
         KTimer kt_(ctx, "region_pass");
@@ -693,10 +810,10 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
         const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, RT, (uint64_t)RADIX * p.maxt1);
         if (ctx->lds_atomic_ordered)
             hipLaunchKernelGGL((rg_pass<true>), dim3(grid), dim3(RT), 0, ctx->stream, r0, p.C0, c0, lim, p.maxt1, sh,
-                               p.B2, r1, p.C1, c1, ctx->d_status, counter, epoch, ctx->d_err, dbg >> 4);
+                               p.B2, r1, p.C1, c1, ctx->d_status, counter, epoch, ctx->d_err, dbg >> 4, stamps[1]);
         else
             hipLaunchKernelGGL((rg_pass<false>), dim3(grid), dim3(RT), 0, ctx->stream, r0, p.C0, c0, lim, p.maxt1,
-                               sh, p.B2, r1, p.C1, c1, ctx->d_status, counter, epoch, ctx->d_err, dbg >> 4);
+                               sh, p.B2, r1, p.C1, c1, ctx->d_status, counter, epoch, ctx->d_err, dbg >> 4, stamps[1]);
         HIP_TRY(ctx, hipGetLastError());
     }
     // finish: one block per region
@@ -704,14 +821,15 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
     {
         KTimer kt_(ctx, "region_finish");
         if (mode == KMAN_FINISH_UNIQ) {
-            if (oval_bytes == 4) launch_finish<RG_UNIQ, uint32_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15);
-            else launch_finish<RG_UNIQ, uint64_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15);
+            if (oval_bytes == 4) launch_finish<RG_UNIQ, uint32_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15, stamps[2]);
+            else launch_finish<RG_UNIQ, uint64_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15, stamps[2]);
         } else {
-            if (oval_bytes == 4) launch_finish<RG_COUNT, uint32_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15);
-            else launch_finish<RG_COUNT, uint64_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15);
+            if (oval_bytes == 4) launch_finish<RG_COUNT, uint32_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15, stamps[2]);
+            else launch_finish<RG_COUNT, uint64_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15, stamps[2]);
         }
         HIP_TRY(ctx, hipGetLastError());
     }
+    if (stamps[0]) KMAN_TRY(report_stamps(ctx, stamps, stamp_rows));
     // results: output count (last region's inclusive), region-0 counts (k-mers), error word
     uint64_t *h = ctx->h_small;
     HIP_TRY(ctx, hipMemcpyAsync(h + 4, ctx->d_status + (nreg - 1), 8, hipMemcpyDeviceToHost, ctx->stream));

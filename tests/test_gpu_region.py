@@ -81,9 +81,14 @@ def test_groups_matches_oracle(dev, golden_inputs, k, rc, mode):
         flags = (N.KMAN_RC if rc else 0) | (N.KMAN_WANT_POS if mode == "uniq" else 0)
         wb = c_uint64(0)
         inside = N.lib().kman_groups_plan(n_bases, k, flags, m, byref(wb)) == N.KMAN_OK
-        # outside: 2k - 8 key bits + the pos bits exceed one u64 item
-        q = max(1, int(n_bases * (2 if rc else 1) - 1).bit_length()) if mode == "uniq" else 0
-        assert inside == (2 * k - 8 + q <= 64)
+        # outside: 2k - 8 key bits + the pos bits exceed one u64 item, or no
+        # key bits left below the 8 + b2 region bits (b2 as region.hip picks it)
+        W = n_bases * (2 if rc else 1)
+        q = max(1, int(W - 1).bit_length()) if mode == "uniq" else 0
+        b2 = 1
+        while b2 < 9 and (W >> (8 + b2)) > 6144:
+            b2 += 1
+        assert inside == (2 * k - 8 + q <= 64 and 2 * k >= 8 + b2 + 1 and (W >> (8 + b2)) <= 7800)
         got = _groups(dev, text, k, rc, mode)
         if not inside:
             assert got is None

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Stage timings of the region path (kman_groups) with timing ablations
 (KMAN_RG_DBG, region.hip): 1 = finish without its LDS sort passes, 2 = finish
-without output writes, 16 = rg_pass without look-back.  Results of ablated
+without output writes, 16 = rg_pass without look-back, 256 = rg_extract
+without look-back.  Results of ablated
 runs are wrong by construction; only their timings are read."""
 import os
 import sys
@@ -18,7 +19,7 @@ text = inputs.syn_numpy(1_000_000_000, 1)
 dev = engine.Device(0)
 pipe = engine.ResidentPipeline(dev, text, 21, mode=mode)
 del text
-for dbg in ["0", "1", "2", "3", "16", "0"]:
+for dbg in ["0", "1", "2", "3", "16", "256", "0"]:
     os.environ["KMAN_RG_DBG"] = dbg
     pipe.step()
     pipe.timing(True)
