@@ -250,14 +250,31 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
 // radix 512 keeps the block at 78 KiB of LDS: two blocks per CU.  The
 // bucket's last tile writes the final region counts.
 constexpr int R1 = 512;  // pass-1 radix bound
+// The input of a digit pass: nbk buckets, each the concatenation of nsg <= 64
+// segments (bucket bk, segment s: seg_cnt[bk * nsg + s] items at seg_base[..],
+// or at (bk * nsg + s) * stride when seg_base is null).  Each bucket is its own
+// look-back chain; its tiles are handed out round robin over the buckets.
+// Output region of digit d: ((bk / gsub) << bits | d) * gsub + bk % gsub (gsub
+// > 1 keeps the sub-buckets' outputs apart, as sub-regions of one region).
+// With tag, bits [tag_shift, tag_shift + tag_bits) of each item are replaced
+// by its segment index as it is loaded (the source rank on N > 1).
+struct PassArgs {
+    const uint64_t *in;
+    const uint64_t *seg_base;
+    const uint32_t *seg_cnt;
+    uint64_t stride;
+    uint32_t nbk, nsg, gsub, maxt;
+    uint32_t shift, bits;
+    uint32_t tag, tag_shift, tag_bits;
+    uint64_t *out;
+    uint64_t C1;
+    uint32_t *cnt1;
+};
+
 template <bool ATOMIC>
-__global__ __launch_bounds__(RT, 4) void rg_pass(const uint64_t *__restrict__ in, uint64_t C0,
-                                                 const uint32_t *__restrict__ cnt0,
-                                                 const uint32_t *__restrict__ lim_p, uint32_t maxt, uint32_t shift,
-                                                 uint32_t bits, uint64_t *__restrict__ out, uint64_t C1,
-                                                 uint32_t *__restrict__ cnt1, uint64_t *__restrict__ status,
-                                                 uint32_t *__restrict__ counter, uint32_t epoch,
-                                                 uint32_t *__restrict__ err, uint32_t dbg,
+__global__ __launch_bounds__(RT, 4) void rg_pass(PassArgs pa, const uint32_t *__restrict__ lim_p,
+                                                 uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
+                                                 uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg,
                                                  uint64_t *__restrict__ stp) {
     constexpr int NT = RT, SI = RSI, TILE = NT * SI, NWAVE = NT / 64;
     static_assert(NT == R1, "one thread per digit");
@@ -267,9 +284,11 @@ __global__ __launch_bounds__(RT, 4) void rg_pass(const uint64_t *__restrict__ in
     __shared__ uint32_t lstart[R1];
     __shared__ uint32_t gexcl[R1];
     __shared__ uint32_t lds_scan[NWAVE];
-    __shared__ uint32_t spre[RS + 1];
+    __shared__ uint32_t spre[65];
+    __shared__ uint64_t sbase[64];
     __shared__ uint32_t lds_tile;
-    static_assert(RS <= 64 && (RS & (RS - 1)) == 0, "region prefixes: one wave, binary search");
+    const uint32_t shift = pa.shift, bits = pa.bits, nsg = pa.nsg;
+    const uint64_t C1 = pa.C1;
 
     // persistent: tile ids until the bucket-major limit (rg_tiles); a block
     // finishes its tile before taking the next, so every predecessor of a
@@ -281,23 +300,26 @@ __global__ __launch_bounds__(RT, 4) void rg_pass(const uint64_t *__restrict__ in
     for (;;) {
         const uint32_t cid = (uint32_t)grab_tile(counter, &lds_tile);
         if (cid >= lim) break;
-        const uint32_t b = cid % RADIX, r = cid / RADIX;
+        const uint32_t b = cid % pa.nbk, r = cid / pa.nbk;
         if (threadIdx.x < 64) {
-            const uint32_t c = threadIdx.x < RS ? cnt0[b * RS + threadIdx.x] : 0u;
+            // segment prefixes (segments >= nsg: empty) and bases
+            const uint32_t sgl = threadIdx.x;
+            const uint64_t gi = (uint64_t)b * nsg + sgl;
+            const uint32_t c = sgl < nsg ? pa.seg_cnt[gi] : 0u;
             const uint32_t inc = wave_inclusive_scan(c, SumU32());
-            if (threadIdx.x < RS) spre[threadIdx.x + 1] = inc;
-            if (threadIdx.x == 0) spre[0] = 0;
+            spre[sgl + 1] = inc;
+            if (sgl == 0) spre[0] = 0;
+            sbase[sgl] = sgl < nsg ? (pa.seg_base ? pa.seg_base[gi] : gi * pa.stride) : 0ull;
         }
         for (int i = threadIdx.x; i < NWAVE * R1 / 2; i += NT) (&whist[0][0])[i] = 0;
         if (!ATOMIC) thist[threadIdx.x] = 0;
         __syncthreads();
-        const uint32_t items = spre[RS];
+        const uint32_t items = spre[64];
         const uint32_t total = (items + TILE - 1) / TILE;
         if (r >= total) continue;  // (block-uniform) past the bucket's tiles
-        const int64_t tile = (int64_t)b * maxt + r;  // status index; a bucket's chain starts at r = 0
+        const int64_t tile = (int64_t)b * pa.maxt + r;  // status index; a bucket's chain starts at r = 0
         const uint32_t t0 = r * TILE;
         const uint32_t n = items - t0 < (uint32_t)TILE ? items - t0 : (uint32_t)TILE;
-        const uint64_t *bin = in + (uint64_t)b * RS * C0;
         RSTAMP(tile, 0);
         const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
         uint64_t key[SI];
@@ -308,9 +330,13 @@ __global__ __launch_bounds__(RT, 4) void rg_pass(const uint64_t *__restrict__ in
             const uint32_t li = t0 + ib + i * 64;
             uint32_t sg = 0;
 #pragma unroll
-            for (int step = RS / 2; step; step >>= 1)
+            for (int step = 32; step; step >>= 1)
                 if (spre[sg + step] <= li) sg += step;
-            key[i] = ib + i * 64 < n ? bin[(uint64_t)sg * C0 + (li - spre[sg])] : 0;
+            key[i] = ib + i * 64 < n ? pa.in[sbase[sg] + (li - spre[sg])] : 0;
+            if (pa.tag) {
+                const uint64_t tm = ((1ull << pa.tag_bits) - 1) << pa.tag_shift;
+                key[i] = (key[i] & ~tm) | ((uint64_t)sg << pa.tag_shift);
+            }
         }
 #define PDIGIT(x) ((uint32_t)((x) >> shift) & dmask)
         if (ATOMIC) {
@@ -408,7 +434,8 @@ __global__ __launch_bounds__(RT, 4) void rg_pass(const uint64_t *__restrict__ in
                 if (incl > C1) atomicOr(err, ERR_REGION);
                 pk |= (uint64_t)(incl < 0x3fffu ? incl : 0x3fffu) << (14 * q);
                 gexcl[d] = ex[q];
-                if (r + 1 == total && d < radix) cnt1[(b << bits) | d] = incl < C1 ? incl : (uint32_t)C1;
+                if (r + 1 == total && d < radix)
+                    pa.cnt1[(((b / pa.gsub) << bits) | d) * pa.gsub + b % pa.gsub] = incl < C1 ? incl : (uint32_t)C1;
             }
             st_store(status + (uint64_t)tile * (R1 / 4) + g, st_make(ST_INCL, epoch, pk));
         }
@@ -421,7 +448,7 @@ __global__ __launch_bounds__(RT, 4) void rg_pass(const uint64_t *__restrict__ in
                 const uint64_t kk = skeys[q];
                 const uint32_t d = PDIGIT(kk);
                 const uint64_t at = (uint64_t)gexcl[d] + (q - lstart[d]);
-                if (at < C1) out[((uint64_t)((b << bits) | d)) * C1 + at] = kk;
+                if (at < C1) pa.out[((uint64_t)(((b / pa.gsub) << bits) | d) * pa.gsub + b % pa.gsub) * C1 + at] = kk;
             }
         }
         RSTAMP(tile, 4);
@@ -429,20 +456,25 @@ __global__ __launch_bounds__(RT, 4) void rg_pass(const uint64_t *__restrict__ in
     }
 }
 
-// tiles of every bucket of pass 1 (from the region counts of pass 0) -> the
-// tile-id limit of the persistent rg_pass: max over buckets x RADIX
-__global__ __launch_bounds__(RADIX) void rg_tiles(const uint32_t *__restrict__ cnt0, uint32_t *__restrict__ lim) {
-    __shared__ uint32_t sc[RADIX / 64];
-    uint32_t items = 0;
-    for (int s = 0; s < RS; s++) items += cnt0[threadIdx.x * RS + s];
-    const uint32_t t = (items + (uint32_t)T1 - 1) / (uint32_t)T1;
-    const uint32_t m = wave_inclusive_scan(t, [](uint32_t a, uint32_t b) { return a > b ? a : b; }, 0u);
-    if (lane_id() == 63) sc[threadIdx.x >> 6] = m;
+// tiles of every bucket of a digit pass (from its segment counts) -> the
+// tile-id limit of the persistent rg_pass: max over buckets x nbk
+__global__ __launch_bounds__(256) void rg_tiles(const uint32_t *__restrict__ cnt, uint32_t nbk, uint32_t nsg,
+                                                uint32_t *__restrict__ lim) {
+    __shared__ uint32_t sc[4];
+    uint32_t mx = 0;
+    for (uint32_t bk = threadIdx.x; bk < nbk; bk += 256) {
+        uint32_t items = 0;
+        for (uint32_t s = 0; s < nsg; s++) items += cnt[(uint64_t)bk * nsg + s];
+        const uint32_t t = (items + (uint32_t)T1 - 1) / (uint32_t)T1;
+        mx = t > mx ? t : mx;
+    }
+    mx = wave_inclusive_scan(mx, [](uint32_t a, uint32_t b) { return a > b ? a : b; }, 0u);
+    if (lane_id() == 63) sc[threadIdx.x >> 6] = mx;
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t mx = 0;
-        for (int w = 0; w < RADIX / 64; w++) mx = sc[w] > mx ? sc[w] : mx;
-        *lim = mx * RADIX;
+        uint32_t m = 0;
+        for (int w = 0; w < 4; w++) m = sc[w] > m ? sc[w] : m;
+        *lim = m * nbk;
     }
 }
 
@@ -691,6 +723,18 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     return KMAN_OK;
 }
 
+void launch_pass(kman_ctx *ctx, const PassArgs &pa, const uint32_t *lim, uint32_t epoch, uint32_t *counter,
+                 uint32_t dbg, uint64_t *stp) {
+    const void *fn = ctx->lds_atomic_ordered ? (const void *)rg_pass<true> : (const void *)rg_pass<false>;
+    const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, RT, (uint64_t)pa.nbk * pa.maxt);
+    if (ctx->lds_atomic_ordered)
+        hipLaunchKernelGGL((rg_pass<true>), dim3(grid), dim3(RT), 0, ctx->stream, pa, lim, ctx->d_status, counter,
+                           epoch, ctx->d_err, dbg, stp);
+    else
+        hipLaunchKernelGGL((rg_pass<false>), dim3(grid), dim3(RT), 0, ctx->stream, pa, lim, ctx->d_status, counter,
+                           epoch, ctx->d_err, dbg, stp);
+}
+
 template <int MODE, typename O>
 void launch_finish(kman_ctx *ctx, const RegionPlan &p, const uint64_t *r1, const uint32_t *c1, uint64_t *okeys,
                    void *ovals, uint32_t nreg, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
@@ -803,17 +847,23 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
     // pass 1: per bucket, by the next B2 bits
     KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)RADIX * p.maxt1 * (R1 / 4), &epoch, &counter));
     {
-        hipLaunchKernelGGL(rg_tiles, dim3(1), dim3(RADIX), 0, ctx->stream, c0, lim);
+        hipLaunchKernelGGL(rg_tiles, dim3(1), dim3(256), 0, ctx->stream, c0, (uint32_t)RADIX, (uint32_t)RS, lim);
         KTimer kt_(ctx, "region_pass");
-        const uint32_t sh = p.Q + p.rest;
-        const void *fn = ctx->lds_atomic_ordered ? (const void *)rg_pass<true> : (const void *)rg_pass<false>;
-        const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, RT, (uint64_t)RADIX * p.maxt1);
-        if (ctx->lds_atomic_ordered)
-            hipLaunchKernelGGL((rg_pass<true>), dim3(grid), dim3(RT), 0, ctx->stream, r0, p.C0, c0, lim, p.maxt1, sh,
-                               p.B2, r1, p.C1, c1, ctx->d_status, counter, epoch, ctx->d_err, dbg >> 4, stamps[1]);
-        else
-            hipLaunchKernelGGL((rg_pass<false>), dim3(grid), dim3(RT), 0, ctx->stream, r0, p.C0, c0, lim, p.maxt1,
-                               sh, p.B2, r1, p.C1, c1, ctx->d_status, counter, epoch, ctx->d_err, dbg >> 4, stamps[1]);
+        PassArgs pa{};
+        pa.in = r0;
+        pa.seg_base = nullptr;
+        pa.seg_cnt = c0;
+        pa.stride = p.C0;
+        pa.nbk = RADIX;
+        pa.nsg = RS;
+        pa.gsub = 1;
+        pa.maxt = p.maxt1;
+        pa.shift = p.Q + p.rest;
+        pa.bits = p.B2;
+        pa.out = r1;
+        pa.C1 = p.C1;
+        pa.cnt1 = c1;
+        launch_pass(ctx, pa, lim, epoch, counter, dbg >> 4, stamps[1]);
         HIP_TRY(ctx, hipGetLastError());
     }
     // finish: one block per region

@@ -99,6 +99,31 @@ def test_groups_matches_oracle(dev, golden_inputs, k, rc, mode):
         np.testing.assert_array_equal(got[1].astype(np.uint64), want[1])
 
 
+@pytest.mark.parametrize("mode", ["count", "uniq"])
+@pytest.mark.parametrize("copies", [3, 100, 1000])
+def test_groups_repeats(dev, mode, copies):
+    """Repeated segments: equal keys share a finish bin; past BINMAX (64)
+    the region takes the in-kernel LSD passes instead of the bin sort."""
+    import inputs
+
+    rng = np.random.default_rng(copies)
+    seg = "".join(rng.choice(list("ACGT"), 300))
+    body = inputs.syn_numpy(200_000, 3).split(b"\n", 1)[1].replace(b"\n", b"")
+    text = b">r\n" + body + b"\n>s\n" + (seg * copies).encode() + b"\n"
+    got = _groups(dev, text, 21, False, mode)
+    want = _oracle(text, 21, False, mode)
+    if got is None:
+        # 1000 copies overflow a region: the engine's general path instead
+        assert copies >= 1000
+        from kman_amd import engine
+
+        out = (engine.count_text if mode == "count" else engine.uniq_text)(text, 21, dev=dev)
+        assert out.count(b"\n") == len(want[0]) * (1 if mode == "count" else 2)
+        return
+    np.testing.assert_array_equal(got[0], want[0])
+    np.testing.assert_array_equal(got[1].astype(np.uint64), want[1])
+
+
 def test_groups_plan_domain():
     """kman_groups_plan: KMAN_EFALLBACK outside the path, a size inside it."""
     from kman_amd import _native as N
