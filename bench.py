@@ -82,7 +82,8 @@ def main() -> None:
     ap.add_argument("--bases", type=int, default=1_000_000_000, help="synthetic bases per GPU (1 GB FASTA)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--path", choices=["region", "split", "full"], default="region",
-                    help="single-GPU engine path (region falls back to split outside its domain)")
+                    help="engine path (region falls back to split outside its domain)")
+    ap.add_argument("--dist", action="store_true", help="run the multi-GPU pipeline even at world size 1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -101,13 +102,16 @@ def main() -> None:
     text = inputs.syn_numpy(args.bases, 1 + rank)
     log("rank %d: generated %.2f GB FASTA in %.1f s" % (rank, len(text) / 1e9, time.time() - t0))
     dev = engine.Device(local)
-    if world > 1:
-        # prefix-range partition + one RCCL all-to-all over xGMI (kman_amd/dist.py)
+    if world > 1 or args.dist:
+        # region path across ranks: one RCCL all-to-all of packed items over
+        # xGMI (kman_amd/dist.py), prefix-range path as the fallback
         from kman_amd import dist as kd
 
         uid = [kd.unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        pipe = kd.DistPipeline(dev, text, args.k, args.mode, world, rank, uid[0])
+        if dist:
+            dist.broadcast_object_list(uid, src=0)
+        pipe = kd.DistPipeline(dev, text, args.k, args.mode, world, rank, uid[0],
+                               path="split" if args.path == "split" else "region")
     else:
         pipe = engine.ResidentPipeline(dev, text, args.k, mode=args.mode, path=args.path)
     fasta_bytes = len(text)
@@ -143,7 +147,8 @@ def main() -> None:
     region = getattr(pipe, "path", "split") == "region"
     n_pass, pass_ms = pipe.timed("region_pass" if region else "sort_pass")
     stages = {}
-    for tag in ("parse", "region_extract", "region_pass", "region_finish", "kmer_hist", "extract_pass", "extract",
+    for tag in ("parse", "region_extract", "dist_gather", "region_pass", "region_pass1b", "region_finish", "kmer_hist",
+                "extract_pass", "extract",
                 "prefix_hist", "partition", "sort_hist", "sort_pass", "finish", "rle_count", "rle_uniq"):
         c, ms = pipe.timed(tag)
         if c:
@@ -186,7 +191,8 @@ def main() -> None:
             "kmers_per_step_per_gpu": pipe.n_kmers,
             "k": args.k,
             "mode": args.mode,
-            "parallelism": "dp%d: prefix-range partition + RCCL all-to-all" % world if world > 1 else "single",
+            "parallelism": ("dp%d: top-8-bit bucket ranges + one RCCL all-to-all" % world
+                            if world > 1 or args.dist else "single"),
             "path": getattr(pipe, "path", "dist"),
             "stages_ms_per_step": stages,
         },

@@ -212,6 +212,36 @@ int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_
                 void *d_work, uint64_t work_bytes, uint64_t *d_okeys, void *d_ovals, uint32_t oval_bytes,
                 uint64_t *n_kmers, uint64_t *n_out);
 
+/* kman_groups across G ranks (one process per GPU; kman_amd/dist.py runs the
+ * collectives in between).  Every rank passes the same
+ * n_bases_q >= every rank's n_bases (it fixes the pos bits of the packed
+ * items) and the same world.
+ *   kman_dgroups_plan     work-area bytes, or KMAN_EFALLBACK outside the path
+ *   kman_dgroups_extract  pass 0 of the rank's shard; all its packed items
+ *                         compacted into d_send (>= n_bases x (RC ? 2 : 1)
+ *                         u64) in bucket order; bucket_counts[256] (host) =
+ *                         items per top-8-bit bucket; *overflow = 1 when a
+ *                         region overflowed (the ranks then fall back together)
+ *   (caller)              all-reduce of the bucket counts, contiguous bucket
+ *                         ranges per rank, all-gather of the counts, one
+ *                         all-to-all of the items (kman_alltoallv, 8 B)
+ *   kman_dgroups_finish   the received items of buckets [b_lo, b_lo + nb)
+ *                         (source chunks in rank order, each in bucket order;
+ *                         counts[src * nb + j] = items of bucket b_lo + j from
+ *                         src) -> this rank's count / uniq output, ascending
+ *                         (uniq pos u64 with the source rank in bits 56-63);
+ *                         KMAN_EFALLBACK on a region overflow.
+ * The ranks' outputs in rank order are the global output (join.py:95-130). */
+int kman_dgroups_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t flags, int mode, uint32_t world,
+                      uint64_t *work_bytes);
+int kman_dgroups_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint64_t n_bases_q, uint32_t k,
+                         uint32_t flags, int mode, uint32_t world, void *d_work, uint64_t work_bytes,
+                         uint64_t *d_send, uint64_t *bucket_counts, uint32_t *overflow);
+int kman_dgroups_finish(kman_ctx *ctx, const uint64_t *d_recv, uint64_t n_bases, uint64_t n_bases_q, uint32_t k,
+                        uint32_t flags, int mode, uint32_t world, uint32_t b_lo, uint32_t nb,
+                        const uint64_t *counts, void *d_work, uint64_t work_bytes, uint64_t *d_okeys,
+                        void *d_ovals, uint32_t oval_bytes, uint64_t *n_out);
+
 /* Run-length count of sorted keys (join.py:95-130 + 266-285):
  * d_ukeys[j], d_counts[j] (u32 if count_bytes == 4 else u64). */
 int kman_rle_count(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint64_t *d_ukeys,

@@ -101,6 +101,17 @@ SIGNATURES = {
         [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_int, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32,
          POINTER(c_uint64), POINTER(c_uint64)],
     ),
+    "kman_dgroups_plan": (c_int, [c_uint64, c_uint64, c_uint32, c_uint32, c_int, c_uint32, POINTER(c_uint64)]),
+    "kman_dgroups_extract": (
+        c_int,
+        [c_void_p, c_void_p, c_uint64, c_uint64, c_uint32, c_uint32, c_int, c_uint32, c_void_p, c_uint64, c_void_p,
+         c_void_p, POINTER(c_uint32)],
+    ),
+    "kman_dgroups_finish": (
+        c_int,
+        [c_void_p, c_void_p, c_uint64, c_uint64, c_uint32, c_uint32, c_int, c_uint32, c_uint32, c_uint32, c_void_p,
+         c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, POINTER(c_uint64)],
+    ),
     "kman_rle_count": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, POINTER(c_uint64)]),
     "kman_rle_uniq": (
         c_int,

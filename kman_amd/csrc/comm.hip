@@ -114,16 +114,33 @@ extern "C" int kman_alltoallv(kman_ctx *ctx, const void *d_send, const uint64_t 
     Comm *c = comm_of(ctx);
     if (!c) return kman_fail(ctx, KMAN_EINVAL, "no communicator");
     const ncclDataType_t t = elem_bytes == 8 ? ncclUint64 : ncclUint32;
-    NCCL_TRY(ctx, ncclGroupStart());
+    // messages in chunks of <= 512 MiB: a single multi-GiB send/recv pair
+    // was observed to move only part of its bytes (RCCL 2.27, 2.4 GB to self);
+    // both ends derive the same chunk sequence from the same count
+    const uint64_t CH = (512ull << 20) / elem_bytes;
+    uint64_t rounds = 0;
     for (int p = 0; p < c->nranks; p++) {
-        if (send_counts[p])
-            NCCL_TRY(ctx, ncclSend((const char *)d_send + send_offsets[p] * elem_bytes, send_counts[p], t, p,
-                                   c->comm, ctx->stream));
-        if (recv_counts[p])
-            NCCL_TRY(ctx, ncclRecv((char *)d_recv + recv_offsets[p] * elem_bytes, recv_counts[p], t, p, c->comm,
-                                   ctx->stream));
+        const uint64_t a = (send_counts[p] + CH - 1) / CH, b = (recv_counts[p] + CH - 1) / CH;
+        rounds = a > rounds ? a : rounds;
+        rounds = b > rounds ? b : rounds;
     }
-    NCCL_TRY(ctx, ncclGroupEnd());
+    for (uint64_t r = 0; r < rounds; r++) {
+        NCCL_TRY(ctx, ncclGroupStart());
+        for (int p = 0; p < c->nranks; p++) {
+            const uint64_t o = r * CH;
+            if (send_counts[p] > o) {
+                const uint64_t n = send_counts[p] - o < CH ? send_counts[p] - o : CH;
+                NCCL_TRY(ctx, ncclSend((const char *)d_send + (send_offsets[p] + o) * elem_bytes, n, t, p, c->comm,
+                                       ctx->stream));
+            }
+            if (recv_counts[p] > o) {
+                const uint64_t n = recv_counts[p] - o < CH ? recv_counts[p] - o : CH;
+                NCCL_TRY(ctx, ncclRecv((char *)d_recv + (recv_offsets[p] + o) * elem_bytes, n, t, p, c->comm,
+                                       ctx->stream));
+            }
+        }
+        NCCL_TRY(ctx, ncclGroupEnd());
+    }
     return KMAN_OK;
 }
 

@@ -489,7 +489,8 @@ enum { RG_COUNT = 1, RG_UNIQ = 2 };
 template <int MODE, typename O, bool ATOMIC>
 __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ in, uint64_t C1,
                                                 const uint32_t *__restrict__ cnt1, uint32_t Q, uint32_t rest,
-                                                uint32_t rc, uint64_t *__restrict__ okeys, O *__restrict__ ovals,
+                                                uint32_t rc, uint64_t rbase, uint32_t tag_shift,
+                                                uint64_t *__restrict__ okeys, O *__restrict__ ovals,
                                                 uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
                                                 uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg,
                                                 uint64_t *__restrict__ stp) {
@@ -647,11 +648,14 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
         if ((emit >> j) & 1u) {
             if constexpr (MODE == RG_UNIQ) {
                 const uint64_t idx = kv[j] & qmask;
-                ov[j] = (O)(rc ? idx : (idx << 1));
+                const uint64_t pos = rc ? idx : (idx << 1);
+                // N > 1: the source rank (tagged into the item by the pass after
+                // the exchange) in bits 56-63, as DistPipeline's payloads
+                ov[j] = (O)(tag_shift ? pos | (((kv[j] >> tag_shift) & 0x1ffull) << 56) : pos);
             } else {
                 ov[j] = (O)cval[j];
             }
-            s[o++] = ((uint64_t)r << rest) | RKEY(kv[j]);
+            s[o++] = ((uint64_t)(r + rbase) << rest) | RKEY(kv[j]);
         }
     }
 #undef RKEY
@@ -735,15 +739,43 @@ void launch_pass(kman_ctx *ctx, const PassArgs &pa, const uint32_t *lim, uint32_
                            epoch, ctx->d_err, dbg, stp);
 }
 
+struct FinishArgs {
+    const uint64_t *in;
+    uint64_t C1;
+    const uint32_t *cnt;
+    uint32_t Q, rest, rc;
+    uint64_t rbase;
+    uint32_t tag_shift;
+    uint32_t nreg;
+};
+
 template <int MODE, typename O>
-void launch_finish(kman_ctx *ctx, const RegionPlan &p, const uint64_t *r1, const uint32_t *c1, uint64_t *okeys,
-                   void *ovals, uint32_t nreg, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
+void launch_finish(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ovals, uint32_t epoch,
+                   uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     if (ctx->lds_atomic_ordered)
-        hipLaunchKernelGGL((rg_finish<MODE, O, true>), dim3(nreg), dim3(FT), 0, ctx->stream, r1, p.C1, c1, p.Q,
-                           p.rest, (uint32_t)p.rc, okeys, (O *)ovals, ctx->d_status, counter, epoch, ctx->d_err, dbg, stp);
+        hipLaunchKernelGGL((rg_finish<MODE, O, true>), dim3(f.nreg), dim3(FT), 0, ctx->stream, f.in, f.C1, f.cnt, f.Q,
+                           f.rest, f.rc, f.rbase, f.tag_shift, okeys, (O *)ovals, ctx->d_status, counter, epoch,
+                           ctx->d_err, dbg, stp);
     else
-        hipLaunchKernelGGL((rg_finish<MODE, O, false>), dim3(nreg), dim3(FT), 0, ctx->stream, r1, p.C1, c1, p.Q,
-                           p.rest, (uint32_t)p.rc, okeys, (O *)ovals, ctx->d_status, counter, epoch, ctx->d_err, dbg, stp);
+        hipLaunchKernelGGL((rg_finish<MODE, O, false>), dim3(f.nreg), dim3(FT), 0, ctx->stream, f.in, f.C1, f.cnt,
+                           f.Q, f.rest, f.rc, f.rbase, f.tag_shift, okeys, (O *)ovals, ctx->d_status, counter, epoch,
+                           ctx->d_err, dbg, stp);
+}
+
+int run_finish(kman_ctx *ctx, const FinishArgs &f, int mode, uint64_t *okeys, void *ovals, uint32_t oval_bytes,
+               uint32_t dbg, uint64_t *stp) {
+    uint32_t epoch, *counter;
+    KMAN_TRY(kman_lookback_begin(ctx, f.nreg, &epoch, &counter));
+    KTimer kt_(ctx, "region_finish");
+    if (mode == KMAN_FINISH_UNIQ) {
+        if (oval_bytes == 4) launch_finish<RG_UNIQ, uint32_t>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
+        else launch_finish<RG_UNIQ, uint64_t>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
+    } else {
+        if (oval_bytes == 4) launch_finish<RG_COUNT, uint32_t>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
+        else launch_finish<RG_COUNT, uint64_t>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
+    }
+    HIP_TRY(ctx, hipGetLastError());
+    return KMAN_OK;
 }
 
 template <int EI, bool RC>
@@ -867,17 +899,9 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
         HIP_TRY(ctx, hipGetLastError());
     }
     // finish: one block per region
-    KMAN_TRY(kman_lookback_begin(ctx, nreg, &epoch, &counter));
     {
-        KTimer kt_(ctx, "region_finish");
-        if (mode == KMAN_FINISH_UNIQ) {
-            if (oval_bytes == 4) launch_finish<RG_UNIQ, uint32_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15, stamps[2]);
-            else launch_finish<RG_UNIQ, uint64_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15, stamps[2]);
-        } else {
-            if (oval_bytes == 4) launch_finish<RG_COUNT, uint32_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15, stamps[2]);
-            else launch_finish<RG_COUNT, uint64_t>(ctx, p, r1, c1, d_okeys, d_ovals, nreg, epoch, counter, dbg & 15, stamps[2]);
-        }
-        HIP_TRY(ctx, hipGetLastError());
+        FinishArgs f{r1, p.C1, c1, p.Q, p.rest, (uint32_t)p.rc, 0, 0, nreg};
+        KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, dbg & 15, stamps[2]));
     }
     if (stamps[0]) KMAN_TRY(report_stamps(ctx, stamps, stamp_rows));
     // results: output count (last region's inclusive), region-0 counts (k-mers), error word
@@ -896,11 +920,326 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
         return kman_fail(ctx, KMAN_ETIMEOUT, "device look-back wait exceeded its bound (code %u)", e);
     }
     const uint64_t wd = h[4];
-    if (((wd >> 56) & 63u) != epoch || (wd >> 62) != ST_INCL)
+    if (((wd >> 56) & 63u) != ctx->epoch || (wd >> 62) != ST_INCL)
         return kman_fail(ctx, KMAN_EHIP, "region output total not published");
     uint64_t nk = 0;
     for (uint32_t v : hc) nk += v;
     *n_kmers = nk;
+    *n_out = wd & ST_VMASK;
+    return KMAN_OK;
+}
+
+namespace {
+// KMAN_RG_VERBOSE: synchronise after each pass of kman_dgroups_finish and
+// report which one raised a region overflow (diagnostics only)
+int rg_check(kman_ctx *ctx, const char *what, const uint32_t *cnt = nullptr, uint64_t n = 0) {
+    static const bool verbose = getenv("KMAN_RG_VERBOSE") != nullptr;
+    if (!verbose) return KMAN_OK;
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    uint32_t e = 0;
+    HIP_TRY(ctx, hipMemcpy(&e, ctx->d_err, 4, hipMemcpyDeviceToHost));
+    uint64_t mx = 0, sum = 0, nz = 0;
+    if (cnt && n) {
+        std::vector<uint32_t> h(n);
+        HIP_TRY(ctx, hipMemcpy(h.data(), cnt, n * 4, hipMemcpyDeviceToHost));
+        for (uint32_t v : h) {
+            mx = v > mx ? v : mx;
+            sum += v;
+            nz += v != 0;
+        }
+        // nonzero counts per block of n/16 entries
+        fprintf(stderr, "  nonzero per 1/16:");
+        for (int q = 0; q < 16; q++) {
+            uint64_t z = 0;
+            for (uint64_t i = q * n / 16; i < (q + 1) * n / 16; i++) z += h[i] != 0;
+            fprintf(stderr, " %llu", (unsigned long long)z);
+        }
+        fprintf(stderr, "\n  first 8:");
+        for (int q = 0; q < 8 && q < (int)n; q++) fprintf(stderr, " %u", h[q]);
+        fprintf(stderr, "\n");
+    }
+    fprintf(stderr, "kman_dgroups: after %s err=%u counts n=%llu nonzero=%llu sum=%llu max=%llu\n", what, e,
+            (unsigned long long)n, (unsigned long long)nz, (unsigned long long)sum, (unsigned long long)mx);
+    return KMAN_OK;
+}
+}  // namespace
+
+// =============================================================== N > 1
+// The region path across G ranks (one process per GPU; kman_amd/dist.py
+// drives the collectives between the calls):
+//   kman_dgroups_extract  pass 0 on the rank's shard, then every region
+//                         compacted into the send buffer in (bucket, segment)
+//                         order; per-bucket counts to the host
+//   (host)                all-reduce of the bucket counts -> contiguous bucket
+//                         ranges per rank; all-gather of the counts; one
+//                         all-to-all of the packed items (RCCL, xGMI)
+//   kman_dgroups_finish   per (bucket, source) chain: pass 1 by 9 bits into
+//                         sub-regions (b, d, src); pass 1b per (b, d) by g =
+//                         ceil(log2 G) more bits, tagging each item with its
+//                         source rank (in the d field, implied from here);
+//                         then the LDS finish.  Output keys of the rank's
+//                         bucket range, ascending, so the ranks' outputs in
+//                         rank order are the global output; uniq pos carry the
+//                         source rank in bits 56-63.
+namespace {
+
+struct DistPlan {
+    uint32_t K, Q, g, rest, world;
+    bool rc;
+    RegionPlan p0;        // pass 0 of the local shard
+    uint64_t C1s, C1;     // pass-1 sub-region / pass-1b region capacities
+    uint32_t nb_max;      // buckets a rank may own
+    uint64_t off_r1, off_c1, off_r2, off_c2, off_tab, off_lim, bytes;
+};
+
+int make_dplan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t flags, int mode, uint32_t world,
+               DistPlan *dp) {
+    if (world < 1 || world > 256) return KMAN_EINVAL;
+    if (n_bases_q < n_bases) return KMAN_EINVAL;
+    RegionPlan p;
+    // pass-0 layout from the local shard; Q from the common bound n_bases_q
+    const int r = make_plan(n_bases ? n_bases : 1, k, flags, mode, &p);
+    if (r != KMAN_OK) return r;
+    DistPlan d{};
+    d.K = 2 * k;
+    d.rc = flags & KMAN_RC;
+    d.world = world;
+    const uint64_t Wq = n_bases_q * (d.rc ? 2 : 1);
+    d.Q = mode == KMAN_FINISH_UNIQ ? (bitlen(Wq - 1) ? bitlen(Wq - 1) : 1u) : 0u;
+    if (d.K - B1 + d.Q > 64) return KMAN_EFALLBACK;
+    p.Q = d.Q;  // pass 0 packs with the common Q
+    uint32_t g = 1;
+    while ((1u << g) < world) g++;
+    d.g = g;
+    if (d.K < B1 + 9 + g + 1) return KMAN_EFALLBACK;
+    d.rest = d.K - B1 - 9 - g;
+    const uint64_t e1 = Wq >> (B1 + 9);                         // per source, bucket and d
+    d.C1s = ceil_div(e1 + e1 / 2 + 256, 64) * 64;
+    const uint64_t e2 = (Wq * world) >> (B1 + 9 + g);          // per final region
+    if (e2 > 7800) return KMAN_EFALLBACK;
+    const uint64_t c2 = ceil_div(e2 + e2 / 2 + 512, 64) * 64;
+    d.C1 = c2 < (uint64_t)FCAP ? c2 : (uint64_t)FCAP;
+    // (kman_amd/dist.py mirrors this bound)
+    const uint32_t per = (RADIX + world - 1) / world;
+    d.nb_max = per + per / 2 + 4 < (uint32_t)RADIX ? per + per / 2 + 4 : (uint32_t)RADIX;
+    const uint64_t nsub = (uint64_t)d.nb_max * 512 * world;    // pass-1 sub-regions
+    const uint64_t nreg = (uint64_t)d.nb_max * 512 << g;      // pass-1b regions
+    d.off_r1 = p.bytes;
+    d.off_c1 = d.off_r1 + nsub * d.C1s * 8;
+    d.off_r2 = d.off_c1 + nsub * 4;
+    d.off_c2 = d.off_r2 + nreg * d.C1 * 8;
+    d.off_tab = d.off_c2 + nreg * 4;
+    // tables: gather offsets [RADIX * RS] u64, pass-1 segment bases [nb_max * world] u64 + counts u32
+    const uint64_t tab = (uint64_t)RADIX * RS * 8 + (uint64_t)d.nb_max * world * 12;
+    d.off_lim = d.off_tab + ceil_div(tab, 64) * 64;
+    d.bytes = d.off_lim + 64;
+    d.p0 = p;
+    *dp = d;
+    return KMAN_OK;
+}
+
+// copy each pass-0 region (b, s) to its place in the compact send buffer
+__global__ __launch_bounds__(256) void rg_gather(const uint64_t *__restrict__ r0, uint64_t C0,
+                                                 const uint32_t *__restrict__ cnt0, const uint64_t *__restrict__ off,
+                                                 uint64_t *__restrict__ send) {
+    const uint32_t g = blockIdx.y;  // region (b * RS + s)
+    const uint32_t c = cnt0[g];
+    const uint64_t *src = r0 + (uint64_t)g * C0;
+    uint64_t *dst = send + off[g];
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < c; i += gridDim.x * 256) dst[i] = src[i];
+}
+
+}  // namespace
+
+extern "C" int kman_dgroups_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t flags, int mode,
+                                 uint32_t world, uint64_t *work_bytes) {
+    if (!work_bytes) return KMAN_EINVAL;
+    DistPlan d;
+    const int r = make_dplan(n_bases, n_bases_q, k, flags, mode, world, &d);
+    *work_bytes = r == KMAN_OK ? d.bytes : 0;
+    return r;
+}
+
+extern "C" int kman_dgroups_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint64_t n_bases_q,
+                                    uint32_t k, uint32_t flags, int mode, uint32_t world, void *d_work,
+                                    uint64_t work_bytes, uint64_t *d_send, uint64_t *bucket_counts,
+                                    uint32_t *overflow) {
+    if (!ctx || !bucket_counts || !overflow) return KMAN_EINVAL;
+    *overflow = 0;
+    memset(bucket_counts, 0, RADIX * sizeof(uint64_t));
+    DistPlan d;
+    const int pr = make_dplan(n_bases, n_bases_q, k, flags, mode, world, &d);
+    if (pr == KMAN_EINVAL) return kman_fail(ctx, KMAN_EINVAL, "kman_dgroups_extract: bad arguments");
+    if (pr != KMAN_OK) return pr;
+    if (!d_codes || !d_work || !d_send) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    if (work_bytes < d.bytes) return kman_fail(ctx, KMAN_ECAP, "work area too small");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const RegionPlan &p = d.p0;
+    uint64_t *r0 = (uint64_t *)d_work;
+    uint32_t *c0 = (uint32_t *)((char *)d_work + p.off_c0);
+    uint64_t *goff = (uint64_t *)((char *)d_work + d.off_tab);
+    HIP_TRY(ctx, hipMemsetAsync(c0, 0, (uint64_t)RADIX * RS * 4, ctx->stream));
+    if (n_bases) {
+        uint32_t epoch, *counter;
+        KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
+        KTimer kt_(ctx, "region_extract");
+        if (p.rc) launch_extract<8, true>(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter, 0, nullptr);
+        else launch_extract<16, false>(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter, 0, nullptr);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    std::vector<uint32_t> hc((size_t)RADIX * RS);
+    HIP_TRY(ctx, hipMemcpyAsync(hc.data(), c0, hc.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small + 8, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    uint32_t e;
+    memcpy(&e, ctx->h_small + 8, 4);
+    if (e) {
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if (e != ERR_REGION) return kman_fail(ctx, KMAN_ETIMEOUT, "device look-back wait exceeded its bound (code %u)", e);
+        *overflow = 1;  // the caller agrees on the fallback collectively
+        return KMAN_OK;
+    }
+    std::vector<uint64_t> off(hc.size());
+    uint64_t acc = 0;
+    for (size_t i = 0; i < hc.size(); i++) {
+        off[i] = acc;
+        acc += hc[i];
+        bucket_counts[i / RS] += hc[i];
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(goff, off.data(), off.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    {
+        KTimer kt_(ctx, "dist_gather");
+        const uint32_t gx = (uint32_t)ceil_div(p.C0, 4096);
+        hipLaunchKernelGGL(rg_gather, dim3(gx < 1 ? 1 : gx, RADIX * RS), dim3(256), 0, ctx->stream, r0, p.C0, c0,
+                           goff, d_send);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // the host copy of off must stay valid until consumed
+    return KMAN_OK;
+}
+
+extern "C" int kman_dgroups_finish(kman_ctx *ctx, const uint64_t *d_recv, uint64_t n_bases, uint64_t n_bases_q,
+                                   uint32_t k, uint32_t flags, int mode, uint32_t world, uint32_t b_lo, uint32_t nb,
+                                   const uint64_t *counts, void *d_work, uint64_t work_bytes, uint64_t *d_okeys,
+                                   void *d_ovals, uint32_t oval_bytes, uint64_t *n_out) {
+    if (!ctx || !n_out || !counts) return KMAN_EINVAL;
+    *n_out = 0;
+    DistPlan d;
+    const int pr = make_dplan(n_bases, n_bases_q, k, flags, mode, world, &d);
+    if (pr == KMAN_EINVAL) return kman_fail(ctx, KMAN_EINVAL, "kman_dgroups_finish: bad arguments");
+    if (pr != KMAN_OK) return pr;
+    if (nb > d.nb_max || b_lo + nb > (uint32_t)RADIX) return KMAN_EFALLBACK;
+    if (work_bytes < d.bytes) return kman_fail(ctx, KMAN_ECAP, "work area too small");
+    if (oval_bytes != 4 && oval_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "oval_bytes must be 4 or 8");
+    if (mode == KMAN_FINISH_UNIQ && oval_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "uniq pos on N > 1 are u64");
+    if (nb == 0) return KMAN_OK;
+    if (!d_recv || !d_work || !d_okeys || !d_ovals) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    char *wk = (char *)d_work;
+    uint64_t *r1 = (uint64_t *)(wk + d.off_r1);
+    uint32_t *c1 = (uint32_t *)(wk + d.off_c1);
+    uint64_t *r2 = (uint64_t *)(wk + d.off_r2);
+    uint32_t *c2 = (uint32_t *)(wk + d.off_c2);
+    uint64_t *sbase = (uint64_t *)(wk + d.off_tab + (uint64_t)RADIX * RS * 8);
+    uint32_t *scnt = (uint32_t *)(sbase + (uint64_t)d.nb_max * world);
+    uint32_t *lim = (uint32_t *)(wk + d.off_lim);
+    const uint32_t G = world;
+    // pass-1 segments: bucket (b, src) = one contiguous run of src's chunk
+    std::vector<uint64_t> hb((size_t)nb * G);
+    std::vector<uint32_t> hn((size_t)nb * G);
+    uint64_t roff = 0, maxc = 0;
+    for (uint32_t src = 0; src < G; src++) {
+        uint64_t at = roff;
+        for (uint32_t j = 0; j < nb; j++) {
+            const uint64_t c = counts[(uint64_t)src * nb + j];
+            if (c > 0xffffffffull) return KMAN_EFALLBACK;
+            hb[(size_t)j * G + src] = at;
+            hn[(size_t)j * G + src] = (uint32_t)c;
+            at += c;
+            maxc = c > maxc ? c : maxc;
+        }
+        roff = at;
+    }
+    const uint32_t nbk = nb * G;
+    const uint32_t maxt1 = (uint32_t)ceil_div(maxc, T1) + 1;
+    HIP_TRY(ctx, hipMemcpyAsync(sbase, hb.data(), hb.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(scnt, hn.data(), hn.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    const uint64_t nsub = (uint64_t)nb * 512 * G;
+    const uint32_t nreg = (uint32_t)((uint64_t)nb * 512 << d.g);
+    HIP_TRY(ctx, hipMemsetAsync(c1, 0, nsub * 4, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(c2, 0, (uint64_t)nreg * 4, ctx->stream));
+    uint32_t epoch, *counter;
+    // pass 1: by the 9 bits below the bucket, per (b, src) chain
+    {
+        hipLaunchKernelGGL(rg_tiles, dim3(1), dim3(256), 0, ctx->stream, scnt, nbk, 1u, lim);
+        KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)nbk * maxt1 * (R1 / 4), &epoch, &counter));
+        KTimer kt_(ctx, "region_pass");
+        PassArgs pa{};
+        pa.in = d_recv;
+        pa.seg_base = sbase;
+        pa.seg_cnt = scnt;
+        pa.nbk = nbk;
+        pa.nsg = 1;
+        pa.gsub = G;
+        pa.maxt = maxt1;
+        pa.shift = d.Q + d.K - B1 - 9;
+        pa.bits = 9;
+        pa.out = r1;
+        pa.C1 = d.C1s;
+        pa.cnt1 = c1;
+        launch_pass(ctx, pa, lim, epoch, counter, 0, nullptr);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    KMAN_TRY(rg_check(ctx, "pass 1", c1, nsub));
+    // pass 1b: per (b, d), its G sub-regions concatenated, by g more bits;
+    // the segment index (source rank) goes into the d field
+    {
+        const uint32_t nbk2 = nb * 512;
+        const uint32_t maxt2 = (uint32_t)ceil_div((uint64_t)G * d.C1s, T1) + 1;
+        hipLaunchKernelGGL(rg_tiles, dim3(1), dim3(256), 0, ctx->stream, c1, nbk2, G, lim);
+        KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)nbk2 * maxt2 * (R1 / 4), &epoch, &counter));
+        KTimer kt_(ctx, "region_pass1b");
+        PassArgs pa{};
+        pa.in = r1;
+        pa.seg_base = nullptr;
+        pa.seg_cnt = c1;
+        pa.stride = d.C1s;
+        pa.nbk = nbk2;
+        pa.nsg = G;
+        pa.gsub = 1;
+        pa.maxt = maxt2;
+        pa.shift = d.Q + d.rest;
+        pa.bits = d.g;
+        pa.tag = mode == KMAN_FINISH_UNIQ;
+        pa.tag_shift = d.Q + d.rest + d.g;
+        pa.tag_bits = 9;
+        pa.out = r2;
+        pa.C1 = d.C1;
+        pa.cnt1 = c2;
+        launch_pass(ctx, pa, lim, epoch, counter, 0, nullptr);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    KMAN_TRY(rg_check(ctx, "pass 1b", c2, nreg));
+    {
+        FinishArgs f{r2, d.C1, c2, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << (9 + d.g),
+                     mode == KMAN_FINISH_UNIQ ? d.Q + d.rest + d.g : 0u, nreg};
+        KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, 0, nullptr));
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small + 4, ctx->d_status + (nreg - 1), 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small + 8, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    uint32_t e;
+    memcpy(&e, ctx->h_small + 8, 4);
+    if (e) {
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if (e == ERR_REGION) return KMAN_EFALLBACK;
+        return kman_fail(ctx, KMAN_ETIMEOUT, "device look-back wait exceeded its bound (code %u)", e);
+    }
+    const uint64_t wd = ctx->h_small[4];
+    if (((wd >> 56) & 63u) != ctx->epoch || (wd >> 62) != ST_INCL)
+        return kman_fail(ctx, KMAN_EHIP, "region output total not published");
     *n_out = wd & ST_VMASK;
     return KMAN_OK;
 }

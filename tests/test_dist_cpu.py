@@ -143,3 +143,19 @@ def test_plan_is_balanced():
     C = np.array([[1, 2], [3, 4]], dtype=np.uint64)
     s, so, r, ro = recv_layout(C, 1)
     assert list(s) == [3, 4] and list(so) == [0, 3] and list(r) == [2, 4] and list(ro) == [0, 2]
+
+
+def test_region_bucket_ranges():
+    """bucket_ranges: contiguous ranges covering the 256 buckets, ~1/G of the
+    k-mers each; within nb_max for uniform counts (skewed counts may exceed it:
+    the ranks then fall back together)."""
+    from kman_amd import dist
+
+    rng = np.random.default_rng(0)
+    for G in (1, 2, 3, 5, 8):
+        g = rng.poisson(3_900_000, 256).astype(np.uint64)
+        b_lo, nb = dist.bucket_ranges(g, G)
+        assert nb.sum() == 256 and b_lo[0] == 0 and (b_lo[1:] == np.cumsum(nb)[:-1]).all()
+        assert (nb <= dist.nb_max(G)).all()
+        share = np.array([g[b_lo[q]:b_lo[q] + nb[q]].sum() for q in range(G)], np.float64) / g.sum()
+        assert np.abs(share - 1 / G).max() < 1.5 / 256 * G / G + 1e-9

@@ -56,8 +56,9 @@ def test_prefix_hist_and_partition(dev, n, buckets):
         b.free()
 
 
+@pytest.mark.parametrize("path", ["region", "split"])
 @pytest.mark.parametrize("mode", ["count", "uniq"])
-def test_dist_pipeline_world1_equals_single(dev, mode):
+def test_dist_pipeline_world1_equals_single(dev, mode, path):
     import sys, os
 
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
@@ -66,9 +67,11 @@ def test_dist_pipeline_world1_equals_single(dev, mode):
     from kman_amd import dist
 
     text = inputs.messy_records(7, n_records=40, max_len=20000)
-    p = dist.DistPipeline(dev, text, 13, mode, 1, 0, dist.unique_id())
+    p = dist.DistPipeline(dev, text, 13, mode, 1, 0, dist.unique_id(), path=path)
     try:
-        p.step()
+        for _ in range(2):
+            p.step()
+            assert p.path == path  # RCCL world 1: no fallback
         keys, vals = p.results()
     finally:
         p.free()
