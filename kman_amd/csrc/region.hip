@@ -264,6 +264,8 @@ struct PassArgs {
     const uint32_t *seg_cnt;
     uint64_t stride;
     uint32_t nbk, nsg, gsub, maxt;
+    uint32_t H;        // chains (parts) per bucket: outputs are H sub-regions per region
+    uint32_t tag_div;  // tag = segment index / tag_div
     uint32_t shift, bits;
     uint32_t tag, tag_shift, tag_bits;
     uint64_t *out;
@@ -272,9 +274,8 @@ struct PassArgs {
 };
 
 template <bool ATOMIC>
-__global__ __launch_bounds__(RT, 4) void rg_pass(PassArgs pa, const uint32_t *__restrict__ lim_p,
-                                                 uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
-                                                 uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg,
+__global__ __launch_bounds__(RT, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
+                                                 uint32_t *__restrict__ err, uint32_t dbg,
                                                  uint64_t *__restrict__ stp) {
     constexpr int NT = RT, SI = RSI, TILE = NT * SI, NWAVE = NT / 64;
     static_assert(NT == R1, "one thread per digit");
@@ -282,201 +283,179 @@ __global__ __launch_bounds__(RT, 4) void rg_pass(PassArgs pa, const uint32_t *__
     __shared__ uint32_t whist[NWAVE][R1 / 2];
     __shared__ uint32_t thist[R1];
     __shared__ uint32_t lstart[R1];
-    __shared__ uint32_t gexcl[R1];
+    __shared__ uint32_t run[R1];  // the chain's running count per digit
     __shared__ uint32_t lds_scan[NWAVE];
-    __shared__ uint32_t spre[65];
-    __shared__ uint64_t sbase[64];
+    __shared__ uint32_t s_items;
     __shared__ uint32_t lds_tile;
-    const uint32_t shift = pa.shift, bits = pa.bits, nsg = pa.nsg;
+    const uint32_t shift = pa.shift, bits = pa.bits, nsg = pa.nsg, H = pa.H;
     const uint64_t C1 = pa.C1;
-
-    // persistent: tile ids until the bucket-major limit (rg_tiles); a block
-    // finishes its tile before taking the next, so every predecessor of a
-    // tile is taken and in progress (forward progress of the look-back)
-    const uint32_t lim = *lim_p;
     const int lane = lane_id();
     const int w = threadIdx.x >> 6;
     const uint32_t radix = 1u << bits, dmask = radix - 1;
+    const uint32_t nchain = pa.nbk * H;
+    (void)dbg;
+
+    // block-owned chains: a block takes a whole chain (bucket b, part h: the
+    // h-th of H runs of the bucket's tiles) and walks its tiles in order,
+    // carrying each digit's running count in LDS, so no tile ever waits on
+    // another block (no look-back, no status words)
     for (;;) {
-        const uint32_t cid = (uint32_t)grab_tile(counter, &lds_tile);
-        if (cid >= lim) break;
-        const uint32_t b = cid % pa.nbk, r = cid / pa.nbk;
-        if (threadIdx.x < 64) {
-            // segment prefixes (segments >= nsg: empty) and bases
-            const uint32_t sgl = threadIdx.x;
+        const uint32_t ch = (uint32_t)grab_tile(counter, &lds_tile);
+        if (ch >= nchain) break;
+        const uint32_t b = ch / H, h = ch % H;
+        // every wave: the bucket's segment prefixes (lane s: items before
+        // segment s; segments >= nsg empty) and bases, in registers
+        uint32_t spre_l;
+        uint64_t sbase_l;
+        {
+            const uint32_t sgl = (uint32_t)lane;
             const uint64_t gi = (uint64_t)b * nsg + sgl;
             const uint32_t c = sgl < nsg ? pa.seg_cnt[gi] : 0u;
             const uint32_t inc = wave_inclusive_scan(c, SumU32());
-            spre[sgl + 1] = inc;
-            if (sgl == 0) spre[0] = 0;
-            sbase[sgl] = sgl < nsg ? (pa.seg_base ? pa.seg_base[gi] : gi * pa.stride) : 0ull;
+            spre_l = inc - c;
+            sbase_l = sgl < nsg ? (pa.seg_base ? pa.seg_base[gi] : gi * pa.stride) : 0ull;
+            if (threadIdx.x == 63) s_items = inc;
         }
-        for (int i = threadIdx.x; i < NWAVE * R1 / 2; i += NT) (&whist[0][0])[i] = 0;
-        if (!ATOMIC) thist[threadIdx.x] = 0;
+        run[threadIdx.x] = 0;
         __syncthreads();
-        const uint32_t items = spre[64];
-        const uint32_t total = (items + TILE - 1) / TILE;
-        if (r >= total) continue;  // (block-uniform) past the bucket's tiles
-        const int64_t tile = (int64_t)b * pa.maxt + r;  // status index; a bucket's chain starts at r = 0
-        const uint32_t t0 = r * TILE;
-        const uint32_t n = items - t0 < (uint32_t)TILE ? items - t0 : (uint32_t)TILE;
-        RSTAMP(tile, 0);
-        const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
-        uint64_t key[SI];
-        uint32_t rank[SI];
-#pragma unroll
-        for (int i = 0; i < SI; i++) {
-            // logical item -> (region s, offset): binary search of the prefixes
-            const uint32_t li = t0 + ib + i * 64;
-            uint32_t sg = 0;
-#pragma unroll
-            for (int step = 32; step; step >>= 1)
-                if (spre[sg + step] <= li) sg += step;
-            key[i] = ib + i * 64 < n ? pa.in[sbase[sg] + (li - spre[sg])] : 0;
-            if (pa.tag) {
-                const uint64_t tm = ((1ull << pa.tag_bits) - 1) << pa.tag_shift;
-                key[i] = (key[i] & ~tm) | ((uint64_t)sg << pa.tag_shift);
-            }
-        }
-#define PDIGIT(x) ((uint32_t)((x) >> shift) & dmask)
-        if (ATOMIC) {
+        const uint32_t items = s_items;
+        const uint32_t tiles = (items + TILE - 1) / TILE;
+        const uint32_t per = (tiles + H - 1) / H;
+        const uint32_t ra = h * per, rb = ra + per < tiles ? ra + per : tiles;
+        // output sub-region of digit d
+        const uint64_t reg0 = (uint64_t)(b / pa.gsub) << bits, rsub = b % pa.gsub;
+#define SUBREG(d) (((reg0 | (d)) * pa.gsub + rsub) * H + h)
+        for (uint32_t r = ra; r < rb; r++) {
+            for (int i = threadIdx.x; i < NWAVE * R1 / 2; i += NT) (&whist[0][0])[i] = 0;
+            if (!ATOMIC) thist[threadIdx.x] = 0;
+            __syncthreads();
+            const uint32_t t0 = r * TILE;
+            const uint32_t n = items - t0 < (uint32_t)TILE ? items - t0 : (uint32_t)TILE;
+            RSTAMP(r, 0);
+            const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
+            uint64_t key[SI];
+            uint32_t rank[SI];
+            uint32_t sgi[SI];
 #pragma unroll
             for (int i = 0; i < SI; i++) {
-                const uint32_t d = PDIGIT(key[i]), hs = (d & 1u) * 16u;
-                rank[i] = ib + i * 64 < n ? (atomicAdd(&whist[w][d >> 1], 1u << hs) >> hs) & 0xffffu : 0u;
+                // logical item -> (segment, offset) with ballots over the
+                // lanes' prefixes: the 64 items of a wave row are consecutive,
+                // so their segment is the row start's, past the (rare)
+                // boundaries inside the row; no LDS and no dependent chain,
+                // so all the loads issue back to back
+                const uint32_t li0 = t0 + (uint32_t)w * (SI * 64) + (uint32_t)i * 64;
+                const uint32_t li = li0 + (uint32_t)lane;
+                uint32_t sg = (uint32_t)__popcll(__ballot(spre_l <= li0) & ~1ull);  // lane 0 (prefix 0) not counted
+                uint64_t inrow = __ballot(spre_l > li0 && spre_l <= li0 + 63);
+                while (inrow) {  // (wave-uniform)
+                    const int s2 = __ffsll((unsigned long long)inrow) - 1;
+                    inrow &= inrow - 1;
+                    if (li >= (uint32_t)__builtin_amdgcn_readlane((int)spre_l, s2)) sg = (uint32_t)s2;
+                }
+                const uint64_t bs = shfl_any(sbase_l, (int)sg);
+                const uint32_t po = (uint32_t)__shfl((int)spre_l, (int)sg, 64);
+                sgi[i] = sg;
+                key[i] = ib + i * 64 < n ? pa.in[bs + (li - po)] : 0;
+            }
+            if (pa.tag) {
+                // (a separate loop, so the loads above are not serialised on it)
+                const uint64_t tm = ((1ull << pa.tag_bits) - 1) << pa.tag_shift;
+#pragma unroll
+                for (int i = 0; i < SI; i++)
+                    key[i] = (key[i] & ~tm) | ((uint64_t)(sgi[i] / pa.tag_div) << pa.tag_shift);
+            }
+#define PDIGIT(x) ((uint32_t)((x) >> shift) & dmask)
+            if (ATOMIC) {
+#pragma unroll
+                for (int i = 0; i < SI; i++) {
+                    const uint32_t d = PDIGIT(key[i]), hs = (d & 1u) * 16u;
+                    rank[i] = ib + i * 64 < n ? (atomicAdd(&whist[w][d >> 1], 1u << hs) >> hs) & 0xffffu : 0u;
+                }
+                __syncthreads();
+                {
+                    const uint32_t d = threadIdx.x, hs = (d & 1u) * 16u;
+                    uint32_t c = 0;
+#pragma unroll
+                    for (int ww = 0; ww < NWAVE; ww++) c += (whist[ww][d >> 1] >> hs) & 0xffffu;
+                    thist[d] = c;
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i < SI; i++)
+                    if (ib + i * 64 < n) atomicAdd(&thist[PDIGIT(key[i])], 1u);
+#pragma unroll
+                for (int i = 0; i < SI; i++) {
+                    const bool valid = ib + i * 64 < n;
+                    const uint32_t d = PDIGIT(key[i]), hs = (d & 1u) * 16u;
+                    uint64_t peers = __ballot(valid);
+                    for (uint32_t bb = 0; bb < bits; bb++) {
+                        const bool set = (d >> bb) & 1u;
+                        const uint64_t mm = __ballot(set);
+                        peers &= set ? mm : ~mm;
+                    }
+                    const uint32_t before = valid ? (whist[w][d >> 1] >> hs) & 0xffffu : 0u;
+                    rank[i] = before + (uint32_t)__popcll(peers & lanemask_lt());
+                    __builtin_amdgcn_wave_barrier();
+                    const int leader = __ffsll((unsigned long long)peers) - 1;
+                    if (valid && lane == leader) atomicAdd(&whist[w][d >> 1], (uint32_t)__popcll(peers) << hs);
+                    __builtin_amdgcn_wave_barrier();
+                }
             }
             __syncthreads();
-            {
-                // every R1 digit (those >= radix count 0): the packed status
-                // words below cover all of them
-                const uint32_t d = threadIdx.x, hs = (d & 1u) * 16u;
-                uint32_t c = 0;
+            // digit pairs (2t, 2t+1), t < R1/2: per-wave exclusive offsets in
+            // place, then the block scan of the digit totals
+            const uint32_t t = threadIdx.x;
+            uint32_t tlo = 0, thi = 0;
+            if (t < R1 / 2) {
 #pragma unroll
-                for (int ww = 0; ww < NWAVE; ww++) c += (whist[ww][d >> 1] >> hs) & 0xffffu;
-                thist[d] = c;
+                for (int ww = 0; ww < NWAVE; ww++) {
+                    const uint32_t c = whist[ww][t];
+                    whist[ww][t] = tlo | (thi << 16);
+                    tlo += c & 0xffffu;
+                    thi += c >> 16;
+                }
             }
-        } else {
-#pragma unroll
-            for (int i = 0; i < SI; i++)
-                if (ib + i * 64 < n) atomicAdd(&thist[PDIGIT(key[i])], 1u);
+            const uint32_t ls = block_exclusive_scan<NT>(tlo + thi, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
+            if (t < R1 / 2) {
+                lstart[2 * t] = ls;
+                lstart[2 * t + 1] = ls + tlo;
+            }
+            __syncthreads();
 #pragma unroll
             for (int i = 0; i < SI; i++) {
-                const bool valid = ib + i * 64 < n;
-                const uint32_t d = PDIGIT(key[i]), hs = (d & 1u) * 16u;
-                uint64_t peers = __ballot(valid);
-                for (uint32_t bb = 0; bb < bits; bb++) {
-                    const bool set = (d >> bb) & 1u;
-                    const uint64_t mm = __ballot(set);
-                    peers &= set ? mm : ~mm;
+                if (ib + i * 64 < n) {
+                    const uint32_t d = PDIGIT(key[i]);
+                    skeys[lstart[d] + ((whist[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rank[i]] = key[i];
                 }
-                const uint32_t before = valid ? (whist[w][d >> 1] >> hs) & 0xffffu : 0u;
-                rank[i] = before + (uint32_t)__popcll(peers & lanemask_lt());
-                __builtin_amdgcn_wave_barrier();
-                const int leader = __ffsll((unsigned long long)peers) - 1;
-                if (valid && lane == leader) atomicAdd(&whist[w][d >> 1], (uint32_t)__popcll(peers) << hs);
-                __builtin_amdgcn_wave_barrier();
             }
-        }
-        __syncthreads();
-        RSTAMP(tile, 1);
-        // digit pairs (2t, 2t+1), t < R1/2: per-wave exclusive offsets in place,
-        // then the block scan of the digit totals
-        const uint32_t t = threadIdx.x;
-        uint32_t tlo = 0, thi = 0;
-        if (t < R1 / 2) {
+            __syncthreads();
+            RSTAMP(r, 1);
 #pragma unroll
-            for (int ww = 0; ww < NWAVE; ww++) {
-                const uint32_t c = whist[ww][t];
-                whist[ww][t] = tlo | (thi << 16);
-                tlo += c & 0xffffu;
-                thi += c >> 16;
-            }
-        }
-        const uint32_t ls = block_exclusive_scan<NT>(tlo + thi, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
-        if (t < R1 / 2) {
-            lstart[2 * t] = ls;
-            lstart[2 * t + 1] = ls + tlo;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < SI; i++) {
-            if (ib + i * 64 < n) {
-                const uint32_t d = PDIGIT(key[i]);
-                skeys[lstart[d] + ((whist[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rank[i]] = key[i];
-            }
-        }
-        RSTAMP(tile, 2);
-        if (threadIdx.x < R1 / 4) {
-            // chained scan, four digits per status word: a bucket's chain has
-            // ~2 tiles in flight and the predecessor's inclusive counts are
-            // usually published by now; region counts are < 2^14 (C1 <=
-            // FCAP), so four fit a word's 56 value bits
-            const uint32_t g = threadIdx.x;
-            uint32_t ex[4] = {0, 0, 0, 0};
-            if (r > 0 && !(dbg & 1)) {  // (dbg & 1: timing ablation only, no chain)
-                const uint64_t *pw = status + (uint64_t)(tile - 1) * (R1 / 4) + g;
-                uint32_t spins = 0;
-                uint64_t v;
-                for (;;) {
-                    v = st_load(pw);
-                    if (st_flag(v, epoch) == ST_INCL) break;
-                    if (spin_give_up(spins, err, 2u)) break;
-                    __builtin_amdgcn_s_sleep(1);
+            for (int rr = 0; rr < SI; rr++) {
+                const uint32_t q = threadIdx.x + rr * NT;
+                if (q < n) {
+                    const uint64_t kk = skeys[q];
+                    const uint32_t d = PDIGIT(kk);
+                    const uint64_t at = (uint64_t)run[d] + (q - lstart[d]);
+                    if (at < C1) pa.out[SUBREG(d) * C1 + at] = kk;
                 }
-#pragma unroll
-                for (int q = 0; q < 4; q++) ex[q] = (uint32_t)(v >> (14 * q)) & 0x3fffu;
             }
-            uint64_t pk = 0;
-#pragma unroll
-            for (int q = 0; q < 4; q++) {
-                const uint32_t d = 4 * g + q;
-                const uint32_t incl = ex[q] + thist[d];
-                if (incl > C1) atomicOr(err, ERR_REGION);
-                pk |= (uint64_t)(incl < 0x3fffu ? incl : 0x3fffu) << (14 * q);
-                gexcl[d] = ex[q];
-                if (r + 1 == total && d < radix)
-                    pa.cnt1[(((b / pa.gsub) << bits) | d) * pa.gsub + b % pa.gsub] = incl < C1 ? incl : (uint32_t)C1;
-            }
-            st_store(status + (uint64_t)tile * (R1 / 4) + g, st_make(ST_INCL, epoch, pk));
-        }
-        __syncthreads();
-        RSTAMP(tile, 3);
-#pragma unroll
-        for (int rr = 0; rr < SI; rr++) {
-            const uint32_t q = threadIdx.x + rr * NT;
-            if (q < n) {
-                const uint64_t kk = skeys[q];
-                const uint32_t d = PDIGIT(kk);
-                const uint64_t at = (uint64_t)gexcl[d] + (q - lstart[d]);
-                if (at < C1) pa.out[((uint64_t)(((b / pa.gsub) << bits) | d) * pa.gsub + b % pa.gsub) * C1 + at] = kk;
-            }
-        }
-        RSTAMP(tile, 4);
+            __syncthreads();  // every read of run[] above before its update
+            run[threadIdx.x] += thist[threadIdx.x];
+            RSTAMP(r, 2);
 #undef PDIGIT
+        }
+        // the chain's sub-region counts (every digit, also of empty chains)
+        __syncthreads();
+        {
+            const uint32_t d = threadIdx.x;
+            if (run[d] > C1) atomicOr(err, ERR_REGION);
+            if (d < radix) pa.cnt1[SUBREG(d)] = run[d] < C1 ? run[d] : (uint32_t)C1;
+        }
+#undef SUBREG
     }
 }
 
-// tiles of every bucket of a digit pass (from its segment counts) -> the
-// tile-id limit of the persistent rg_pass: max over buckets x nbk
-__global__ __launch_bounds__(256) void rg_tiles(const uint32_t *__restrict__ cnt, uint32_t nbk, uint32_t nsg,
-                                                uint32_t *__restrict__ lim) {
-    __shared__ uint32_t sc[4];
-    uint32_t mx = 0;
-    for (uint32_t bk = threadIdx.x; bk < nbk; bk += 256) {
-        uint32_t items = 0;
-        for (uint32_t s = 0; s < nsg; s++) items += cnt[(uint64_t)bk * nsg + s];
-        const uint32_t t = (items + (uint32_t)T1 - 1) / (uint32_t)T1;
-        mx = t > mx ? t : mx;
-    }
-    mx = wave_inclusive_scan(mx, [](uint32_t a, uint32_t b) { return a > b ? a : b; }, 0u);
-    if (lane_id() == 63) sc[threadIdx.x >> 6] = mx;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t m = 0;
-        for (int w = 0; w < 4; w++) m = sc[w] > m ? sc[w] : m;
-        *lim = m * nbk;
-    }
-}
 
 // ---------------------------------------------------------------- finish
 // One block per region r (regions in key order = grab order): LSD sort of the
@@ -489,7 +468,7 @@ enum { RG_COUNT = 1, RG_UNIQ = 2 };
 template <int MODE, typename O, bool ATOMIC>
 __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ in, uint64_t C1,
                                                 const uint32_t *__restrict__ cnt1, uint32_t Q, uint32_t rest,
-                                                uint32_t rc, uint64_t rbase, uint32_t tag_shift,
+                                                uint32_t rc, uint64_t rbase, uint32_t tag_shift, uint32_t fsub,
                                                 uint64_t *__restrict__ okeys, O *__restrict__ ovals,
                                                 uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
                                                 uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg,
@@ -505,14 +484,25 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
     __syncthreads();
     const uint32_t r = s_tile;
     const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
-    const uint32_t m = cnt1[r];
+    // the region = fsub (1 or 2) sub-regions of capacity C1, concatenated
+    const uint32_t m0 = cnt1[(uint64_t)r * fsub];
+    const uint32_t m1 = fsub > 1 ? cnt1[(uint64_t)r * fsub + 1] : 0u;
+    uint32_t m = m0 + m1;
+    if (m > (uint32_t)FCAP) {  // (block-uniform) more than the LDS holds
+        if (t == 0) atomicOr(err, ERR_REGION);
+        m = 0;
+    }
     RSTAMP(r, 0);
-    const uint64_t *src = in + (uint64_t)r * C1;
+    const uint64_t *src = in + (uint64_t)r * fsub * C1;
+    const uint64_t *src1 = src + C1 - m0;  // position p >= m0 of the region: src1[p]
     const uint64_t rmask = (1ull << rest) - 1;
     const uint32_t pw = (uint32_t)w * (FIPT * 64) + (uint32_t)lane;  // wave-striped positions
     uint64_t x[FIPT];
 #pragma unroll
-    for (int i = 0; i < FIPT; i++) x[i] = pw + i * 64 < m ? src[pw + i * 64] : 0;
+    for (int i = 0; i < FIPT; i++) {
+        const uint32_t p = pw + i * 64;
+        x[i] = p < m ? (p < m0 ? src[p] : src1[p]) : 0;
+    }
 
     // stable LSD passes of <= 9 bits.  Ranks: per-wave u16 counters packed two
     // to a word (a wave ranks <= 64 * FIPT items), same-word LDS atomics of one
@@ -680,6 +670,8 @@ struct RegionPlan {
     bool rc;
     uint64_t W;          // windows (x2 with rc): bound on the k-mers
     uint64_t C0, C1;     // region capacities (items)
+    uint32_t H;          // pass-1 chains (sub-regions) per bucket
+    uint64_t C1h;        // pass-1 sub-region capacity
     uint32_t n_tiles0, seg_tiles, maxt1;
     uint32_t ei;         // windows per thread of pass 0
     uint64_t off_r1, off_c0, off_c1, off_lim, bytes;
@@ -716,27 +708,29 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     const uint64_t e1 = p.W >> (B1 + b2);
     uint64_t c1 = ceil_div(e1 + e1 / 2 + 512, 64) * 64;
     p.C1 = c1 < (uint64_t)FCAP ? c1 : (uint64_t)FCAP;
-    p.maxt1 = (uint32_t)ceil_div((uint64_t)RS * p.C0, T1);
+    // pass 1 runs H = 2 block-owned chains per bucket (its first and second
+    // half of tiles) into H sub-regions per region that the finish
+    // concatenates: 512 chains for the 512 resident blocks
+    p.H = 2;
+    p.C1h = p.C1;  // either half may hold most of a region (position-skewed repeats)
+    p.maxt1 = (uint32_t)ceil_div((uint64_t)(RS / p.H) * p.C0, T1);
     const uint64_t nreg = 1ull << (B1 + b2);
     p.off_r1 = (uint64_t)RADIX * RS * p.C0 * 8;
-    p.off_c0 = p.off_r1 + nreg * p.C1 * 8;
+    p.off_c0 = p.off_r1 + nreg * p.H * p.C1h * 8;
     p.off_c1 = p.off_c0 + (uint64_t)RADIX * RS * 4;
-    p.off_lim = p.off_c1 + nreg * 4;
+    p.off_lim = p.off_c1 + nreg * p.H * 4;
     p.bytes = p.off_lim + 64;
     *pl = p;
     return KMAN_OK;
 }
 
-void launch_pass(kman_ctx *ctx, const PassArgs &pa, const uint32_t *lim, uint32_t epoch, uint32_t *counter,
-                 uint32_t dbg, uint64_t *stp) {
+void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     const void *fn = ctx->lds_atomic_ordered ? (const void *)rg_pass<true> : (const void *)rg_pass<false>;
-    const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, RT, (uint64_t)pa.nbk * pa.maxt);
+    const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, RT, (uint64_t)pa.nbk * pa.H);
     if (ctx->lds_atomic_ordered)
-        hipLaunchKernelGGL((rg_pass<true>), dim3(grid), dim3(RT), 0, ctx->stream, pa, lim, ctx->d_status, counter,
-                           epoch, ctx->d_err, dbg, stp);
+        hipLaunchKernelGGL((rg_pass<true>), dim3(grid), dim3(RT), 0, ctx->stream, pa, counter, ctx->d_err, dbg, stp);
     else
-        hipLaunchKernelGGL((rg_pass<false>), dim3(grid), dim3(RT), 0, ctx->stream, pa, lim, ctx->d_status, counter,
-                           epoch, ctx->d_err, dbg, stp);
+        hipLaunchKernelGGL((rg_pass<false>), dim3(grid), dim3(RT), 0, ctx->stream, pa, counter, ctx->d_err, dbg, stp);
 }
 
 struct FinishArgs {
@@ -747,6 +741,7 @@ struct FinishArgs {
     uint64_t rbase;
     uint32_t tag_shift;
     uint32_t nreg;
+    uint32_t fsub = 1;  // sub-regions per region (cnt and in indexed per sub-region)
 };
 
 template <int MODE, typename O>
@@ -754,12 +749,12 @@ void launch_finish(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ov
                    uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     if (ctx->lds_atomic_ordered)
         hipLaunchKernelGGL((rg_finish<MODE, O, true>), dim3(f.nreg), dim3(FT), 0, ctx->stream, f.in, f.C1, f.cnt, f.Q,
-                           f.rest, f.rc, f.rbase, f.tag_shift, okeys, (O *)ovals, ctx->d_status, counter, epoch,
-                           ctx->d_err, dbg, stp);
+                           f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status, counter,
+                           epoch, ctx->d_err, dbg, stp);
     else
         hipLaunchKernelGGL((rg_finish<MODE, O, false>), dim3(f.nreg), dim3(FT), 0, ctx->stream, f.in, f.C1, f.cnt,
-                           f.Q, f.rest, f.rc, f.rbase, f.tag_shift, okeys, (O *)ovals, ctx->d_status, counter, epoch,
-                           ctx->d_err, dbg, stp);
+                           f.Q, f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status, counter,
+                           epoch, ctx->d_err, dbg, stp);
 }
 
 int run_finish(kman_ctx *ctx, const FinishArgs &f, int mode, uint64_t *okeys, void *ovals, uint32_t oval_bytes,
@@ -857,11 +852,10 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
     uint64_t *r1 = (uint64_t *)((char *)d_work + p.off_r1);
     uint32_t *c0 = (uint32_t *)((char *)d_work + p.off_c0);
     uint32_t *c1 = (uint32_t *)((char *)d_work + p.off_c1);
-    uint32_t *lim = (uint32_t *)((char *)d_work + p.off_lim);
     const uint32_t nreg = 1u << (B1 + p.B2);
     HIP_TRY(ctx, hipMemsetAsync(c0, 0, p.bytes - p.off_c0, ctx->stream));
     uint64_t *stamps[3] = {nullptr, nullptr, nullptr};
-    const uint64_t stamp_rows[3] = {p.n_tiles0, (uint64_t)RADIX * p.maxt1, nreg};
+    const uint64_t stamp_rows[3] = {p.n_tiles0, (uint64_t)p.maxt1 * RADIX, nreg};
     if (getenv("KMAN_RG_STAMPS"))
         for (int q = 0; q < 3; q++) {
             HIP_TRY(ctx, hipMalloc((void **)&stamps[q], stamp_rows[q] * 64));
@@ -876,10 +870,9 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
         else launch_extract<16, false>(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter, dbg >> 8, stamps[0]);
         HIP_TRY(ctx, hipGetLastError());
     }
-    // pass 1: per bucket, by the next B2 bits
-    KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)RADIX * p.maxt1 * (R1 / 4), &epoch, &counter));
+    // pass 1: per bucket, by the next B2 bits (H block-owned chains per bucket)
+    KMAN_TRY(kman_lookback_begin(ctx, 1, &epoch, &counter));  // (the chain counter only)
     {
-        hipLaunchKernelGGL(rg_tiles, dim3(1), dim3(256), 0, ctx->stream, c0, (uint32_t)RADIX, (uint32_t)RS, lim);
         KTimer kt_(ctx, "region_pass");
         PassArgs pa{};
         pa.in = r0;
@@ -889,18 +882,19 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
         pa.nbk = RADIX;
         pa.nsg = RS;
         pa.gsub = 1;
-        pa.maxt = p.maxt1;
+        pa.H = p.H;
         pa.shift = p.Q + p.rest;
         pa.bits = p.B2;
         pa.out = r1;
-        pa.C1 = p.C1;
+        pa.C1 = p.C1h;
         pa.cnt1 = c1;
-        launch_pass(ctx, pa, lim, epoch, counter, dbg >> 4, stamps[1]);
+        launch_pass(ctx, pa, counter, dbg >> 4, stamps[1]);
         HIP_TRY(ctx, hipGetLastError());
     }
     // finish: one block per region
     {
-        FinishArgs f{r1, p.C1, c1, p.Q, p.rest, (uint32_t)p.rc, 0, 0, nreg};
+        FinishArgs f{r1, p.C1h, c1, p.Q, p.rest, (uint32_t)p.rc, 0, 0, nreg};
+        f.fsub = p.H;
         KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, dbg & 15, stamps[2]));
     }
     if (stamps[0]) KMAN_TRY(report_stamps(ctx, stamps, stamp_rows));
@@ -1014,7 +1008,9 @@ int make_dplan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t flags,
     if (d.K < B1 + 9 + g + 1) return KMAN_EFALLBACK;
     d.rest = d.K - B1 - 9 - g;
     const uint64_t e1 = Wq >> (B1 + 9);                         // per source, bucket and d
-    d.C1s = ceil_div(e1 + e1 / 2 + 256, 64) * 64;
+    // pass 1 runs two block-owned chains per (bucket, source): sub-regions
+    // (b, d, src, h) of ~e1 / 2 items each
+    d.C1s = ceil_div(e1 / 2 + e1 / 4 + 256, 64) * 64;
     const uint64_t e2 = (Wq * world) >> (B1 + 9 + g);          // per final region
     if (e2 > 7800) return KMAN_EFALLBACK;
     const uint64_t c2 = ceil_div(e2 + e2 / 2 + 512, 64) * 64;
@@ -1022,7 +1018,7 @@ int make_dplan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t flags,
     // (kman_amd/dist.py mirrors this bound)
     const uint32_t per = (RADIX + world - 1) / world;
     d.nb_max = per + per / 2 + 4 < (uint32_t)RADIX ? per + per / 2 + 4 : (uint32_t)RADIX;
-    const uint64_t nsub = (uint64_t)d.nb_max * 512 * world;    // pass-1 sub-regions
+    const uint64_t nsub = (uint64_t)d.nb_max * 512 * world * 2;  // pass-1 sub-regions
     const uint64_t nreg = (uint64_t)d.nb_max * 512 << g;      // pass-1b regions
     d.off_r1 = p.bytes;
     d.off_c1 = d.off_r1 + nsub * d.C1s * 8;
@@ -1143,7 +1139,6 @@ extern "C" int kman_dgroups_finish(kman_ctx *ctx, const uint64_t *d_recv, uint64
     uint32_t *c2 = (uint32_t *)(wk + d.off_c2);
     uint64_t *sbase = (uint64_t *)(wk + d.off_tab + (uint64_t)RADIX * RS * 8);
     uint32_t *scnt = (uint32_t *)(sbase + (uint64_t)d.nb_max * world);
-    uint32_t *lim = (uint32_t *)(wk + d.off_lim);
     const uint32_t G = world;
     // pass-1 segments: bucket (b, src) = one contiguous run of src's chunk
     std::vector<uint64_t> hb((size_t)nb * G);
@@ -1162,18 +1157,18 @@ extern "C" int kman_dgroups_finish(kman_ctx *ctx, const uint64_t *d_recv, uint64
         roff = at;
     }
     const uint32_t nbk = nb * G;
-    const uint32_t maxt1 = (uint32_t)ceil_div(maxc, T1) + 1;
     HIP_TRY(ctx, hipMemcpyAsync(sbase, hb.data(), hb.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(scnt, hn.data(), hn.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-    const uint64_t nsub = (uint64_t)nb * 512 * G;
+    (void)maxc;
+    const uint64_t nsub = (uint64_t)nb * 512 * G * 2;
     const uint32_t nreg = (uint32_t)((uint64_t)nb * 512 << d.g);
     HIP_TRY(ctx, hipMemsetAsync(c1, 0, nsub * 4, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(c2, 0, (uint64_t)nreg * 4, ctx->stream));
     uint32_t epoch, *counter;
-    // pass 1: by the 9 bits below the bucket, per (b, src) chain
+    // pass 1: by the 9 bits below the bucket, two chains per (b, src) into
+    // sub-regions (b, d, src, h)
     {
-        hipLaunchKernelGGL(rg_tiles, dim3(1), dim3(256), 0, ctx->stream, scnt, nbk, 1u, lim);
-        KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)nbk * maxt1 * (R1 / 4), &epoch, &counter));
+        KMAN_TRY(kman_lookback_begin(ctx, 1, &epoch, &counter));
         KTimer kt_(ctx, "region_pass");
         PassArgs pa{};
         pa.in = d_recv;
@@ -1182,23 +1177,21 @@ extern "C" int kman_dgroups_finish(kman_ctx *ctx, const uint64_t *d_recv, uint64
         pa.nbk = nbk;
         pa.nsg = 1;
         pa.gsub = G;
-        pa.maxt = maxt1;
+        pa.H = 2;
         pa.shift = d.Q + d.K - B1 - 9;
         pa.bits = 9;
         pa.out = r1;
         pa.C1 = d.C1s;
         pa.cnt1 = c1;
-        launch_pass(ctx, pa, lim, epoch, counter, 0, nullptr);
+        launch_pass(ctx, pa, counter, 0, nullptr);
         HIP_TRY(ctx, hipGetLastError());
     }
     KMAN_TRY(rg_check(ctx, "pass 1", c1, nsub));
-    // pass 1b: per (b, d), its G sub-regions concatenated, by g more bits;
-    // the segment index (source rank) goes into the d field
+    // pass 1b: per (b, d), its 2G sub-regions concatenated, by g more bits;
+    // the source rank (segment index / 2) goes into the d field
     {
         const uint32_t nbk2 = nb * 512;
-        const uint32_t maxt2 = (uint32_t)ceil_div((uint64_t)G * d.C1s, T1) + 1;
-        hipLaunchKernelGGL(rg_tiles, dim3(1), dim3(256), 0, ctx->stream, c1, nbk2, G, lim);
-        KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)nbk2 * maxt2 * (R1 / 4), &epoch, &counter));
+        KMAN_TRY(kman_lookback_begin(ctx, 1, &epoch, &counter));
         KTimer kt_(ctx, "region_pass1b");
         PassArgs pa{};
         pa.in = r1;
@@ -1206,18 +1199,19 @@ extern "C" int kman_dgroups_finish(kman_ctx *ctx, const uint64_t *d_recv, uint64
         pa.seg_cnt = c1;
         pa.stride = d.C1s;
         pa.nbk = nbk2;
-        pa.nsg = G;
+        pa.nsg = 2 * G;
         pa.gsub = 1;
-        pa.maxt = maxt2;
+        pa.H = 1;
         pa.shift = d.Q + d.rest;
         pa.bits = d.g;
         pa.tag = mode == KMAN_FINISH_UNIQ;
+        pa.tag_div = 2;
         pa.tag_shift = d.Q + d.rest + d.g;
         pa.tag_bits = 9;
         pa.out = r2;
         pa.C1 = d.C1;
         pa.cnt1 = c2;
-        launch_pass(ctx, pa, lim, epoch, counter, 0, nullptr);
+        launch_pass(ctx, pa, counter, 0, nullptr);
         HIP_TRY(ctx, hipGetLastError());
     }
     KMAN_TRY(rg_check(ctx, "pass 1b", c2, nreg));

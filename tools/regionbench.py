@@ -19,7 +19,10 @@ text = inputs.syn_numpy(1_000_000_000, 1)
 dev = engine.Device(0)
 pipe = engine.ResidentPipeline(dev, text, 21, mode=mode)
 del text
-for dbg in ["0", "1", "2", "3", "16", "256", "0"]:
+for dbg in (sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "1", "2", "3", "16", "256", "0"]):
+    if ":" in dbg:  # NAME=VALUE:dbg also sets another knob (empty VALUE = unset)
+        kv, dbg = dbg.split(":")
+        os.environ[kv.split("=")[0]] = kv.split("=")[1]
     os.environ["KMAN_RG_DBG"] = dbg
     pipe.step()
     pipe.timing(True)
