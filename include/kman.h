@@ -201,9 +201,10 @@ int kman_finish(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_keys_alt, void *d_v
  *   COUNT  d_okeys[j], d_ovals[j] = group size (oval_bytes 4 | 8)
  *   UNIQ   d_okeys[j], d_ovals[j] = pos of the keys that occur once
  * in ascending key order; *n_kmers = k-mers extracted, *n_out = rows.
+ * With KMAN_CANONICAL the keys are min(forward, reverse complement), one per
+ * window.
  * kman_groups_plan gives the work-area size, or KMAN_EFALLBACK when the input
- * is outside the path (canonical, k > 25, too many k-mers for the region
- * capacities).  kman_groups returns KMAN_EFALLBACK also when a region
+ * is outside the path (k > 25, too many k-mers for the region capacities).  kman_groups returns KMAN_EFALLBACK also when a region
  * overflowed (a strongly skewed prefix distribution); the outputs are then
  * undefined and the caller runs the general path.  d_okeys / d_ovals hold
  * up to n_bases x (RC ? 2 : 1) entries. */
@@ -241,6 +242,15 @@ int kman_dgroups_finish(kman_ctx *ctx, const uint64_t *d_recv, uint64_t n_bases,
                         uint32_t flags, int mode, uint32_t world, uint32_t b_lo, uint32_t nb,
                         const uint64_t *counts, void *d_work, uint64_t work_bytes, uint64_t *d_okeys,
                         void *d_ovals, uint32_t oval_bytes, uint64_t *n_out);
+
+/* Abundance spectrum of a count output (BASELINE config 5; not
+ * in the reference): d_hist[c] = number of distinct k-mers seen c times, the
+ * last bin collecting every count >= nbins - 1 (bin 0 stays 0).  With
+ * KMAN_CANONICAL counts (kman_groups) this is the canonical k-mer spectrum;
+ * for odd k those counts equal the `kmer count -r` rows with key <= rc(key)
+ * (the reference's -r emits both strands, seq.py:274-282). */
+int kman_count_hist(kman_ctx *ctx, const void *d_counts, uint32_t count_bytes, uint64_t n, uint64_t *d_hist,
+                    uint32_t nbins);
 
 /* Run-length count of sorted keys (join.py:95-130 + 266-285):
  * d_ukeys[j], d_counts[j] (u32 if count_bytes == 4 else u64). */

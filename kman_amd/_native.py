@@ -112,6 +112,7 @@ SIGNATURES = {
         [c_void_p, c_void_p, c_uint64, c_uint64, c_uint32, c_uint32, c_int, c_uint32, c_uint32, c_uint32, c_void_p,
          c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, POINTER(c_uint64)],
     ),
+    "kman_count_hist": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_uint32]),
     "kman_rle_count": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, POINTER(c_uint64)]),
     "kman_rle_uniq": (
         c_int,

@@ -93,7 +93,7 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 // packed above the 2k key bits), ranked by the top 8 key bits, digit counts
 // published early, grouped look-back per digit along the segment's chain,
 // LDS-staged coalesced scatter into region (b, s).
-template <int EI, bool RC, bool ATOMIC>
+template <int EI, bool RC, bool ATOMIC, bool CANON = false>
 __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
                                                  uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
                                                  uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ cnt0,
@@ -138,7 +138,8 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
 
     uint64_t kf[EI], kr[EI];
     const uint32_t w0 = threadIdx.x * EI;
-    const uint32_t valid = roll<EI, false>(scodes, w0, k, keymask, wb + w0, n_bases, kf, kr);
+    // (CANON: kf = min(forward, reverse complement), one key per window)
+    const uint32_t valid = roll<EI, CANON>(scodes, w0, k, keymask, wb + w0, n_bases, kf, kr);
     uint32_t tcnt;
     const uint32_t off = block_exclusive_scan<NT>((uint32_t)__popc(valid) * (RC ? 2u : 1u), SumU32(), 0u, lds_scan,
                                                   &tcnt);
@@ -669,6 +670,7 @@ struct RegionPlan {
     uint32_t K, Q, B2, rest;
     bool rc;
     uint64_t W;          // windows (x2 with rc): bound on the k-mers
+    bool canon;          // canonical keys (KMAN_CANONICAL)
     uint64_t C0, C1;     // region capacities (items)
     uint32_t H;          // pass-1 chains (sub-regions) per bucket
     uint64_t C1h;        // pass-1 sub-region capacity
@@ -684,9 +686,11 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     if (k < 2 || k > 32) return KMAN_EINVAL;
     if (getenv("KMAN_NO_REGION")) return KMAN_EFALLBACK;
     // k <= 25: the tile-local window index rides above the key bits in pass 0
-    if ((flags & KMAN_CANONICAL) || k > 25 || n_bases == 0) return KMAN_EFALLBACK;
+    if (k > 25 || n_bases == 0) return KMAN_EFALLBACK;
     RegionPlan p{};
-    p.rc = flags & KMAN_RC;
+    // canonical: one key per window, min(forward, reverse complement)
+    p.canon = flags & KMAN_CANONICAL;
+    p.rc = (flags & KMAN_RC) && !p.canon;
     p.K = 2 * k;
     p.W = n_bases * (p.rc ? 2 : 1);
     p.Q = mode == KMAN_FINISH_UNIQ ? (bitlen(p.W - 1) ? bitlen(p.W - 1) : 1u) : 0u;
@@ -773,16 +777,25 @@ int run_finish(kman_ctx *ctx, const FinishArgs &f, int mode, uint64_t *okeys, vo
     return KMAN_OK;
 }
 
-template <int EI, bool RC>
+template <int EI, bool RC, bool CANON = false>
 void launch_extract(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                     uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     const uint32_t grid = RS * p.seg_tiles;
     if (ctx->lds_atomic_ordered)
-        hipLaunchKernelGGL((rg_extract<EI, RC, true>), dim3(grid), dim3(RT), 0, ctx->stream, codes, n_bases, (int)k,
-                           p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch, ctx->d_err, dbg, stp);
+        hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON>), dim3(grid), dim3(RT), 0, ctx->stream, codes, n_bases,
+                           (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch,
+                           ctx->d_err, dbg, stp);
     else
-        hipLaunchKernelGGL((rg_extract<EI, RC, false>), dim3(grid), dim3(RT), 0, ctx->stream, codes, n_bases, (int)k,
-                           p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch, ctx->d_err, dbg, stp);
+        hipLaunchKernelGGL((rg_extract<EI, RC, false, CANON>), dim3(grid), dim3(RT), 0, ctx->stream, codes, n_bases,
+                           (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch,
+                           ctx->d_err, dbg, stp);
+}
+
+void launch_extract_any(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
+                        uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
+    if (p.canon) launch_extract<16, false, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
+    else if (p.rc) launch_extract<8, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
+    else launch_extract<16, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
 }
 
 // mean phase durations (us) per kernel from the stamp rows; frees the buffers
@@ -866,8 +879,7 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
     KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
     {
         KTimer kt_(ctx, "region_extract");
-        if (p.rc) launch_extract<8, true>(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter, dbg >> 8, stamps[0]);
-        else launch_extract<16, false>(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter, dbg >> 8, stamps[0]);
+        launch_extract_any(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter, dbg >> 8, stamps[0]);
         HIP_TRY(ctx, hipGetLastError());
     }
     // pass 1: per bucket, by the next B2 bits (H block-owned chains per bucket)
@@ -996,7 +1008,7 @@ int make_dplan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t flags,
     if (r != KMAN_OK) return r;
     DistPlan d{};
     d.K = 2 * k;
-    d.rc = flags & KMAN_RC;
+    d.rc = p.rc;
     d.world = world;
     const uint64_t Wq = n_bases_q * (d.rc ? 2 : 1);
     d.Q = mode == KMAN_FINISH_UNIQ ? (bitlen(Wq - 1) ? bitlen(Wq - 1) : 1u) : 0u;
@@ -1079,8 +1091,7 @@ extern "C" int kman_dgroups_extract(kman_ctx *ctx, const uint8_t *d_codes, uint6
         uint32_t epoch, *counter;
         KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
         KTimer kt_(ctx, "region_extract");
-        if (p.rc) launch_extract<8, true>(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter, 0, nullptr);
-        else launch_extract<16, false>(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter, 0, nullptr);
+        launch_extract_any(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter, 0, nullptr);
         HIP_TRY(ctx, hipGetLastError());
     }
     std::vector<uint32_t> hc((size_t)RADIX * RS);
@@ -1236,4 +1247,49 @@ extern "C" int kman_dgroups_finish(kman_ctx *ctx, const uint64_t *d_recv, uint64
         return kman_fail(ctx, KMAN_EHIP, "region output total not published");
     *n_out = wd & ST_VMASK;
     return KMAN_OK;
+}
+
+// ====================================================== abundance histogram
+// hist[min(count, nbins - 1)] += 1 over the count output of kman_groups /
+// kman_finish (COUNT): the k-mer abundance spectrum of BASELINE config 5
+// (not in the reference).  hist: nbins u64, zeroed here.
+namespace {
+template <typename C>
+__global__ __launch_bounds__(256) void count_hist_kernel(const C *__restrict__ counts, uint64_t n, uint32_t nbins,
+                                                         unsigned long long *__restrict__ hist) {
+    extern __shared__ uint32_t lh[];
+    for (uint32_t i = threadIdx.x; i < nbins; i += 256) lh[i] = 0;
+    __syncthreads();
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t c = counts[i];
+        atomicAdd(&lh[c < nbins ? c : nbins - 1], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nbins; i += 256)
+        if (lh[i]) atomicAdd(&hist[i], (unsigned long long)lh[i]);
+}
+}  // namespace
+
+extern "C" int kman_count_hist(kman_ctx *ctx, const void *d_counts, uint32_t count_bytes, uint64_t n,
+                               uint64_t *d_hist, uint32_t nbins) {
+    if (!ctx) return KMAN_EINVAL;
+    if (count_bytes != 4 && count_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "count_bytes must be 4 or 8");
+    if (nbins < 2 || nbins > 16384) return kman_fail(ctx, KMAN_EINVAL, "nbins must be in [2, 16384]");
+    if (!d_hist || (n && !d_counts)) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipMemsetAsync(d_hist, 0, (size_t)nbins * 8, ctx->stream));
+    if (n) {
+        const uint64_t blocks = ceil_div(n, 256 * 64);
+        const uint32_t g = (uint32_t)(blocks < 4096 ? blocks : 4096);
+        KTimer kt_(ctx, "count_hist");
+        if (count_bytes == 4)
+            hipLaunchKernelGGL(count_hist_kernel<uint32_t>, dim3(g), dim3(256), nbins * 4, ctx->stream,
+                               (const uint32_t *)d_counts, n, nbins, (unsigned long long *)d_hist);
+        else
+            hipLaunchKernelGGL(count_hist_kernel<uint64_t>, dim3(g), dim3(256), nbins * 4, ctx->stream,
+                               (const uint64_t *)d_counts, n, nbins, (unsigned long long *)d_hist);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return kman_check_device_error(ctx);
 }

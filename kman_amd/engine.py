@@ -293,13 +293,13 @@ def extract(p: Parsed, k: int, rc: bool, want_pos: bool, canonical: bool = False
                  hist_valid=True)
 
 
-def extract_sorted(p: Parsed, k: int, rc: bool, want_pos: bool) -> Kmers:
+def extract_sorted(p: Parsed, k: int, rc: bool, want_pos: bool, canonical: bool = False) -> Kmers:
     """kman_extract_sorted: the k-mers already stably sorted by their prefix
     bits [lo, 2k) (first prefix pass fused into the extraction)."""
     _check_k(k)
     dev = p.dev
     L = N.lib()
-    bound = p.n_bases * (2 if rc else 1)
+    bound = p.n_bases * (2 if rc and not canonical else 1)
     n = max(bound, 1)
     pos_bytes = 4 if 2 * p.n_bases <= 0xFFFFFFFF else 8
     keys, alt = dev.alloc(8 * n), dev.alloc(8 * n)
@@ -307,7 +307,8 @@ def extract_sorted(p: Parsed, k: int, rc: bool, want_pos: bool) -> Kmers:
     pos_alt = dev.alloc(pos_bytes * n) if want_pos else None
     lo = split_bits(bound, 2 * k)
     out, res = c_uint64(0), c_int(0)
-    N.check(dev.ctx, L.kman_extract_sorted(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k, flags_for(rc, want_pos), lo,
+    N.check(dev.ctx, L.kman_extract_sorted(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
+                                           flags_for(rc, want_pos, canonical), lo,
                                            c_void_p(keys.ptr), c_void_p(alt.ptr),
                                            c_void_p(pos.ptr if pos else None), c_void_p(pos_alt.ptr if pos else None),
                                            pos_bytes, bound, byref(out), byref(res)), "kman_extract_sorted")
@@ -415,20 +416,20 @@ def rle_uniq(km: Kmers, dev: Device) -> UniqResult:
     return UniqResult(okeys, opos, km.pos_bytes, int(out.value), km.k)
 
 
-def groups(p: Parsed, k: int, rc: bool, mode: str):
+def groups(p: Parsed, k: int, rc: bool, mode: str, canonical: bool = False):
     """kman_groups: count / uniq of the whole stream straight from the codes
     (region.hip).  Returns a CountResult / UniqResult, or None when the input
     is outside the region path (kman_groups_plan / a region overflow said
     KMAN_EFALLBACK): the caller then runs extract_sorted + rle_*."""
     L, dev = N.lib(), p.dev
     m = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
-    flags = flags_for(rc, mode == "uniq")
+    flags = flags_for(rc, mode == "uniq", canonical)
     wb = c_uint64(0)
     rc_ = L.kman_groups_plan(p.n_bases, k, flags, m, byref(wb))
     if rc_ == N.KMAN_EFALLBACK:
         return None
     N.check(dev.ctx, rc_, "kman_groups_plan")
-    cap = max(1, p.n_bases * (2 if rc else 1))
+    cap = max(1, p.n_bases * (2 if rc and not canonical else 1))
     vb = (4 if 2 * p.n_bases <= 0xFFFFFFFF else 8) if mode == "uniq" else (4 if cap <= 0xFFFFFFFF else 8)
     work = dev.alloc(int(wb.value))
     okeys = dev.alloc(8 * cap)
@@ -546,6 +547,58 @@ def read_input(path: str) -> bytes:
             return fh.read()
     with open(path, "rb") as fh:
         return fh.read()
+
+
+def count_groups(p: Parsed, k: int, rc: bool = False, canonical: bool = False) -> CountResult:
+    """(key, count) per distinct k-mer on the device: the region path, else
+    the prefix-split path (None only when there are no k-mers)."""
+    r = groups(p, k, rc, "count", canonical)
+    if r is not None:
+        return r
+    km = extract_sorted(p, k, rc, want_pos=False, canonical=canonical)
+    try:
+        if km.n == 0:
+            return None
+        return rle_count(km, p.dev)
+    finally:
+        km.free()
+
+
+def abundance_hist(text: bytes, k: int, canonical: bool = True, nbins: int = 10001,
+                   dev: Optional[Device] = None) -> np.ndarray:
+    """k-mer abundance spectrum (BASELINE config 5; SURVEY §8f-1, not in the
+    reference): h[c] = distinct (canonical) k-mers seen c times, h[-1] every
+    count >= nbins - 1 (kman_count_hist over the count output)."""
+    dev = dev or default_device()
+    _check_k(k)
+    p = parse(dev, text)
+    try:
+        r = count_groups(p, k, False, canonical)
+        d_h = dev.alloc(8 * nbins)
+        try:
+            if r is None:
+                return np.zeros(nbins, np.uint64)
+            try:
+                N.check(dev.ctx, N.lib().kman_count_hist(dev.ctx, c_void_p(r.counts.ptr), r.count_bytes, r.n,
+                                                         c_void_p(d_h.ptr), nbins), "kman_count_hist")
+                return dev.download(d_h, nbins, np.uint64)
+            finally:
+                r.ukeys.free()
+                r.counts.free()
+        finally:
+            d_h.free()
+    finally:
+        p.free()
+
+
+def format_hist(h: np.ndarray) -> bytes:
+    """``"%d\t%d\n" % (count, n_kmers)`` for every non-empty bin; the last bin
+    reads ``">=N"``."""
+    out = []
+    last = len(h) - 1
+    for c in np.nonzero(h)[0].tolist():
+        out.append("%s\t%d\n" % ((">=%d" % c) if c == last else str(c), int(h[c])))
+    return "".join(out).encode()
 
 
 def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = None) -> bytes:

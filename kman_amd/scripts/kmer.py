@@ -156,5 +156,30 @@ def batch(input_path: str, output_path: str, k: int, reverse: bool = False, scan
     logging.info("That's all!")
 
 
+@main.command(name="hist", context_settings=CONTEXT_SETTINGS, help="""
+Abundance spectrum of the (canonical) k-mers of INPUT: one line per
+abundance c, "c<TAB>number of distinct k-mers seen c times".
+
+Not part of the reference kman CLI (SURVEY.md §8f-1, BASELINE config 5):
+canonical k-mers are min(k-mer, reverse complement); for odd k their counts
+are the `kmer count -r` rows whose sequence is <= its reverse complement.
+The INPUT file can be gzipped.
+""")
+@args.input_path()
+@args.output_path(file_okay=True)
+@args.k()
+@click.option("--forward", is_flag=True, help="Count forward k-mers instead of canonical ones.")
+@click.option("--max-count", type=click.INT, default=10000, show_default=True,
+              help="Abundances from this one up share the last line (>=N).")
+def hist(input_path: str, output_path: str, k: int, forward: bool = False, max_count: int = 10000) -> None:
+    from .. import engine
+
+    input_file_exists(input_path)
+    h = engine.abundance_hist(engine.read_input(input_path), k, canonical=not forward, nbins=max_count + 1)
+    with open(output_path, "wb") as fh:
+        fh.write(engine.format_hist(h))
+    logging.info("That's all!")
+
+
 if __name__ == "__main__":
     main()
