@@ -98,6 +98,9 @@ int kman_sync(kman_ctx *ctx);
 /* ------------------------------------------------------------------- memory */
 int kman_malloc(kman_ctx *ctx, void **dptr, size_t bytes);
 int kman_free(kman_ctx *ctx, void *dptr);
+/* free / total HBM of the context's device: the sizing of the key ranges of
+ * a multi-batch join (kman_extract_range) */
+int kman_mem_info(kman_ctx *ctx, size_t *free_bytes, size_t *total_bytes);
 int kman_host_alloc(kman_ctx *ctx, void **hptr, size_t bytes); /* pinned */
 int kman_host_free(kman_ctx *ctx, void *hptr);
 int kman_memcpy_h2d(kman_ctx *ctx, void *dst, const void *src, size_t bytes);
@@ -141,6 +144,20 @@ int kman_count_kmers(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, ui
 int kman_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k,
                  uint32_t flags, uint64_t *d_keys, void *d_pos, uint32_t pos_bytes, uint64_t cap,
                  uint64_t *d_hist, uint64_t *n_kmers);
+
+/* kman_extract restricted to the keys in [key_lo, key_hi] (inclusive), in
+ * stream order: one key range of a multi-batch join (inputs whose k-mers do
+ * not fit the device at once are processed range by range; the ranges'
+ * outputs concatenate to the global sorted output, join.py:63-130).  Keys of
+ * the range past `cap` are counted, not written: KMAN_ECAP then.  Size the
+ * ranges with kman_kmer_prefix_hist. */
+int kman_extract_range(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                       uint64_t key_lo, uint64_t key_hi, uint64_t *d_keys, void *d_pos, uint32_t pos_bytes,
+                       uint64_t cap, uint64_t *d_hist, uint64_t *n_kmers);
+/* Histogram of the top 8 key bits of the stream (256 u64 into d_hist256) and
+ * the k-mer count; flags: KMAN_RC (not KMAN_CANONICAL). */
+int kman_kmer_prefix_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                          uint64_t *d_hist256, uint64_t *n_kmers);
 
 /* LSD radix sort plan for keys with key_bits significant bits:
  * npass digit passes of bits[i] bits each, starting at bit shift[i]. */

@@ -54,6 +54,7 @@ SIGNATURES = {
     "kman_last_error": (c_char_p, [c_void_p]),
     "kman_sync": (c_int, [c_void_p]),
     "kman_malloc": (c_int, [c_void_p, POINTER(c_void_p), c_size_t]),
+    "kman_mem_info": (c_int, [c_void_p, POINTER(c_size_t), POINTER(c_size_t)]),
     "kman_free": (c_int, [c_void_p, c_void_p]),
     "kman_host_alloc": (c_int, [c_void_p, POINTER(c_void_p), c_size_t]),
     "kman_host_free": (c_int, [c_void_p, c_void_p]),
@@ -72,6 +73,12 @@ SIGNATURES = {
         [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p,
          POINTER(c_uint64)],
     ),
+    "kman_extract_range": (
+        c_int,
+        [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_uint64, c_uint64, c_void_p, c_void_p, c_uint32, c_uint64,
+         c_void_p, POINTER(c_uint64)],
+    ),
+    "kman_kmer_prefix_hist": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_void_p, POINTER(c_uint64)]),
     "kman_sort_plan": (c_int, [c_uint32, POINTER(c_uint32), POINTER(c_uint32), POINTER(c_uint32)]),
     "kman_sort": (
         c_int,

@@ -44,7 +44,7 @@ __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__
                                                      P *__restrict__ pos, uint64_t *__restrict__ status,
                                                      uint32_t *__restrict__ counter, uint32_t epoch,
                                                      uint32_t *__restrict__ err, uint64_t *__restrict__ hist,
-                                                     Plan plan) {
+                                                     Plan plan, uint64_t key_lo, uint64_t key_hi, uint64_t cap) {
     constexpr int TILE = ET * EI;
     constexpr int KPT = RC && !CANON ? 2 * EI : EI;  // keys per thread, max
     constexpr int MAXKEYS = ET * KPT;
@@ -69,7 +69,16 @@ __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__
         uint64_t kf[EI], kr[EI];
         const uint64_t p0 = tb + (uint64_t)threadIdx.x * EI;
         const uint32_t valid = roll<EI, CANON>(scodes, threadIdx.x * EI, k, mask, p0, n_bases, kf, kr);
-        const uint32_t cnt = __popc(valid) * (RC && !CANON ? 2 : 1);
+        // keys inside [key_lo, key_hi] only (kman_extract_range; the full range otherwise)
+        uint32_t vf = 0, vr = 0;
+#pragma unroll
+        for (int j = 0; j < EI; j++) {
+            vf |= (uint32_t)(kf[j] >= key_lo && kf[j] <= key_hi) << j;
+            if (RC && !CANON) vr |= (uint32_t)(kr[j] >= key_lo && kr[j] <= key_hi) << j;
+        }
+        vf &= valid;
+        vr &= valid;
+        const uint32_t cnt = __popc(vf) + (RC && !CANON ? __popc(vr) : 0);
         uint32_t total;
         const uint32_t loff = block_exclusive_scan<ET>(cnt, SumU32(), 0u, lds_scan, &total);
 #if defined(KMAN_ABL) && (KMAN_ABL & 32)
@@ -89,17 +98,15 @@ __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__
             uint32_t o = loff;
 #pragma unroll
             for (int j = 0; j < EI; j++) {
-                if ((valid >> j) & 1u) {
-                    skeys[o++] = kf[j];
-                    if (RC && !CANON) skeys[o++] = kr[j];
-                }
+                if ((vf >> j) & 1u) skeys[o++] = kf[j];
+                if (RC && !CANON && ((vr >> j) & 1u)) skeys[o++] = kr[j];
             }
         }
         __syncthreads();
         const uint64_t base = lds_base;
         for (uint32_t q = threadIdx.x; q < total; q += ET) {
             const uint64_t key = skeys[q];
-            keys[base + q] = key;
+            if (base + q < cap) keys[base + q] = key;  // (a key range past cap: counted, not written)
 #if defined(KMAN_ABL) && (KMAN_ABL & 64)
             if (false) {
 #else
@@ -117,14 +124,13 @@ __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__
             uint32_t o = loff;
 #pragma unroll
             for (int j = 0; j < EI; j++) {
-                if ((valid >> j) & 1u) {
-                    const P pv = (P)((p0 + j) << 1);
-                    spos[o++] = pv;
-                    if (RC && !CANON) spos[o++] = pv | 1;
-                }
+                const P pv = (P)((p0 + j) << 1);
+                if ((vf >> j) & 1u) spos[o++] = pv;
+                if (RC && !CANON && ((vr >> j) & 1u)) spos[o++] = pv | 1;
             }
             __syncthreads();
-            for (uint32_t q = threadIdx.x; q < total; q += ET) pos[base + q] = spos[q];
+            for (uint32_t q = threadIdx.x; q < total; q += ET)
+                if (base + q < cap) pos[base + q] = spos[q];
         }
         __syncthreads();
     }
@@ -246,7 +252,7 @@ __global__ __launch_bounds__(ET) void kmer_hist_kernel(const uint8_t *__restrict
 
 template <int EI, bool RC, bool CANON, typename P>
 int launch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k, uint64_t *keys, P *pos,
-                   uint64_t *hist, const Plan &plan) {
+                   uint64_t *hist, const Plan &plan, uint64_t klo, uint64_t khi, uint64_t cap) {
     const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * EI);
     uint32_t epoch, *counter;
     KMAN_TRY(kman_lookback_begin(ctx, n_tiles, &epoch, &counter));
@@ -254,17 +260,19 @@ int launch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k,
     const int grid = kman_persistent_grid(ctx, (const void *)fn, ET, n_tiles);
     KTimer kt_(ctx, "extract");
     hipLaunchKernelGGL(fn, dim3(grid), dim3(ET), 0, ctx->stream, codes, n_bases, n_tiles, k, keys, pos,
-                       ctx->d_status, counter, epoch, ctx->d_err, hist, plan);
+                       ctx->d_status, counter, epoch, ctx->d_err, hist, plan, klo, khi, cap);
     HIP_TRY(ctx, hipGetLastError());
     return KMAN_OK;
 }
 
 template <typename P>
 int dispatch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k, uint32_t flags, uint64_t *keys,
-                     P *pos, uint64_t *hist, const Plan &plan) {
-    if (flags & KMAN_CANONICAL) return launch_extract<16, false, true, P>(ctx, codes, n_bases, k, keys, pos, hist, plan);
-    if (flags & KMAN_RC) return launch_extract<8, true, false, P>(ctx, codes, n_bases, k, keys, pos, hist, plan);
-    return launch_extract<16, false, false, P>(ctx, codes, n_bases, k, keys, pos, hist, plan);
+                     P *pos, uint64_t *hist, const Plan &plan, uint64_t klo, uint64_t khi, uint64_t cap) {
+    if (flags & KMAN_CANONICAL)
+        return launch_extract<16, false, true, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap);
+    if (flags & KMAN_RC)
+        return launch_extract<8, true, false, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap);
+    return launch_extract<16, false, false, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap);
 }
 
 }  // namespace
@@ -294,6 +302,14 @@ extern "C" int kman_count_kmers(kman_ctx *ctx, const uint8_t *d_codes, uint64_t 
 extern "C" int kman_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
                             uint64_t *d_keys, void *d_pos, uint32_t pos_bytes, uint64_t cap, uint64_t *d_hist,
                             uint64_t *n_kmers) {
+    return kman_extract_range(ctx, d_codes, n_bases, k, flags, 0, ~0ull, d_keys, d_pos, pos_bytes, cap, d_hist,
+                              n_kmers);
+}
+
+extern "C" int kman_extract_range(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                                  uint64_t key_lo, uint64_t key_hi, uint64_t *d_keys, void *d_pos, uint32_t pos_bytes,
+                                  uint64_t cap, uint64_t *d_hist, uint64_t *n_kmers) {
+    const bool ranged = key_lo != 0 || key_hi != ~0ull;
     if (!ctx || !n_kmers) return KMAN_EINVAL;
     if (k < 2 || k > 32) return kman_fail(ctx, KMAN_EINVAL, "k must be in [2, 32] on the GPU path, got %u", k);
     const bool want_pos = flags & KMAN_WANT_POS;
@@ -308,11 +324,14 @@ extern "C" int kman_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_ba
     const uint64_t bound = (flags & KMAN_RC) && !(flags & KMAN_CANONICAL) ? 2 * n_bases : n_bases;
     if (cap < bound) {
         // only size exactly when the caller's buffer is below the trivial bound
+        // (a key range is sized by the caller: kman_kmer_prefix_hist)
         uint64_t need;
-        KMAN_TRY(kman_count_kmers(ctx, d_codes, n_bases, k, flags, &need));
-        if (need > cap)
-            return kman_fail(ctx, KMAN_ECAP, "key capacity %llu < %llu", (unsigned long long)cap,
-                             (unsigned long long)need);
+        if (!ranged) {
+            KMAN_TRY(kman_count_kmers(ctx, d_codes, n_bases, k, flags, &need));
+            if (need > cap)
+                return kman_fail(ctx, KMAN_ECAP, "key capacity %llu < %llu", (unsigned long long)cap,
+                                 (unsigned long long)need);
+        }
     }
     Plan plan{};
     uint32_t np, sh[MAXPASS], bi[MAXPASS];
@@ -327,17 +346,39 @@ extern "C" int kman_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_ba
         plan.bits[i] = (uint8_t)bi[i];
     }
     if (!want_pos) {
-        KMAN_TRY(dispatch_extract<NoPos>(ctx, d_codes, n_bases, (int)k, flags, d_keys, nullptr, d_hist, plan));
+        KMAN_TRY(dispatch_extract<NoPos>(ctx, d_codes, n_bases, (int)k, flags, d_keys, nullptr, d_hist, plan, key_lo,
+                                         key_hi, cap));
     } else if (pos_bytes == 4) {
         KMAN_TRY(dispatch_extract<uint32_t>(ctx, d_codes, n_bases, (int)k, flags, d_keys, (uint32_t *)d_pos, d_hist,
-                                            plan));
+                                            plan, key_lo, key_hi, cap));
     } else {
         KMAN_TRY(dispatch_extract<uint64_t>(ctx, d_codes, n_bases, (int)k, flags, d_keys, (uint64_t *)d_pos, d_hist,
-                                            plan));
+                                            plan, key_lo, key_hi, cap));
     }
     // the last tile's inclusive prefix is the number of k-mers written
     const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * ((flags & KMAN_RC) && !(flags & KMAN_CANONICAL) ? 8 : 16));
-    return kman_lookback_total(ctx, n_tiles, n_kmers);
+    KMAN_TRY(kman_lookback_total(ctx, n_tiles, n_kmers));
+    if (*n_kmers > cap)
+        return kman_fail(ctx, KMAN_ECAP, "key range holds %llu keys > capacity %llu", (unsigned long long)*n_kmers,
+                         (unsigned long long)cap);
+    return KMAN_OK;
+}
+
+// top-8-bit histogram of the stream's keys (the k-mer count is its sum): the
+// sizing of kman_extract_range's key ranges
+extern "C" int kman_kmer_prefix_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k,
+                                     uint32_t flags, uint64_t *d_hist256, uint64_t *n_kmers) {
+    if (!ctx || !n_kmers || !d_hist256) return KMAN_EINVAL;
+    if (k < 2 || k > 32) return kman_fail(ctx, KMAN_EINVAL, "k must be in [2, 32] on the GPU path, got %u", k);
+    if (flags & KMAN_CANONICAL) return kman_fail(ctx, KMAN_EINVAL, "prefix histogram of canonical keys: not built");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    *n_kmers = 0;
+    if (n_bases == 0) {
+        HIP_TRY(ctx, hipMemsetAsync(d_hist256, 0, 256 * 8, ctx->stream));
+        return KMAN_OK;
+    }
+    const uint32_t lo = 2 * k > 8 ? 2 * k - 8 : 0;
+    return kman_kmer_hist(ctx, d_codes, n_bases, k, flags & KMAN_RC, lo, 1, 1ull << 62, d_hist256, n_kmers);
 }
 
 // pre-pass of kman_extract_sorted: n_kmers and d_hist (zeroed here) for the

@@ -283,6 +283,13 @@ int kman_malloc(kman_ctx *ctx, void **dptr, size_t bytes) {
     return KMAN_OK;
 }
 
+int kman_mem_info(kman_ctx *ctx, size_t *free_bytes, size_t *total_bytes) {
+    if (!ctx || !free_bytes || !total_bytes) return KMAN_EINVAL;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    HIP_TRY(ctx, hipMemGetInfo(free_bytes, total_bytes));
+    return KMAN_OK;
+}
+
 int kman_free(kman_ctx *ctx, void *dptr) {
     if (!ctx) return KMAN_EINVAL;
     if (!dptr) return KMAN_OK;

@@ -25,7 +25,7 @@ import ctypes
 import os
 from ctypes import byref, c_int, c_size_t, c_uint32, c_uint64, c_void_p
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import List, Optional, Tuple
 
 import numpy as np
 
@@ -450,6 +450,119 @@ def groups(p: Parsed, k: int, rc: bool, mode: str, canonical: bool = False):
     return CountResult(okeys, ovals, vb, int(no.value), k)
 
 
+def mem_info(dev: Device) -> Tuple[int, int]:
+    """(free, total) HBM bytes of the device (kman_mem_info)."""
+    f, t = c_size_t(0), c_size_t(0)
+    N.check(dev.ctx, N.lib().kman_mem_info(dev.ctx, byref(f), byref(t)), "kman_mem_info")
+    return int(f.value), int(t.value)
+
+
+def prefix_hist(p: Parsed, k: int, rc: bool) -> Tuple[np.ndarray, int]:
+    """Histogram of the top 8 key bits of the stream (kman_kmer_prefix_hist):
+    4^k bins when 2k < 8.  Returns (hist, n_kmers)."""
+    _check_k(k)
+    dev = p.dev
+    h = dev.alloc(8 * 256)
+    try:
+        n = c_uint64(0)
+        N.check(dev.ctx, N.lib().kman_kmer_prefix_hist(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
+                                                        N.KMAN_RC if rc else 0, c_void_p(h.ptr), byref(n)),
+                "kman_kmer_prefix_hist")
+        bins = 256 if 2 * k >= 8 else 1 << (2 * k)
+        return dev.download(h, bins, np.uint64), int(n.value)
+    finally:
+        h.free()
+
+
+def key_ranges(hist: np.ndarray, k: int, max_keys: int) -> List[Tuple[int, int, int]]:
+    """Consecutive top-8-bit prefixes grouped into key ranges of at most
+    max_keys k-mers: [(key_lo, key_hi, n)] in key order, empty ranges dropped.
+    The batches of a multi-batch join (join.py:63-130) cut by key instead of
+    by stream position: their n-way merge is then their concatenation."""
+    shift = max(0, 2 * k - 8)
+    out, lo, acc = [], 0, 0
+    for b, c in enumerate(hist.tolist()):
+        if c > max_keys:
+            raise MemoryError("%d k-mers share one 8-bit prefix: more than a batch of %d" % (c, max_keys))
+        if acc and acc + c > max_keys:
+            out.append((lo << shift, (b << shift) - 1, acc))
+            lo, acc = b, 0
+        acc += c
+    if acc:
+        out.append((lo << shift, (len(hist) << shift) - 1, acc))
+    return out
+
+
+class _At:
+    """A device pointer inside a buffer (an output slice) for _finish."""
+
+    def __init__(self, buf: DeviceBuffer, offset: int):
+        self.ptr = buf.ptr + int(offset)
+
+
+def ranged_groups(p: Parsed, k: int, rc: bool, mode: str, max_keys: Optional[int] = None):
+    """Multi-batch device join (BASELINE config 3): count / uniq of a stream
+    whose k-mers do not fit the device at once.  The stream is cut into key
+    ranges of at most max_keys k-mers (prefix_hist + key_ranges); each range
+    is extracted from the resident codes (kman_extract_range, stream order),
+    prefix-sorted (kman_sort_range) and finished in LDS (kman_finish), its
+    output appended to the global output, which is therefore in key order.
+    Same results as groups() / extract_sorted + rle_* (join.py:95-130,
+    244-285 over batch.py:156-168)."""
+    _check_k(k)
+    dev, L = p.dev, N.lib()
+    want_pos = mode == "uniq"
+    hist, n = prefix_hist(p, k, rc)
+    pos_bytes = 4 if 2 * p.n_bases <= 0xFFFFFFFF else 8
+    vb = pos_bytes if want_pos else (4 if n <= 0xFFFFFFFF else 8)
+    per_key = 16 + (2 * pos_bytes if want_pos else 0)
+    if max_keys is None:
+        free, _ = mem_info(dev)
+        max_keys = max(1 << 20, (int(free * 0.85) - (8 + vb) * n) // per_key)
+    ranges = key_ranges(hist, k, max_keys)
+    okeys = dev.alloc(8 * max(n, 1))
+    ovals = dev.alloc(vb * max(n, 1))
+    if not ranges:
+        return (UniqResult if want_pos else CountResult)(okeys, ovals, vb, 0, k)
+    cap = max(r[2] for r in ranges)
+    keys, alt = dev.alloc(8 * cap), dev.alloc(8 * cap)
+    pos = dev.alloc(pos_bytes * cap) if want_pos else None
+    pos_alt = dev.alloc(pos_bytes * cap) if want_pos else None
+    hbuf = dev.alloc(8 * 256 * 8)
+    flags = flags_for(rc, want_pos)
+    fmode = N.KMAN_FINISH_UNIQ if want_pos else N.KMAN_FINISH_COUNT
+    total = 0
+    try:
+        shift = max(0, 2 * k - 8)
+        for lo_key, hi_key, nr in ranges:
+            # the range's keys fill (hi - lo + 1) of the len(hist) prefixes:
+            # segment bits as for a stream that dense over the whole key space
+            lo = split_bits(nr * len(hist) // (((hi_key - lo_key) >> shift) + 1), 2 * k)
+            dev.memset(hbuf, 0, 8 * 256 * 8)
+            got = c_uint64(0)
+            N.check(dev.ctx, L.kman_extract_range(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
+                                                  flags | N.KMAN_HIST_LO(lo), lo_key, hi_key, c_void_p(keys.ptr),
+                                                  c_void_p(pos.ptr if pos else None), pos_bytes, cap,
+                                                  c_void_p(hbuf.ptr), byref(got)), "kman_extract_range")
+            if int(got.value) != nr:
+                raise RuntimeError("key range [%x, %x]: %d k-mers extracted, histogram said %d"
+                                   % (lo_key, hi_key, got.value, nr))
+            km = Kmers(keys, alt, pos, pos_alt, pos_bytes if want_pos else 0, nr, k, hbuf, lo_bit=lo,
+                       hist_valid=True)
+            _sort_prefix(km, dev, 2 * k)
+            total += _finish(km, dev, 2 * k, fmode, _At(okeys, 8 * total), _At(ovals, vb * total), vb)
+            keys, alt, pos, pos_alt = km.keys, km.alt, km.pos, km.pos_alt
+    except BaseException:
+        okeys.free()
+        ovals.free()
+        raise
+    finally:
+        for b in (keys, alt, pos, pos_alt, hbuf):
+            if b is not None:
+                b.free()
+    return (UniqResult if want_pos else CountResult)(okeys, ovals, vb, total, k)
+
+
 # ------------------------------------------------------------------ formatting
 
 
@@ -601,14 +714,28 @@ def format_hist(h: np.ndarray) -> bytes:
     return "".join(out).encode()
 
 
-def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = None) -> bytes:
-    """``kmer count`` output bytes for a FASTA text (SEQ_COUNT mode)."""
+def _fits(p: Parsed, k: int, rc: bool, mode: str) -> bool:
+    """Does the single-batch general path (extract_sorted + rle_*) fit the
+    free HBM?  If not, the multi-batch join (ranged_groups) takes the input."""
+    n = p.n_bases * (2 if rc else 1)
+    pb = 4 if 2 * p.n_bases <= 0xFFFFFFFF else 8
+    need = n * (16 + 8 + (3 * pb if mode == "uniq" else (4 if n <= 0xFFFFFFFF else 8)))
+    return need <= 0.85 * mem_info(p.dev)[0]
+
+
+def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = None,
+               max_keys: Optional[int] = None) -> bytes:
+    """``kmer count`` output bytes for a FASTA text (SEQ_COUNT mode).
+    max_keys: run the multi-batch join with key ranges of at most that many
+    k-mers (by default only when the single batch does not fit the HBM)."""
     dev = dev or default_device()
     _check_k(k)
     p = parse(dev, text)
     try:
         check_empty_names(p, k)
-        r = groups(p, k, rc, "count")
+        r = groups(p, k, rc, "count") if max_keys is None else None
+        if r is None and (max_keys is not None or not _fits(p, k, rc, "count")):
+            r = ranged_groups(p, k, rc, "count", max_keys)
         if r is None:
             km = extract_sorted(p, k, rc, want_pos=False)
             try:
@@ -627,14 +754,18 @@ def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = No
         p.free()
 
 
-def uniq_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = None) -> bytes:
-    """``kmer uniq`` output bytes for a FASTA text (UNIQUE mode)."""
+def uniq_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = None,
+              max_keys: Optional[int] = None) -> bytes:
+    """``kmer uniq`` output bytes for a FASTA text (UNIQUE mode); max_keys as
+    in count_text."""
     dev = dev or default_device()
     _check_k(k)
     p = parse(dev, text)
     try:
         check_empty_names(p, k)
-        r = groups(p, k, rc, "uniq")
+        r = groups(p, k, rc, "uniq") if max_keys is None else None
+        if r is None and (max_keys is not None or not _fits(p, k, rc, "uniq")):
+            r = ranged_groups(p, k, rc, "uniq", max_keys)
         if r is None:
             km = extract_sorted(p, k, rc, want_pos=True)
             try:
