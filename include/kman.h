@@ -330,6 +330,18 @@ int kman_format_uniq(const uint64_t *keys, const void *pos, uint32_t pos_bytes, 
                      const uint64_t *rec_seq, uint64_t n_records, char *out, size_t cap,
                      size_t *used, int threads);
 
+/* The same writers on the device: the output text is built in
+ * HBM (d_out, 16-byte aligned) from device-resident results, so only the text
+ * crosses PCIe.  Byte-identical to kman_format_count / kman_format_uniq.
+ * *used = the text size; KMAN_ECAP when it exceeds cap (nothing past cap is
+ * written; d_out = NULL sizes only).  The rows are independent: a slice of
+ * the result arrays formats to the matching slice of the text. */
+int kman_format_count_dev(kman_ctx *ctx, const uint64_t *d_ukeys, const void *d_counts, uint32_t count_bytes,
+                          uint64_t n, uint32_t k, char *d_out, size_t cap, size_t *used);
+int kman_format_uniq_dev(kman_ctx *ctx, const uint64_t *d_keys, const void *d_pos, uint32_t pos_bytes, uint64_t n,
+                         uint32_t k, const char *d_names, const uint64_t *d_name_off, const uint64_t *d_rec_seq,
+                         uint64_t n_records, char *d_out, size_t cap, size_t *used);
+
 #ifdef __cplusplus
 }
 #endif

@@ -54,6 +54,14 @@ SIGNATURES = {
     "kman_last_error": (c_char_p, [c_void_p]),
     "kman_sync": (c_int, [c_void_p]),
     "kman_malloc": (c_int, [c_void_p, POINTER(c_void_p), c_size_t]),
+    "kman_format_count_dev": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_size_t, POINTER(c_size_t)],
+    ),
+    "kman_format_uniq_dev": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p,
+         c_size_t, POINTER(c_size_t)],
+    ),
     "kman_mem_info": (c_int, [c_void_p, POINTER(c_size_t), POINTER(c_size_t)]),
     "kman_free": (c_int, [c_void_p, c_void_p]),
     "kman_host_alloc": (c_int, [c_void_p, POINTER(c_void_p), c_size_t]),

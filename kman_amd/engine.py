@@ -457,19 +457,22 @@ def mem_info(dev: Device) -> Tuple[int, int]:
     return int(f.value), int(t.value)
 
 
+def _prefix_hist_into(p: Parsed, k: int, rc: bool, h: DeviceBuffer) -> Tuple[np.ndarray, int]:
+    n = c_uint64(0)
+    N.check(p.dev.ctx, N.lib().kman_kmer_prefix_hist(p.dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
+                                                      N.KMAN_RC if rc else 0, c_void_p(h.ptr), byref(n)),
+            "kman_kmer_prefix_hist")
+    bins = 256 if 2 * k >= 8 else 1 << (2 * k)
+    return p.dev.download(h, bins, np.uint64), int(n.value)
+
+
 def prefix_hist(p: Parsed, k: int, rc: bool) -> Tuple[np.ndarray, int]:
     """Histogram of the top 8 key bits of the stream (kman_kmer_prefix_hist):
     4^k bins when 2k < 8.  Returns (hist, n_kmers)."""
     _check_k(k)
-    dev = p.dev
-    h = dev.alloc(8 * 256)
+    h = p.dev.alloc(8 * 256)
     try:
-        n = c_uint64(0)
-        N.check(dev.ctx, N.lib().kman_kmer_prefix_hist(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
-                                                        N.KMAN_RC if rc else 0, c_void_p(h.ptr), byref(n)),
-                "kman_kmer_prefix_hist")
-        bins = 256 if 2 * k >= 8 else 1 << (2 * k)
-        return dev.download(h, bins, np.uint64), int(n.value)
+        return _prefix_hist_into(p, k, rc, h)
     finally:
         h.free()
 
@@ -500,7 +503,7 @@ class _At:
         self.ptr = buf.ptr + int(offset)
 
 
-def ranged_groups(p: Parsed, k: int, rc: bool, mode: str, max_keys: Optional[int] = None):
+class RangedJoin:
     """Multi-batch device join (BASELINE config 3): count / uniq of a stream
     whose k-mers do not fit the device at once.  The stream is cut into key
     ranges of at most max_keys k-mers (prefix_hist + key_ranges); each range
@@ -508,59 +511,100 @@ def ranged_groups(p: Parsed, k: int, rc: bool, mode: str, max_keys: Optional[int
     prefix-sorted (kman_sort_range) and finished in LDS (kman_finish), its
     output appended to the global output, which is therefore in key order.
     Same results as groups() / extract_sorted + rle_* (join.py:95-130,
-    244-285 over batch.py:156-168)."""
-    _check_k(k)
-    dev, L = p.dev, N.lib()
-    want_pos = mode == "uniq"
-    hist, n = prefix_hist(p, k, rc)
-    pos_bytes = 4 if 2 * p.n_bases <= 0xFFFFFFFF else 8
-    vb = pos_bytes if want_pos else (4 if n <= 0xFFFFFFFF else 8)
-    per_key = 16 + (2 * pos_bytes if want_pos else 0)
-    if max_keys is None:
-        free, _ = mem_info(dev)
-        max_keys = max(1 << 20, (int(free * 0.85) - (8 + vb) * n) // per_key)
-    ranges = key_ranges(hist, k, max_keys)
-    okeys = dev.alloc(8 * max(n, 1))
-    ovals = dev.alloc(vb * max(n, 1))
-    if not ranges:
-        return (UniqResult if want_pos else CountResult)(okeys, ovals, vb, 0, k)
-    cap = max(r[2] for r in ranges)
-    keys, alt = dev.alloc(8 * cap), dev.alloc(8 * cap)
-    pos = dev.alloc(pos_bytes * cap) if want_pos else None
-    pos_alt = dev.alloc(pos_bytes * cap) if want_pos else None
-    hbuf = dev.alloc(8 * 256 * 8)
-    flags = flags_for(rc, want_pos)
-    fmode = N.KMAN_FINISH_UNIQ if want_pos else N.KMAN_FINISH_COUNT
-    total = 0
-    try:
+    244-285 over batch.py:156-168).  Every buffer is allocated here, once:
+    ``step()`` re-plans (prefix histogram) and runs the batches."""
+
+    def __init__(self, p: Parsed, k: int, rc: bool, mode: str, max_keys: Optional[int] = None):
+        _check_k(k)
+        self.p, self.k, self.rc, self.mode = p, k, rc, mode
+        dev = self.dev = p.dev
+        self.want_pos = mode == "uniq"
+        self._bufs = []
+        self.phist = self._alloc(8 * 256)
+        hist, n = _prefix_hist_into(p, k, rc, self.phist)
+        self.n_kmers = n
+        self.pos_bytes = 4 if 2 * p.n_bases <= 0xFFFFFFFF else 8
+        self.vb = self.pos_bytes if self.want_pos else (4 if n <= 0xFFFFFFFF else 8)
+        per_key = 16 + (2 * self.pos_bytes if self.want_pos else 0)
+        if max_keys is None:
+            free, _ = mem_info(dev)
+            max_keys = max(1 << 20, (int(free * 0.85) - (8 + self.vb) * n) // per_key)
+        self.max_keys = int(max_keys)
+        self.ranges = key_ranges(hist, k, self.max_keys)
+        self.cap = max([r[2] for r in self.ranges] + [1])
+        self.okeys = self._alloc(8 * max(n, 1))
+        self.ovals = self._alloc(self.vb * max(n, 1))
+        self.keys, self.alt = self._alloc(8 * self.cap), self._alloc(8 * self.cap)
+        self.pos = self._alloc(self.pos_bytes * self.cap) if self.want_pos else None
+        self.pos_alt = self._alloc(self.pos_bytes * self.cap) if self.want_pos else None
+        self.hbuf = self._alloc(8 * 256 * 8)
+        self.n_out = 0
+
+    def _alloc(self, nbytes: int) -> DeviceBuffer:
+        try:
+            b = self.dev.alloc(nbytes)
+        except BaseException:
+            self.free()
+            raise
+        self._bufs.append(b)
+        return b
+
+    def step(self) -> int:
+        """One whole join: plan the key ranges, then extract + sort + finish
+        each range into the output.  Returns the number of k-mers joined."""
+        dev, L, k, p = self.dev, N.lib(), self.k, self.p
+        hist, n = _prefix_hist_into(p, k, self.rc, self.phist)
+        ranges = key_ranges(hist, k, self.max_keys)
+        if n != self.n_kmers or any(r[2] > self.cap for r in ranges):
+            raise RuntimeError("the stream changed under a planned RangedJoin")
+        flags = flags_for(self.rc, self.want_pos)
+        fmode = N.KMAN_FINISH_UNIQ if self.want_pos else N.KMAN_FINISH_COUNT
         shift = max(0, 2 * k - 8)
+        vb, pb = self.vb, self.pos_bytes
+        total = 0
         for lo_key, hi_key, nr in ranges:
             # the range's keys fill (hi - lo + 1) of the len(hist) prefixes:
             # segment bits as for a stream that dense over the whole key space
             lo = split_bits(nr * len(hist) // (((hi_key - lo_key) >> shift) + 1), 2 * k)
-            dev.memset(hbuf, 0, 8 * 256 * 8)
+            dev.memset(self.hbuf, 0, 8 * 256 * 8)
             got = c_uint64(0)
             N.check(dev.ctx, L.kman_extract_range(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
-                                                  flags | N.KMAN_HIST_LO(lo), lo_key, hi_key, c_void_p(keys.ptr),
-                                                  c_void_p(pos.ptr if pos else None), pos_bytes, cap,
-                                                  c_void_p(hbuf.ptr), byref(got)), "kman_extract_range")
+                                                  flags | N.KMAN_HIST_LO(lo), lo_key, hi_key,
+                                                  c_void_p(self.keys.ptr),
+                                                  c_void_p(self.pos.ptr if self.pos else None), pb, self.cap,
+                                                  c_void_p(self.hbuf.ptr), byref(got)), "kman_extract_range")
             if int(got.value) != nr:
                 raise RuntimeError("key range [%x, %x]: %d k-mers extracted, histogram said %d"
                                    % (lo_key, hi_key, got.value, nr))
-            km = Kmers(keys, alt, pos, pos_alt, pos_bytes if want_pos else 0, nr, k, hbuf, lo_bit=lo,
-                       hist_valid=True)
+            km = Kmers(self.keys, self.alt, self.pos, self.pos_alt, pb if self.want_pos else 0, nr, k, self.hbuf,
+                       lo_bit=lo, hist_valid=True)
             _sort_prefix(km, dev, 2 * k)
-            total += _finish(km, dev, 2 * k, fmode, _At(okeys, 8 * total), _At(ovals, vb * total), vb)
-            keys, alt, pos, pos_alt = km.keys, km.alt, km.pos, km.pos_alt
-    except BaseException:
-        okeys.free()
-        ovals.free()
-        raise
+            total += _finish(km, dev, 2 * k, fmode, _At(self.okeys, 8 * total), _At(self.ovals, vb * total), vb)
+            self.keys, self.alt, self.pos, self.pos_alt = km.keys, km.alt, km.pos, km.pos_alt
+        self.n_out = total
+        return n
+
+    def result(self):
+        """The output (CountResult / UniqResult); its buffers now belong to
+        the caller."""
+        r = (UniqResult if self.want_pos else CountResult)(self.okeys, self.ovals, self.vb, self.n_out, self.k)
+        self._bufs = [b for b in self._bufs if b is not self.okeys and b is not self.ovals]
+        return r
+
+    def free(self) -> None:
+        for b in self._bufs:
+            b.free()
+        self._bufs = []
+
+
+def ranged_groups(p: Parsed, k: int, rc: bool, mode: str, max_keys: Optional[int] = None):
+    """RangedJoin in one call: the CountResult / UniqResult of the stream."""
+    j = RangedJoin(p, k, rc, mode, max_keys)
+    try:
+        j.step()
+        return j.result()
     finally:
-        for b in (keys, alt, pos, pos_alt, hbuf):
-            if b is not None:
-                b.free()
-    return (UniqResult if want_pos else CountResult)(okeys, ovals, vb, total, k)
+        j.free()
 
 
 # ------------------------------------------------------------------ formatting
@@ -596,6 +640,141 @@ def format_fasta(keys: np.ndarray, pos: np.ndarray, k: int, p: Parsed) -> bytes:
     return _format(N.lib().kman_format_uniq, keys.ctypes.data_as(c_void_p), pos.ctypes.data_as(c_void_p),
                    pos.dtype.itemsize, len(keys), k, names, off.ctypes.data_as(c_void_p),
                    rs.ctypes.data_as(c_void_p), p.n_records)
+
+
+# device-side formatting: the text is built in HBM and only
+# the text crosses PCIe; slices of at most _FMT_CHUNK text bytes per launch
+_FMT_CHUNK = 1 << 31
+
+
+def _format_dev(dev: Device, n: int, row_bytes: int, call, sink=None):
+    """Run a kman_format_*_dev call over row slices.  call(i0, rows, d_out,
+    cap, used) formats rows [i0, i0 + rows); row_bytes bounds one row.
+    Returns the text (a bytearray filled straight from the device), or, with
+    a sink (a binary file), writes it there chunk by chunk through a pinned
+    staging buffer and returns None."""
+    if n == 0:
+        return None if sink is not None else bytearray()
+    rows = max(1, min(n, _FMT_CHUNK // max(1, row_bytes)))
+    cap = rows * row_bytes + 16
+    used = c_size_t(0)
+    L = N.lib()
+    out, stage = None, None
+    if sink is None:
+        rc_ = call(0, n, None, 0, used)  # sizing pass over every row
+        if rc_ not in (N.KMAN_OK, N.KMAN_ECAP):
+            N.check(dev.ctx, rc_, "kman_format_*_dev")
+        out = bytearray(int(used.value))
+    else:
+        hp = c_void_p()
+        N.check(dev.ctx, L.kman_host_alloc(dev.ctx, byref(hp), cap), "kman_host_alloc")
+        stage = hp
+    buf = dev.alloc(cap)
+    try:
+        at = 0
+        for i0 in range(0, n, rows):
+            m = min(rows, n - i0)
+            N.check(dev.ctx, call(i0, m, c_void_p(buf.ptr), cap, used), "kman_format_*_dev")
+            u = int(used.value)
+            if not u:
+                continue
+            if out is not None:
+                dst = (ctypes.c_char * u).from_buffer(out, at)
+                N.check(dev.ctx, L.kman_memcpy_d2h(dev.ctx, dst, c_void_p(buf.ptr), u), "d2h")
+            else:
+                N.check(dev.ctx, L.kman_memcpy_d2h(dev.ctx, stage, c_void_p(buf.ptr), u), "d2h")
+                sink.write(memoryview((ctypes.c_char * u).from_address(stage.value)).cast("B"))
+            at += u
+    finally:
+        buf.free()
+        if stage is not None:
+            L.kman_host_free(dev.ctx, stage)
+    if out is not None:
+        assert at == len(out)
+    return out
+
+
+def format_count_dev(dev: Device, r: CountResult, sink=None):
+    """``"%s\t%d\n" % (seq, count)`` per group (join.py:283-284), built on
+    the device from the device-resident result (kman_format_count_dev)."""
+    L, cb = N.lib(), r.count_bytes
+
+    def call(i0, m, d_out, cap, used):
+        return L.kman_format_count_dev(dev.ctx, c_void_p(r.ukeys.ptr + 8 * i0), c_void_p(r.counts.ptr + cb * i0), cb,
+                                       m, r.k, d_out, cap, byref(used))
+
+    return _format_dev(dev, r.n, r.k + 2 + (10 if cb == 4 else 20), call, sink)
+
+
+class DeviceNames:
+    """The record table of a Parsed input on the device (names blob, name
+    offsets, first base of each record) for kman_format_uniq_dev."""
+
+    def __init__(self, p: Parsed):
+        dev = p.dev
+        self.names = dev.alloc(max(16, len(p.names_blob)))
+        self.off = dev.alloc(8 * (p.n_records + 1))
+        self.rec = dev.alloc(8 * max(1, p.n_records))
+        if p.names_blob:
+            dev.upload(self.names, p.names_blob)
+        dev.upload(self.off, np.ascontiguousarray(p.name_off, dtype=np.uint64))
+        if p.n_records:
+            dev.upload(self.rec, np.ascontiguousarray(p.rec_seq, dtype=np.uint64))
+        self.n_records = p.n_records
+        self.max_name = int(np.diff(p.name_off).max()) if p.n_records else 0
+        self.n_bases = p.n_bases
+
+    def free(self) -> None:
+        for b in (self.names, self.off, self.rec):
+            b.free()
+
+
+def format_uniq_dev(p: Parsed, r: UniqResult, sink=None):
+    """``">%s\n%s\n" % (header, seq)`` (join.py:262 / seq.py:495), built on
+    the device (kman_format_uniq_dev)."""
+    dev, L, pb = p.dev, N.lib(), r.pos_bytes
+    nm = DeviceNames(p)
+    try:
+        D = len(str(p.n_bases + r.k))
+
+        def call(i0, m, d_out, cap, used):
+            return L.kman_format_uniq_dev(dev.ctx, c_void_p(r.keys.ptr + 8 * i0), c_void_p(r.pos.ptr + pb * i0), pb,
+                                          m, r.k, c_void_p(nm.names.ptr), c_void_p(nm.off.ptr), c_void_p(nm.rec.ptr),
+                                          nm.n_records, d_out, cap, byref(used))
+
+        return _format_dev(dev, r.n, 1 + nm.max_name + 1 + D + 1 + D + 3 + r.k + 1, call, sink)
+    finally:
+        nm.free()
+
+
+def host_format() -> bool:
+    """KMAN_HOST_FORMAT=1: format on host threads (kman_format_*) from
+    downloaded results instead of on the device."""
+    return os.environ.get("KMAN_HOST_FORMAT", "0") not in ("", "0")
+
+
+def _to(sink, data):
+    if sink is None:
+        return data
+    sink.write(data)
+    return None
+
+
+def emit_count(dev: Device, r: CountResult, sink=None):
+    """The count output text of a device-resident result: returned, or
+    written to the binary file `sink`."""
+    if host_format():
+        ukeys, counts = download_count(dev, r)
+        return _to(sink, format_count(ukeys, counts, r.k))
+    return format_count_dev(dev, r, sink)
+
+
+def emit_uniq(p: Parsed, r: UniqResult, sink=None):
+    """The uniq output text of a device-resident result over one input."""
+    if host_format():
+        keys, pos = download_uniq(p.dev, r)
+        return _to(sink, format_fasta(keys, pos, r.k, p))
+    return format_uniq_dev(p, r, sink)
 
 
 def download_count(dev: Device, r: CountResult):
@@ -745,11 +924,10 @@ def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = No
             finally:
                 km.free()
         try:
-            ukeys, counts = download_count(dev, r)
+            return emit_count(dev, r)
         finally:
             r.ukeys.free()
             r.counts.free()
-        return format_count(ukeys, counts, k)
     finally:
         p.free()
 
@@ -775,11 +953,10 @@ def uniq_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = Non
             finally:
                 km.free()
         try:
-            keys, pos = download_uniq(dev, r)
+            return emit_uniq(p, r)
         finally:
             r.keys.free()
             r.pos.free()
-        return format_fasta(keys, pos, k, p)
     finally:
         p.free()
 

@@ -181,17 +181,17 @@ class KJoiner:
                 "abundance vectors (VEC_*) are out of this engine's scope; the reference raises the same "
                 "NotImplementedError (kmermaid/abundance.py:60,123)")
         print("Joining...")
-        data = join_bytes(batches, self.mode == self.MODE.SEQ_COUNT)
         with open(outpath, "wb") as OH:
-            OH.write(data)
+            join_bytes(batches, self.mode == self.MODE.SEQ_COUNT, sink=OH)
 
 
-def join_bytes(batches: List[Batch], count: bool) -> bytes:
-    """Device join of the batches: gather + stable sort + RLE, then format."""
+def join_bytes(batches: List[Batch], count: bool, sink=None):
+    """Device join of the batches: gather + stable sort + RLE, then format.
+    Returns the output text, or writes it to the binary file `sink`."""
     entries = _entries(batches)
     if not entries:
         logging.error("nothing to crawl")  # join.py:110; the output stays empty
-        return b""
+        return None if sink is not None else b""
     from .source import gather_sorted
 
     whole = _whole_stream(entries)
@@ -203,10 +203,8 @@ def join_bytes(batches: List[Batch], count: bool) -> bytes:
         if r is not None:
             try:
                 if count:
-                    ukeys, counts = engine.download_count(whole.dev, r)
-                    return engine.format_count(ukeys, counts, whole.k)
-                keys, pos = engine.download_uniq(whole.dev, r)
-                return whole.format_fasta(keys, pos)
+                    return engine.emit_count(whole.dev, r, sink)
+                return engine.emit_uniq(whole.parsed, r, sink)
             finally:
                 for b in ((r.ukeys, r.counts) if count else (r.keys, r.pos)):
                     b.free()
@@ -217,11 +215,10 @@ def join_bytes(batches: List[Batch], count: bool) -> bytes:
         if count:
             r = engine.rle_count(km, dev)
             try:
-                ukeys, counts = engine.download_count(dev, r)
+                return engine.emit_count(dev, r, sink)
             finally:
                 r.ukeys.free()
                 r.counts.free()
-            return engine.format_count(ukeys, counts, k)
         r = engine.rle_uniq(km, dev)
         try:
             keys, pos = engine.download_uniq(dev, r)
@@ -231,11 +228,11 @@ def join_bytes(batches: List[Batch], count: bool) -> bytes:
     finally:
         km.free()
     if not tagged:
-        return srcs[0].format_fasta(keys, pos)
+        return engine._to(sink, srcs[0].format_fasta(keys, pos))
     out = []
     for key, p in zip(keys.tolist(), pos.tolist()):
         out.append(">%s\n%s\n" % (srcs[p >> 56].header(p & ((1 << 56) - 1)), engine.decode_key(key, k)))
-    return "".join(out).encode("utf-8", "surrogateescape")
+    return engine._to(sink, "".join(out).encode("utf-8", "surrogateescape"))
 
 
 class KJoinerThreading(KJoiner):
