@@ -274,12 +274,15 @@ struct PassArgs {
     uint32_t *cnt1;
 };
 
-template <bool ATOMIC>
-__global__ __launch_bounds__(RT, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
+// NT threads x SI items per tile: (512, 16) runs two blocks per CU, (1024, 8)
+// one block per CU (half the blocks, so half the open output lines per L2)
+// with the next tile's loads issued behind this tile's stores (PF).
+template <bool ATOMIC, int NT, int SI, bool PF>
+__global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
                                                  uint32_t *__restrict__ err, uint32_t dbg,
                                                  uint64_t *__restrict__ stp) {
-    constexpr int NT = RT, SI = RSI, TILE = NT * SI, NWAVE = NT / 64;
-    static_assert(NT == R1, "one thread per digit");
+    constexpr int TILE = NT * SI, NWAVE = NT / 64;
+    static_assert(NT >= R1 && SI % 4 == 0 && 64 * SI <= 65535, "a thread per digit; u16 wave counters");
     __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
     __shared__ uint32_t whist[NWAVE][R1 / 2];
     __shared__ uint32_t thist[R1];
@@ -317,7 +320,7 @@ __global__ __launch_bounds__(RT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
             sbase_l = sgl < nsg ? (pa.seg_base ? pa.seg_base[gi] : gi * pa.stride) : 0ull;
             if (threadIdx.x == 63) s_items = inc;
         }
-        run[threadIdx.x] = 0;
+        if (threadIdx.x < R1) run[threadIdx.x] = 0;
         __syncthreads();
         const uint32_t items = s_items;
         const uint32_t tiles = (items + TILE - 1) / TILE;
@@ -326,25 +329,22 @@ __global__ __launch_bounds__(RT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
         // output sub-region of digit d
         const uint64_t reg0 = (uint64_t)(b / pa.gsub) << bits, rsub = b % pa.gsub;
 #define SUBREG(d) (((reg0 | (d)) * pa.gsub + rsub) * H + h)
-        for (uint32_t r = ra; r < rb; r++) {
-            for (int i = threadIdx.x; i < NWAVE * R1 / 2; i += NT) (&whist[0][0])[i] = 0;
-            if (!ATOMIC) thist[threadIdx.x] = 0;
-            __syncthreads();
-            const uint32_t t0 = r * TILE;
-            const uint32_t n = items - t0 < (uint32_t)TILE ? items - t0 : (uint32_t)TILE;
-            RSTAMP(r, 0);
-            const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
-            uint64_t key[SI];
-            uint32_t rank[SI];
-            uint32_t sgi[SI];
+        const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
+        uint64_t key[SI];
+        uint32_t sgp[SI / 4];  // the items' segments, 8 bits each (for the tag)
+        // the keys of tile rt into key[] (logical item -> (segment, offset)
+        // with ballots over the lanes' prefixes: the 64 items of a wave row
+        // are consecutive, so their segment is the row start's, past the
+        // (rare) boundaries inside the row; no LDS and no dependent chain, so
+        // all the loads issue back to back)
+        auto load_tile = [&](uint32_t rt) {
+            const uint32_t tt0 = rt * TILE;
+            const uint32_t nn = items - tt0 < (uint32_t)TILE ? items - tt0 : (uint32_t)TILE;
+#pragma unroll
+            for (int i = 0; i < SI / 4; i++) sgp[i] = 0;
 #pragma unroll
             for (int i = 0; i < SI; i++) {
-                // logical item -> (segment, offset) with ballots over the
-                // lanes' prefixes: the 64 items of a wave row are consecutive,
-                // so their segment is the row start's, past the (rare)
-                // boundaries inside the row; no LDS and no dependent chain,
-                // so all the loads issue back to back
-                const uint32_t li0 = t0 + (uint32_t)w * (SI * 64) + (uint32_t)i * 64;
+                const uint32_t li0 = tt0 + (uint32_t)w * (SI * 64) + (uint32_t)i * 64;
                 const uint32_t li = li0 + (uint32_t)lane;
                 uint32_t sg = (uint32_t)__popcll(__ballot(spre_l <= li0) & ~1ull);  // lane 0 (prefix 0) not counted
                 uint64_t inrow = __ballot(spre_l > li0 && spre_l <= li0 + 63);
@@ -355,15 +355,34 @@ __global__ __launch_bounds__(RT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                 }
                 const uint64_t bs = shfl_any(sbase_l, (int)sg);
                 const uint32_t po = (uint32_t)__shfl((int)spre_l, (int)sg, 64);
-                sgi[i] = sg;
-                key[i] = ib + i * 64 < n ? pa.in[bs + (li - po)] : 0;
+                sgp[i >> 2] |= sg << (8 * (i & 3));
+#ifdef RG_PASS_ABL
+                if (dbg & 16) {  // timing ablation: no loads (uniform synthetic keys)
+                    key[i] = ib + i * 64 < nn ? (uint64_t)(li + 1) * 0x9E3779B97F4A7C15ull : 0;
+                    continue;
+                }
+#endif
+                key[i] = ib + i * 64 < nn ? pa.in[bs + (li - po)] : 0;
             }
+        };
+        if (PF && ra < rb) load_tile(ra);
+        for (uint32_t r = ra; r < rb; r++) {
+            for (int i = threadIdx.x; i < NWAVE * R1 / 2; i += NT) (&whist[0][0])[i] = 0;
+            if (!ATOMIC && threadIdx.x < R1) thist[threadIdx.x] = 0;
+            __syncthreads();
+            const uint32_t t0 = r * TILE;
+            const uint32_t n = items - t0 < (uint32_t)TILE ? items - t0 : (uint32_t)TILE;
+            RSTAMP(r, 0);
+            uint32_t rank[SI];
+            if (!PF) load_tile(r);
             if (pa.tag) {
                 // (a separate loop, so the loads above are not serialised on it)
                 const uint64_t tm = ((1ull << pa.tag_bits) - 1) << pa.tag_shift;
 #pragma unroll
-                for (int i = 0; i < SI; i++)
-                    key[i] = (key[i] & ~tm) | ((uint64_t)(sgi[i] / pa.tag_div) << pa.tag_shift);
+                for (int i = 0; i < SI; i++) {
+                    const uint32_t sg = (sgp[i >> 2] >> (8 * (i & 3))) & 0xffu;
+                    key[i] = (key[i] & ~tm) | ((uint64_t)(sg / pa.tag_div) << pa.tag_shift);
+                }
             }
 #define PDIGIT(x) ((uint32_t)((x) >> shift) & dmask)
             if (ATOMIC) {
@@ -373,7 +392,7 @@ __global__ __launch_bounds__(RT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                     rank[i] = ib + i * 64 < n ? (atomicAdd(&whist[w][d >> 1], 1u << hs) >> hs) & 0xffffu : 0u;
                 }
                 __syncthreads();
-                {
+                if (threadIdx.x < R1) {
                     const uint32_t d = threadIdx.x, hs = (d & 1u) * 16u;
                     uint32_t c = 0;
 #pragma unroll
@@ -431,24 +450,56 @@ __global__ __launch_bounds__(RT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
             }
             __syncthreads();
             RSTAMP(r, 1);
+            if (!PF) {
+                // one store per LDS read: the compiler reuses one register
+                // pair and waits for each store before the next read, which
+                // keeps one store in flight per wave -- measured faster than
+                // 16 back to back (5.7 vs 5.9 ms) with two blocks per CU
 #pragma unroll
-            for (int rr = 0; rr < SI; rr++) {
-                const uint32_t q = threadIdx.x + rr * NT;
-                if (q < n) {
-                    const uint64_t kk = skeys[q];
+                for (int rr = 0; rr < SI; rr++) {
+                    const uint32_t q = threadIdx.x + rr * NT;
+                    if (q < n) {
+                        const uint64_t kk = skeys[q];
+                        const uint32_t d = PDIGIT(kk);
+                        const uint64_t at = (uint64_t)run[d] + (q - lstart[d]);
+#ifdef RG_PASS_ABL
+                        // timing ablations: no stores (4); stores streamed to
+                        // the chain's own contiguous area, not scattered (8)
+                        if (dbg & 4) continue;
+                        if (dbg & 8) {
+                            pa.out[(uint64_t)ch * radix * C1 + (uint64_t)(r - ra) * TILE + q] = kk;
+                            continue;
+                        }
+#endif
+                        if (at < C1) pa.out[SUBREG(d) * C1 + at] = kk;
+                    }
+                }
+            } else {
+                // every LDS read and address first, the stores back to back,
+                // then the next tile's loads behind them
+                uint64_t wat[SI];
+#pragma unroll
+                for (int rr = 0; rr < SI; rr++) {
+                    const uint32_t q = threadIdx.x + rr * NT;
+                    const uint64_t kk = skeys[q < n ? q : 0];
                     const uint32_t d = PDIGIT(kk);
                     const uint64_t at = (uint64_t)run[d] + (q - lstart[d]);
-                    if (at < C1) pa.out[SUBREG(d) * C1 + at] = kk;
+                    key[rr] = kk;
+                    wat[rr] = q < n && at < C1 ? SUBREG(d) * C1 + at : ~0ull;
                 }
+#pragma unroll
+                for (int rr = 0; rr < SI; rr++)
+                    if (wat[rr] != ~0ull) pa.out[wat[rr]] = key[rr];
+                if (r + 1 < rb) load_tile(r + 1);
             }
             __syncthreads();  // every read of run[] above before its update
-            run[threadIdx.x] += thist[threadIdx.x];
+            if (threadIdx.x < R1) run[threadIdx.x] += thist[threadIdx.x];
             RSTAMP(r, 2);
 #undef PDIGIT
         }
         // the chain's sub-region counts (every digit, also of empty chains)
         __syncthreads();
-        {
+        if (threadIdx.x < R1) {
             const uint32_t d = threadIdx.x;
             if (run[d] > C1) atomicOr(err, ERR_REGION);
             if (d < radix) pa.cnt1[SUBREG(d)] = run[d] < C1 ? run[d] : (uint32_t)C1;
@@ -728,13 +779,28 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     return KMAN_OK;
 }
 
-void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
-    const void *fn = ctx->lds_atomic_ordered ? (const void *)rg_pass<true> : (const void *)rg_pass<false>;
-    const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, RT, (uint64_t)pa.nbk * pa.H);
+template <int NT, int SI, bool PF>
+void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
+    const void *fn = ctx->lds_atomic_ordered ? (const void *)rg_pass<true, NT, SI, PF>
+                                             : (const void *)rg_pass<false, NT, SI, PF>;
+    const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, NT, (uint64_t)pa.nbk * pa.H);
     if (ctx->lds_atomic_ordered)
-        hipLaunchKernelGGL((rg_pass<true>), dim3(grid), dim3(RT), 0, ctx->stream, pa, counter, ctx->d_err, dbg, stp);
+        hipLaunchKernelGGL((rg_pass<true, NT, SI, PF>), dim3(grid), dim3(NT), 0, ctx->stream, pa, counter, ctx->d_err,
+                           dbg, stp);
     else
-        hipLaunchKernelGGL((rg_pass<false>), dim3(grid), dim3(RT), 0, ctx->stream, pa, counter, ctx->d_err, dbg, stp);
+        hipLaunchKernelGGL((rg_pass<false, NT, SI, PF>), dim3(grid), dim3(NT), 0, ctx->stream, pa, counter, ctx->d_err,
+                           dbg, stp);
+}
+
+// block shape of the digit pass: KMAN_RG_PASS = 0 (512 x 16, two blocks per
+// CU; default), 1 (the same with the next tile prefetched), 2 (1024 x 8, one
+// block per CU, prefetched)
+void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
+    const char *e = getenv("KMAN_RG_PASS");
+    const int shape = e ? atoi(e) : 0;
+    if (shape == 2) launch_pass_as<1024, 8, true>(ctx, pa, counter, dbg, stp);
+    else if (shape == 1) launch_pass_as<RT, RSI, true>(ctx, pa, counter, dbg, stp);
+    else launch_pass_as<RT, RSI, false>(ctx, pa, counter, dbg, stp);
 }
 
 struct FinishArgs {

@@ -134,7 +134,7 @@ def test_groups_plan_domain():
     assert L.kman_groups_plan(1_000_000_000, 21, N.KMAN_WANT_POS, U, byref(wb)) == N.KMAN_OK and wb.value > 0
     assert L.kman_groups_plan(1_000_000_000, 21, 0, C, byref(wb)) == N.KMAN_OK
     assert L.kman_groups_plan(1000, 31, 0, C, byref(wb)) == N.KMAN_EFALLBACK  # k > 25
-    assert L.kman_groups_plan(1000, 21, N.KMAN_CANONICAL, C, byref(wb)) == N.KMAN_EFALLBACK
+    assert L.kman_groups_plan(1000, 21, N.KMAN_CANONICAL, C, byref(wb)) == N.KMAN_OK  # canonical keys: in
     assert L.kman_groups_plan(1000, 4, 0, C, byref(wb)) == N.KMAN_EFALLBACK  # too few key bits
     assert L.kman_groups_plan(4_000_000_000, 21, 0, C, byref(wb)) == N.KMAN_EFALLBACK  # regions too full
     assert L.kman_groups_plan(1000, 21, 0, 0, byref(wb)) == N.KMAN_EINVAL  # SORT is not a groups mode
