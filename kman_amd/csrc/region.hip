@@ -456,14 +456,13 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
             RSTAMP(r, 1);
             if (WC) {
                 // a digit whose partial line completes in this tile: its
-                // pending items go out first (thread d)
-                if (threadIdx.x < R1) {
-                    const uint32_t d = threadIdx.x, rn = run[d], p = rn & 15u;
-                    if (p && ((rn + thist[d]) >> 4) > (rn >> 4)) {
-                        uint64_t *o = pa.out + SUBREG(d) * C1;
-                        for (uint32_t j = 0; j < p; j++)
-                            if (rn - p + j < C1) o[rn - p + j] = wcb[d][j];
-                    }
+                // pending items go out first, 16 lanes per digit (one line
+                // per quarter wave, so a store covers 4 lines)
+#pragma unroll
+                for (uint32_t d = threadIdx.x >> 4; d < (uint32_t)R1; d += NT / 16) {
+                    const uint32_t j = threadIdx.x & 15u, rn = run[d], p = rn & 15u;
+                    if (j < p && ((rn + thist[d]) >> 4) > (rn >> 4) && rn - p + j < C1)
+                        pa.out[SUBREG(d) * C1 + rn - p + j] = wcb[d][j];
                 }
                 __syncthreads();  // those wcb reads before the leftovers below
                 // items of whole lines to HBM, the new partial line to LDS
@@ -535,14 +534,15 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
         }
         // the chain's sub-region counts (every digit, also of empty chains)
         __syncthreads();
+        if (WC) {  // the last partial lines, 16 lanes per digit
+#pragma unroll
+            for (uint32_t d = threadIdx.x >> 4; d < (uint32_t)R1; d += NT / 16) {
+                const uint32_t j = threadIdx.x & 15u, rn = run[d], p = rn & 15u;
+                if (j < p && rn - p + j < C1) pa.out[SUBREG(d) * C1 + rn - p + j] = wcb[d][j];
+            }
+        }
         if (threadIdx.x < R1) {
             const uint32_t d = threadIdx.x;
-            if (WC) {  // the last partial lines
-                const uint32_t rn = run[d], p = rn & 15u;
-                uint64_t *o = pa.out + SUBREG(d) * C1;
-                for (uint32_t j = 0; j < p; j++)
-                    if (rn - p + j < C1) o[rn - p + j] = wcb[d][j];
-            }
             if (run[d] > C1) atomicOr(err, ERR_REGION);
             if (d < radix) pa.cnt1[SUBREG(d)] = run[d] < C1 ? run[d] : (uint32_t)C1;
         }
