@@ -280,7 +280,10 @@ struct PassArgs {
 // WC: write combining -- each digit's last partial 128-byte line (< 16 items)
 // stays in LDS until a later tile completes it, so only whole lines leave the
 // CU, each written within one tile's store phase (64 KiB of LDS: NT = 1024).
-template <bool ATOMIC, int NT, int SI, bool PF, bool WC = false>
+// BR: rank by one block-wide LDS atomic per item (no per-wave counters: the
+// order of equal digits inside a tile is then not stable, which the finish
+// does not need -- it sorts every remaining key bit and compares keys only).
+template <bool ATOMIC, int NT, int SI, bool PF, bool WC = false, bool BR = false>
 __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
                                                  uint32_t *__restrict__ err, uint32_t dbg,
                                                  uint64_t *__restrict__ stp) {
@@ -288,7 +291,7 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
     static_assert(NT >= R1 && SI % 4 == 0 && 64 * SI <= 65535, "a thread per digit; u16 wave counters");
     __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
     __shared__ uint64_t wcb[WC ? R1 : 1][16];  // WC: the pending items of digit d at wcb[d][pos % 16]
-    __shared__ uint32_t whist[NWAVE][R1 / 2];
+    __shared__ uint32_t whist[BR ? 1 : NWAVE][R1 / 2];
     __shared__ uint32_t thist[R1];
     __shared__ uint32_t lstart[R1];
     __shared__ uint32_t run[R1];  // the chain's running count per digit
@@ -361,7 +364,7 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                 const uint32_t po = (uint32_t)__shfl((int)spre_l, (int)sg, 64);
                 sgp[i >> 2] |= sg << (8 * (i & 3));
 #ifdef RG_PASS_ABL
-                if (dbg & 16) {  // timing ablation: no loads (uniform synthetic keys)
+                if (dbg & 32) {  // timing ablation: no loads (uniform synthetic keys)
                     key[i] = ib + i * 64 < nn ? (uint64_t)(li + 1) * 0x9E3779B97F4A7C15ull : 0;
                     continue;
                 }
@@ -371,8 +374,9 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
         };
         if (PF && ra < rb) load_tile(ra);
         for (uint32_t r = ra; r < rb; r++) {
-            for (int i = threadIdx.x; i < NWAVE * R1 / 2; i += NT) (&whist[0][0])[i] = 0;
-            if (!ATOMIC && threadIdx.x < R1) thist[threadIdx.x] = 0;
+            if (!BR)
+                for (int i = threadIdx.x; i < NWAVE * R1 / 2; i += NT) (&whist[0][0])[i] = 0;
+            if ((BR || !ATOMIC) && threadIdx.x < R1) thist[threadIdx.x] = 0;
             __syncthreads();
             const uint32_t t0 = r * TILE;
             const uint32_t n = items - t0 < (uint32_t)TILE ? items - t0 : (uint32_t)TILE;
@@ -389,6 +393,19 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                 }
             }
 #define PDIGIT(x) ((uint32_t)((x) >> shift) & dmask)
+            if (BR) {
+#pragma unroll
+                for (int i = 0; i < SI; i++)
+                    rank[i] = ib + i * 64 < n ? atomicAdd(&thist[PDIGIT(key[i])], 1u) : 0u;
+                __syncthreads();
+                const uint32_t ls = block_exclusive_scan<NT>(threadIdx.x < R1 ? thist[threadIdx.x] : 0u, SumU32(), 0u,
+                                                             lds_scan, (uint32_t *)nullptr);
+                if (threadIdx.x < R1) lstart[threadIdx.x] = ls;
+                __syncthreads();
+#pragma unroll
+                for (int i = 0; i < SI; i++)
+                    if (ib + i * 64 < n) skeys[lstart[PDIGIT(key[i])] + rank[i]] = key[i];
+            } else {
             if (ATOMIC) {
 #pragma unroll
                 for (int i = 0; i < SI; i++) {
@@ -452,6 +469,7 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                     skeys[lstart[d] + ((whist[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rank[i]] = key[i];
                 }
             }
+            }  // !BR
             __syncthreads();
             RSTAMP(r, 1);
             if (WC) {
@@ -461,6 +479,9 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
 #pragma unroll
                 for (uint32_t d = threadIdx.x >> 4; d < (uint32_t)R1; d += NT / 16) {
                     const uint32_t j = threadIdx.x & 15u, rn = run[d], p = rn & 15u;
+#ifdef RG_PASS_ABL
+                    if (dbg & 4) continue;  // timing ablation: no stores
+#endif
                     if (j < p && ((rn + thist[d]) >> 4) > (rn >> 4) && rn - p + j < C1)
                         pa.out[SUBREG(d) * C1 + rn - p + j] = wcb[d][j];
                 }
@@ -475,6 +496,9 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                         const uint32_t rn = run[d];
                         const uint32_t at = rn + (q - lstart[d]);
                         if (at < ((rn + thist[d]) & ~15u)) {
+#ifdef RG_PASS_ABL
+                            if (dbg & 4) continue;  // timing ablation: no stores
+#endif
                             if (at < C1) pa.out[SUBREG(d) * C1 + at] = kk;
                         } else {
                             wcb[d][at & 15u] = kk;
@@ -821,8 +845,15 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     return KMAN_OK;
 }
 
-template <int NT, int SI, bool PF, bool WC = false>
+template <int NT, int SI, bool PF, bool WC = false, bool BR = false>
 void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
+    if (BR) {  // no ordered LDS atomics needed
+        const void *fn = (const void *)rg_pass<true, NT, SI, PF, WC, BR>;
+        const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, NT, (uint64_t)pa.nbk * pa.H);
+        hipLaunchKernelGGL((rg_pass<true, NT, SI, PF, WC, BR>), dim3(grid), dim3(NT), 0, ctx->stream, pa, counter,
+                           ctx->d_err, dbg, stp);
+        return;
+    }
     const void *fn = ctx->lds_atomic_ordered ? (const void *)rg_pass<true, NT, SI, PF, WC>
                                              : (const void *)rg_pass<false, NT, SI, PF, WC>;
     const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, NT, (uint64_t)pa.nbk * pa.H);
@@ -837,11 +868,14 @@ void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32
 // block shape of the digit pass: KMAN_RG_PASS = 0 (512 x 16, two blocks per
 // CU), 1 (the same with the next tile prefetched), 2 (1024 x 8, one block per
 // CU, prefetched), 3 (1024 x 8 with write combining), 4 (the same with
-// prefetch; default: 4.85 vs 5.65 ms for 0 on one box)
+// prefetch), 5 (4 with the block-wide rank; the default), 6 (0 with the
+// block-wide rank).  One box, ms: 0 4.66, 4 4.29, 5 3.78, 6 4.69.
 void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     const char *e = getenv("KMAN_RG_PASS");
-    const int shape = e ? atoi(e) : 4;
-    if (shape == 4) launch_pass_as<1024, 8, true, true>(ctx, pa, counter, dbg, stp);
+    const int shape = e ? atoi(e) : 5;
+    if (shape == 5) launch_pass_as<1024, 8, true, true, true>(ctx, pa, counter, dbg, stp);
+    else if (shape == 6) launch_pass_as<RT, RSI, false, false, true>(ctx, pa, counter, dbg, stp);
+    else if (shape == 4) launch_pass_as<1024, 8, true, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 3) launch_pass_as<1024, 8, false, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 2) launch_pass_as<1024, 8, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 1) launch_pass_as<RT, RSI, true>(ctx, pa, counter, dbg, stp);
