@@ -288,7 +288,7 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                                                  uint32_t *__restrict__ err, uint32_t dbg,
                                                  uint64_t *__restrict__ stp) {
     constexpr int TILE = NT * SI, NWAVE = NT / 64;
-    static_assert(NT >= R1 && SI % 4 == 0 && 64 * SI <= 65535, "a thread per digit; u16 wave counters");
+    static_assert(NT >= R1 && 64 * SI <= 65535, "a thread per digit; u16 wave counters");
     __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
     __shared__ uint64_t wcb[WC ? R1 : 1][16];  // WC: the pending items of digit d at wcb[d][pos % 16]
     __shared__ uint32_t whist[BR ? 1 : NWAVE][R1 / 2];
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
 #define SUBREG(d) (((reg0 | (d)) * pa.gsub + rsub) * H + h)
         const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
         uint64_t key[SI];
-        uint32_t sgp[SI / 4];  // the items' segments, 8 bits each (for the tag)
+        uint32_t sgp[(SI + 3) / 4];  // the items' segments, 8 bits each (for the tag)
         // the keys of tile rt into key[] (logical item -> (segment, offset)
         // with ballots over the lanes' prefixes: the 64 items of a wave row
         // are consecutive, so their segment is the row start's, past the
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
             const uint32_t tt0 = rt * TILE;
             const uint32_t nn = items - tt0 < (uint32_t)TILE ? items - tt0 : (uint32_t)TILE;
 #pragma unroll
-            for (int i = 0; i < SI / 4; i++) sgp[i] = 0;
+            for (int i = 0; i < (SI + 3) / 4; i++) sgp[i] = 0;
 #pragma unroll
             for (int i = 0; i < SI; i++) {
                 const uint32_t li0 = tt0 + (uint32_t)w * (SI * 64) + (uint32_t)i * 64;
@@ -847,13 +847,12 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
 
 template <int NT, int SI, bool PF, bool WC = false, bool BR = false>
 void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
-    if (BR) {  // no ordered LDS atomics needed
+    if constexpr (BR) {  // no ordered LDS atomics needed
         const void *fn = (const void *)rg_pass<true, NT, SI, PF, WC, BR>;
         const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, NT, (uint64_t)pa.nbk * pa.H);
         hipLaunchKernelGGL((rg_pass<true, NT, SI, PF, WC, BR>), dim3(grid), dim3(NT), 0, ctx->stream, pa, counter,
                            ctx->d_err, dbg, stp);
-        return;
-    }
+    } else {
     const void *fn = ctx->lds_atomic_ordered ? (const void *)rg_pass<true, NT, SI, PF, WC>
                                              : (const void *)rg_pass<false, NT, SI, PF, WC>;
     const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, NT, (uint64_t)pa.nbk * pa.H);
@@ -863,17 +862,20 @@ void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32
     else
         hipLaunchKernelGGL((rg_pass<false, NT, SI, PF, WC>), dim3(grid), dim3(NT), 0, ctx->stream, pa, counter,
                            ctx->d_err, dbg, stp);
+    }
 }
 
 // block shape of the digit pass: KMAN_RG_PASS = 0 (512 x 16, two blocks per
 // CU), 1 (the same with the next tile prefetched), 2 (1024 x 8, one block per
 // CU, prefetched), 3 (1024 x 8 with write combining), 4 (the same with
-// prefetch), 5 (4 with the block-wide rank; the default), 6 (0 with the
-// block-wide rank).  One box, ms: 0 4.66, 4 4.29, 5 3.78, 6 4.69.
+// prefetch), 5 (4 with the block-wide rank), 6 (0 with the block-wide rank),
+// 7 (5 with 10 items per thread; the default).  One box, ms: 0 4.66, 4 4.29,
+// 5 3.78, 6 4.69; another: 5 3.92-3.97, 7 3.86-3.87.
 void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     const char *e = getenv("KMAN_RG_PASS");
-    const int shape = e ? atoi(e) : 5;
+    const int shape = e ? atoi(e) : 7;
     if (shape == 5) launch_pass_as<1024, 8, true, true, true>(ctx, pa, counter, dbg, stp);
+    else if (shape == 7) launch_pass_as<1024, 10, true, true, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 6) launch_pass_as<RT, RSI, false, false, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 4) launch_pass_as<1024, 8, true, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 3) launch_pass_as<1024, 8, false, true>(ctx, pa, counter, dbg, stp);
