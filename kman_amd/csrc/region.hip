@@ -93,7 +93,9 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 // packed above the 2k key bits), ranked by the top 8 key bits, digit counts
 // published early, grouped look-back per digit along the segment's chain,
 // LDS-staged coalesced scatter into region (b, s).
-template <int EI, bool RC, bool ATOMIC, bool CANON = false>
+// BR: rank by one block-wide LDS atomic per item (unstable inside a tile;
+// nothing downstream needs the order of a region's items).
+template <int EI, bool RC, bool ATOMIC, bool CANON = false, bool BR = false>
 __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
                                                  uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
                                                  uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ cnt0,
@@ -107,7 +109,7 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
     constexpr int SI = TILE / NT;
     static_assert(WIN + 64 <= TILE * 8, "codes fit in the key staging area");
     __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
-    __shared__ uint32_t whist[NWAVE][RADIX];
+    __shared__ uint32_t whist[BR ? 1 : NWAVE][RADIX];
     __shared__ uint32_t thist[RADIX];
     __shared__ uint32_t lstart[RADIX];
     __shared__ uint64_t gexcl[RADIX];
@@ -131,7 +133,8 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
     const uint64_t wb = (uint64_t)tile * WIN;
     uint8_t *scodes = reinterpret_cast<uint8_t *>(skeys);
     stage_codes<NT, EI>(codes, n_bases, wb, scodes);
-    for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&whist[0][0])[i] = 0;
+    if (!BR)
+        for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&whist[0][0])[i] = 0;
     if (threadIdx.x < RADIX) thist[threadIdx.x] = 0;
     __syncthreads();
     RSTAMP(tile, 1);
@@ -163,7 +166,12 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
 #pragma unroll
     for (int i = 0; i < SI; i++) key[i] = ib + i * 64 < tcnt ? skeys[ib + i * 64] : 0;
 #define XDIGIT(x) ((uint32_t)(((x) & keymask) >> shift))
-    if (ATOMIC) {
+    if (BR) {
+#pragma unroll
+        for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&thist[XDIGIT(key[i])], 1u) : 0u;
+        __syncthreads();
+        if (threadIdx.x < RADIX) digit_publish(status + threadIdx.x, tile, first, thist[threadIdx.x], epoch);
+    } else if (ATOMIC) {
 #pragma unroll
         for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&whist[w][XDIGIT(key[i])], 1u) : 0u;
         __syncthreads();
@@ -187,7 +195,9 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
     RSTAMP(tile, 3);
     const uint32_t d0 = threadIdx.x;
     uint32_t tot = 0;
-    if (d0 < RADIX) {
+    if (BR) {
+        if (d0 < RADIX) tot = thist[d0];
+    } else if (d0 < RADIX) {
 #pragma unroll
         for (int ww = 0; ww < NWAVE; ww++) {
             const uint32_t c = whist[ww][d0];
@@ -202,7 +212,7 @@ __global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ 
     for (int i = 0; i < SI; i++) {
         if (ib + i * 64 < tcnt) {
             const uint32_t d = XDIGIT(key[i]);
-            skeys[lstart[d] + whist[w][d] + rank[i]] = key[i];
+            skeys[lstart[d] + (BR ? 0u : whist[w][d]) + rank[i]] = key[i];
         }
     }
     {
@@ -928,7 +938,12 @@ template <int EI, bool RC, bool CANON = false>
 void launch_extract(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                     uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     const uint32_t grid = RS * p.seg_tiles;
-    if (ctx->lds_atomic_ordered)
+    const char *e = getenv("KMAN_RG_EXTRACT");  // 1 (default): block-wide rank; 0: stable per-wave rank
+    if (!e || atoi(e) != 0)
+        hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true>), dim3(grid), dim3(RT), 0, ctx->stream, codes,
+                           n_bases, (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch,
+                           ctx->d_err, dbg, stp);
+    else if (ctx->lds_atomic_ordered)
         hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON>), dim3(grid), dim3(RT), 0, ctx->stream, codes, n_bases,
                            (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch,
                            ctx->d_err, dbg, stp);
