@@ -301,6 +301,10 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
     static_assert(NT >= R1 && 64 * SI <= 65535, "a thread per digit; u16 wave counters");
     __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
     __shared__ uint64_t wcb[WC ? R1 : 1][16];  // WC: the pending items of digit d at wcb[d][pos % 16]
+    // WC, per digit for the store loop: output index of tile item q = obase[d]
+    // + q; qpar[d] = (q bound of the whole-line items << 32) | (run - lstart)
+    __shared__ uint64_t obase[WC ? R1 : 1];
+    __shared__ uint64_t qpar[WC ? R1 : 1];
     __shared__ uint32_t whist[BR ? 1 : NWAVE][R1 / 2];
     __shared__ uint32_t thist[R1];
     __shared__ uint32_t lstart[R1];
@@ -363,15 +367,25 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
             for (int i = 0; i < SI; i++) {
                 const uint32_t li0 = tt0 + (uint32_t)w * (SI * 64) + (uint32_t)i * 64;
                 const uint32_t li = li0 + (uint32_t)lane;
-                uint32_t sg = (uint32_t)__popcll(__ballot(spre_l <= li0) & ~1ull);  // lane 0 (prefix 0) not counted
+                // the row start's segment is wave-uniform: its base and
+                // prefix come from readlanes (scalar), not LDS permutes
+                const int sg0 = __popcll(__ballot(spre_l <= li0) & ~1ull);  // lane 0 (prefix 0) not counted
+                uint32_t sg = (uint32_t)sg0;
+                uint64_t bs = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(sbase_l >> 32), sg0) << 32) |
+                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sbase_l, sg0);
+                uint32_t po = (uint32_t)__builtin_amdgcn_readlane((int)spre_l, sg0);
                 uint64_t inrow = __ballot(spre_l > li0 && spre_l <= li0 + 63);
                 while (inrow) {  // (wave-uniform)
                     const int s2 = __ffsll((unsigned long long)inrow) - 1;
                     inrow &= inrow - 1;
-                    if (li >= (uint32_t)__builtin_amdgcn_readlane((int)spre_l, s2)) sg = (uint32_t)s2;
+                    const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)spre_l, s2);
+                    if (li >= p2) {
+                        sg = (uint32_t)s2;
+                        po = p2;
+                        bs = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(sbase_l >> 32), s2) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sbase_l, s2);
+                    }
                 }
-                const uint64_t bs = shfl_any(sbase_l, (int)sg);
-                const uint32_t po = (uint32_t)__shfl((int)spre_l, (int)sg, 64);
                 sgp[i >> 2] |= sg << (8 * (i & 3));
 #ifdef RG_PASS_ABL
                 if (dbg & 32) {  // timing ablation: no loads (uniform synthetic keys)
@@ -495,6 +509,17 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                     if (j < p && ((rn + thist[d]) >> 4) > (rn >> 4) && rn - p + j < C1)
                         pa.out[SUBREG(d) * C1 + rn - p + j] = wcb[d][j];
                 }
+                if (threadIdx.x < R1) {
+                    // item q of digit d goes to position at = q + off; whole
+                    // lines end at fe; positions >= C1 are dropped (an
+                    // overflowing region raises ERR_REGION and the whole
+                    // call falls back, so where its items go is moot)
+                    const uint32_t d = threadIdx.x, rn = run[d], off = rn - lstart[d];
+                    const int32_t fe = (int32_t)((rn + thist[d]) & ~15u);
+                    const int32_t qlim = (fe < (int32_t)C1 ? fe : (int32_t)C1) - (int32_t)off;
+                    obase[d] = SUBREG(d) * C1 + (uint64_t)(int64_t)(int32_t)off;
+                    qpar[d] = ((uint64_t)(uint32_t)qlim << 32) | off;
+                }
                 __syncthreads();  // those wcb reads before the leftovers below
                 // items of whole lines to HBM, the new partial line to LDS
 #pragma unroll
@@ -503,15 +528,14 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                     if (q < n) {
                         const uint64_t kk = skeys[q];
                         const uint32_t d = PDIGIT(kk);
-                        const uint32_t rn = run[d];
-                        const uint32_t at = rn + (q - lstart[d]);
-                        if (at < ((rn + thist[d]) & ~15u)) {
+                        const uint64_t qp = qpar[d];
+                        if ((int32_t)q < (int32_t)(qp >> 32)) {
 #ifdef RG_PASS_ABL
                             if (dbg & 4) continue;  // timing ablation: no stores
 #endif
-                            if (at < C1) pa.out[SUBREG(d) * C1 + at] = kk;
+                            pa.out[obase[d] + q] = kk;
                         } else {
-                            wcb[d][at & 15u] = kk;
+                            wcb[d][(q + (uint32_t)qp) & 15u] = kk;
                         }
                     }
                 }
@@ -879,11 +903,13 @@ void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32
 // CU), 1 (the same with the next tile prefetched), 2 (1024 x 8, one block per
 // CU, prefetched), 3 (1024 x 8 with write combining), 4 (the same with
 // prefetch), 5 (4 with the block-wide rank), 6 (0 with the block-wide rank),
-// 7 (5 with 10 items per thread; the default).  One box, ms: 0 4.66, 4 4.29,
-// 5 3.78, 6 4.69; another: 5 3.92-3.97, 7 3.86-3.87.
+// 7 (5 with 10 items per thread: it spills registers since the store loop
+// takes per-digit parameters from LDS).  5 is the default.  One box, ms: 0
+// 4.66, 4 4.29, 5 3.78, 6 4.69; another: 5 3.49-3.58 (7 before the per-digit
+// parameters 3.80, after 4.2-4.6).
 void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     const char *e = getenv("KMAN_RG_PASS");
-    const int shape = e ? atoi(e) : 7;
+    const int shape = e ? atoi(e) : 5;
     if (shape == 5) launch_pass_as<1024, 8, true, true, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 7) launch_pass_as<1024, 10, true, true, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 6) launch_pass_as<RT, RSI, false, false, true>(ctx, pa, counter, dbg, stp);
