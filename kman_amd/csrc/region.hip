@@ -301,9 +301,10 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
     static_assert(NT >= R1 && 64 * SI <= 65535, "a thread per digit; u16 wave counters");
     __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
     __shared__ uint64_t wcb[WC ? R1 : 1][16];  // WC: the pending items of digit d at wcb[d][pos % 16]
-    // WC, per digit for the store loop: output index of tile item q = obase[d]
-    // + q; qpar[d] = (q bound of the whole-line items << 32) | (run - lstart)
-    __shared__ uint64_t obase[WC ? R1 : 1];
+    // WC, per digit for the store loop: qpar[d] = (q bound of the whole-line
+    // items << 32) | the output index of tile item 0 relative to the chain's
+    // first sub-region (digit d's sub-region is d * gsub * H after it, and
+    // C1 is a multiple of 16, so the low 4 bits are the line slot)
     __shared__ uint64_t qpar[WC ? R1 : 1];
     __shared__ uint32_t whist[BR ? 1 : NWAVE][R1 / 2];
     __shared__ uint32_t thist[R1];
@@ -350,6 +351,9 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
         // output sub-region of digit d
         const uint64_t reg0 = (uint64_t)(b / pa.gsub) << bits, rsub = b % pa.gsub;
 #define SUBREG(d) (((reg0 | (d)) * pa.gsub + rsub) * H + h)
+        // WC: digit d's sub-region is d * dstride items after digit 0's
+        uint64_t *const obase0 = pa.out + SUBREG(0u) * C1;
+        const uint32_t dstride = pa.gsub * H * (uint32_t)C1;
         const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
         uint64_t key[SI];
         uint32_t sgp[(SI + 3) / 4];  // the items' segments, 8 bits each (for the tag)
@@ -507,7 +511,7 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                     if (dbg & 4) continue;  // timing ablation: no stores
 #endif
                     if (j < p && ((rn + thist[d]) >> 4) > (rn >> 4) && rn - p + j < C1)
-                        pa.out[SUBREG(d) * C1 + rn - p + j] = wcb[d][j];
+                        obase0[d * dstride + rn - p + j] = wcb[d][j];
                 }
                 if (threadIdx.x < R1) {
                     // item q of digit d goes to position at = q + off; whole
@@ -517,8 +521,7 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                     const uint32_t d = threadIdx.x, rn = run[d], off = rn - lstart[d];
                     const int32_t fe = (int32_t)((rn + thist[d]) & ~15u);
                     const int32_t qlim = (fe < (int32_t)C1 ? fe : (int32_t)C1) - (int32_t)off;
-                    obase[d] = SUBREG(d) * C1 + (uint64_t)(int64_t)(int32_t)off;
-                    qpar[d] = ((uint64_t)(uint32_t)qlim << 32) | off;
+                    qpar[d] = ((uint64_t)(uint32_t)qlim << 32) | (d * dstride + off);
                 }
                 __syncthreads();  // those wcb reads before the leftovers below
                 // items of whole lines to HBM, the new partial line to LDS
@@ -529,13 +532,14 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                         const uint64_t kk = skeys[q];
                         const uint32_t d = PDIGIT(kk);
                         const uint64_t qp = qpar[d];
+                        const uint32_t rel = (uint32_t)qp + q;
                         if ((int32_t)q < (int32_t)(qp >> 32)) {
 #ifdef RG_PASS_ABL
                             if (dbg & 4) continue;  // timing ablation: no stores
 #endif
-                            pa.out[obase[d] + q] = kk;
+                            obase0[rel] = kk;
                         } else {
-                            wcb[d][(q + (uint32_t)qp) & 15u] = kk;
+                            wcb[d][rel & 15u] = kk;
                         }
                     }
                 }
@@ -903,14 +907,14 @@ void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32
 // CU), 1 (the same with the next tile prefetched), 2 (1024 x 8, one block per
 // CU, prefetched), 3 (1024 x 8 with write combining), 4 (the same with
 // prefetch), 5 (4 with the block-wide rank), 6 (0 with the block-wide rank),
-// 7 (5 with 10 items per thread: it spills registers since the store loop
-// takes per-digit parameters from LDS).  5 is the default.  One box, ms: 0
-// 4.66, 4 4.29, 5 3.78, 6 4.69; another: 5 3.49-3.58 (7 before the per-digit
-// parameters 3.80, after 4.2-4.6).
+// 7 (5 with 10 items per thread).  5 is the default.  One box, ms: 0 4.66,
+// 4 4.29, 5 3.78, 6 4.69; later boxes: 5 3.49-3.58 with per-digit store
+// parameters, 3.54 with 32-bit relative output indices (7: 3.56).
 void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     const char *e = getenv("KMAN_RG_PASS");
     const int shape = e ? atoi(e) : 5;
     if (shape == 5) launch_pass_as<1024, 8, true, true, true>(ctx, pa, counter, dbg, stp);
+    else if (shape == 7) launch_pass_as<1024, 10, true, true, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 7) launch_pass_as<1024, 10, true, true, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 6) launch_pass_as<RT, RSI, false, false, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 4) launch_pass_as<1024, 8, true, true>(ctx, pa, counter, dbg, stp);
