@@ -449,9 +449,8 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                     thist[d] = c;
                 }
             } else {
-#pragma unroll
-                for (int i = 0; i < SI; i++)
-                    if (ib + i * 64 < n) atomicAdd(&thist[PDIGIT(key[i])], 1u);
+                // ballot match ranks: no atomics on a few hot addresses (the
+                // small-radix passes of the multi-GPU path use this)
 #pragma unroll
                 for (int i = 0; i < SI; i++) {
                     const bool valid = ib + i * 64 < n;
@@ -468,6 +467,14 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                     const int leader = __ffsll((unsigned long long)peers) - 1;
                     if (valid && lane == leader) atomicAdd(&whist[w][d >> 1], (uint32_t)__popcll(peers) << hs);
                     __builtin_amdgcn_wave_barrier();
+                }
+                __syncthreads();
+                if (threadIdx.x < R1) {
+                    const uint32_t d = threadIdx.x, hs = (d & 1u) * 16u;
+                    uint32_t c = 0;
+#pragma unroll
+                    for (int ww = 0; ww < NWAVE; ww++) c += (whist[ww][d >> 1] >> hs) & 0xffffu;
+                    thist[d] = c;
                 }
             }
             __syncthreads();
@@ -913,8 +920,28 @@ void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32
 void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     const char *e = getenv("KMAN_RG_PASS");
     const int shape = e ? atoi(e) : 5;
+    if (pa.bits <= 4 && shape >= 3) {
+        // a few digits (the multi-GPU pass 1b: 1-3 bits): block-wide or
+        // per-wave LDS atomics would all hit the same few counters, so rank
+        // by ballots (rg_pass<false>: per-wave counters, one update per
+        // distinct digit of a row)
+        // (KMAN_RG_SMALL=0: 512-thread blocks without write combining, for
+        // A/B timing; pass 1b at world 1, ms: 8.7 vs 7.2 for the default)
+        const char *e2 = getenv("KMAN_RG_SMALL");
+        if (!e2 || atoi(e2) != 0) {
+            const void *fn = (const void *)rg_pass<false, 1024, 8, true, true, false>;
+            const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, 1024, (uint64_t)pa.nbk * pa.H);
+            hipLaunchKernelGGL((rg_pass<false, 1024, 8, true, true, false>), dim3(grid), dim3(1024), 0, ctx->stream,
+                               pa, counter, ctx->d_err, dbg, stp);
+        } else {
+            const void *fn = (const void *)rg_pass<false, RT, RSI, false, false, false>;
+            const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, RT, (uint64_t)pa.nbk * pa.H);
+            hipLaunchKernelGGL((rg_pass<false, RT, RSI, false, false, false>), dim3(grid), dim3(RT), 0, ctx->stream,
+                               pa, counter, ctx->d_err, dbg, stp);
+        }
+        return;
+    }
     if (shape == 5) launch_pass_as<1024, 8, true, true, true>(ctx, pa, counter, dbg, stp);
-    else if (shape == 7) launch_pass_as<1024, 10, true, true, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 7) launch_pass_as<1024, 10, true, true, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 6) launch_pass_as<RT, RSI, false, false, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 4) launch_pass_as<1024, 8, true, true>(ctx, pa, counter, dbg, stp);
