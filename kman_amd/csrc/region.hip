@@ -877,7 +877,10 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     // pass 1 runs H = 2 block-owned chains per bucket (its first and second
     // half of tiles) into H sub-regions per region that the finish
     // concatenates: 512 chains for the 512 resident blocks
-    p.H = 2;
+    {
+        const char *e = getenv("KMAN_RG_H");  // A/B timing only
+        p.H = e && atoi(e) == 1 ? 1u : 2u;
+    }
     p.C1h = p.C1;  // either half may hold most of a region (position-skewed repeats)
     p.maxt1 = (uint32_t)ceil_div((uint64_t)(RS / p.H) * p.C0, T1);
     const uint64_t nreg = 1ull << (B1 + b2);
