@@ -96,7 +96,7 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 // BR: rank by one block-wide LDS atomic per item (unstable inside a tile;
 // nothing downstream needs the order of a region's items).
 template <int EI, bool RC, bool ATOMIC, bool CANON = false, bool BR = false>
-__global__ __launch_bounds__(RT, 4) void rg_extract(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
+__global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI == 8 ? 8 : 4)))) void rg_extract(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
                                                  uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
                                                  uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ cnt0,
                                                  uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
@@ -865,7 +865,17 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     if (p.K < B1 + b2 + 1) return KMAN_EFALLBACK;
     p.B2 = b2;
     p.rest = p.K - B1 - b2;
-    p.ei = p.rc ? 8 : 16;
+    {
+        // windows per thread: 12 (6 with -r: two items per window) makes
+        // 6144-item tiles, 53 KiB of LDS, three blocks per CU: 3.92 ms vs 4.77
+        // with the 16-window tiles (two blocks per CU) and 4.63 with 8
+        // (four blocks, but twice the tiles and look-back steps).
+        // KMAN_RG_EI=16 / 8 select those for A/B timing.
+        const char *e = getenv("KMAN_RG_EI");
+        const int ei = e ? atoi(e) : 12;
+        if (p.rc) p.ei = ei == 16 ? 8u : 6u;  // two windows per item slot
+        else p.ei = ei == 16 ? 16u : (ei == 8 && !p.canon ? 8u : 12u);
+    }
     const uint64_t win = (uint64_t)RT * p.ei;
     p.n_tiles0 = (uint32_t)ceil_div(n_bases, win);
     p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, RS);
@@ -1015,8 +1025,12 @@ void launch_extract(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, ui
 
 void launch_extract_any(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                         uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
-    if (p.canon) launch_extract<16, false, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
+    if (p.canon && p.ei == 12) launch_extract<12, false, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
+    else if (p.canon) launch_extract<16, false, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
+    else if (p.rc && p.ei == 6) launch_extract<6, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
     else if (p.rc) launch_extract<8, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
+    else if (p.ei == 12) launch_extract<12, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
+    else if (p.ei == 8) launch_extract<8, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
     else launch_extract<16, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
 }
 
