@@ -269,7 +269,9 @@ KMAN_DEV Xf chunk_xf(const Chunk &ch) {
     return x;
 }
 
-__global__ __launch_bounds__(PT) void parse_reduce(const uint8_t *__restrict__ text, uint64_t n,
+// (PT, 3): three waves per SIMD (168 VGPRs, a few spilled) instead of the two
+// that 179 VGPRs allow: 0.85 -> 0.69 ms per launch on 1 GB of text
+__global__ __launch_bounds__(PT, 3) void parse_reduce(const uint8_t *__restrict__ text, uint64_t n,
                                                    Xf64 *__restrict__ tiles) {
     __shared__ Xf lds[PT / 64];
     const uint64_t pos = (uint64_t)blockIdx.x * PTILE + (uint64_t)threadIdx.x * PB;
@@ -337,7 +339,7 @@ __global__ __launch_bounds__(SCAN_T) void parse_scan_top(const Xf64 *__restrict_
     }
 }
 
-__global__ __launch_bounds__(PT) void parse_emit(const uint8_t *__restrict__ text, uint64_t n,
+__global__ __launch_bounds__(PT, 3) void parse_emit(const uint8_t *__restrict__ text, uint64_t n,
                                                  const Xf64 *__restrict__ local, const Xf64 *__restrict__ bpre,
                                                  uint8_t *__restrict__ codes,
                                                  uint64_t *__restrict__ rec_hdr, uint64_t *__restrict__ rec_seq) {
