@@ -83,6 +83,15 @@ def recv_layout(count_matrix: np.ndarray, rank: int) -> Tuple[np.ndarray, np.nda
     return send, send_off, recv, recv_off
 
 
+def split_overflow(count_matrix: np.ndarray, cap: int) -> Optional[Tuple[int, int]]:
+    """(rank, keys) of the first rank whose receive size exceeds cap, else
+    None.  A function of the all-gathered matrix only, so every rank reaches
+    the same verdict."""
+    recv = np.asarray(count_matrix, dtype=np.uint64).sum(axis=0)
+    bad = np.nonzero(recv > np.uint64(cap))[0]
+    return (int(bad[0]), int(recv[bad[0]])) if len(bad) else None
+
+
 def _u64p(a: np.ndarray):
     return a.ctypes.data_as(c_void_p)
 
@@ -354,8 +363,11 @@ class DistPipeline:
         C = dev.download(self.d_cmat, self.world * self.world, np.uint64).reshape(self.world, self.world)
         send, send_off, recv, recv_off = recv_layout(C, self.rank)
         nrecv = int(recv.sum())
-        if nrecv > self.cap:
-            raise RuntimeError("rank %d receives %d keys > capacity %d (prefix skew)" % (self.rank, nrecv, self.cap))
+        # every rank holds C: all of them see the same overflow and raise
+        # before the exchange (a lone raise would leave the peers hanging in it)
+        over = split_overflow(C, self.cap)
+        if over is not None:
+            raise RuntimeError("rank %d would receive %d keys > capacity %d (prefix skew)" % (over[0], over[1], self.cap))
         N.check(ctx, L.kman_alltoallv(ctx, c_void_p(lp.alt.ptr), _u64p(send), _u64p(send_off),
                                        c_void_p(self.recv_keys.ptr), _u64p(recv), _u64p(recv_off), 8), "alltoallv")
         if vb:

@@ -212,13 +212,22 @@ def check_empty_names(p: Parsed, k: int) -> None:
         e = int(p.rec_seq[r + 1]) if r + 1 < p.n_records else p.n_bases
         if e - b < k:
             continue
-        codes = p.dev.download(p.codes, e - b, np.uint8, offset=b) & 7
-        run = 0
-        for i, c in enumerate(codes.tolist()):
-            run = run + 1 if c < 4 else 0
-            if run >= k:
-                st = i - k + 1
-                raise AssertionError("incompatible string: :%d-%d:+" % (st, st + k))
+        st = first_window(p.dev.download(p.codes, e - b, np.uint8, offset=b), k)
+        if st >= 0:
+            raise AssertionError("incompatible string: :%d-%d:+" % (st, st + k))
+
+
+def first_window(codes: np.ndarray, k: int) -> int:
+    """Start of the first run of k ACGT codes (code & 7 < 4) in one record's
+    codes, or -1 (vectorised: run starts and ends of the valid positions)."""
+    ok = (np.asarray(codes) & 7) < 4
+    if len(ok) < k or not ok.any():
+        return -1
+    d = np.diff(np.concatenate([[0], ok.view(np.int8), [0]]))
+    starts = np.nonzero(d == 1)[0]
+    ends = np.nonzero(d == -1)[0]
+    long = np.nonzero(ends - starts >= k)[0]
+    return int(starts[long[0]]) if len(long) else -1
 
 
 # ------------------------------------------------------------------- extract
@@ -902,6 +911,33 @@ def _fits(p: Parsed, k: int, rc: bool, mode: str) -> bool:
     return need <= 0.85 * mem_info(p.dev)[0]
 
 
+def join_groups(p: Parsed, k: int, rc: bool, mode: str, max_keys: Optional[int] = None):
+    """The count / uniq result of the whole stream of p on the device, by the
+    fastest path that takes it: the region path (kman_groups); the multi-batch
+    join (RangedJoin) when the single-batch general path does not fit the
+    free HBM or max_keys asks for it; else the general path (extract_sorted +
+    rle_*).  None when the stream has no k-mers."""
+    r = groups(p, k, rc, mode) if max_keys is None else None
+    if r is None and (max_keys is not None or not _fits(p, k, rc, mode)):
+        r = ranged_groups(p, k, rc, mode, max_keys)
+    if r is None:
+        km = extract_sorted(p, k, rc, want_pos=mode == "uniq")
+        try:
+            if km.n == 0:
+                return None
+            r = rle_count(km, p.dev) if mode == "count" else rle_uniq(km, p.dev)
+        finally:
+            km.free()
+    return r
+
+
+def free_result(r) -> None:
+    if r is None:
+        return
+    for b in ((r.ukeys, r.counts) if isinstance(r, CountResult) else (r.keys, r.pos)):
+        b.free()
+
+
 def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = None,
                max_keys: Optional[int] = None) -> bytes:
     """``kmer count`` output bytes for a FASTA text (SEQ_COUNT mode).
@@ -912,22 +948,13 @@ def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = No
     p = parse(dev, text)
     try:
         check_empty_names(p, k)
-        r = groups(p, k, rc, "count") if max_keys is None else None
-        if r is None and (max_keys is not None or not _fits(p, k, rc, "count")):
-            r = ranged_groups(p, k, rc, "count", max_keys)
+        r = join_groups(p, k, rc, "count", max_keys)
         if r is None:
-            km = extract_sorted(p, k, rc, want_pos=False)
-            try:
-                if km.n == 0:
-                    return b""
-                r = rle_count(km, dev)
-            finally:
-                km.free()
+            return b""
         try:
             return emit_count(dev, r)
         finally:
-            r.ukeys.free()
-            r.counts.free()
+            free_result(r)
     finally:
         p.free()
 
@@ -941,22 +968,13 @@ def uniq_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = Non
     p = parse(dev, text)
     try:
         check_empty_names(p, k)
-        r = groups(p, k, rc, "uniq") if max_keys is None else None
-        if r is None and (max_keys is not None or not _fits(p, k, rc, "uniq")):
-            r = ranged_groups(p, k, rc, "uniq", max_keys)
+        r = join_groups(p, k, rc, "uniq", max_keys)
         if r is None:
-            km = extract_sorted(p, k, rc, want_pos=True)
-            try:
-                if km.n == 0:
-                    return b""
-                r = rle_uniq(km, dev)
-            finally:
-                km.free()
+            return b""
         try:
             return emit_uniq(p, r)
         finally:
-            r.keys.free()
-            r.pos.free()
+            free_result(r)
     finally:
         p.free()
 
@@ -1013,11 +1031,22 @@ class ResidentPipeline:
             m = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
             r = N.lib().kman_groups_plan(self.n_bases, k, flags_for(rc, want_pos), m, byref(wb))
             if r == N.KMAN_EFALLBACK:
-                self.path = "split"
+                self._to_split()
             else:
                 N.check(dev.ctx, r, "kman_groups_plan")
                 self.work = dev.alloc(int(wb.value))
                 self.work_bytes = int(wb.value)
+
+    def _to_split(self) -> None:
+        """Switch to the prefix-split path with its own digit plan (the region
+        path plans no prefix passes: lo_bit 0 would run every key bit through
+        the global passes)."""
+        self.path = "split"
+        if self.work is not None:
+            self.work.free()
+            self.work = None
+        self.lo_bit = split_bits(self.bound, 2 * self.k)
+        self.flags = flags_for(self.rc, self.mode == "uniq") | N.KMAN_HIST_LO(self.lo_bit)
 
     def _parse(self) -> None:
         info = N.ParseInfo()
@@ -1058,9 +1087,7 @@ class ResidentPipeline:
                 self.n_kmers, self.n_out = int(nk.value), int(no.value)
                 return self.n_kmers
             # a region overflowed (skewed input): the general path from here on
-            self.path = "split"
-            self.work.free()
-            self.work = None
+            self._to_split()
         n = c_uint64(0)
         res = c_int(0)
         pos = c_void_p(self.pos.ptr) if self.pos else c_void_p(None)

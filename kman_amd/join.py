@@ -197,17 +197,19 @@ def join_bytes(batches: List[Batch], count: bool, sink=None):
     whole = _whole_stream(entries)
     if whole is not None:
         # the batches are one FASTA stream, each k-mer once: count / uniq do
-        # not depend on the batch cut, so the region path takes
-        # the stream straight from the codes
-        r = engine.groups(whole.parsed, whole.k, whole.rc, "count" if count else "uniq")
-        if r is not None:
-            try:
-                if count:
-                    return engine.emit_count(whole.dev, r, sink)
-                return engine.emit_uniq(whole.parsed, r, sink)
-            finally:
-                for b in ((r.ukeys, r.counts) if count else (r.keys, r.pos)):
-                    b.free()
+        # not depend on the batch cut, so the stream goes
+        # straight from the codes: region path, else the multi-batch join when
+        # one batch does not fit the HBM, else the general path (no copy of a
+        # cached extraction either way)
+        r = engine.join_groups(whole.parsed, whole.k, whole.rc, "count" if count else "uniq")
+        if r is None:
+            return None if sink is not None else b""
+        try:
+            if count:
+                return engine.emit_count(whole.dev, r, sink)
+            return engine.emit_uniq(whole.parsed, r, sink)
+        finally:
+            engine.free_result(r)
     km, srcs, tagged = gather_sorted(entries, want_pos=not count)
     dev = srcs[0].dev
     k = srcs[0].k
