@@ -1,25 +1,40 @@
 #!/usr/bin/env python3
 """Headline benchmark: k-mers/s extract+sort+join, k=21 synthetic FASTA.
 
-Workload (BASELINE.json configs[1]): 1 GB synthetic FASTA (numpy PCG64 seed
-1 + rank, i.i.d. uniform ACGT, 80 columns, records of <= 256 Mbp named
-syn<i>), k=21, extract + radix sort + uniq (``kmer uniq``: keys and their
-pos payload) as one device batch.  A "step" is one full pass of the hot path
-over the FASTA bytes that are already resident in HBM:
-    parse -> k-mer digit histograms -> extraction fused with the first prefix
-    pass -> 2 more onesweep digit passes over the top 21 key bits -> finish
-    (segments sorted in LDS + uniq, one pass)
-leaving the (k-mer, header pos) result device-resident.  Text formatting and
-the file write are not part of the step (reported separately by the CLI).
+N = 1 (BASELINE.json configs[1]): 1 GB synthetic FASTA (numpy PCG64 seed 1,
+i.i.d. uniform ACGT, 80 columns, records of <= 256 Mbp named syn<i>), k=21,
+``kmer uniq`` (extract + radix sort + join: keys that occur once, with their
+header pos) as one device batch.  A "step" is one pass of the hot path over
+the FASTA bytes already resident in HBM:
+    parse -> rg_extract (windows scattered by the top 8 key bits into
+    regions) -> rg_pass (per bucket, by the next 9 bits) -> rg_finish (one
+    LDS block per region: sort the rest, run-length uniq, compacted output)
+leaving the (k-mer, pos) rows device-resident.  ``value`` is that rate.
+Reported beside it:
+  * ``pinned_host``: the same step starting from pinned host bytes: chunked
+    H2D copies on a copy stream overlapping the parse of the previous chunk
+    (shard.StreamedPipeline), plus the plain H2D time of the text;
+  * ``output``: device text formatting and the file write of a bounded
+    slice of the rows, as rates and as ms extrapolated to all rows;
+  * ``file_to_file``: the CLI (`kmer count`) on a bounded FASTA file;
+  * ``roofline``: the dominant kernel of the step (largest stage), its
+    algorithmic bytes per launch over its HIP-event duration, against the
+    8 TB/s HBM peak; ``sort_pass_roofline``: the digit pass (the north star's
+    >= 60 % bar); ``traffic`` from the committed rocprofv3 PMC passes;
+  * ``cpu_baseline``: the C restatement of the reference algorithm
+    (oracle/kman_oracle) on a bounded sample, 1 core and one process per
+    core on the host's cores (count stated).
 
-Prints ONE JSON line (rank 0).  ``roofline`` is measured live: the average
-duration of the onesweep sort-pass kernel from HIP events recorded on the
-engine's own stream around every launch in the timed steps.
-``cpu_baseline`` times the C restatement of the reference algorithm
-(oracle/kman_oracle, 1 thread) on a bounded sample of the same workload.
-
-Multi-GPU: ``python -m torch.distributed.run --nproc-per-node N bench.py
---gpus N``; every rank holds its own 1 GB shard (weak scaling).
+N > 1 (``python -m torch.distributed.run --nproc-per-node N bench.py --gpus
+N``, or ``--dist`` at N = 1): ONE global synthetic FASTA of N x 1 GB (seed 1,
+kman_synth_fasta / inputs.SynthLayout), byte-range sharded (each rank
+generates its own bytes + halo on its GPU); per step every rank runs the
+shard histogram, the key rounds (extraction into the send buffer, one RCCL
+all-to-all of packed items over xGMI, per-bucket passes + LDS finish).  The
+rendezvous is RCCL only: rank 0 writes the RCCL id to a file, the barrier and
+the max-over-ranks time are RCCL collectives (no torch.distributed).
+``--shard-gb 12.5`` gives the per-rank shape of BASELINE config 4
+(100 GB over 8 GPUs).
 """
 
 from __future__ import annotations
@@ -45,31 +60,314 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(k: int, mode: str, target_s: float = 12.0) -> dict:
-    """oracle/kman_oracle (C restatement, 1 thread) on a sample of the same
-    synthetic workload; the sample is scaled to ~target_s seconds."""
+def cpu_baseline(k: int, mode: str, target_s: float = 10.0) -> dict:
+    """oracle/kman_oracle (C restatement of the reference algorithm) on a
+    sample of the same synthetic workload scaled to ~target_s seconds: one
+    process (1 core), then one process per core on independent samples of
+    the same size (aggregate k-mers / wall time)."""
     import inputs
 
     exe = os.path.join(ROOT, "oracle", "kman_oracle")
     if not os.path.isfile(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
     with tempfile.TemporaryDirectory() as d:
-        def run(nbases):
-            src = os.path.join(d, "s.fa")
+        def sample(nbases, seed):
+            src = os.path.join(d, "s%d.fa" % seed)
             with open(src, "wb") as fh:
-                fh.write(inputs.syn_numpy(nbases, 1))
-            r = subprocess.run([exe, mode, src, os.path.join(d, "o.txt"), str(k), "-t"], capture_output=True,
-                               text=True, check=True)
-            m = re.search(r"kmers=(\d+) seconds=([0-9.]+)", r.stdout)
-            return int(m.group(1)), float(m.group(2))
+                fh.write(inputs.syn_numpy(nbases, seed))
+            return src
 
-        n, s = run(2_000_000)
-        scale = max(1.0, min(32.0, target_s / max(s, 1e-3)))
-        nb = int(2_000_000 * scale)
-        n, s = run(nb)
-    return {"value": n / s, "unit": "k-mers/s", "cores": 1, "kind": "port",
-            "sample": "%d-base prefix-shaped sample of the same generator (seed 1), %s k=%d, %d k-mers in %.2f s"
-                      % (nb, mode, k, n, s)}
+        def run(srcs):
+            t0 = time.perf_counter()
+            ps = [subprocess.Popen([exe, mode, s, s + ".out", str(k), "-t"], stdout=subprocess.PIPE, text=True)
+                  for s in srcs]
+            outs = [p.communicate()[0] for p in ps]
+            wall = time.perf_counter() - t0
+            n = sum(int(re.search(r"kmers=(\d+)", o).group(1)) for o in outs)
+            s = max(float(re.search(r"seconds=([0-9.]+)", o).group(1)) for o in outs)
+            return n, s, wall
+
+        n, s, _ = run([sample(2_000_000, 1)])
+        nb = int(2_000_000 * max(1.0, min(32.0, target_s / max(s, 1e-3))))
+        n1, s1, _ = run([sample(nb, 1)])
+        nbp = max(2_000_000, nb // 2)
+        srcs = [sample(nbp, 1 + i) for i in range(cores)]
+        nP, _, wallP = run(srcs)
+    return {"value": n1 / s1, "unit": "k-mers/s", "cores": 1, "kind": "port",
+            "sample": "%d-base sample of the same generator (seed 1), %s k=%d, %d k-mers in %.2f s, 1 thread"
+                      % (nb, mode, k, n1, s1),
+            "all_cores": {"value": nP / wallP, "cores": cores, "nproc": os.cpu_count(),
+                          "sample": "%d processes on independent %d-base samples (seeds 1..%d), %d k-mers in %.2f s "
+                                    "wall" % (cores, nbp, cores, nP, wallP)}}
+
+
+def pmc_traffic(kernel: str, mode: str, k: int, bases: int):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary of this workload (profiles/pmc_current.json), else None."""
+    p = os.path.join(ROOT, "profiles", "pmc_current.json")
+    if not os.path.isfile(p):
+        return None
+    with open(p) as fh:
+        d = json.load(fh)
+    meta = d.get("_meta", {})
+    if meta.get("mode") != mode or meta.get("k") != k or meta.get("bases") != bases:
+        return None
+    hits = [v for n, v in d.items() if n != "_meta" and n.startswith(kernel)]
+    return max(hits, key=lambda v: v["launches"])["hbm_bytes_per_launch"] if hits else None
+
+
+def roofline(pipe, stages, steps, mode, k, bases):
+    """(dominant-kernel roofline, digit-pass roofline) of the region path.
+    Algorithmic bytes per k-mer: rg_extract 1 code read + 8 B
+    item write; rg_pass 8 + 8; rg_finish 8 B item read + 12 B per output row
+    (8 B key + 4 B count | pos)."""
+    n, rows = pipe.n_kmers, pipe.n_out
+    per = {"region_extract": ("rg_extract", 9.0 * n), "region_pass": ("rg_pass", 16.0 * n),
+           "region_finish": ("rg_finish", 8.0 * n + 12.0 * rows)}
+
+    def line(tag):
+        kern, alg = per[tag]
+        c, ms = pipe.timed(tag)
+        avg = ms / max(c, 1) / 1e3
+        a = alg / avg / 1e9
+        return {"kernel": kern, "bound": "hbm", "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": a / HBM_PEAK_GBS, "traffic": pmc_traffic(kern, mode, k, bases),
+                "algorithmic_bytes_per_launch": alg, "avg_launch_ms": avg * 1e3, "launches_per_step": c // steps}
+
+    dom = max(per, key=lambda t: stages.get(t, 0.0))
+    return line(dom), line("region_pass")
+
+
+def output_lines(dev, pipe, k, mode, rows_max=100_000_000):
+    """Device formatting + file write of the first rows_max rows of the
+    result: rates and ms extrapolated to every row."""
+    from kman_amd import engine
+
+    m = min(pipe.n_out, rows_max)
+    if m == 0:
+        return None
+    ob = pipe.count_bytes if mode == "count" else pipe.pos_bytes
+    t0 = time.perf_counter()
+    if mode == "count":
+        text = engine.format_count_dev(dev, engine.CountResult(pipe.out_keys, pipe.out_vals, ob, m, k))
+    else:
+        import numpy as np
+
+        # the generator's record table: syn<i> of 256 Mbp each (inputs.syn_numpy)
+        R = (pipe.n_bases + (256 << 20) - 1) // (256 << 20)
+        names = [b"syn%d" % i for i in range(R)]
+        off = np.concatenate([[0], np.cumsum([len(x) for x in names])]).astype(np.uint64)
+        p = engine.Parsed(dev, None, pipe.n_bases, R, None, np.arange(R, dtype=np.uint64) * np.uint64(256 << 20),
+                          names, b"".join(names), off)
+        text = engine.format_uniq_dev(p, engine.UniqResult(pipe.out_keys, pipe.out_vals, ob, m, k))
+    t1 = time.perf_counter()
+    with tempfile.NamedTemporaryFile(dir=os.environ.get("TMPDIR", "/tmp"), delete=True) as fh:
+        fh.write(text)
+        fh.flush()
+        os.fsync(fh.fileno())
+        t2 = time.perf_counter()
+    scale = pipe.n_out / m
+    return {"rows": m, "text_bytes": len(text), "format_ms": (t1 - t0) * 1e3 * scale,
+            "write_ms": (t2 - t1) * 1e3 * scale, "format_gbs": len(text) / (t1 - t0) / 1e9,
+            "write_gbs": len(text) / (t2 - t1) / 1e9,
+            "note": "device formatting (kman_format_*_dev) + D2H, then write+fsync, of the first %d of %d rows; "
+                    "ms scaled to all rows" % (m, pipe.n_out)}
+
+
+def file_to_file(k: int, nbases: int = 100_000_000):
+    """`kmer count IN OUT k` through the CLI on a bounded synthetic file."""
+    import inputs
+
+    with tempfile.TemporaryDirectory() as d:
+        src, out = os.path.join(d, "in.fa"), os.path.join(d, "out.txt")
+        with open(src, "wb") as fh:
+            fh.write(inputs.syn_numpy(nbases, 3))
+        t0 = time.perf_counter()
+        subprocess.run([sys.executable, "-m", "kman_amd", "count", src, out, str(k)], check=True, cwd=ROOT,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        s = time.perf_counter() - t0
+        size = os.path.getsize(out)
+    n = nbases - k + 1
+    return {"value": n / s, "unit": "k-mers/s", "seconds": s, "output_bytes": size,
+            "sample": "%d-base FASTA, `python -m kman_amd count` k=%d, process start to output file closed "
+                      "(includes interpreter + device init)" % (nbases, k)}
+
+
+def run_single(args):
+    import numpy as np  # noqa: F401
+    import inputs
+    from kman_amd import engine, shard
+
+    t0 = time.time()
+    text = inputs.syn_numpy(args.bases, 1)
+    log("generated %.2f GB FASTA in %.1f s" % (len(text) / 1e9, time.time() - t0))
+    dev = engine.Device(0)
+    pipe = engine.ResidentPipeline(dev, text, args.k, mode=args.mode, path=args.path)
+    fasta_bytes = len(text)
+    for _ in range(args.warmup):
+        pipe.step()
+    pipe.timing(True)
+    dev.sync()
+    t0 = time.perf_counter()
+    kmers = 0
+    for _ in range(args.steps):
+        kmers += pipe.step()
+    dev.sync()
+    elapsed = time.perf_counter() - t0
+    stages = {}
+    for tag in ("parse", "region_extract", "region_pass", "region_finish", "kmer_hist", "extract_pass", "extract",
+                "sort_hist", "sort_pass", "finish", "rle_count", "rle_uniq"):
+        c, ms = pipe.timed(tag)
+        if c:
+            stages[tag] = round(ms / args.steps, 3)
+    region = pipe.path == "region"
+    dom, sp = roofline(pipe, stages, args.steps, args.mode, args.k, args.bases) if region else (None, None)
+    out = {
+        "metric": METRIC, "value": kmers / elapsed, "unit": "k-mers/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+        "data": "synthetic (numpy PCG64 seed 1, uniform ACGT, 80 col), HBM-resident at the start of a step",
+        "config": {"workload": "%.2f GB synthetic FASTA, k=%d, extract+radix-sort+%s single batch"
+                               % (fasta_bytes / 1e9, args.k, args.mode),
+                   "fasta_bytes_per_gpu": fasta_bytes, "kmers_per_step_per_gpu": pipe.n_kmers, "k": args.k,
+                   "mode": args.mode, "parallelism": "single", "path": pipe.path, "stages_ms_per_step": stages},
+        "roofline": dom, "sort_pass_roofline": sp, "cpu_baseline": None,
+    }
+    pipe.timing(False)
+    if not args.quick:
+        try:
+            out["output"] = output_lines(dev, pipe, args.k, args.mode)
+        except Exception as e:  # reported, never fatal to the GPU number
+            out["output"] = {"error": repr(e)}
+    pipe.free()
+    if not args.quick:
+        # the same step from pinned host bytes (chunked H2D overlapping the parse)
+        rd = shard.PinnedReader(dev, text)
+        del text
+        try:
+            buf = dev.alloc(rd.size + 64)
+            t0 = time.perf_counter()
+            dev.upload(buf, rd.array)
+            h2d = time.perf_counter() - t0
+            buf.free()
+            sp_ = shard.StreamedPipeline(dev, rd, args.k, args.mode, chunk_bytes=args.chunk_mb << 20)
+            for _ in range(args.warmup):
+                sp_.step()
+            dev.sync()
+            t0 = time.perf_counter()
+            n = 0
+            for _ in range(args.steps):
+                n += sp_.step()
+            dev.sync()
+            el = time.perf_counter() - t0
+            sp_.free()
+            out["pinned_host"] = {"value": n / el, "unit": "k-mers/s", "ms_per_step": el / args.steps * 1e3,
+                                  "h2d_ms": h2d * 1e3, "h2d_gbs": rd.size / h2d / 1e9, "chunk_mb": args.chunk_mb,
+                                  "note": "step from pinned host bytes: %d MiB chunks copied on a copy stream behind "
+                                          "the parse of the previous chunk, then the region path; h2d_ms = one "
+                                          "plain copy of the whole text" % args.chunk_mb}
+        except Exception as e:
+            out["pinned_host"] = {"error": repr(e)}
+        finally:
+            rd.free()
+        try:
+            out["file_to_file"] = file_to_file(args.k)
+        except Exception as e:
+            out["file_to_file"] = {"error": repr(e)}
+    if not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.k, args.mode)
+        except Exception as e:  # reported, never fatal to the GPU number
+            out["cpu_baseline"] = {"error": repr(e)}
+    print(json.dumps(out), flush=True)
+    dev.close()
+
+
+def _rendezvous(rank: int, world: int) -> bytes:
+    """The 128-byte RCCL id through a file keyed by the launcher's port (one
+    node: every rank sees the same /tmp)."""
+    from kman_amd import dist
+
+    if world == 1:
+        return dist.unique_id()
+    path = os.path.join(tempfile.gettempdir(), "kman_rccl_id_%s_%s" % (os.environ.get("MASTER_PORT", "0"),
+                                                                      os.environ.get("TORCHELASTIC_RUN_ID", "")))
+    if rank == 0:
+        uid = dist.unique_id()
+        with open(path + ".tmp", "wb") as fh:
+            fh.write(uid)
+        os.replace(path + ".tmp", path)
+        return uid
+    t0 = time.time()
+    while not os.path.isfile(path):
+        if time.time() - t0 > 120:
+            raise RuntimeError("no RCCL id from rank 0 at %s" % path)
+        time.sleep(0.05)
+    with open(path, "rb") as fh:
+        return fh.read()
+
+
+def run_dist(args, world: int, rank: int, local: int):
+    import numpy as np
+    import inputs
+    from kman_amd import dist, engine, shard
+
+    dev = engine.Device(local)
+    per = int(args.shard_gb * 1e9) if args.shard_gb else args.bases
+    lay = inputs.SynthLayout(per * world, 1)
+    rd = shard.SynthReader(lay)
+    uid = _rendezvous(rank, world)
+    t0 = time.time()
+    pipe = dist.DistPipeline(dev, rd, args.k, args.mode, world, rank, uid, chunk_bytes=1 << 30)
+    log("rank %d: shard %d..%d (%.2f GB) generated + parsed on the device, setup %.1f s"
+        % (rank, pipe.spec.start, pipe.spec.own_end, (pipe.spec.own_end - pipe.spec.start) / 1e9, time.time() - t0))
+    comm = pipe.comm
+    for _ in range(args.warmup):
+        pipe.step()
+    pipe.timing(True)
+    comm.allreduce(np.zeros(1, np.uint64))  # barrier
+    dev.sync()
+    t0 = time.perf_counter()
+    kmers = 0
+    for _ in range(args.steps):
+        kmers += pipe.step()
+    dev.sync()
+    elapsed = time.perf_counter() - t0
+    el = comm.allgather(np.array([int(elapsed * 1e9)], np.uint64))
+    tot = comm.allreduce(np.array([kmers], np.uint64))
+    elapsed, total = float(el.max()) / 1e9, int(tot[0])
+    stages = {}
+    for tag in ("parse", "shard_hist", "region_extract", "region_pass", "region_pass1b", "region_finish",
+                "extract", "sort_pass", "finish"):
+        c, ms = pipe.timed(tag)
+        if c:
+            stages[tag] = round(ms / args.steps, 3)
+    n_pass, pass_ms = pipe.timed("region_pass")
+    if rank == 0:
+        avg = pass_ms / max(n_pass, 1) / 1e3
+        ach = 16.0 * pipe.n_recv / max(n_pass // args.steps, 1) / avg / 1e9 if n_pass else None
+        out = {
+            "metric": METRIC, "value": total / elapsed, "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u64",
+            "data": "synthetic: ONE global FASTA (kman_synth_fasta seed 1, uniform ACGT, 80 col) of %d x %.2f GB, "
+                    "byte-range sharded, each rank's bytes generated in its HBM" % (world, per / 1e9),
+            "config": {"workload": "%.2f GB synthetic FASTA in %d byte-range shards, k=%d, extract+radix-sort+%s, "
+                                   "key rounds + one RCCL all-to-all per round" % (lay.size / 1e9, world, args.k,
+                                                                                    args.mode),
+                       "fasta_bytes": lay.size, "kmers_per_step": total // max(args.steps, 1), "k": args.k,
+                       "mode": args.mode, "parallelism": "dp%d: top-8-bit bucket parts + RCCL all-to-all" % world,
+                       "path": pipe.path, "rounds": pipe.rounds, "fallback_rounds": pipe.fallback_rounds,
+                       "stages_ms_per_step_rank0": stages},
+            "roofline": {"kernel": "rg_pass (pass 1 after the exchange, rank 0)", "bound": "hbm", "achieved": ach,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS if ach else None,
+                         "traffic": None, "avg_launch_ms": avg * 1e3},
+            "cpu_baseline": None,
+        }
+        print(json.dumps(out), flush=True)
+    pipe.free()
+    dev.close()
 
 
 def main() -> None:
@@ -80,145 +378,22 @@ def main() -> None:
     ap.add_argument("--k", type=int, default=21)
     ap.add_argument("--mode", choices=["uniq", "count"], default="uniq")
     ap.add_argument("--bases", type=int, default=1_000_000_000, help="synthetic bases per GPU (1 GB FASTA)")
+    ap.add_argument("--shard-gb", type=float, default=None, help="FASTA GB per rank on the multi-GPU path "
+                                                                 "(12.5 = BASELINE config 4's shape)")
+    ap.add_argument("--chunk-mb", type=int, default=128, help="chunk size of the pinned-host line")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--quick", action="store_true", help="HBM-resident line only (profiling runs)")
     ap.add_argument("--path", choices=["region", "split", "full"], default="region",
-                    help="engine path (region falls back to split outside its domain)")
+                    help="single-GPU engine path (region falls back to split outside its domain)")
     ap.add_argument("--dist", action="store_true", help="run the multi-GPU pipeline even at world size 1")
     args = ap.parse_args()
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist  # gloo, host-side barrier / max only
-
-        dist.init_process_group("gloo")
-
-    import inputs
-    from kman_amd import engine
-
-    t0 = time.time()
-    text = inputs.syn_numpy(args.bases, 1 + rank)
-    log("rank %d: generated %.2f GB FASTA in %.1f s" % (rank, len(text) / 1e9, time.time() - t0))
-    dev = engine.Device(local)
     if world > 1 or args.dist:
-        # region path across ranks: one RCCL all-to-all of packed items over
-        # xGMI (kman_amd/dist.py), prefix-range path as the fallback
-        from kman_amd import dist as kd
-
-        uid = [kd.unique_id() if rank == 0 else None]
-        if dist:
-            dist.broadcast_object_list(uid, src=0)
-        pipe = kd.DistPipeline(dev, text, args.k, args.mode, world, rank, uid[0],
-                               path="split" if args.path == "split" else "region")
+        run_dist(args, world, rank, local)
     else:
-        pipe = engine.ResidentPipeline(dev, text, args.k, mode=args.mode, path=args.path)
-    fasta_bytes = len(text)
-    del text
-
-    for _ in range(args.warmup):
-        pipe.step()
-    pipe.timing(True)
-    if dist:
-        dist.barrier()
-    dev.sync()
-    t0 = time.perf_counter()
-    kmers = 0
-    for _ in range(args.steps):
-        kmers += pipe.step()
-    dev.sync()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    if dist:
-        import torch
-
-        t = torch.tensor([elapsed, float(kmers)], dtype=torch.float64)
-        mx = t.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = t.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        elapsed, total_kmers = float(mx[0]), float(sm[1])
-    else:
-        total_kmers = float(kmers)
-
-    # live roofline of the dominant kernel (the digit pass), from HIP events
-    # recorded on the engine's own stream around every launch
-    region = getattr(pipe, "path", "split") == "region"
-    n_pass, pass_ms = pipe.timed("region_pass" if region else "sort_pass")
-    stages = {}
-    for tag in ("parse", "region_extract", "dist_gather", "region_pass", "region_pass1b", "region_finish", "kmer_hist",
-                "extract_pass", "extract",
-                "prefix_hist", "partition", "sort_hist", "sort_pass", "finish", "rle_count", "rle_uniq"):
-        c, ms = pipe.timed(tag)
-        if c:
-            stages[tag] = round(ms / args.steps, 3)
-    avg_pass_s = pass_ms / n_pass / 1e3
-    # region path: one packed u64 item read + written per k-mer; LSD path: the
-    # key read + written, plus the pos payload read + written (uniq)
-    bytes_per_key = 16 if region else 16 + (2 * pipe.pos_bytes if args.mode == "uniq" else 0)
-    achieved = bytes_per_key * pipe.n_sorted / avg_pass_s / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_sort_pass.json")
-    if os.path.isfile(pmc):
-        with open(pmc) as fh:
-            p = json.load(fh)
-        if (p.get("mode") == args.mode and p.get("k") == args.k and p.get("bases") == args.bases
-                and p.get("kernel", "onesweep_pass") == ("rg_pass" if region else "onesweep_pass")):
-            traffic = p.get("hbm_bytes_per_launch")
-
-    if rank != 0:
-        if dist:
-            dist.destroy_process_group()
-        return
-    out = {
-        "metric": METRIC,
-        "value": total_kmers / elapsed,
-        "unit": "k-mers/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "u64",
-        "data": "synthetic (numpy PCG64 seed 1+rank, uniform ACGT, 80 col)",
-        "config": {
-            "workload": "%.2f GB synthetic FASTA per GPU, k=%d, extract+radix-sort+%s single batch"
-                        % (fasta_bytes / 1e9, args.k, args.mode),
-            "fasta_bytes_per_gpu": fasta_bytes,
-            "kmers_per_step_per_gpu": pipe.n_kmers,
-            "k": args.k,
-            "mode": args.mode,
-            "parallelism": ("dp%d: top-8-bit bucket ranges + one RCCL all-to-all" % world
-                            if world > 1 or args.dist else "single"),
-            "path": getattr(pipe, "path", "dist"),
-            "stages_ms_per_step": stages,
-        },
-        "roofline": {
-            "kernel": ("rg_pass (per-bucket MSD digit pass over packed u64 items, %d per step)" if region else
-                       "onesweep_pass (LSD digit pass, %d per step)") % (n_pass // args.steps),
-            "bound": "hbm",
-            "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
-            "traffic": traffic,
-            "algorithmic_bytes_per_key": bytes_per_key,
-            "avg_launch_ms": avg_pass_s * 1e3,
-        },
-        "cpu_baseline": None,
-    }
-    if world == 1 and not args.no_cpu_baseline:
-        try:
-            out["cpu_baseline"] = cpu_baseline(args.k, args.mode)
-        except Exception as e:  # reported, never fatal to the GPU number
-            out["cpu_baseline"] = {"error": repr(e)}
-    print(json.dumps(out), flush=True)
-    pipe.free()
-    if dist:
-        dist.destroy_process_group()
+        run_single(args)
 
 
 if __name__ == "__main__":

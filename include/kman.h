@@ -106,6 +106,13 @@ int kman_host_free(kman_ctx *ctx, void *hptr);
 int kman_memcpy_h2d(kman_ctx *ctx, void *dst, const void *src, size_t bytes);
 int kman_memcpy_d2h(kman_ctx *ctx, void *dst, const void *src, size_t bytes);
 int kman_memset(kman_ctx *ctx, void *dst, int value, size_t bytes);
+/* Chunked uploads that overlap the context's work: kman_copy_h2d_async
+ * enqueues a copy (from pinned memory for real overlap) on the context's copy
+ * stream and marks event `slot` (0..3); kman_copy_wait makes the work stream
+ * wait for that event; kman_copy_sync drains the copy stream. */
+int kman_copy_h2d_async(kman_ctx *ctx, void *dst, const void *src, size_t bytes, int slot);
+int kman_copy_wait(kman_ctx *ctx, int slot);
+int kman_copy_sync(kman_ctx *ctx);
 
 /* ------------------------------------------------------------------- timing
  * Optional per-kernel timing with HIP events recorded on the context's own
@@ -130,6 +137,18 @@ int kman_timing_query(kman_ctx *ctx, const char *tag, uint64_t *launches, double
 int kman_parse_fasta(kman_ctx *ctx, const uint8_t *d_text, uint64_t n_bytes, uint8_t *d_codes,
                      uint64_t *d_rec_hdr, uint64_t *d_rec_seq, uint64_t rec_cap,
                      kman_parse_info *info);
+/* One chunk of a FASTA parsed into d_codes from code_off on (chunked H2D
+ * streams and byte-range shards, kman_amd/shard.py).  The chunk starts at a
+ * line start; flags KMAN_PARSE_IN_RECORD: the chunk continues a record (its
+ * leading lines are sequence lines of the record opened before it; it may
+ * hold no header, or nothing at all).  d_rec_seq entries and the 64 pad bytes
+ * are at code_off + the chunk's own indices; d_rec_hdr holds byte offsets
+ * within the chunk.  d_text and d_codes 16-byte aligned (code_off need not
+ * be). */
+#define KMAN_PARSE_IN_RECORD 1u
+int kman_parse_fasta_at(kman_ctx *ctx, const uint8_t *d_text, uint64_t n_bytes, uint32_t flags, uint8_t *d_codes,
+                        uint64_t code_off, uint64_t *d_rec_hdr, uint64_t *d_rec_seq, uint64_t rec_cap,
+                        kman_parse_info *info);
 
 /* Number of k-mers kman_extract will emit (valid windows x (RC ? 2 : 1)). */
 int kman_count_kmers(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k,
@@ -230,35 +249,47 @@ int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_
                 void *d_work, uint64_t work_bytes, uint64_t *d_okeys, void *d_ovals, uint32_t oval_bytes,
                 uint64_t *n_kmers, uint64_t *n_out);
 
-/* kman_groups across G ranks (one process per GPU; kman_amd/dist.py runs the
- * collectives in between).  Every rank passes the same
- * n_bases_q >= every rank's n_bases (it fixes the pos bits of the packed
- * items) and the same world.
- *   kman_dgroups_plan     work-area bytes, or KMAN_EFALLBACK outside the path
- *   kman_dgroups_extract  pass 0 of the rank's shard; all its packed items
- *                         compacted into d_send (>= n_bases x (RC ? 2 : 1)
- *                         u64) in bucket order; bucket_counts[256] (host) =
- *                         items per top-8-bit bucket; *overflow = 1 when a
- *                         region overflowed (the ranks then fall back together)
- *   (caller)              all-reduce of the bucket counts, contiguous bucket
- *                         ranges per rank, all-gather of the counts, one
- *                         all-to-all of the items (kman_alltoallv, 8 B)
- *   kman_dgroups_finish   the received items of buckets [b_lo, b_lo + nb)
- *                         (source chunks in rank order, each in bucket order;
- *                         counts[src * nb + j] = items of bucket b_lo + j from
- *                         src) -> this rank's count / uniq output, ascending
- *                         (uniq pos u64 with the source rank in bits 56-63);
- *                         KMAN_EFALLBACK on a region overflow.
- * The ranks' outputs in rank order are the global output (join.py:95-130). */
-int kman_dgroups_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t flags, int mode, uint32_t world,
-                      uint64_t *work_bytes);
-int kman_dgroups_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint64_t n_bases_q, uint32_t k,
-                         uint32_t flags, int mode, uint32_t world, void *d_work, uint64_t work_bytes,
-                         uint64_t *d_send, uint64_t *bucket_counts, uint32_t *overflow);
-int kman_dgroups_finish(kman_ctx *ctx, const uint64_t *d_recv, uint64_t n_bases, uint64_t n_bases_q, uint32_t k,
-                        uint32_t flags, int mode, uint32_t world, uint32_t b_lo, uint32_t nb,
-                        const uint64_t *counts, void *d_work, uint64_t work_bytes, uint64_t *d_okeys,
-                        void *d_ovals, uint32_t oval_bytes, uint64_t *n_out);
+/* kman_groups across G ranks, in key rounds (one process per GPU over RCCL;
+ * kman_amd/dist.py runs the collectives in between).  Rank q
+ * holds one byte-range shard of ONE FASTA (its own bytes plus a (k-1)-base
+ * halo, see kman_parse_fasta_at); every rank passes the same n_bases_q >=
+ * every shard's n_bases (it fixes the pos bits of the packed 8-byte items).
+ *   kman_dshard_plan     KMAN_OK, or KMAN_EFALLBACK outside the path (k > 25,
+ *                        uniq pos bits + 2k - 8 > 64)
+ *   kman_dshard_hist     exact item counts of the shard per (top-8-bit
+ *                        bucket b, position segment s): hist[b * 64 + s]
+ *                        (host copy of d_hist, 256 x 64 u32)
+ *   (caller)             all-gather of the bucket totals; buckets cut into
+ *                        G x R contiguous parts: rank q owns parts q*R ..
+ *                        q*R+R-1, round r handles part q*R+r of every q
+ *   kman_dshard_extract  one round's pass 0: the items of the buckets with
+ *                        d_rtab[b * 64 + s] != ~0 written straight into
+ *                        d_send, region (b, s) at d_rtab[b * 64 + s]
+ *                        (destination-major, no padding, no gather)
+ *   (caller)             one all-to-all of the items (kman_alltoallv, 8 B)
+ *   kman_dround_plan     arena sizes of one round's finish on a rank
+ *   kman_dround_finish   the received items of buckets [b_lo, b_lo + nb)
+ *                        (source chunks in rank order, each in bucket order;
+ *                        counts[src * nb + j] = items of bucket b_lo + j from
+ *                        src) -> the round's count / uniq rows, ascending
+ *                        (uniq pos u64 with the source rank in bits 56-63);
+ *                        KMAN_EFALLBACK on a region overflow (skewed keys).
+ *                        d_a (>= a_bytes) may be the send buffer, d_b (>=
+ *                        b_bytes) may be d_recv itself.
+ * A rank's rounds emit its key range in order; the ranks' outputs in rank
+ * order are the global output (Crawler.do_records / do_batch over all
+ * batches, join.py:63-130). */
+int kman_dshard_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t flags, int mode);
+int kman_dshard_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint64_t n_bases_q, uint32_t k,
+                     uint32_t flags, int mode, uint32_t *d_hist, uint32_t *hist);
+int kman_dshard_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint64_t n_bases_q, uint32_t k,
+                        uint32_t flags, int mode, const uint32_t *d_hist, const uint64_t *d_rtab, uint64_t *d_send);
+int kman_dround_plan(uint32_t k, uint32_t flags, int mode, uint32_t world, uint64_t n_bases_q, uint32_t nb,
+                     const uint64_t *counts, uint64_t *a_bytes, uint64_t *b_bytes);
+int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_t k, uint32_t flags, int mode, uint32_t world,
+                       uint64_t n_bases_q, uint32_t b_lo, uint32_t nb, const uint64_t *counts, void *d_a,
+                       uint64_t a_bytes, void *d_b, uint64_t b_bytes, uint64_t *d_okeys, void *d_ovals,
+                       uint32_t oval_bytes, uint64_t *n_out);
 
 /* Abundance spectrum of a count output (BASELINE config 5; not
  * in the reference): d_hist[c] = number of distinct k-mers seen c times, the
@@ -315,6 +346,18 @@ int kman_tag_batches(kman_ctx *ctx, uint64_t *d_keys, uint64_t n, uint32_t key_b
 int kman_or_u64(kman_ctx *ctx, uint64_t *d_v, uint64_t n, uint64_t value);
 int kman_widen_u32(kman_ctx *ctx, const uint32_t *d_in, uint64_t *d_out, uint64_t n, uint64_t value);
 int kman_memcpy_d2d(kman_ctx *ctx, void *dst, const void *src, size_t bytes);
+/* kman_rebase_pos: uniq pos tagged with their source shard (bits 56-63) ->
+ *   global pos: (pos & (2^56 - 1)) + (offsets[source] << 1), offsets = the
+ *   global base index of each shard's first base (host array, nsrc <= 256).
+ * kman_synth_fasta: bytes [byte_lo, byte_lo + n_bytes) of the synthetic
+ *   benchmark FASTA into d_out (16-byte aligned): records r = 0.. with header
+ *   ">syn<r>\n" at byte rec_tab[3r], first base index rec_tab[3r + 1] and
+ *   rec_tab[3r + 2] bases in lines of `line` bases + "\n"; base i of the file
+ *   = "ACGT"[splitmix64(seed * 0xD1B54A32D192ED03 + i) >> 62] (the same
+ *   generator as tests/golden/inputs.py synth_np). */
+int kman_rebase_pos(kman_ctx *ctx, uint64_t *d_pos, uint64_t n, const uint64_t *offsets, uint32_t nsrc);
+int kman_synth_fasta(kman_ctx *ctx, uint8_t *d_out, uint64_t byte_lo, uint64_t n_bytes, uint64_t seed,
+                     const uint64_t *rec_tab, uint32_t n_records, uint32_t line);
 
 /* ------------------------------------------------------------- formatting
  * Host-side writers that produce the reference's exact bytes.  They run on

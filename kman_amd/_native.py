@@ -35,6 +35,7 @@ KMAN_CANONICAL = 4
 KMAN_FINISH_SORT = 0
 KMAN_FINISH_COUNT = 1
 KMAN_FINISH_UNIQ = 2
+KMAN_PARSE_IN_RECORD = 1
 
 
 def KMAN_HIST_LO(b: int) -> int:
@@ -116,16 +117,18 @@ SIGNATURES = {
         [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_int, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32,
          POINTER(c_uint64), POINTER(c_uint64)],
     ),
-    "kman_dgroups_plan": (c_int, [c_uint64, c_uint64, c_uint32, c_uint32, c_int, c_uint32, POINTER(c_uint64)]),
-    "kman_dgroups_extract": (
-        c_int,
-        [c_void_p, c_void_p, c_uint64, c_uint64, c_uint32, c_uint32, c_int, c_uint32, c_void_p, c_uint64, c_void_p,
-         c_void_p, POINTER(c_uint32)],
+    "kman_dshard_plan": (c_int, [c_uint64, c_uint64, c_uint32, c_uint32, c_int]),
+    "kman_dshard_hist": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_uint32, c_uint32, c_int, c_void_p, c_void_p]),
+    "kman_dshard_extract": (
+        c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_uint32, c_uint32, c_int, c_void_p, c_void_p, c_void_p],
     ),
-    "kman_dgroups_finish": (
+    "kman_dround_plan": (
+        c_int, [c_uint32, c_uint32, c_int, c_uint32, c_uint64, c_uint32, c_void_p, POINTER(c_uint64), POINTER(c_uint64)],
+    ),
+    "kman_dround_finish": (
         c_int,
-        [c_void_p, c_void_p, c_uint64, c_uint64, c_uint32, c_uint32, c_int, c_uint32, c_uint32, c_uint32, c_void_p,
-         c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, POINTER(c_uint64)],
+        [c_void_p, c_void_p, c_uint32, c_uint32, c_int, c_uint32, c_uint64, c_uint32, c_uint32, c_void_p, c_void_p,
+         c_uint64, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, POINTER(c_uint64)],
     ),
     "kman_count_hist": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_uint32]),
     "kman_rle_count": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, POINTER(c_uint64)]),
@@ -149,6 +152,14 @@ SIGNATURES = {
     "kman_or_u64": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64]),
     "kman_widen_u32": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_uint64]),
     "kman_memcpy_d2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+    "kman_rebase_pos": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_uint32]),
+    "kman_synth_fasta": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32]),
+    "kman_copy_h2d_async": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int]),
+    "kman_copy_wait": (c_int, [c_void_p, c_int]),
+    "kman_copy_sync": (c_int, [c_void_p]),
+    "kman_parse_fasta_at": (
+        c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p],
+    ),
     "kman_format_count": (
         c_int,
         [c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_size_t, POINTER(c_size_t), c_int],

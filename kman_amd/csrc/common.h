@@ -49,6 +49,9 @@ struct kman_ctx {
     // lane order on this device (observed on gfx950, not architectural); the
     // sort uses atomic ranking only when true
     bool lds_atomic_ordered = false;
+    // H2D copies that overlap the work of `stream` (chunked FASTA uploads)
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t copy_ev[4] = {nullptr, nullptr, nullptr, nullptr};
 };
 
 // RAII launch timer: records an event pair around the launches in its scope.

@@ -320,7 +320,8 @@ __global__ __launch_bounds__(SCAN_T) void parse_scan_blocks(const Xf64 *__restri
 // Level 2 (one block): exclusive prefixes of the block totals, and the file
 // totals (n_bases, n_records).
 __global__ __launch_bounds__(SCAN_T) void parse_scan_top(const Xf64 *__restrict__ btot, uint64_t NB,
-                                                         Xf64 *__restrict__ bpre, uint64_t *__restrict__ info) {
+                                                         Xf64 *__restrict__ bpre, uint64_t *__restrict__ info,
+                                                         uint32_t s0) {
     __shared__ Xf64 lds[SCAN_T / 64];
     const Xf64 id = xf64_id();
     ComposeXf64 op;
@@ -334,14 +335,14 @@ __global__ __launch_bounds__(SCAN_T) void parse_scan_top(const Xf64 *__restrict_
         carry = op(carry, tot);
     }
     if (threadIdx.x == 0) {
-        info[0] = carry.kept[S_PRE];  // n_bases
+        info[0] = s0 == S_PRE ? carry.kept[S_PRE] : carry.kept[S_SEQ];  // n_bases
         info[1] = carry.nhdr;         // n_records
     }
 }
 
 __global__ __launch_bounds__(PT, 3) void parse_emit(const uint8_t *__restrict__ text, uint64_t n,
                                                  const Xf64 *__restrict__ local, const Xf64 *__restrict__ bpre,
-                                                 uint8_t *__restrict__ codes,
+                                                 uint8_t *__restrict__ codes, uint64_t code_off, uint32_t s0,
                                                  uint64_t *__restrict__ rec_hdr, uint64_t *__restrict__ rec_seq) {
     __shared__ Xf lds[PT / 64];
     __shared__ __attribute__((aligned(16))) uint8_t stage[PTILE + 32];
@@ -359,8 +360,8 @@ __global__ __launch_bounds__(PT, 3) void parse_emit(const uint8_t *__restrict__ 
     TileIn ti;
     {
         const Xf64 p = ComposeXf64()(bpre[blockIdx.x / SCAN_T], local[blockIdx.x]);
-        ti.state = xf_out(p.outs, S_PRE);
-        ti.kept = p.kept[S_PRE];
+        ti.state = xf_out(p.outs, s0);
+        ti.kept = s0 == S_PRE ? p.kept[S_PRE] : p.kept[S_SEQ];
         ti.nhdr = p.nhdr;
     }
     const uint32_t s = xf_out(pre.outs, ti.state);  // state entering this thread's chunk
@@ -374,12 +375,13 @@ __global__ __launch_bounds__(PT, 3) void parse_emit(const uint8_t *__restrict__ 
         for (uint64_t m = ch.hls; m; m &= m - 1) {
             const int h = __ffsll((unsigned long long)m) - 1;
             rec_hdr[nh] = pos + h;
-            rec_seq[nh] = ti.kept + lk0 + __popcll(em & bits_below(h));
+            rec_seq[nh] = code_off + ti.kept + lk0 + __popcll(em & bits_below(h));
             nh++;
         }
     }
     // codes staged at the tile's output alignment, so LDS and HBM agree mod 16
-    const uint32_t al = (uint32_t)(ti.kept & 15u);
+    // (codes holds 16-byte aligned memory; this call writes from code_off on)
+    const uint32_t al = (uint32_t)((code_off + ti.kept) & 15u);
     uint32_t cw[PB / 4];
 #pragma unroll
     for (int v = 0; v < PB / 4; v++) cw[v] = codes4(ch.w[v]);
@@ -396,7 +398,7 @@ __global__ __launch_bounds__(PT, 3) void parse_emit(const uint8_t *__restrict__ 
     __syncthreads();
     // [al, al + tile_kept) of stage -> codes + ti.kept: whole 16-byte words as
     // vectors, the two partial end words (shared with the neighbour tiles) bytewise
-    uint8_t *dst = codes + (ti.kept - al);
+    uint8_t *dst = codes + (code_off + ti.kept - al);
     const uint32_t end = al + tile_kept;
     const uint32_t nwords = (end + 15) / 16;
     for (uint32_t q = threadIdx.x; q < nwords; q += PT) {
@@ -425,9 +427,21 @@ __global__ void mark_records(uint8_t *__restrict__ codes, const uint64_t *__rest
 extern "C" int kman_parse_fasta(kman_ctx *ctx, const uint8_t *d_text, uint64_t n_bytes, uint8_t *d_codes,
                                 uint64_t *d_rec_hdr, uint64_t *d_rec_seq, uint64_t rec_cap,
                                 kman_parse_info *info) {
+    return kman_parse_fasta_at(ctx, d_text, n_bytes, 0, d_codes, 0, d_rec_hdr, d_rec_seq, rec_cap, info);
+}
+
+extern "C" int kman_parse_fasta_at(kman_ctx *ctx, const uint8_t *d_text, uint64_t n_bytes, uint32_t flags,
+                                   uint8_t *d_codes, uint64_t code_off, uint64_t *d_rec_hdr, uint64_t *d_rec_seq,
+                                   uint64_t rec_cap, kman_parse_info *info) {
     if (!ctx || !info) return KMAN_EINVAL;
+    info->n_bases = info->n_records = 0;
+    const bool cont = flags & KMAN_PARSE_IN_RECORD;
+    // a continuation chunk (inside a record) may be empty or hold no header
+    if (cont && n_bytes == 0) return KMAN_OK;
     if (n_bytes && (!d_text || !d_codes)) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
     if (((uintptr_t)d_text & 15) != 0) return kman_fail(ctx, KMAN_EINVAL, "text must be 16-byte aligned");
+    if (((uintptr_t)d_codes & 15) != 0) return kman_fail(ctx, KMAN_EINVAL, "codes must be 16-byte aligned");
+    const uint32_t s0 = cont ? S_SEQ : S_PRE;
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     const uint64_t T = n_bytes ? ceil_div(n_bytes, PTILE) : 0;
     if (T == 0) return kman_fail(ctx, KMAN_EFORMAT, "premature end of file or empty file");
@@ -446,23 +460,24 @@ extern "C" int kman_parse_fasta(kman_ctx *ctx, const uint8_t *d_text, uint64_t n
     { KTimer kt_(ctx, "parse");
     hipLaunchKernelGGL(parse_reduce, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf);
     hipLaunchKernelGGL(parse_scan_blocks, dim3((uint32_t)NB), dim3(SCAN_T), 0, ctx->stream, d_xf, T, d_local, d_btot);
-    hipLaunchKernelGGL(parse_scan_top, dim3(1), dim3(SCAN_T), 0, ctx->stream, d_btot, NB, d_bpre, d_info); }
+    hipLaunchKernelGGL(parse_scan_top, dim3(1), dim3(SCAN_T), 0, ctx->stream, d_btot, NB, d_bpre, d_info, s0); }
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small, d_info, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     info->n_bases = ctx->h_small[0];
     info->n_records = ctx->h_small[1];
-    if (info->n_records == 0) return kman_fail(ctx, KMAN_EFORMAT, "premature end of file or empty file");
+    if (info->n_records == 0 && !cont) return kman_fail(ctx, KMAN_EFORMAT, "premature end of file or empty file");
     if (info->n_records > rec_cap)
         return kman_fail(ctx, KMAN_ECAP, "record capacity %llu < %llu", (unsigned long long)rec_cap,
                          (unsigned long long)info->n_records);
     { KTimer kt_(ctx, "parse");
     hipLaunchKernelGGL(parse_emit, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_local, d_bpre, d_codes,
-                       d_rec_hdr, d_rec_seq);
+                       code_off, s0, d_rec_hdr, d_rec_seq);
     const uint64_t R = info->n_records;
-    hipLaunchKernelGGL(mark_records, dim3((uint32_t)ceil_div(R, 256)), dim3(256), 0, ctx->stream, d_codes,
-                       d_rec_seq, R, info->n_bases); }
+    if (R)
+        hipLaunchKernelGGL(mark_records, dim3((uint32_t)ceil_div(R, 256)), dim3(256), 0, ctx->stream, d_codes,
+                           d_rec_seq, R, code_off + info->n_bases); }
     HIP_TRY(ctx, hipGetLastError());
-    HIP_TRY(ctx, hipMemsetAsync(d_codes + info->n_bases, 4, 64, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(d_codes + code_off + info->n_bases, 4, 64, ctx->stream));
     return KMAN_OK;
 }

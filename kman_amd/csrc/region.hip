@@ -95,13 +95,17 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 // LDS-staged coalesced scatter into region (b, s).
 // BR: rank by one block-wide LDS atomic per item (unstable inside a tile;
 // nothing downstream needs the order of a region's items).
-template <int EI, bool RC, bool ATOMIC, bool CANON = false, bool BR = false>
+// EX (the multi-GPU shard path, kman_dshard_extract): no padded regions --
+// region (b, s) is written at rtab[b * RS + s] (exact sizes from rg_hist, in
+// cnt0, which is then read-only); buckets with rtab == ~0 are not kept this
+// round, and their windows are dropped before the rank (keep bitmap).
+template <int EI, bool RC, bool ATOMIC, bool CANON = false, bool BR = false, bool EX = false>
 __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI == 8 ? 8 : 4)))) void rg_extract(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
                                                  uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
                                                  uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ cnt0,
                                                  uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
                                                  uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg,
-                                                 uint64_t *__restrict__ stp) {
+                                                 uint64_t *__restrict__ stp, const uint64_t *__restrict__ rtab = nullptr) {
     constexpr int NT = RT;
     constexpr int NWAVE = NT / 64;
     constexpr int WIN = NT * EI;
@@ -115,6 +119,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     __shared__ uint64_t gexcl[RADIX];
     __shared__ uint32_t lds_scan[NWAVE];
     __shared__ uint32_t lds_tile;
+    __shared__ uint32_t keep[EX ? RADIX / 32 : 1];
 
     const uint32_t cid = (uint32_t)grab_tile(counter, &lds_tile);
     const uint32_t sgi = cid % RS, jj = cid / RS;
@@ -136,6 +141,11 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     if (!BR)
         for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&whist[0][0])[i] = 0;
     if (threadIdx.x < RADIX) thist[threadIdx.x] = 0;
+    if (EX && threadIdx.x < RADIX / 32) {
+        uint32_t m = 0;
+        for (int b = 0; b < 32; b++) m |= (uint32_t)(rtab[(uint64_t)(threadIdx.x * 32 + b) * RS + sgi] != ~0ull) << b;
+        keep[threadIdx.x] = m;
+    }
     __syncthreads();
     RSTAMP(tile, 1);
 
@@ -143,18 +153,27 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     const uint32_t w0 = threadIdx.x * EI;
     // (CANON: kf = min(forward, reverse complement), one key per window)
     const uint32_t valid = roll<EI, CANON>(scodes, w0, k, keymask, wb + w0, n_bases, kf, kr);
+    uint32_t vf = valid, vr = RC ? valid : 0u;
+    if (EX) {  // only the buckets kept this round
+#pragma unroll
+        for (int j = 0; j < EI; j++) {
+            const uint32_t df = (uint32_t)(kf[j] >> shift);
+            vf &= ~((uint32_t)!((keep[df >> 5] >> (df & 31)) & 1u) << j);
+            if (RC) {
+                const uint32_t dr = (uint32_t)(kr[j] >> shift);
+                vr &= ~((uint32_t)!((keep[dr >> 5] >> (dr & 31)) & 1u) << j);
+            }
+        }
+    }
     uint32_t tcnt;
-    const uint32_t off = block_exclusive_scan<NT>((uint32_t)__popc(valid) * (RC ? 2u : 1u), SumU32(), 0u, lds_scan,
-                                                  &tcnt);
+    const uint32_t off = block_exclusive_scan<NT>((uint32_t)(__popc(vf) + __popc(vr)), SumU32(), 0u, lds_scan, &tcnt);
     {
         uint32_t o = off;
 #pragma unroll
         for (int j = 0; j < EI; j++) {
-            if ((valid >> j) & 1u) {
-                const uint64_t tag = (uint64_t)((w0 + j) << 1) << kb;
-                skeys[o++] = kf[j] | tag;
-                if (RC) skeys[o++] = kr[j] | tag | (1ull << kb);
-            }
+            const uint64_t tag = (uint64_t)((w0 + j) << 1) << kb;
+            if ((vf >> j) & 1u) skeys[o++] = kf[j] | tag;
+            if (RC && ((vr >> j) & 1u)) skeys[o++] = kr[j] | tag | (1ull << kb);
         }
     }
     __syncthreads();
@@ -223,10 +242,18 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
                 (dbg & 1) ? 0ull  // timing ablation only: no look-back (wrong offsets)
                           : group_lookback<TPD>(status + d, tile, first, thist[d], epoch, err);
             if (threadIdx.x % TPD == 0) {
-                gexcl[d] = excl;
                 const uint64_t incl = excl + thist[d];
-                if (incl > C0) atomicOr(err, ERR_REGION);
-                if (tile == (int64_t)t1 - 1) cnt0[d * RS + sgi] = (uint32_t)(incl < C0 ? incl : C0);
+                if (EX) {
+                    // exact region: base from the table, size from rg_hist
+                    const uint64_t rb = rtab[(uint64_t)d * RS + sgi];
+                    const bool over = incl > cnt0[d * RS + sgi];
+                    if (over && rb != ~0ull) atomicOr(err, ERR_REGION);  // (the input changed under the plan)
+                    gexcl[d] = rb == ~0ull || over ? ~0ull : rb + excl;
+                } else {
+                    gexcl[d] = excl;
+                    if (incl > C0) atomicOr(err, ERR_REGION);
+                    if (tile == (int64_t)t1 - 1) cnt0[d * RS + sgi] = (uint32_t)(incl < C0 ? incl : C0);
+                }
             }
         }
     }
@@ -240,11 +267,14 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
             const uint64_t kk = skeys[q];
             const uint32_t d = XDIGIT(kk);
             const uint64_t at = gexcl[d] + (q - lstart[d]);
-            if (at < C0) {
-                const uint64_t f = kk >> kb;  // tile-local (window << 1 | strand)
-                const uint64_t win = wb + (f >> 1);
-                const uint64_t idx = RC ? ((win << 1) | (f & 1u)) : win;
-                out[((uint64_t)d * RS + sgi) * C0 + at] = Q ? (((kk & restmask) << Q) | idx) : (kk & restmask);
+            const uint64_t f = kk >> kb;  // tile-local (window << 1 | strand)
+            const uint64_t win = wb + (f >> 1);
+            const uint64_t idx = RC ? ((win << 1) | (f & 1u)) : win;
+            const uint64_t v = Q ? (((kk & restmask) << Q) | idx) : (kk & restmask);
+            if (EX) {
+                if (gexcl[d] != ~0ull) out[at] = v;
+            } else if (at < C0) {
+                out[((uint64_t)d * RS + sgi) * C0 + at] = v;
             }
         }
     }
@@ -1207,210 +1237,306 @@ int rg_check(kman_ctx *ctx, const char *what, const uint32_t *cnt = nullptr, uin
 }  // namespace
 
 // =============================================================== N > 1
-// The region path across G ranks (one process per GPU; kman_amd/dist.py
-// drives the collectives between the calls):
-//   kman_dgroups_extract  pass 0 on the rank's shard, then every region
-//                         compacted into the send buffer in (bucket, segment)
-//                         order; per-bucket counts to the host
-//   (host)                all-reduce of the bucket counts -> contiguous bucket
-//                         ranges per rank; all-gather of the counts; one
-//                         all-to-all of the packed items (RCCL, xGMI)
-//   kman_dgroups_finish   per (bucket, source) chain: pass 1 by 9 bits into
-//                         sub-regions (b, d, src); pass 1b per (b, d) by g =
-//                         ceil(log2 G) more bits, tagging each item with its
-//                         source rank (in the d field, implied from here);
-//                         then the LDS finish.  Output keys of the rank's
-//                         bucket range, ascending, so the ranks' outputs in
-//                         rank order are the global output; uniq pos carry the
-//                         source rank in bits 56-63.
+// The region path across G ranks, in key rounds (one process per GPU;
+// kman_amd/dist.py drives the collectives between the calls).  Each rank holds
+// one byte-range shard of the FASTA (codes + a (k-1)-base halo):
+//   kman_dshard_hist     exact item counts per (top-8-bit bucket b, position
+//                        segment s) of the shard, in rg_extract's tile geometry
+//   (host)               all-gather of the per-bucket counts; the 256 buckets
+//                        cut into G x R contiguous parts of ~equal k-mers:
+//                        rank q owns parts q*R .. q*R+R-1, round r handles part
+//                        q*R + r of every rank q, so a rank's rounds produce
+//                        its key range in order and the ranks' outputs in
+//                        rank order are the global output
+//   per round r:
+//   kman_dshard_extract  pass 0 of the shard over the round's buckets only,
+//                        written straight into the send buffer: region (b, s)
+//                        at rtab[b * RS + s] (exact, destination-major, so no
+//                        gather pass and no padding)
+//   (host)               one all-to-all of the packed items (RCCL, xGMI)
+//   kman_dround_finish   per (bucket, source) chain: pass 1 by 9 bits into
+//                        sub-regions (b, d, src, h); pass 1b per (b, d) by g
+//                        more bits (g >= ceil(log2 G), more when the round's
+//                        buckets are large), tagging each item with its source
+//                        rank in the now implied d field; then the LDS finish,
+//                        appending the round's rows to the rank's output.
+// Uniq pos carry the source rank in bits 56-63.  The round working set is
+// two arenas: A = the send buffer, then pass-1 sub-regions; B = the receive
+// buffer, then pass-1b regions (the receive buffer is dead after pass 1).
 namespace {
 
-struct DistPlan {
-    uint32_t K, Q, g, rest, world;
-    bool rc;
-    RegionPlan p0;        // pass 0 of the local shard
-    uint64_t C1s, C1;     // pass-1 sub-region / pass-1b region capacities
-    uint32_t nb_max;      // buckets a rank may own
-    uint64_t off_r1, off_c1, off_r2, off_c2, off_tab, off_lim, bytes;
-};
+constexpr uint32_t HIST_BLOCKS_PER_SEG = 32;
 
-int make_dplan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t flags, int mode, uint32_t world,
-               DistPlan *dp) {
-    if (world < 1 || world > 256) return KMAN_EINVAL;
-    if (n_bases_q < n_bases) return KMAN_EINVAL;
-    RegionPlan p;
-    // pass-0 layout from the local shard; Q from the common bound n_bases_q
-    const int r = make_plan(n_bases ? n_bases : 1, k, flags, mode, &p);
-    if (r != KMAN_OK) return r;
-    DistPlan d{};
-    d.K = 2 * k;
-    d.rc = p.rc;
-    d.world = world;
-    const uint64_t Wq = n_bases_q * (d.rc ? 2 : 1);
-    d.Q = mode == KMAN_FINISH_UNIQ ? (bitlen(Wq - 1) ? bitlen(Wq - 1) : 1u) : 0u;
-    if (d.K - B1 + d.Q > 64) return KMAN_EFALLBACK;
-    p.Q = d.Q;  // pass 0 packs with the common Q
-    uint32_t g = 1;
-    while ((1u << g) < world) g++;
-    d.g = g;
-    if (d.K < B1 + 9 + g + 1) return KMAN_EFALLBACK;
-    d.rest = d.K - B1 - 9 - g;
-    const uint64_t e1 = Wq >> (B1 + 9);                         // per source, bucket and d
-    // pass 1 runs two block-owned chains per (bucket, source): sub-regions
-    // (b, d, src, h) of ~e1 / 2 items each
-    d.C1s = ceil_div(e1 / 2 + e1 / 4 + 256, 64) * 64;
-    const uint64_t e2 = (Wq * world) >> (B1 + 9 + g);          // per final region
-    if (e2 > 7800) return KMAN_EFALLBACK;
-    const uint64_t c2 = ceil_div(e2 + e2 / 2 + 512, 64) * 64;
-    d.C1 = c2 < (uint64_t)FCAP ? c2 : (uint64_t)FCAP;
-    // (kman_amd/dist.py mirrors this bound)
-    const uint32_t per = (RADIX + world - 1) / world;
-    d.nb_max = per + per / 2 + 4 < (uint32_t)RADIX ? per + per / 2 + 4 : (uint32_t)RADIX;
-    const uint64_t nsub = (uint64_t)d.nb_max * 512 * world * 2;  // pass-1 sub-regions
-    const uint64_t nreg = (uint64_t)d.nb_max * 512 << g;      // pass-1b regions
-    d.off_r1 = p.bytes;
-    d.off_c1 = d.off_r1 + nsub * d.C1s * 8;
-    d.off_r2 = d.off_c1 + nsub * 4;
-    d.off_c2 = d.off_r2 + nreg * d.C1 * 8;
-    d.off_tab = d.off_c2 + nreg * 4;
-    // tables: gather offsets [RADIX * RS] u64, pass-1 segment bases [nb_max * world] u64 + counts u32
-    const uint64_t tab = (uint64_t)RADIX * RS * 8 + (uint64_t)d.nb_max * world * 12;
-    d.off_lim = d.off_tab + ceil_div(tab, 64) * 64;
-    d.bytes = d.off_lim + 64;
-    d.p0 = p;
-    *dp = d;
+// exact (bucket, segment) counts of rg_extract's items: block (j, s) rolls
+// the tiles j, j + J, ... of segment s
+template <int EI, bool RC, bool CANON>
+__global__ __launch_bounds__(RT) void rg_hist(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
+                                             uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ hist) {
+    constexpr int NT = RT, NWAVE = NT / 64, WIN = NT * EI;
+    __shared__ __attribute__((aligned(16))) uint8_t scodes[WIN + 64];
+    __shared__ uint32_t wh[NWAVE][RADIX];
+    const uint32_t sgi = blockIdx.y;
+    const uint32_t t0 = sgi * seg_tiles;
+    const uint32_t t1 = t0 + seg_tiles < n_tiles ? t0 + seg_tiles : n_tiles;
+    const int w = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&wh[0][0])[i] = 0;
+    const uint32_t kb = 2u * (uint32_t)k, shift = kb - B1;
+    const uint64_t keymask = kb >= 64 ? ~0ull : ((1ull << kb) - 1);
+    const uint32_t w0 = threadIdx.x * EI;
+    for (uint32_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) {
+        const uint64_t wb = (uint64_t)t * WIN;
+        __syncthreads();  // the previous tile's rolls read scodes
+        stage_codes<NT, EI>(codes, n_bases, wb, scodes);
+        __syncthreads();
+        uint64_t kf[EI], kr[EI];
+        const uint32_t valid = roll<EI, CANON>(scodes, w0, k, keymask, wb + w0, n_bases, kf, kr);
+#pragma unroll
+        for (int j = 0; j < EI; j++) {
+            if ((valid >> j) & 1u) {
+                atomicAdd(&wh[w][(uint32_t)(kf[j] >> shift)], 1u);
+                if (RC) atomicAdd(&wh[w][(uint32_t)(kr[j] >> shift)], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < (uint32_t)RADIX; d += NT) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int ww = 0; ww < NWAVE; ww++) c += wh[ww][d];
+        if (c) atomicAdd(&hist[d * RS + sgi], c);
+    }
+}
+
+// the shard's pass-0 geometry (rg_extract / rg_hist): no capacity limits,
+// no region area (the exact layout needs none); Q from the common bound
+int make_shard_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t flags, int mode, RegionPlan *pl) {
+    if (mode != KMAN_FINISH_COUNT && mode != KMAN_FINISH_UNIQ) return KMAN_EINVAL;
+    if (k < 2 || k > 32 || n_bases_q < n_bases) return KMAN_EINVAL;
+    if (getenv("KMAN_NO_REGION")) return KMAN_EFALLBACK;
+    if (k > 25) return KMAN_EFALLBACK;  // the tile-local window index rides above the key bits
+    RegionPlan p{};
+    p.canon = flags & KMAN_CANONICAL;
+    p.rc = (flags & KMAN_RC) && !p.canon;
+    p.K = 2 * k;
+    p.W = n_bases * (p.rc ? 2 : 1);
+    const uint64_t Wq = n_bases_q * (p.rc ? 2 : 1);
+    p.Q = mode == KMAN_FINISH_UNIQ ? (bitlen(Wq - 1) ? bitlen(Wq - 1) : 1u) : 0u;
+    if (p.K - B1 + p.Q > 64) return KMAN_EFALLBACK;
+    p.ei = p.rc ? 6u : 12u;
+    const uint64_t win = (uint64_t)RT * p.ei;
+    p.n_tiles0 = (uint32_t)ceil_div(n_bases ? n_bases : 1, win);
+    p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, RS);
+    *pl = p;
     return KMAN_OK;
 }
 
-// copy each pass-0 region (b, s) to its place in the compact send buffer
-__global__ __launch_bounds__(256) void rg_gather(const uint64_t *__restrict__ r0, uint64_t C0,
-                                                 const uint32_t *__restrict__ cnt0, const uint64_t *__restrict__ off,
-                                                 uint64_t *__restrict__ send) {
-    const uint32_t g = blockIdx.y;  // region (b * RS + s)
-    const uint32_t c = cnt0[g];
-    const uint64_t *src = r0 + (uint64_t)g * C0;
-    uint64_t *dst = send + off[g];
-    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < c; i += gridDim.x * 256) dst[i] = src[i];
+struct RoundPlan {
+    uint32_t K, Q, g, rest, G, nb;
+    bool rc;
+    uint64_t C1s, C1;     // pass-1 sub-region / pass-1b region capacities
+    uint64_t nsub, nreg;
+    // arena A: r1 | c1 | pass-1 segment bases (u64) + counts (u32); arena B: r2 | c2
+    uint64_t off_c1, off_tab, a_bytes, off_c2, b_bytes;
+};
+
+// counts[src * nb + j] = items of bucket b_lo + j from rank src
+int make_rplan(uint32_t k, uint32_t flags, int mode, uint32_t world, uint64_t n_bases_q, uint32_t nb,
+               const uint64_t *counts, RoundPlan *rp) {
+    if (mode != KMAN_FINISH_COUNT && mode != KMAN_FINISH_UNIQ) return KMAN_EINVAL;
+    if (k < 2 || k > 32 || world < 1 || world > 32 || nb > (uint32_t)RADIX) return KMAN_EINVAL;
+    if (nb && !counts) return KMAN_EINVAL;
+    RoundPlan d{};
+    const bool canon = flags & KMAN_CANONICAL;
+    d.rc = (flags & KMAN_RC) && !canon;
+    d.K = 2 * k;
+    d.G = world;
+    d.nb = nb;
+    const uint64_t Wq = n_bases_q * (d.rc ? 2 : 1);
+    d.Q = mode == KMAN_FINISH_UNIQ ? (bitlen(Wq - 1) ? bitlen(Wq - 1) : 1u) : 0u;
+    if (d.K - B1 + d.Q > 64) return KMAN_EFALLBACK;
+    uint64_t maxsb = 0, maxb = 0;  // largest (bucket, source) chunk, largest bucket
+    for (uint32_t j = 0; j < nb; j++) {
+        uint64_t t = 0;
+        for (uint32_t src = 0; src < world; src++) {
+            const uint64_t c = counts[(uint64_t)src * nb + j];
+            if (c > 0xffffffffull) return KMAN_EFALLBACK;  // (pass-1 chain lengths are u32)
+            maxsb = c > maxsb ? c : maxsb;
+            t += c;
+        }
+        maxb = t > maxb ? t : maxb;
+    }
+    // pass 1b bits: at least the source tag's ceil(log2 G), more until a final
+    // region expects <= 6144 items (the LDS finish holds FCAP = 8704)
+    uint32_t g = 1;
+    while ((1u << g) < world) g++;
+    {
+        const char *e = getenv("KMAN_DROUND_MIN_G");  // tests: the wide pass-1b digits of huge rounds
+        const uint32_t gm = e ? (uint32_t)atoi(e) : 0u;
+        g = gm > g && gm <= 9 ? gm : g;
+    }
+    while (g < 9 && ((maxb >> 9) >> g) > 6144) g++;
+    if (((maxb >> 9) >> g) > 7800) return KMAN_EFALLBACK;
+    if (d.K < B1 + 9 + g + 1) return KMAN_EFALLBACK;
+    d.g = g;
+    d.rest = d.K - B1 - 9 - g;
+    // pass 1: two block-owned chains per (bucket, source), 512 digits
+    const uint64_t e1 = maxsb >> 10;
+    d.C1s = ceil_div(e1 + e1 / 2 + 256, 64) * 64;
+    if ((uint64_t)512 * world * 2 * d.C1s >= (1ull << 31)) return KMAN_EFALLBACK;  // (32-bit WC offsets)
+    const uint64_t e2 = (maxb >> 9) >> g;
+    const uint64_t c2 = ceil_div(e2 + e2 / 2 + 512, 64) * 64;
+    d.C1 = c2 < (uint64_t)FCAP ? c2 : (uint64_t)FCAP;
+    d.nsub = (uint64_t)nb * 512 * world * 2;
+    d.nreg = (uint64_t)nb * 512 << g;
+    d.off_c1 = d.nsub * d.C1s * 8;
+    d.off_tab = ceil_div(d.off_c1 + d.nsub * 4, 64) * 64;
+    d.a_bytes = d.off_tab + ceil_div((uint64_t)nb * world * 12 + 64, 64) * 64;
+    d.off_c2 = d.nreg * d.C1 * 8;
+    d.b_bytes = d.off_c2 + ceil_div(d.nreg * 4 + 64, 64) * 64;
+    *rp = d;
+    return KMAN_OK;
+}
+
+int read_err(kman_ctx *ctx, uint32_t *e) {
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small + 8, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    memcpy(e, ctx->h_small + 8, 4);
+    if (*e) {
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        if (*e != ERR_REGION)
+            return kman_fail(ctx, KMAN_ETIMEOUT, "device look-back wait exceeded its bound (code %u)", *e);
+    }
+    return KMAN_OK;
+}
+
+template <int EI, bool RC, bool CANON>
+void launch_hist(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
+                 uint32_t *hist) {
+    const uint32_t gx = p.seg_tiles < HIST_BLOCKS_PER_SEG ? p.seg_tiles : HIST_BLOCKS_PER_SEG;
+    hipLaunchKernelGGL((rg_hist<EI, RC, CANON>), dim3(gx, RS), dim3(RT), 0, ctx->stream, codes, n_bases, (int)k,
+                       p.seg_tiles, p.n_tiles0, hist);
+}
+
+template <int EI, bool RC, bool CANON>
+void launch_extract_ex(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
+                       uint64_t *out, uint32_t *cnt, const uint64_t *rtab, uint32_t epoch, uint32_t *counter) {
+    const uint32_t grid = RS * p.seg_tiles;
+    hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, true>), dim3(grid), dim3(RT), 0, ctx->stream, codes,
+                       n_bases, (int)k, p.Q, out, (uint64_t)0, p.seg_tiles, p.n_tiles0, cnt, ctx->d_status, counter,
+                       epoch, ctx->d_err, 0u, nullptr, rtab);
 }
 
 }  // namespace
 
-extern "C" int kman_dgroups_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t flags, int mode,
-                                 uint32_t world, uint64_t *work_bytes) {
-    if (!work_bytes) return KMAN_EINVAL;
-    DistPlan d;
-    const int r = make_dplan(n_bases, n_bases_q, k, flags, mode, world, &d);
-    *work_bytes = r == KMAN_OK ? d.bytes : 0;
-    return r;
+extern "C" int kman_dshard_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t flags, int mode) {
+    RegionPlan p;
+    return make_shard_plan(n_bases, n_bases_q, k, flags, mode, &p);
 }
 
-extern "C" int kman_dgroups_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint64_t n_bases_q,
-                                    uint32_t k, uint32_t flags, int mode, uint32_t world, void *d_work,
-                                    uint64_t work_bytes, uint64_t *d_send, uint64_t *bucket_counts,
-                                    uint32_t *overflow) {
-    if (!ctx || !bucket_counts || !overflow) return KMAN_EINVAL;
-    *overflow = 0;
-    memset(bucket_counts, 0, RADIX * sizeof(uint64_t));
-    DistPlan d;
-    const int pr = make_dplan(n_bases, n_bases_q, k, flags, mode, world, &d);
-    if (pr == KMAN_EINVAL) return kman_fail(ctx, KMAN_EINVAL, "kman_dgroups_extract: bad arguments");
+extern "C" int kman_dshard_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint64_t n_bases_q,
+                                uint32_t k, uint32_t flags, int mode, uint32_t *d_hist, uint32_t *hist) {
+    if (!ctx || !d_hist || !hist) return KMAN_EINVAL;
+    RegionPlan p;
+    const int pr = make_shard_plan(n_bases, n_bases_q, k, flags, mode, &p);
+    if (pr == KMAN_EINVAL) return kman_fail(ctx, KMAN_EINVAL, "kman_dshard_hist: bad arguments");
     if (pr != KMAN_OK) return pr;
-    if (!d_codes || !d_work || !d_send) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
-    if (work_bytes < d.bytes) return kman_fail(ctx, KMAN_ECAP, "work area too small");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    const RegionPlan &p = d.p0;
-    uint64_t *r0 = (uint64_t *)d_work;
-    uint32_t *c0 = (uint32_t *)((char *)d_work + p.off_c0);
-    uint64_t *goff = (uint64_t *)((char *)d_work + d.off_tab);
-    HIP_TRY(ctx, hipMemsetAsync(c0, 0, (uint64_t)RADIX * RS * 4, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(d_hist, 0, (size_t)RADIX * RS * 4, ctx->stream));
     if (n_bases) {
-        uint32_t epoch, *counter;
-        KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
-        KTimer kt_(ctx, "region_extract");
-        launch_extract_any(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter, 0, nullptr);
+        if (!d_codes) return kman_fail(ctx, KMAN_EINVAL, "null codes");
+        KTimer kt_(ctx, "shard_hist");
+        if (p.canon) launch_hist<12, false, true>(ctx, p, d_codes, n_bases, k, d_hist);
+        else if (p.rc) launch_hist<6, true, false>(ctx, p, d_codes, n_bases, k, d_hist);
+        else launch_hist<12, false, false>(ctx, p, d_codes, n_bases, k, d_hist);
         HIP_TRY(ctx, hipGetLastError());
     }
-    std::vector<uint32_t> hc((size_t)RADIX * RS);
-    HIP_TRY(ctx, hipMemcpyAsync(hc.data(), c0, hc.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small + 8, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(hist, d_hist, (size_t)RADIX * RS * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    uint32_t e;
-    memcpy(&e, ctx->h_small + 8, 4);
-    if (e) {
-        HIP_TRY(ctx, hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        if (e != ERR_REGION) return kman_fail(ctx, KMAN_ETIMEOUT, "device look-back wait exceeded its bound (code %u)", e);
-        *overflow = 1;  // the caller agrees on the fallback collectively
-        return KMAN_OK;
-    }
-    std::vector<uint64_t> off(hc.size());
-    uint64_t acc = 0;
-    for (size_t i = 0; i < hc.size(); i++) {
-        off[i] = acc;
-        acc += hc[i];
-        bucket_counts[i / RS] += hc[i];
-    }
-    HIP_TRY(ctx, hipMemcpyAsync(goff, off.data(), off.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-    {
-        KTimer kt_(ctx, "dist_gather");
-        const uint32_t gx = (uint32_t)ceil_div(p.C0, 4096);
-        hipLaunchKernelGGL(rg_gather, dim3(gx < 1 ? 1 : gx, RADIX * RS), dim3(256), 0, ctx->stream, r0, p.C0, c0,
-                           goff, d_send);
-        HIP_TRY(ctx, hipGetLastError());
-    }
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // the host copy of off must stay valid until consumed
     return KMAN_OK;
 }
 
-extern "C" int kman_dgroups_finish(kman_ctx *ctx, const uint64_t *d_recv, uint64_t n_bases, uint64_t n_bases_q,
-                                   uint32_t k, uint32_t flags, int mode, uint32_t world, uint32_t b_lo, uint32_t nb,
-                                   const uint64_t *counts, void *d_work, uint64_t work_bytes, uint64_t *d_okeys,
-                                   void *d_ovals, uint32_t oval_bytes, uint64_t *n_out) {
-    if (!ctx || !n_out || !counts) return KMAN_EINVAL;
-    *n_out = 0;
-    DistPlan d;
-    const int pr = make_dplan(n_bases, n_bases_q, k, flags, mode, world, &d);
-    if (pr == KMAN_EINVAL) return kman_fail(ctx, KMAN_EINVAL, "kman_dgroups_finish: bad arguments");
+extern "C" int kman_dshard_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint64_t n_bases_q,
+                                   uint32_t k, uint32_t flags, int mode, const uint32_t *d_hist,
+                                   const uint64_t *d_rtab, uint64_t *d_send) {
+    if (!ctx) return KMAN_EINVAL;
+    RegionPlan p;
+    const int pr = make_shard_plan(n_bases, n_bases_q, k, flags, mode, &p);
+    if (pr == KMAN_EINVAL) return kman_fail(ctx, KMAN_EINVAL, "kman_dshard_extract: bad arguments");
     if (pr != KMAN_OK) return pr;
-    if (nb > d.nb_max || b_lo + nb > (uint32_t)RADIX) return KMAN_EFALLBACK;
-    if (work_bytes < d.bytes) return kman_fail(ctx, KMAN_ECAP, "work area too small");
+    if (!n_bases) return KMAN_OK;
+    if (!d_codes || !d_hist || !d_rtab || !d_send) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    uint32_t epoch, *counter;
+    KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
+    {
+        KTimer kt_(ctx, "region_extract");
+        uint32_t *cnt = const_cast<uint32_t *>(d_hist);  // read-only in EX mode
+        if (p.canon) launch_extract_ex<12, false, true>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
+        else if (p.rc) launch_extract_ex<6, true, false>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
+        else launch_extract_ex<12, false, false>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    uint32_t e;
+    KMAN_TRY(read_err(ctx, &e));
+    if (e) return kman_fail(ctx, KMAN_EHIP, "kman_dshard_extract: a region outgrew its rg_hist count");
+    return KMAN_OK;
+}
+
+extern "C" int kman_dround_plan(uint32_t k, uint32_t flags, int mode, uint32_t world, uint64_t n_bases_q, uint32_t nb,
+                                const uint64_t *counts, uint64_t *a_bytes, uint64_t *b_bytes) {
+    if (!a_bytes || !b_bytes) return KMAN_EINVAL;
+    *a_bytes = *b_bytes = 0;
+    RoundPlan d;
+    const int r = make_rplan(k, flags, mode, world, n_bases_q, nb, counts, &d);
+    if (r != KMAN_OK) return r;
+    *a_bytes = d.a_bytes;
+    *b_bytes = d.b_bytes;
+    return KMAN_OK;
+}
+
+extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_t k, uint32_t flags, int mode,
+                                  uint32_t world, uint64_t n_bases_q, uint32_t b_lo, uint32_t nb,
+                                  const uint64_t *counts, void *d_a, uint64_t a_bytes, void *d_b, uint64_t b_bytes,
+                                  uint64_t *d_okeys, void *d_ovals, uint32_t oval_bytes, uint64_t *n_out) {
+    if (!ctx || !n_out) return KMAN_EINVAL;
+    *n_out = 0;
+    RoundPlan d;
+    const int pr = make_rplan(k, flags, mode, world, n_bases_q, nb, counts, &d);
+    if (pr == KMAN_EINVAL) return kman_fail(ctx, KMAN_EINVAL, "kman_dround_finish: bad arguments");
+    if (pr != KMAN_OK) return pr;
+    if (b_lo + nb > (uint32_t)RADIX) return kman_fail(ctx, KMAN_EINVAL, "bucket range past 256");
+    if (a_bytes < d.a_bytes || b_bytes < d.b_bytes)
+        return kman_fail(ctx, KMAN_ECAP, "round arenas %llu / %llu < %llu / %llu bytes", (unsigned long long)a_bytes,
+                         (unsigned long long)b_bytes, (unsigned long long)d.a_bytes, (unsigned long long)d.b_bytes);
     if (oval_bytes != 4 && oval_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "oval_bytes must be 4 or 8");
     if (mode == KMAN_FINISH_UNIQ && oval_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "uniq pos on N > 1 are u64");
     if (nb == 0) return KMAN_OK;
-    if (!d_recv || !d_work || !d_okeys || !d_ovals) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    if (!d_recv || !d_a || !d_b || !d_okeys || !d_ovals) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    char *wk = (char *)d_work;
-    uint64_t *r1 = (uint64_t *)(wk + d.off_r1);
-    uint32_t *c1 = (uint32_t *)(wk + d.off_c1);
-    uint64_t *r2 = (uint64_t *)(wk + d.off_r2);
-    uint32_t *c2 = (uint32_t *)(wk + d.off_c2);
-    uint64_t *sbase = (uint64_t *)(wk + d.off_tab + (uint64_t)RADIX * RS * 8);
-    uint32_t *scnt = (uint32_t *)(sbase + (uint64_t)d.nb_max * world);
+    char *wa = (char *)d_a, *wb = (char *)d_b;
+    uint64_t *r1 = (uint64_t *)wa;
+    uint32_t *c1 = (uint32_t *)(wa + d.off_c1);
+    uint64_t *sbase = (uint64_t *)(wa + d.off_tab);
+    uint32_t *scnt = (uint32_t *)(sbase + (uint64_t)nb * world);
+    uint64_t *r2 = (uint64_t *)wb;
+    uint32_t *c2 = (uint32_t *)(wb + d.off_c2);
     const uint32_t G = world;
     // pass-1 segments: bucket (b, src) = one contiguous run of src's chunk
     std::vector<uint64_t> hb((size_t)nb * G);
     std::vector<uint32_t> hn((size_t)nb * G);
-    uint64_t roff = 0, maxc = 0;
+    uint64_t roff = 0;
     for (uint32_t src = 0; src < G; src++) {
-        uint64_t at = roff;
         for (uint32_t j = 0; j < nb; j++) {
             const uint64_t c = counts[(uint64_t)src * nb + j];
-            if (c > 0xffffffffull) return KMAN_EFALLBACK;
-            hb[(size_t)j * G + src] = at;
+            hb[(size_t)j * G + src] = roff;
             hn[(size_t)j * G + src] = (uint32_t)c;
-            at += c;
-            maxc = c > maxc ? c : maxc;
+            roff += c;
         }
-        roff = at;
     }
-    const uint32_t nbk = nb * G;
     HIP_TRY(ctx, hipMemcpyAsync(sbase, hb.data(), hb.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(scnt, hn.data(), hn.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-    (void)maxc;
-    const uint64_t nsub = (uint64_t)nb * 512 * G * 2;
-    const uint32_t nreg = (uint32_t)((uint64_t)nb * 512 << d.g);
-    HIP_TRY(ctx, hipMemsetAsync(c1, 0, nsub * 4, ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(c2, 0, (uint64_t)nreg * 4, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(c1, 0, d.nsub * 4, ctx->stream));
     uint32_t epoch, *counter;
     // pass 1: by the 9 bits below the bucket, two chains per (b, src) into
     // sub-regions (b, d, src, h)
@@ -1421,7 +1547,7 @@ extern "C" int kman_dgroups_finish(kman_ctx *ctx, const uint64_t *d_recv, uint64
         pa.in = d_recv;
         pa.seg_base = sbase;
         pa.seg_cnt = scnt;
-        pa.nbk = nbk;
+        pa.nbk = nb * G;
         pa.nsg = 1;
         pa.gsub = G;
         pa.H = 2;
@@ -1433,11 +1559,12 @@ extern "C" int kman_dgroups_finish(kman_ctx *ctx, const uint64_t *d_recv, uint64
         launch_pass(ctx, pa, counter, 0, nullptr);
         HIP_TRY(ctx, hipGetLastError());
     }
-    KMAN_TRY(rg_check(ctx, "pass 1", c1, nsub));
+    KMAN_TRY(rg_check(ctx, "pass 1", c1, d.nsub));
+    // (c2 may lie in the receive buffer: cleared only once pass 1 has read it)
+    HIP_TRY(ctx, hipMemsetAsync(c2, 0, d.nreg * 4, ctx->stream));
     // pass 1b: per (b, d), its 2G sub-regions concatenated, by g more bits;
     // the source rank (segment index / 2) goes into the d field
     {
-        const uint32_t nbk2 = nb * 512;
         KMAN_TRY(kman_lookback_begin(ctx, 1, &epoch, &counter));
         KTimer kt_(ctx, "region_pass1b");
         PassArgs pa{};
@@ -1445,7 +1572,7 @@ extern "C" int kman_dgroups_finish(kman_ctx *ctx, const uint64_t *d_recv, uint64
         pa.seg_base = nullptr;
         pa.seg_cnt = c1;
         pa.stride = d.C1s;
-        pa.nbk = nbk2;
+        pa.nbk = nb * 512;
         pa.nsg = 2 * G;
         pa.gsub = 1;
         pa.H = 1;
@@ -1461,23 +1588,16 @@ extern "C" int kman_dgroups_finish(kman_ctx *ctx, const uint64_t *d_recv, uint64
         launch_pass(ctx, pa, counter, 0, nullptr);
         HIP_TRY(ctx, hipGetLastError());
     }
-    KMAN_TRY(rg_check(ctx, "pass 1b", c2, nreg));
+    KMAN_TRY(rg_check(ctx, "pass 1b", c2, d.nreg));
     {
         FinishArgs f{r2, d.C1, c2, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << (9 + d.g),
-                     mode == KMAN_FINISH_UNIQ ? d.Q + d.rest + d.g : 0u, nreg};
+                     mode == KMAN_FINISH_UNIQ ? d.Q + d.rest + d.g : 0u, (uint32_t)d.nreg};
         KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, 0, nullptr));
     }
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small + 4, ctx->d_status + (nreg - 1), 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small + 8, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small + 4, ctx->d_status + (d.nreg - 1), 8, hipMemcpyDeviceToHost, ctx->stream));
     uint32_t e;
-    memcpy(&e, ctx->h_small + 8, 4);
-    if (e) {
-        HIP_TRY(ctx, hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        if (e == ERR_REGION) return KMAN_EFALLBACK;
-        return kman_fail(ctx, KMAN_ETIMEOUT, "device look-back wait exceeded its bound (code %u)", e);
-    }
+    KMAN_TRY(read_err(ctx, &e));  // synchronises
+    if (e) return KMAN_EFALLBACK;  // a region overflowed (skewed keys): outputs invalid
     const uint64_t wd = ctx->h_small[4];
     if (((wd >> 56) & 63u) != ctx->epoch || (wd >> 62) != ST_INCL)
         return kman_fail(ctx, KMAN_EHIP, "region output total not published");

@@ -264,6 +264,12 @@ void kman_destroy(kman_ctx *ctx) {
     if (ctx->d_aux) (void)hipFree(ctx->d_aux);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->h_small) (void)hipHostFree(ctx->h_small);
+    if (ctx->copy_stream) {
+        (void)hipStreamSynchronize(ctx->copy_stream);
+        (void)hipStreamDestroy(ctx->copy_stream);
+    }
+    for (auto e : ctx->copy_ev)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -324,6 +330,28 @@ int kman_memcpy_d2h(kman_ctx *ctx, void *dst, const void *src, size_t bytes) {
     if (!bytes) return KMAN_OK;
     HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return KMAN_OK;
+}
+
+int kman_copy_h2d_async(kman_ctx *ctx, void *dst, const void *src, size_t bytes, int slot) {
+    if (!ctx || slot < 0 || slot >= 4) return KMAN_EINVAL;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (!ctx->copy_stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    if (!ctx->copy_ev[slot]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->copy_ev[slot], hipEventDisableTiming));
+    if (bytes) HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->copy_stream));
+    HIP_TRY(ctx, hipEventRecord(ctx->copy_ev[slot], ctx->copy_stream));
+    return KMAN_OK;
+}
+
+int kman_copy_wait(kman_ctx *ctx, int slot) {
+    if (!ctx || slot < 0 || slot >= 4 || !ctx->copy_ev[slot]) return KMAN_EINVAL;
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->copy_ev[slot], 0));
+    return KMAN_OK;
+}
+
+int kman_copy_sync(kman_ctx *ctx) {
+    if (!ctx) return KMAN_EINVAL;
+    if (ctx->copy_stream) HIP_TRY(ctx, hipStreamSynchronize(ctx->copy_stream));
     return KMAN_OK;
 }
 

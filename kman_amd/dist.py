@@ -1,45 +1,48 @@
-"""Multi-GPU k-mer join: prefix-range partition + one all-to-all.
+"""Multi-GPU k-mer join over byte-range shards of ONE FASTA.
 
-One process per GPU.  Every rank extracts the k-mers of its own FASTA shard,
-then:
+One process per GPU.  Rank q of G loads the bytes [start_q, start_{q+1}) of
+the input plus a (k-1)-base halo (kman_amd/shard.py: cuts at line starts, a
+window belongs to the shard holding its first base), so the union of the
+shards' windows is the reference's one k-mer stream over all records
+(kmermaid/batcher.py:386-392, seq.py:285-328).  Then, per step:
 
-1. histograms the top ``hb`` key bits            (kman_prefix_hist)
-2. all-reduces the histogram                      (kman_allreduce_u64, RCCL)
-3. cuts the prefix space into ``world`` contiguous ranges of ~equal k-mer
-   count                                          (``plan_lut``, host)
-4. stably partitions its keys (+ pos) by destination rank
-                                                  (kman_partition, 1 onesweep pass)
-5. exchanges per-destination counts and then the keys (+ pos)
-                                                  (kman_allgather_u64 + kman_alltoallv)
-6. sorts what it received by prefix and finishes it in LDS with the count / uniq
-   output (kman_sort_range + kman_finish).
+1. ``kman_dshard_hist``: exact item counts per (top-8-bit bucket, position
+   segment) of the shard; the bucket totals are all-gathered (C[src][b]).
+2. The 256 buckets are cut into G x R contiguous parts of ~equal k-mers
+   (``part_cuts``): rank q owns parts q*R .. q*R+R-1 -- a contiguous key
+   range -- and round r handles part q*R + r of every rank q.  R is the
+   fewest rounds whose working set fits every rank's arenas (12.5 GB of FASTA
+   per rank, BASELINE config 4, takes several).
+3. Per round: ``kman_dshard_extract`` writes the items of the round's buckets
+   straight into the send buffer, destination-major (exact offsets from the
+   histogram: no gather pass); ONE all-to-all of the packed 8-byte items
+   (RCCL over xGMI); ``kman_dround_finish`` runs the per-bucket passes and the
+   LDS finish, appending the round's rows to the rank's output.
+4. The abundance spectrum (BASELINE config 5) is the local ``kman_count_hist``
+   of the rank's counts, all-reduced.
 
-Rank r then holds the complete count/uniq result for its prefix range; the
-ranges are in rank order, so concatenating the ranks' outputs is the global
-sorted output of the reference (join.py:95-130) over all shards.  uniq
-payloads carry the source rank in bits 56-63 so headers resolve against the
-right shard's record table.
+Rank q's output is the slice of the global sorted output for its key range
+(join.py:95-130 over all batches); the ranks' outputs in rank order are the
+global output, and ``emit`` writes each rank's text at its offset of one file.
+Uniq pos carry the source rank in bits 56-63 and are rebased to global base
+indices (``kman_rebase_pos``) before the headers are formatted against the
+all-gathered record table.
 
-The planning functions are pure numpy and shared with the CPU rehearsal in
-tests/test_dist_cpu.py (gloo, world_size 2), which checks the partition +
-exchange logic end to end without GPUs.
+A region overflow (a key repeated more often than a region holds) is agreed
+on collectively and only that round is redone through the general path (key
+ranges by ``kman_extract_range``, exchanged keys + pos, ``kman_sort_range`` +
+``kman_finish``), which also serves k > 25 and uniq shards too large for the
+packed items.
 
-The default path is the region path across ranks (``_region_step``, C ABI
-kman_dgroups_*): every rank runs the extraction pass of region.hip on its
-shard (items grouped by their top 8 key bits), the 256 bucket counts are
-all-reduced, each rank gets a contiguous bucket range of ~1/G of the k-mers
-(``plan_lut``), the packed 8-byte items move in ONE all-to-all (half the bytes
-of the key + pos exchange above), and each rank finishes its buckets with the
-per-bucket passes and the LDS finish.  Any region overflow (skewed input) is
-agreed on collectively and the step falls back to the prefix-range path.
-The step is a generator that yields its collectives, so a test can drive G
-ranks in one process on one GPU (``SimGroup``) and the real run executes them
-with RCCL (``RcclComm``).
+Every step is a generator that yields its collectives: ``RcclComm`` runs
+them with RCCL for the one rank of this process, ``SimGroup`` runs G ranks in
+one process on one GPU (tests: host-side reductions, device-to-device copies).
 """
 
 from __future__ import annotations
 
 import ctypes
+import os
 from ctypes import byref, c_int, c_uint64, c_void_p
 from typing import List, Optional, Tuple
 
@@ -47,97 +50,174 @@ import numpy as np
 
 from . import _native as N
 from . import engine
+from . import shard as S
 
 RANK_SHIFT = 56
-
-
-def hist_bits(k: int) -> int:
-    return min(14, 2 * k)
+NB = 256  # top-8-bit buckets
+RS = 64   # position segments of the shard's pass 0
 
 
 def plan_lut(global_hist: np.ndarray, world: int) -> np.ndarray:
-    """Destination rank of every prefix bin: contiguous ranges, each holding
-    ~total/world keys (a bin goes to the rank owning its midpoint)."""
+    """Part of every bin: contiguous ranges, each holding ~total/world items
+    (a bin goes to the part owning its midpoint)."""
     h = np.asarray(global_hist, dtype=np.float64)
     total = h.sum()
     if total == 0:
-        return np.zeros(len(h), dtype=np.uint8)
+        return np.zeros(len(h), dtype=np.int64)
     mid = np.cumsum(h) - h / 2
     dest = np.floor(mid * world / total).astype(np.int64)
-    return np.clip(dest, 0, world - 1).astype(np.uint8)
+    return np.clip(dest, 0, world - 1)
 
 
-def bucket_counts(local_hist: np.ndarray, lut: np.ndarray, world: int) -> np.ndarray:
-    return np.bincount(lut.astype(np.int64), weights=np.asarray(local_hist, np.float64),
-                       minlength=world).astype(np.uint64)
+def part_cuts(totals: np.ndarray, nparts: int) -> np.ndarray:
+    """nparts + 1 bucket cuts: part p = buckets [cuts[p], cuts[p+1])."""
+    lut = plan_lut(totals, nparts)
+    return np.searchsorted(lut, np.arange(nparts + 1), side="left").astype(np.int64)
 
 
-def recv_layout(count_matrix: np.ndarray, rank: int) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
-    """(send_counts, send_offsets, recv_counts, recv_offsets) of ``rank`` from
-    the world x world matrix C[src][dst] of partition sizes."""
-    C = np.asarray(count_matrix, dtype=np.uint64)
-    send = C[rank].copy()
-    send_off = np.concatenate([[0], np.cumsum(send)[:-1]]).astype(np.uint64)
-    recv = C[:, rank].copy()
-    recv_off = np.concatenate([[0], np.cumsum(recv)[:-1]]).astype(np.uint64)
-    return send, send_off, recv, recv_off
+def part_of(cuts: np.ndarray, R: int, q: int, r: int) -> Tuple[int, int]:
+    p = q * R + r
+    return int(cuts[p]), int(cuts[p + 1])
 
 
-def split_overflow(count_matrix: np.ndarray, cap: int) -> Optional[Tuple[int, int]]:
-    """(rank, keys) of the first rank whose receive size exceeds cap, else
-    None.  A function of the all-gathered matrix only, so every rank reaches
-    the same verdict."""
-    recv = np.asarray(count_matrix, dtype=np.uint64).sum(axis=0)
-    bad = np.nonzero(recv > np.uint64(cap))[0]
-    return (int(bad[0]), int(recv[bad[0]])) if len(bad) else None
+def round_send(H: np.ndarray, cuts: np.ndarray, G: int, R: int, r: int):
+    """Send layout of round r on a rank with (bucket, segment) counts H
+    [256, 64]: region base table (u64 [256 * 64], ~0 = bucket not in this
+    round), per-destination counts and offsets."""
+    H = np.asarray(H, dtype=np.uint64).reshape(NB, RS)
+    rtab = np.full(NB * RS, np.uint64(0xFFFFFFFFFFFFFFFF), dtype=np.uint64)
+    sc = np.zeros(G, dtype=np.uint64)
+    off = 0
+    for q in range(G):
+        lo, hi = part_of(cuts, R, q, r)
+        blk = H[lo:hi].reshape(-1)
+        if len(blk):
+            ex = np.concatenate([[0], np.cumsum(blk)[:-1]]).astype(np.uint64)
+            rtab[lo * RS:hi * RS] = ex + np.uint64(off)
+            sc[q] = int(blk.sum())
+            off += int(sc[q])
+    so = np.concatenate([[0], np.cumsum(sc)[:-1]]).astype(np.uint64)
+    return rtab, sc, so
+
+
+def round_recv(C: np.ndarray, cuts: np.ndarray, R: int, rank: int, r: int):
+    """(b_lo, nb, counts [G, nb], recv counts, recv offsets) of round r on
+    `rank` from the all-gathered bucket totals C [G, 256]."""
+    lo, hi = part_of(cuts, R, rank, r)
+    counts = np.ascontiguousarray(np.asarray(C, dtype=np.uint64)[:, lo:hi])
+    rc = counts.sum(axis=1).astype(np.uint64)
+    ro = np.concatenate([[0], np.cumsum(rc)[:-1]]).astype(np.uint64)
+    return lo, hi - lo, counts, rc, ro
+
+
+def round_sizes(C: np.ndarray, cuts: np.ndarray, G: int, R: int):
+    """send[q, r] / recv[q, r] items of every rank and round."""
+    C = np.asarray(C, dtype=np.uint64)
+    send = np.zeros((G, R), dtype=np.uint64)
+    recv = np.zeros((G, R), dtype=np.uint64)
+    for r in range(R):
+        for q in range(G):
+            lo, hi = part_of(cuts, R, q, r)
+            recv[q, r] = C[:, lo:hi].sum()
+            send[:, r] += C[:, lo:hi].sum(axis=1)
+    return send, recv
 
 
 def _u64p(a: np.ndarray):
     return a.ctypes.data_as(c_void_p)
 
 
-def nb_max(world: int) -> int:
-    """Buckets one rank may own on the region path (region.hip make_dplan)."""
-    per = (256 + world - 1) // world
-    return min(256, per + per // 2 + 4)
+class RoundPlanner:
+    """The rounds of one step, identical on every rank (a function of C, the
+    common budget and the common flags only)."""
+
+    def __init__(self, k: int, flags: int, mode: int, world: int, n_bases_q: int):
+        self.k, self.flags, self.mode, self.G, self.nbq = k, flags, mode, world, n_bases_q
+
+    def arenas(self, C, cuts, R, q: int, r: int) -> Optional[Tuple[int, int]]:
+        """(a, b) bytes of round r on rank q, or None when the region finish
+        cannot take it (then the round runs the general path)."""
+        lo, nb, counts, rc, _ = round_recv(C, cuts, R, q, r)
+        a, b = c_uint64(0), c_uint64(0)
+        ret = N.lib().kman_dround_plan(self.k, self.flags, self.mode, self.G, self.nbq, nb,
+                                       _u64p(np.ascontiguousarray(counts.reshape(-1))), byref(a), byref(b))
+        if ret != N.KMAN_OK:
+            return None
+        return int(a.value), max(int(b.value), 8 * int(rc.sum()))
+
+    def plan(self, C, budget: int, max_round_items: Optional[int] = None, max_rounds: int = 64):
+        """(R, cuts, a_bytes, b_bytes): the fewest rounds whose largest arenas
+        (over ranks and rounds) fit `budget` bytes (and whose rounds receive
+        at most max_round_items on any rank)."""
+        G = self.G
+        tot = np.asarray(C, dtype=np.uint64).sum(axis=0)
+        for R in range(1, max_rounds + 1):
+            if G * R > NB and R > 1:
+                break
+            cuts = part_cuts(tot, G * R)
+            send, recv = round_sizes(C, cuts, G, R)
+            if max_round_items is not None and int(recv.max()) > max_round_items and R < max_rounds:
+                continue
+            a = b = 0
+            ok = True
+            for q in range(G):
+                for r in range(R):
+                    ab = self.arenas(C, cuts, R, q, r)
+                    if ab is None:
+                        ok = False
+                        continue
+                    a, b = max(a, ab[0]), max(b, ab[1])
+            a = max(a, 8 * int(send.max()))
+            if a + b <= budget or R == max_rounds or not ok:
+                return R, cuts, a, b
+        cuts = part_cuts(tot, G * R)
+        send, recv = round_sizes(C, cuts, G, R)
+        return R, cuts, 8 * int(send.max()), 8 * int(recv.max())
 
 
-def bucket_ranges(global_counts: np.ndarray, world: int) -> Tuple[np.ndarray, np.ndarray]:
-    """(b_lo, nb) per rank: contiguous ranges of the 256 top-8-bit buckets with
-    ~1/world of the k-mers each (plan_lut over the buckets)."""
-    lut = plan_lut(np.asarray(global_counts, np.uint64), world).astype(np.int64)
-    nb = np.bincount(lut, minlength=world).astype(np.int64)
-    b_lo = np.concatenate([[0], np.cumsum(nb)[:-1]]).astype(np.int64)
-    return b_lo, nb
+# ------------------------------------------------------------------ comms
 
 
 class RcclComm:
-    """Executes a region step's collectives with RCCL on the context's stream."""
+    """Executes one rank's collectives with RCCL on the context's stream."""
 
-    def __init__(self, dev: engine.Device, world: int):
-        self.dev, self.world = dev, world
-        self.d_vec = dev.alloc(8 * 512)
-        self.d_mat = dev.alloc(8 * 256 * world)
+    def __init__(self, dev: engine.Device, world: int, rank: int, uid: bytes):
+        self.dev, self.world, self.rank = dev, world, rank
+        idb = ctypes.create_string_buffer(bytes(uid), 128)
+        N.check(dev.ctx, N.lib().kman_comm_init(dev.ctx, idb, world, rank), "kman_comm_init")
+        self.cap = 0
+        self.d_vec = self.d_mat = None
+
+    def _bufs(self, n: int) -> None:
+        if n > self.cap:
+            for b in (self.d_vec, self.d_mat):
+                if b is not None:
+                    b.free()
+            self.cap = max(n, 1024)
+            self.d_vec = self.dev.alloc(8 * self.cap)
+            self.d_mat = self.dev.alloc(8 * self.cap * self.world)
 
     def allreduce(self, x: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(x, np.uint64)
+        self._bufs(len(x))
         self.dev.upload(self.d_vec, x)
         N.check(self.dev.ctx, N.lib().kman_allreduce_u64(self.dev.ctx, c_void_p(self.d_vec.ptr), len(x)), "allreduce")
         return self.dev.download(self.d_vec, len(x), np.uint64)
 
     def allgather(self, x: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(x, np.uint64)
+        self._bufs(len(x))
         self.dev.upload(self.d_vec, x)
         N.check(self.dev.ctx, N.lib().kman_allgather_u64(self.dev.ctx, c_void_p(self.d_vec.ptr),
                                                           c_void_p(self.d_mat.ptr), len(x)), "allgather")
         return self.dev.download(self.d_mat, len(x) * self.world, np.uint64).reshape(self.world, len(x))
 
-    def alltoallv(self, send, sc, so, recv, rc, ro) -> None:
-        N.check(self.dev.ctx, N.lib().kman_alltoallv(self.dev.ctx, c_void_p(send.ptr), _u64p(sc), _u64p(so),
-                                                      c_void_p(recv.ptr), _u64p(rc), _u64p(ro), 8), "alltoallv")
+    def alltoallv(self, send, sc, so, recv, rc, ro, eb=8) -> None:
+        N.check(self.dev.ctx, N.lib().kman_alltoallv(self.dev.ctx, c_void_p(send), _u64p(sc), _u64p(so),
+                                                      c_void_p(recv), _u64p(rc), _u64p(ro), eb), "alltoallv")
 
     def run(self, gen):
-        """Drive one rank's step generator to its result."""
+        """Drive this rank's generator to its result."""
         try:
             req = next(gen)
             while True:
@@ -153,25 +233,34 @@ class RcclComm:
             return e.value
 
     def free(self) -> None:
-        self.d_vec.free()
-        self.d_mat.free()
+        N.lib().kman_comm_destroy(self.dev.ctx)
+        for b in (self.d_vec, self.d_mat):
+            if b is not None:
+                b.free()
 
 
 class SimGroup:
-    """G ranks of region steps in ONE process on one GPU (tests): collectives
-    are computed on the host and the all-to-all is device-to-device copies."""
+    """G ranks in ONE process on one GPU (tests): collectives computed on the
+    host, the all-to-all as device-to-device copies."""
 
     def __init__(self, pipes):
         self.pipes = pipes
 
-    def step(self):
-        gens = [p._region_step() for p in self.pipes]
-        reqs = [next(g) for g in gens]
+    def run(self, make_gen):
+        gens = [make_gen(p) for p in self.pipes]
         results = [None] * len(gens)
-        live = list(range(len(gens)))
+        reqs = [None] * len(gens)
+        live = []
+        for i, g in enumerate(gens):
+            try:
+                reqs[i] = next(g)
+                live.append(i)
+            except StopIteration as e:
+                results[i] = e.value
         while live:
             op = reqs[live[0]][0]
             assert all(reqs[i][0] == op for i in live), "ranks diverged"
+            assert len(live) == len(gens), "a rank finished early"
             if op == "allreduce":
                 tot = sum(np.asarray(reqs[i][1], np.uint64) for i in live)
                 outs = [tot.copy() for _ in live]
@@ -182,14 +271,13 @@ class SimGroup:
                 L = N.lib()
                 for dst in live:
                     pd = self.pipes[dst]
-                    _, _, _, recv, rcnt, roff = reqs[dst][1]
+                    _, _, _, recv, rcnt, roff, eb = reqs[dst][1]
                     for src in live:
                         send, scnt, soff = reqs[src][1][:3]
                         c = int(scnt[dst])
                         if c:
-                            N.check(pd.dev.ctx, L.kman_memcpy_d2d(pd.dev.ctx, c_void_p(recv.ptr + 8 * int(roff[src])),
-                                                                   c_void_p(send.ptr + 8 * int(soff[dst])), 8 * c),
-                                    "d2d")
+                            N.check(pd.dev.ctx, L.kman_memcpy_d2d(pd.dev.ctx, c_void_p(recv + eb * int(roff[src])),
+                                                                   c_void_p(send + eb * int(soff[dst])), eb * c), "d2d")
                     pd.dev.sync()
                 outs = [None for _ in live]
             nxt = []
@@ -202,199 +290,284 @@ class SimGroup:
             live = nxt
         return results
 
+    def step(self):
+        return self.run(lambda p: p.step_gen())
+
+
+# --------------------------------------------------------------- pipeline
+
+
+class _Grow:
+    """A device buffer that grows (never shrinks) to the largest request."""
+
+    def __init__(self, dev: engine.Device):
+        self.dev, self.buf = dev, None
+
+    def get(self, nbytes: int) -> engine.DeviceBuffer:
+        if self.buf is None or self.buf.nbytes < nbytes:
+            if self.buf is not None:
+                self.buf.free()
+                self.buf = None
+            self.buf = self.dev.alloc(max(nbytes, 64))
+        return self.buf
+
+    def free(self) -> None:
+        if self.buf is not None:
+            self.buf.free()
+            self.buf = None
+
 
 class DistPipeline:
-    """Resident multi-GPU pipeline for one FASTA shard per rank (bench.py).
+    """One rank of the multi-GPU join (bench.py, CLI, tests).
 
-    ``step()`` = the region path across ranks (``_region_step``), or with
-    path="split" / after a collective fallback: parse -> extract -> prefix
-    hist -> all-reduce -> partition -> all-to-all -> sort -> count|uniq,
-    leaving rank-local results on device."""
+    reader: the whole FASTA (shard.BytesReader / PinnedReader / SynthReader);
+    every rank cuts the same shards and loads its own.  uid: the RCCL id
+    (None: the caller drives the generators, SimGroup).  canonical: keys
+    min(fwd, rc) (config 5).  path: "region" (default; per-round fallback to
+    the general path) or "general".  max_round_items: force more rounds
+    (tests).  reload: re-upload + re-parse the shard in every step (the
+    pinned-host benchmark line)."""
 
-    def __init__(self, dev: engine.Device, text: bytes, k: int, mode: str, world: int, rank: int,
-                 uid: Optional[bytes], slack: float = 1.25, path: str = "region", n_bases_q: Optional[int] = None):
+    def __init__(self, dev: engine.Device, reader, k: int, mode: str, world: int, rank: int,
+                 uid: Optional[bytes] = None, canonical: bool = False, rc: bool = False, path: str = "region",
+                 max_round_items: Optional[int] = None, chunk_bytes: int = 256 << 20, reload: bool = False,
+                 mem_frac: float = 0.85):
         engine._check_k(k)
+        if mode not in ("count", "uniq"):
+            raise ValueError(mode)
+        if canonical and mode != "count":
+            raise ValueError("canonical k-mers are counted (config 5), not uniq'd")
         self.dev, self.k, self.mode, self.world, self.rank = dev, k, mode, world, rank
-        L = N.lib()
-        self.sim = uid is None  # SimGroup (tests): no RCCL, no split fallback
-        if not self.sim:
-            idb = ctypes.create_string_buffer(bytes(uid), 128)
-            N.check(dev.ctx, L.kman_comm_init(dev.ctx, idb, world, rank), "kman_comm_init")
-        self.comm = None if self.sim else RcclComm(dev, world)
-        self.local = engine.ResidentPipeline(dev, text, k, mode=mode, rc=False, pos_bytes=8, path="split")
-        self.path = path
-        self.rwork = self.send = self.recv = None
-        if path == "region":
-            self._region_init(n_bases_q)
-        self.hb = hist_bits(k)
-        self.hshift = 2 * k - self.hb
-        self.d_hist = dev.alloc(8 << self.hb)
-        self.d_ghist = dev.alloc(8 << self.hb)
-        self.d_lut = dev.alloc(1 << self.hb)
-        self.d_cnt = dev.alloc(8 * world)
-        self.d_cmat = dev.alloc(8 * world * world)
-        cap = int(self.local.bound * slack) + (1 << 20)
-        self.cap = cap
-        self.recv_keys = dev.alloc(8 * cap)
-        self.recv_alt = dev.alloc(8 * cap)
-        want_pos = mode == "uniq"
-        self.recv_pos = dev.alloc(8 * cap) if want_pos else None
-        self.recv_pos_alt = dev.alloc(8 * cap) if want_pos else None
-        self.out_keys = dev.alloc(8 * cap)
-        self.out_vals = dev.alloc(8 * cap)
-        self.n_local = 0
-        self.n_recv = 0
-        self.n_out = 0
-        self.sorted_in_alt = False
+        self.canonical, self.rc = canonical, rc and not canonical
+        self.path, self.max_round_items, self.reload, self.mem_frac = path, max_round_items, reload, mem_frac
+        self.fmode = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
+        self.flags = engine.flags_for(self.rc, mode == "uniq", canonical)
+        self.reader = reader
+        self.spec = S.shard_specs(reader, world, k)[rank]
+        self.loader = S.ShardLoader(dev, reader, self.spec, k, chunk_bytes)
+        self.shard = self.loader.load()
+        self.comm = RcclComm(dev, world, rank, uid) if uid is not None else None
+        self.d_hist = dev.alloc(4 * NB * RS)
+        self.d_rtab = dev.alloc(8 * NB * RS)
+        self.d_small = dev.alloc(8 * 16384)  # prefix / abundance histograms
+        self.arena_a, self.arena_b = _Grow(dev), _Grow(dev)
+        self.out_keys, self.out_vals = _Grow(dev), _Grow(dev)
+        self.gen_bufs = [_Grow(dev) for _ in range(6)]  # general path: send/recv keys, pos, alt keys, alt pos
+        self.n_local = self.n_out = self.n_recv = 0
+        self.rounds = 0
+        self.fallback_rounds = 0
+        self.ready = False
+        if self.comm is not None:
+            self.comm.run(self.setup_gen())
 
-    # ------------------------------------------------------------ region path
-    def _region_init(self, n_bases_q: Optional[int]) -> None:
-        L, dev = N.lib(), self.dev
-        lp = self.local
-        lp._parse()
-        self.n_bases = lp.n_bases
-        if n_bases_q is None:  # every rank's n_bases, all-reduced (one-hot)
-            v = np.zeros(self.world, np.uint64)
-            v[self.rank] = self.n_bases
-            n_bases_q = int(self.comm.allreduce(v).max())
-        self.n_bases_q = n_bases_q
-        self.rmode = N.KMAN_FINISH_UNIQ if self.mode == "uniq" else N.KMAN_FINISH_COUNT
-        self.rflags = engine.flags_for(False, self.mode == "uniq")
-        wb = c_uint64(0)
-        ok = L.kman_dgroups_plan(self.n_bases, n_bases_q, self.k, self.rflags, self.rmode, self.world, byref(wb))
-        if not self.sim:  # every rank must take the same path
-            ok = int(self.comm.allreduce(np.array([0 if ok == N.KMAN_OK else 1], np.uint64))[0])
-        if ok != N.KMAN_OK:
-            self.path = "split"
-            return
-        self.rwork_bytes = int(wb.value)
-        self.rwork = dev.alloc(self.rwork_bytes)
-        self.send = dev.alloc(8 * max(self.n_bases, 1))
-        self.recv_cap = int(1.3 * n_bases_q) + (1 << 20)  # ~1/G of the k-mers of G shards of <= n_bases_q
-        self.recv = dev.alloc(8 * self.recv_cap)
-        self.out_keys_r = dev.alloc(8 * self.recv_cap)
-        self.out_vals_r = dev.alloc(8 * self.recv_cap)
+    # ---------------------------------------------------------------- setup
+    def setup_gen(self):
+        """Collectives of the first step: global record table, common pos
+        bound, path agreement, common memory budget."""
+        sh, G = self.shard, self.world
+        R = len(sh.names)
+        nlen = sum(len(x) for x in sh.names)
+        ok = 1 if self.path == "region" else 0
+        M = yield ("allgather", np.array([sh.n_own, sh.n_eff, R, nlen], np.uint64))
+        self.n_own_all = M[:, 0].astype(np.int64)
+        self.n_bases_q = max(1, int(M[:, 1].max()))
+        self.base_off = np.concatenate([[0], np.cumsum(self.n_own_all)[:-1]]).astype(np.uint64)
+        if ok and N.lib().kman_dshard_plan(sh.n_eff, self.n_bases_q, self.k, self.flags, self.fmode) != N.KMAN_OK:
+            ok = 0
+        # record table: every rank's record first bases and names
+        rmax, lmax = int(M[:, 2].max()), int(M[:, 3].max())
+        seqs = np.zeros(rmax + 1, np.uint64)
+        seqs[:R] = sh.rec_seq
+        seqs_all = yield ("allgather", seqs)
+        lens = np.zeros(rmax + 1, np.uint64)
+        lens[:R] = [len(x) for x in sh.names]
+        lens_all = yield ("allgather", lens)
+        blob = np.zeros((lmax + 7) // 8 + 1, np.uint64)
+        bb = b"".join(sh.names)
+        blob.view(np.uint8)[:len(bb)] = np.frombuffer(bb, np.uint8)
+        blobs = yield ("allgather", blob)
+        names, rec_seq = [], []
+        for q in range(G):
+            raw = blobs[q].view(np.uint8).tobytes()
+            at = 0
+            for j in range(int(M[q, 2])):
+                ln = int(lens_all[q, j])
+                names.append(raw[at:at + ln])
+                at += ln
+                rec_seq.append(int(seqs_all[q, j]) + int(self.base_off[q]))
+        self.names, self.g_rec_seq = names, np.asarray(rec_seq, dtype=np.uint64)
+        self.n_bases_total = int(self.n_own_all.sum())
+        # empty record names with a k-mer raise before any output (seq.py:106-127)
+        flag = np.array([0 if ok else 1, self._empty_name_kmer()], np.uint64)
+        f = yield ("allreduce", flag)
+        if int(f[1]):
+            raise AssertionError("incompatible string: a record with an empty name yields k-mers")
+        self.path = "region" if int(f[0]) == 0 else "general"
+        free, _ = engine.mem_info(self.dev)
+        bud = yield ("allgather", np.array([int(free * self.mem_frac)], np.uint64))
+        self.budget = int(bud.min())
+        self.ready = True
 
-    def _region_step(self):
-        """One step as a generator of collectives: ("allreduce", host u64
-        array) -> summed array; ("allgather", array) -> (world, len) matrix;
-        ("alltoallv", args) -> None.  Returns n_kmers of the local shard, or
-        None when the ranks agreed to fall back."""
-        L, ctx, dev = N.lib(), self.dev.ctx, self.dev
-        lp = self.local
-        lp._parse()
-        counts = np.zeros(256, np.uint64)
-        ovf = ctypes.c_uint32(0)
-        N.check(ctx, L.kman_dgroups_extract(ctx, c_void_p(lp.codes.ptr), lp.n_bases, self.n_bases_q, self.k,
-                                             self.rflags, self.rmode, self.world, c_void_p(self.rwork.ptr),
-                                             self.rwork_bytes, c_void_p(self.send.ptr), _u64p(counts), byref(ovf)),
-                "kman_dgroups_extract")
-        g = yield ("allreduce", np.concatenate([counts, [ovf.value]]).astype(np.uint64))
-        if g[256]:
-            return None
-        b_lo, nb = bucket_ranges(g[:256], self.world)
-        C = yield ("allgather", counts)  # C[src][bucket]
-        # every rank checks every rank's receive size and bucket count: one decision
-        per_rank = np.array([C[:, b_lo[q]:b_lo[q] + nb[q]].sum() for q in range(self.world)], np.uint64)
-        if (per_rank > self.recv_cap).any() or (nb > nb_max(self.world)).any():
-            return None
-        sc = np.array([counts[b_lo[q]:b_lo[q] + nb[q]].sum() for q in range(self.world)], np.uint64)
-        so = np.concatenate([[0], np.cumsum(sc)[:-1]]).astype(np.uint64)
-        me_lo, me_nb = int(b_lo[self.rank]), int(nb[self.rank])
-        mine = np.ascontiguousarray(C[:, me_lo:me_lo + me_nb], np.uint64)  # [src][j]
-        rcnt = mine.sum(axis=1).astype(np.uint64)
-        roff = np.concatenate([[0], np.cumsum(rcnt)[:-1]]).astype(np.uint64)
-        yield ("alltoallv", (self.send, sc, so, self.recv, rcnt, roff))
-        self.n_recv = int(rcnt.sum())
-        out = c_uint64(0)
-        r = L.kman_dgroups_finish(ctx, c_void_p(self.recv.ptr), lp.n_bases, self.n_bases_q, self.k, self.rflags,
-                                  self.rmode, self.world, me_lo, me_nb, _u64p(mine.reshape(-1)),
-                                  c_void_p(self.rwork.ptr), self.rwork_bytes, c_void_p(self.out_keys_r.ptr),
-                                  c_void_p(self.out_vals_r.ptr), 8, byref(out))
-        fb = 1 if r == N.KMAN_EFALLBACK else 0
-        if not fb:
-            N.check(ctx, r, "kman_dgroups_finish")
-        f = yield ("allreduce", np.array([fb], np.uint64))
-        if f[0]:
-            return None
-        self.n_out = int(out.value)
-        self.n_local = int(sum(counts))
-        self._out = (self.out_keys_r, self.out_vals_r)
+    def _empty_name_kmer(self) -> int:
+        """1 when a record that starts in this shard has an empty name and
+        yields a window (checked on this shard's own codes; a record that
+        continues past the shard is checked on its first shard's part)."""
+        sh = self.shard
+        for j, nm in enumerate(sh.names):
+            if nm:
+                continue
+            b = int(sh.rec_seq[j])
+            e = int(sh.rec_seq[j + 1]) if j + 1 < len(sh.names) else sh.n_eff
+            if e - b >= self.k:
+                codes = self.dev.download(sh.codes, e - b, np.uint8, offset=b)
+                if engine.first_window(codes, self.k) >= 0:
+                    return 1
+        return 0
+
+    # ----------------------------------------------------------------- step
+    def step(self) -> int:
+        if self.comm is None:
+            raise RuntimeError("a simulated rank is stepped by SimGroup")
+        return self.comm.run(self.step_gen())
+
+    def step_gen(self):
+        if not self.ready:
+            yield from self.setup_gen()
+        L, ctx, dev, sh = N.lib(), self.dev.ctx, self.dev, self.shard
+        if self.reload:
+            self.shard = sh = self.loader.load()
+        G, me = self.world, self.rank
+        # 1. (bucket, segment) counts of the shard, bucket totals all-gathered
+        H = np.zeros(NB * RS, np.uint32)
+        if self.path == "region":
+            N.check(ctx, L.kman_dshard_hist(ctx, c_void_p(sh.codes.ptr), sh.n_eff, self.n_bases_q, self.k, self.flags,
+                                            self.fmode, c_void_p(self.d_hist.ptr), H.ctypes.data_as(c_void_p)),
+                    "kman_dshard_hist")
+            c_local = H.reshape(NB, RS).sum(axis=1).astype(np.uint64)
+        else:
+            c_local = self._prefix_hist()
+        C = yield ("allgather", c_local)
+        self.n_local = int(c_local.sum())
+        # 2. rounds
+        pl = RoundPlanner(self.k, self.flags, self.fmode, G, self.n_bases_q)
+        tot = int(np.asarray(C, np.uint64).sum())
+        out_bytes = (8 + self._vb(C)) * (tot if G == 1 else int(tot * 1.1 / G) + (1 << 20))
+        R, cuts, a_need, b_need = pl.plan(C, max(1, self.budget - out_bytes), self.max_round_items)
+        self.rounds = R
+        _, recv = round_sizes(C, cuts, G, R)
+        cap = int(recv[me].sum())
+        vb = self._vb(C)
+        ok_, ov_ = self.out_keys.get(8 * max(cap, 1)), self.out_vals.get(vb * max(cap, 1))
+        n_out = 0
+        self.fallback_rounds = 0
+        for r in range(R):
+            if self.path == "region":
+                A, B = self.arena_a.get(a_need), self.arena_b.get(b_need)
+                rtab, sc, so = round_send(H, cuts, G, R, r)
+                dev.upload(self.d_rtab, rtab)
+                N.check(ctx, L.kman_dshard_extract(ctx, c_void_p(sh.codes.ptr), sh.n_eff, self.n_bases_q, self.k,
+                                                   self.flags, self.fmode, c_void_p(self.d_hist.ptr),
+                                                   c_void_p(self.d_rtab.ptr), c_void_p(A.ptr)), "kman_dshard_extract")
+                lo, nb, counts, rcnt, roff = round_recv(C, cuts, R, me, r)
+                yield ("alltoallv", (A.ptr, sc, so, B.ptr, rcnt, roff, 8))
+                got = c_uint64(0)
+                ret = L.kman_dround_finish(ctx, c_void_p(B.ptr), self.k, self.flags, self.fmode, G, self.n_bases_q,
+                                           lo, nb, _u64p(np.ascontiguousarray(counts.reshape(-1))),
+                                           c_void_p(A.ptr), A.nbytes, c_void_p(B.ptr), B.nbytes,
+                                           c_void_p(ok_.ptr + 8 * n_out), c_void_p(ov_.ptr + vb * n_out), vb,
+                                           byref(got))
+                fb = 1 if ret == N.KMAN_EFALLBACK else 0
+                if not fb:
+                    N.check(ctx, ret, "kman_dround_finish")
+                f = yield ("allreduce", np.array([fb], np.uint64))
+                if int(f[0]) == 0:
+                    n_out += int(got.value)
+                    continue
+                self.fallback_rounds += 1
+            # the general path for this round (every rank together)
+            n_out += yield from self._general_round(C, cuts, R, r, ok_, ov_, n_out, vb)
+        self.n_out = n_out
+        self.n_recv = cap
+        self._out = (ok_, ov_, vb)
         return self.n_local
 
-    def step(self) -> int:
-        if self.path == "region":
-            n = self.comm.run(self._region_step())
-            if n is not None:
-                return n
-            self.path = "split"  # agreed by every rank
-        return self._step_split()
+    def _vb(self, C) -> int:
+        if self.mode == "uniq":
+            return 8
+        return 4 if int(np.asarray(C, np.uint64).sum()) <= 0xFFFFFFFF else 8
 
-    def _step_split(self) -> int:
-        L, ctx, dev = N.lib(), self.dev.ctx, self.dev
-        lp = self.local
-        n = lp.extract_only()
-        self.n_local = n
-        if self.mode == "uniq":  # tag payloads with the source rank
-            N.check(ctx, L.kman_or_u64(ctx, c_void_p(lp.pos.ptr), n, self.rank << RANK_SHIFT), "tag")
-        # 1-2. prefix histogram, all-reduced
-        dev.memset(self.d_hist, 0, 8 << self.hb)
-        N.check(ctx, L.kman_prefix_hist(ctx, c_void_p(lp.keys.ptr), n, self.hshift, self.hb,
-                                         c_void_p(self.d_hist.ptr)), "prefix_hist")
-        N.check(ctx, L.kman_memcpy_d2d(ctx, c_void_p(self.d_ghist.ptr), c_void_p(self.d_hist.ptr), 8 << self.hb),
-                "d2d")
-        N.check(ctx, L.kman_allreduce_u64(ctx, c_void_p(self.d_ghist.ptr), 1 << self.hb), "allreduce")
-        ghist = dev.download(self.d_ghist, 1 << self.hb, np.uint64)
-        lhist = dev.download(self.d_hist, 1 << self.hb, np.uint64)
-        # 3. plan
-        lut = plan_lut(ghist, self.world)
-        dev.upload(self.d_lut, lut)
-        counts = bucket_counts(lhist, lut, self.world)
-        # 4. stable partition by destination
-        vb = 8 if self.mode == "uniq" else 0
-        N.check(ctx, L.kman_partition(ctx, c_void_p(lp.keys.ptr), c_void_p(lp.alt.ptr),
-                                       c_void_p(lp.pos.ptr if vb else None), c_void_p(lp.pos_alt.ptr if vb else None),
-                                       vb, n, c_void_p(self.d_lut.ptr), self.hshift, self.world, _u64p(counts)),
-                "partition")
-        # 5. counts exchange, then the data
-        dev.upload(self.d_cnt, counts)
-        N.check(ctx, L.kman_allgather_u64(ctx, c_void_p(self.d_cnt.ptr), c_void_p(self.d_cmat.ptr), self.world),
-                "allgather")
-        C = dev.download(self.d_cmat, self.world * self.world, np.uint64).reshape(self.world, self.world)
-        send, send_off, recv, recv_off = recv_layout(C, self.rank)
-        nrecv = int(recv.sum())
-        # every rank holds C: all of them see the same overflow and raise
-        # before the exchange (a lone raise would leave the peers hanging in it)
-        over = split_overflow(C, self.cap)
-        if over is not None:
-            raise RuntimeError("rank %d would receive %d keys > capacity %d (prefix skew)" % (over[0], over[1], self.cap))
-        N.check(ctx, L.kman_alltoallv(ctx, c_void_p(lp.alt.ptr), _u64p(send), _u64p(send_off),
-                                       c_void_p(self.recv_keys.ptr), _u64p(recv), _u64p(recv_off), 8), "alltoallv")
-        if vb:
-            N.check(ctx, L.kman_alltoallv(ctx, c_void_p(lp.pos_alt.ptr), _u64p(send), _u64p(send_off),
-                                           c_void_p(self.recv_pos.ptr), _u64p(recv), _u64p(recv_off), 8),
-                    "alltoallv")
-        self.n_recv = nrecv
-        # 6. local prefix sort + finish (segments sorted in LDS, count | uniq)
+    def _prefix_hist(self) -> np.ndarray:
+        """Top-8-bit bucket totals of the shard (general path)."""
+        if self.canonical:
+            raise NotImplementedError("canonical keys with k > 25 across ranks")
+        sh = self.shard
+        h = self.d_small
+        n = c_uint64(0)
+        N.check(self.dev.ctx, N.lib().kman_kmer_prefix_hist(self.dev.ctx, c_void_p(sh.codes.ptr), sh.n_eff, self.k,
+                                                            N.KMAN_RC if self.rc else 0, c_void_p(h.ptr), byref(n)),
+                "kman_kmer_prefix_hist")
+        bins = NB if 2 * self.k >= 8 else 1 << (2 * self.k)
+        out = np.zeros(NB, np.uint64)
+        out[:bins] = self.dev.download(h, bins, np.uint64)
+        return out
+
+    def _general_round(self, C, cuts, R, r, ok_, ov_, n_out, vb):
+        """Round r through key ranges: per destination q, kman_extract_range
+        of part (q, r) into the send buffers; the keys (+ pos tagged with the
+        source rank) exchanged; kman_sort_range + kman_finish appended to the
+        output.  Generator; returns the rows written."""
+        L, ctx, dev, sh = N.lib(), self.dev.ctx, self.dev, self.shard
+        G, me, k = self.world, self.rank, self.k
+        uniq = self.mode == "uniq"
+        send, recv = round_sizes(C, cuts, G, R)
+        ns, nr = int(send[me, r]), int(recv[me, r])
+        sk, rk, ak = (self.gen_bufs[i].get(8 * max(1, n)) for i, n in ((0, ns), (1, nr), (2, nr)))
+        sp = rp = ap = None
+        if uniq:
+            sp, rp, ap = (self.gen_bufs[i].get(8 * max(1, n)) for i, n in ((3, ns), (4, nr), (5, nr)))
+        shift = max(0, 2 * k - 8)
+        sc = np.zeros(G, np.uint64)
+        at = 0
+        flags = engine.flags_for(self.rc, uniq, self.canonical)
+        for q in range(G):
+            lo, hi = part_of(cuts, R, q, r)
+            want = int(np.asarray(C, np.uint64)[me, lo:hi].sum())
+            if want:
+                got = c_uint64(0)
+                key_hi = (hi << shift) - 1 if hi < NB else (1 << (2 * k)) - 1
+                N.check(ctx, L.kman_extract_range(ctx, c_void_p(sh.codes.ptr), sh.n_eff, k, flags, lo << shift, key_hi,
+                                                  c_void_p(sk.ptr + 8 * at), c_void_p(sp.ptr + 8 * at) if uniq else None,
+                                                  8, want, None, byref(got)), "kman_extract_range")
+                if int(got.value) != want:
+                    raise RuntimeError("rank %d part (%d, %d): %d k-mers, histogram said %d"
+                                       % (me, q, r, got.value, want))
+                if uniq:
+                    N.check(ctx, L.kman_or_u64(ctx, c_void_p(sp.ptr + 8 * at), want, me << RANK_SHIFT), "tag")
+            sc[q] = want
+            at += want
+        so = np.concatenate([[0], np.cumsum(sc)[:-1]]).astype(np.uint64)
+        _, _, _, rcnt, roff = round_recv(C, cuts, R, me, r)
+        yield ("alltoallv", (sk.ptr, sc, so, rk.ptr, rcnt, roff, 8))
+        if uniq:
+            yield ("alltoallv", (sp.ptr, sc, so, rp.ptr, rcnt, roff, 8))
+        if nr == 0:
+            return 0
         res = c_int(0)
-        lo = engine.split_bits(nrecv, 2 * self.k)
-        rp = c_void_p(self.recv_pos.ptr if vb else None)
-        rpa = c_void_p(self.recv_pos_alt.ptr if vb else None)
-        N.check(ctx, L.kman_sort_range(ctx, c_void_p(self.recv_keys.ptr), c_void_p(self.recv_alt.ptr), rp, rpa, vb,
-                                       nrecv, lo, 2 * self.k, None, byref(res)), "kman_sort_range")
-        self.sorted_in_alt = bool(res.value)
-        skeys, okeys = (self.recv_alt, self.recv_keys) if res.value else (self.recv_keys, self.recv_alt)
-        spos, opos = (rpa, rp) if res.value else (rp, rpa)
+        lo_bit = engine.split_bits(nr, 2 * k)
+        vbytes = 8 if uniq else 0
+        N.check(ctx, L.kman_sort_range(ctx, c_void_p(rk.ptr), c_void_p(ak.ptr), c_void_p(rp.ptr) if uniq else None,
+                                       c_void_p(ap.ptr) if uniq else None, vbytes, nr, lo_bit, 2 * k, None, byref(res)),
+                "kman_sort_range")
+        keys, alt = (ak, rk) if res.value else (rk, ak)
+        pos, palt = ((ap, rp) if res.value else (rp, ap)) if uniq else (None, None)
         out = c_uint64(0)
-        mode = N.KMAN_FINISH_COUNT if self.mode == "count" else N.KMAN_FINISH_UNIQ
-        N.check(ctx, L.kman_finish(ctx, c_void_p(skeys.ptr), c_void_p(okeys.ptr), spos, opos, vb, nrecv, 2 * self.k,
-                                   lo, mode, c_void_p(self.out_keys.ptr), c_void_p(self.out_vals.ptr), 8, byref(out)),
+        N.check(ctx, L.kman_finish(ctx, c_void_p(keys.ptr), c_void_p(alt.ptr), c_void_p(pos.ptr) if uniq else None,
+                                   c_void_p(palt.ptr) if uniq else None, vbytes, nr, 2 * k, lo_bit, self.fmode,
+                                   c_void_p(ok_.ptr + 8 * n_out), c_void_p(ov_.ptr + vb * n_out), vb, byref(out)),
                 "kman_finish")
-        self.n_out = int(out.value)
-        self._out = (self.out_keys, self.out_vals)
-        return n
+        return int(out.value)
 
-    # bench.py interface (same as engine.ResidentPipeline)
+    # -------------------------------------------------------------- results
     @property
     def n_kmers(self) -> int:
         return self.n_local
@@ -403,31 +576,92 @@ class DistPipeline:
     def n_sorted(self) -> int:
         return self.n_recv
 
+    def results(self):
+        """Rank-local (keys, counts | pos) on the host; uniq pos keep the
+        source rank in bits 56-63 (tests)."""
+        ok_, ov_, vb = self._out
+        keys = self.dev.download(ok_, self.n_out, np.uint64)
+        vals = self.dev.download(ov_, self.n_out, np.uint32 if vb == 4 else np.uint64).astype(np.uint64)
+        return keys, vals
+
+    def hist_gen(self, nbins: int = 10001):
+        """Abundance spectrum of the global counts: local kman_count_hist of
+        this rank's rows, all-reduced (config 5).  Generator."""
+        ok_, ov_, vb = self._out
+        if nbins > 16384:
+            raise ValueError("at most 16384 histogram bins")
+        d_h = self.d_small
+        N.check(self.dev.ctx, N.lib().kman_count_hist(self.dev.ctx, c_void_p(ov_.ptr), vb, self.n_out,
+                                                      c_void_p(d_h.ptr), nbins), "kman_count_hist")
+        h = self.dev.download(d_h, nbins, np.uint64)
+        return (yield ("allreduce", h))
+
+    def global_parsed(self) -> engine.Parsed:
+        """The all-gathered record table as a Parsed (for the uniq formatter;
+        no codes)."""
+        names = self.names
+        name_off = np.zeros(len(names) + 1, dtype=np.uint64)
+        if names:
+            name_off[1:] = np.cumsum([len(x) for x in names], dtype=np.uint64)
+        return engine.Parsed(self.dev, None, self.n_bases_total, len(names), np.zeros(len(names), np.uint64),
+                             self.g_rec_seq, names, b"".join(names), name_off)
+
+    def text(self) -> bytes:
+        """This rank's slice of the reference's output text (count rows, or
+        uniq records with global headers), built on the device."""
+        ok_, ov_, vb = self._out
+        if self.mode == "count":
+            r = engine.CountResult(ok_, ov_, vb, self.n_out, self.k)
+            return bytes(engine.emit_count(self.dev, r) or b"")
+        pos = self.dev.alloc(8 * max(1, self.n_out))
+        try:
+            N.check(self.dev.ctx, N.lib().kman_memcpy_d2d(self.dev.ctx, c_void_p(pos.ptr), c_void_p(ov_.ptr),
+                                                          8 * self.n_out), "d2d")
+            off = np.ascontiguousarray(self.base_off, dtype=np.uint64)
+            N.check(self.dev.ctx, N.lib().kman_rebase_pos(self.dev.ctx, c_void_p(pos.ptr), self.n_out, _u64p(off),
+                                                          self.world), "kman_rebase_pos")
+            r = engine.UniqResult(ok_, pos, 8, self.n_out, self.k)
+            return bytes(engine.emit_uniq(self.global_parsed(), r) or b"")
+        finally:
+            pos.free()
+
+    def emit_gen(self, path: str):
+        """Write the global output file: every rank formats its rows, the text
+        sizes are all-gathered and each rank writes at its offset (the ranks'
+        texts in rank order = the reference's output).  Generator."""
+        t = self.text()
+        sizes = yield ("allgather", np.array([len(t)], np.uint64))
+        off = int(sizes[:self.rank, 0].sum())
+        total = int(sizes[:, 0].sum())
+        fd = os.open(path, os.O_WRONLY | os.O_CREAT, 0o644)
+        try:
+            if self.rank == 0:
+                os.ftruncate(fd, total)
+            if t:
+                os.pwrite(fd, t, off)
+        finally:
+            os.close(fd)
+        yield ("allreduce", np.zeros(1, np.uint64))  # every slice written before anyone reads
+        return total
+
+    # bench.py interface
     pos_bytes = 8
 
     def timing(self, enable: bool) -> None:
-        self.local.timing(enable)
+        N.check(self.dev.ctx, N.lib().kman_timing_enable(self.dev.ctx, 1 if enable else 0), "timing")
 
     def timed(self, tag: str):
-        return self.local.timed(tag)
-
-    def results(self):
-        """Rank-local (keys, counts|pos) on the host (tests)."""
-        ok, ov = self._out
-        keys = self.dev.download(ok, self.n_out, np.uint64)
-        vals = self.dev.download(ov, self.n_out, np.uint64)
-        return keys, vals
+        n, ms = c_uint64(0), ctypes.c_double(0)
+        N.check(self.dev.ctx, N.lib().kman_timing_query(self.dev.ctx, tag.encode(), byref(n), byref(ms)), "timing")
+        return int(n.value), float(ms.value)
 
     def free(self) -> None:
-        if not self.sim:
-            N.lib().kman_comm_destroy(self.dev.ctx)
+        if self.comm is not None:
             self.comm.free()
-        self.local.free()
-        for b in (self.d_hist, self.d_ghist, self.d_lut, self.d_cnt, self.d_cmat, self.recv_keys, self.recv_alt,
-                  self.recv_pos, self.recv_pos_alt, self.out_keys, self.out_vals, self.rwork, self.send, self.recv,
-                  getattr(self, "out_keys_r", None), getattr(self, "out_vals_r", None)):
-            if b is not None:
-                b.free()
+            self.comm = None
+        for b in [self.d_hist, self.d_rtab, self.d_small, self.arena_a, self.arena_b, self.out_keys, self.out_vals] + self.gen_bufs:
+            b.free()
+        self.loader.free()
 
 
 def unique_id() -> bytes:
@@ -438,37 +672,59 @@ def unique_id() -> bytes:
     return buf.raw
 
 
+__all__ = ["plan_lut", "part_cuts", "part_of", "round_send", "round_recv", "round_sizes", "RoundPlanner",
+           "DistPipeline", "RcclComm", "SimGroup", "unique_id", "rehearse", "List"]
+
+
 # ------------------------------------------------------------- CPU rehearsal
 
 
-def rehearse(keys: np.ndarray, vals: Optional[np.ndarray], k: int, world: int, rank: int, comm) -> Tuple:
-    """The same partition/exchange on host arrays with a ``comm`` object that
-    provides ``allreduce(np.ndarray)``, ``allgather(np.ndarray)`` and
-    ``alltoallv(list_of_arrays) -> list_of_arrays`` (gloo in the tests).
-    Returns this rank's sorted (keys, vals) after the exchange."""
-    hb = hist_bits(k)
-    shift = 2 * k - hb
-    lhist = np.bincount((keys >> np.uint64(shift)).astype(np.int64), minlength=1 << hb).astype(np.uint64)
-    ghist = comm.allreduce(lhist)
-    lut = plan_lut(ghist, world)
-    dest = lut[(keys >> np.uint64(shift)).astype(np.int64)]
-    order = np.argsort(dest, kind="stable")  # the stable partition kman_partition performs
-    counts = bucket_counts(lhist, lut, world)
-    assert (np.bincount(dest, minlength=world).astype(np.uint64) == counts).all()
-    C = comm.allgather(counts).reshape(world, world)
-    send, send_off, recv, recv_off = recv_layout(C, rank)
-    pk = keys[order]
-    parts = [pk[int(o):int(o + c)] for o, c in zip(send_off, send)]
-    got = comm.alltoallv(parts)
-    rk = np.concatenate(got) if got else np.zeros(0, np.uint64)
-    rv = None
-    if vals is not None:
-        pv = vals[order]
-        gv = comm.alltoallv([pv[int(o):int(o + c)] for o, c in zip(send_off, send)])
-        rv = np.concatenate(gv)
-    o2 = np.argsort(rk, kind="stable")
-    return rk[o2], (rv[o2] if rv is not None else None), lut
-
-
-__all__ = ["plan_lut", "bucket_counts", "recv_layout", "bucket_ranges", "nb_max", "DistPipeline", "RcclComm",
-           "SimGroup", "unique_id", "rehearse", "List"]
+def rehearse(keys: np.ndarray, k: int, world: int, rank: int, comm, n_bases_q: int, mode: str = "count",
+             canonical: bool = False, max_round_items: Optional[int] = None, budget: int = 1 << 62, fail=()):
+    """The planning and exchanges of DistPipeline.step_gen on host arrays
+    (tests/test_dist_cpu.py over gloo): bucket totals all-gathered, the same
+    RoundPlanner, per round the items of the round's buckets sent
+    destination-major as round_send lays them out, one all-to-all, the finish
+    by numpy; `fail` = {(rank, round)} raises a region overflow there, agreed
+    by an all-reduce exactly like the device path (the round is then redone as
+    a general round: the same keys by key range).  comm: allgather(a) ->
+    flat array, allreduce(a), alltoallv(list) -> list.  Returns (keys,
+    counts, R, cuts, rounds_redone)."""
+    shift = max(0, 2 * k - 8)
+    keys = np.asarray(keys, dtype=np.uint64)
+    b = (keys >> np.uint64(shift)).astype(np.int64)
+    c_local = np.bincount(b, minlength=NB).astype(np.uint64)
+    C = comm.allgather(c_local).reshape(world, NB)
+    fm = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
+    pl = RoundPlanner(k, engine.flags_for(False, mode == "uniq", canonical), fm, world, n_bases_q)
+    R, cuts, _, _ = pl.plan(C, budget, max_round_items)
+    outk, outc, redone = [], [], []
+    for r in range(R):
+        parts = []
+        for q in range(world):
+            lo, hi = part_of(cuts, R, q, r)
+            parts.append(keys[(b >= lo) & (b < hi)])
+        _, sc, _ = round_send(np.pad(c_local.reshape(NB, 1), ((0, 0), (0, RS - 1))), cuts, world, R, r)
+        assert [len(p) for p in parts] == sc.tolist(), "send layout disagrees with the histogram"
+        got = comm.alltoallv(parts)
+        _, _, _, rc, _ = round_recv(C, cuts, R, rank, r)
+        assert [len(g) for g in got] == rc.tolist(), "receive sizes disagree with the all-gathered counts"
+        f = comm.allreduce(np.array([1 if (rank, r) in fail else 0], np.uint64))
+        if int(f[0]):
+            redone.append(r)
+            # general round: destination q gets the key range of part (q, r)
+            parts = []
+            for q in range(world):
+                ql, qh = part_of(cuts, R, q, r)
+                sel = (keys >= np.uint64(ql << shift)) & (keys < np.uint64(qh << shift)) if qh > ql else np.zeros(
+                    len(keys), bool)
+                if qh == NB and qh > ql:
+                    sel = keys >= np.uint64(ql << shift)
+                parts.append(keys[sel])
+            got = comm.alltoallv(parts)
+        rk = np.sort(np.concatenate(got)) if got else np.zeros(0, np.uint64)
+        u, c = np.unique(rk, return_counts=True)
+        outk.append(u)
+        outc.append(c.astype(np.uint64))
+    return (np.concatenate(outk) if outk else np.zeros(0, np.uint64),
+            np.concatenate(outc) if outc else np.zeros(0, np.uint64), R, cuts, redone)

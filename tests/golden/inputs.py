@@ -62,6 +62,124 @@ def syn_numpy(n_bases: int, seed: int, record_len: int = 256 << 20, width: int =
     return b"".join(out)
 
 
+class SynthLayout:
+    """The ONE global synthetic FASTA of the multi-GPU benchmark (SURVEY §8d
+    config 4: byte-range sharded across ranks): records ``syn<i>`` of at most
+    record_len bases in lines of ``width`` bases; base j of the file is
+    "ACGT"[splitmix64(seed * 0xD1B54A32D192ED03 + j) >> 62], so any byte range
+    can be generated on its own -- here (synth_np) or on the device
+    (kman_synth_fasta, byte-identical)."""
+
+    def __init__(self, n_bases: int, seed: int, record_len: int = 256 << 20, width: int = 80):
+        self.n_bases, self.seed, self.width = int(n_bases), int(seed), int(width)
+        lens, hb, bb = [], [], []
+        at = bat = 0
+        left, r = self.n_bases, 0
+        while left > 0:
+            L = min(left, record_len)
+            hb.append(at)
+            bb.append(bat)
+            lens.append(L)
+            at += 5 + len(str(r)) + L + (L + width - 1) // width
+            bat += L
+            left -= L
+            r += 1
+        self.size = at
+        self.tab = np.array([v for t in zip(hb, bb, lens) for v in t], dtype=np.uint64)
+        self.n_records = len(lens)
+
+    def read(self, lo: int, hi: int) -> bytes:
+        return synth_np(self, lo, hi)
+
+
+_M64 = (1 << 64) - 1
+
+
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return x ^ (x >> np.uint64(31))
+
+
+def synth_np(lay: "SynthLayout", lo: int, hi: int) -> bytes:
+    """Bytes [lo, hi) of the global synthetic FASTA (numpy restatement of
+    kman_synth_fasta)."""
+    lo, hi = max(0, int(lo)), min(int(hi), lay.size)
+    if hi <= lo:
+        return b""
+    g = np.arange(lo, hi, dtype=np.uint64)
+    tab = lay.tab.reshape(-1, 3)
+    r = np.searchsorted(tab[:, 0], g, side="right").astype(np.int64) - 1
+    hb, bb, L = tab[r, 0], tab[r, 1], tab[r, 2]
+    rel = g - hb
+    nd = np.array([len(str(x)) for x in range(lay.n_records)], dtype=np.uint64)[r]
+    hl = np.uint64(5) + nd
+    out = np.empty(len(g), dtype=np.uint8)
+    inh = rel < hl
+    w = np.uint64(lay.width)
+    rel2 = np.where(inh, np.uint64(0), rel - hl)
+    ln, col = rel2 // (w + np.uint64(1)), rel2 % (w + np.uint64(1))
+    bi = ln * w + col
+    nl = (col == w) | (bi >= L)
+    with np.errstate(over="ignore"):
+        h = _splitmix64(np.uint64(lay.seed) * np.uint64(0xD1B54A32D192ED03) + bb + bi)
+    out[:] = np.frombuffer(b"ACGT", dtype=np.uint8)[(h >> np.uint64(62)).astype(np.int64)]
+    out[nl] = ord("\n")
+    for j in np.nonzero(inh)[0].tolist():  # header bytes (few)
+        hdr = (">syn%d\n" % int(r[j])).encode()
+        out[j] = hdr[int(rel[j])]
+    return out.tobytes()
+
+
+def grch38_like(seed: int, n_bases: int = 1_000_000, n_records: int = 5, width: int = 60) -> bytes:
+    """A GRCh38-shaped synthetic FASTA (BASELINE config 5 stand-in: GRCh38 is
+    not in this container): records ``chr<i> AC:... description``, 60-column
+    lines, soft-masked (lower-case) stretches, N runs (telomere / gap blocks),
+    interspersed copies of a few repeat elements (~300 bp, a few % mutated)
+    and tandem satellite arrays, so k-mer counts are skewed like a genome's."""
+    rng = np.random.default_rng(seed)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    elems = [rng.integers(0, 4, size=int(rng.integers(200, 400)), dtype=np.uint8) for _ in range(4)]
+    sat = rng.integers(0, 4, size=171, dtype=np.uint8)
+    out = []
+    per = n_bases // n_records
+    for r in range(n_records):
+        L = per if r + 1 < n_records else n_bases - per * (n_records - 1)
+        seq = rng.integers(0, 4, size=L, dtype=np.uint8)
+        # repeat copies
+        for _ in range(L // 2500):
+            e = elems[int(rng.integers(0, len(elems)))].copy()
+            mut = rng.random(len(e)) < 0.03
+            e[mut] = rng.integers(0, 4, size=int(mut.sum()), dtype=np.uint8)
+            at = int(rng.integers(0, max(1, L - len(e))))
+            seq[at:at + len(e)] = e[:L - at]
+        # one satellite array
+        n_sat = min(L // 10, 40 * len(sat))
+        at = int(rng.integers(0, max(1, L - n_sat)))
+        seq[at:at + n_sat] = np.tile(sat, n_sat // len(sat) + 1)[:n_sat]
+        chars = acgt[seq].copy()
+        # soft-masking: ~half the repeats' bases lower-case, in runs
+        for _ in range(L // 5000):
+            a = int(rng.integers(0, L))
+            chars[a:a + int(rng.integers(50, 1500))] += 32
+        # N runs: the record ends and a few gaps
+        nN = min(L // 20, 1000)
+        chars[:nN] = ord("N")
+        chars[L - nN:] = ord("N")
+        for _ in range(3):
+            a = int(rng.integers(0, L))
+            chars[a:a + int(rng.integers(10, 500))] = ord("N")
+        out.append(b">chr%d AC:CM0006%02d.2 gi:5688%02d LN:%d rl:Chromosome M5:x AS:GRCh38\n" % (r + 1, r, r, L))
+        full = L // width
+        body = chars[:full * width].reshape(full, width)
+        out.append(b"\n".join(bytes(x) for x in body) + b"\n")
+        if L > full * width:
+            out.append(bytes(chars[full * width:]) + b"\n")
+    return b"".join(out)
+
+
 def messy_records(seed: int, n_records: int = 24, max_len: int = 3000) -> bytes:
     """Multi-record FASTA exercising the parser/extractor edge cases of §8c/§A:
     descriptions after the name, a tab inside the title, lowercase runs, N and

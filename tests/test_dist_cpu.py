@@ -1,9 +1,16 @@
-"""Multi-GPU join logic rehearsed on CPU: 2 ranks over gloo run the same
-prefix-histogram / balanced-splitter / stable-partition / all-to-all-v plan as
-kman_amd.dist.DistPipeline (shared code: plan_lut, bucket_counts,
-recv_layout), with numpy standing in for the per-rank device sort.  The
-rank-ordered concatenation of per-rank count/uniq results must equal the
-single-process result over all shards."""
+"""Multi-GPU join logic rehearsed on CPU (no GPU needed).
+
+* Byte-range shards of ONE FASTA (kman_amd/shard.py): every shard's own
+  windows, with the halo, concatenated in rank order are exactly the windows
+  of the whole file (np_oracle over the file, seq.py:285-328).
+* 2 ranks over gloo run the planning and exchanges of
+  DistPipeline.step_gen (dist.rehearse: all-gathered bucket totals, the same
+  RoundPlanner, round_send / round_recv layouts, one all-to-all per round, a
+  region overflow agreed by all-reduce and the round redone by key range),
+  with numpy standing in for the device passes.  The rank-ordered
+  concatenation of the per-rank counts equals the single-process count.
+* The round planner accepts BASELINE config 4 (100 GB over 8 ranks,
+  12.5 G bases per rank) within one MI355X's HBM."""
 
 from __future__ import annotations
 
@@ -61,18 +68,77 @@ class GlooComm:
         return out
 
 
-def _shard_kmers(rank, k):
+def _shard_windows(text: bytes, world: int, k: int):
+    """(keys, global pos) of every shard's own windows, in rank order, the
+    way the device shard sees them: (a record opener if the shard starts in a
+    record) + its bytes + halo; windows starting in its own bases only."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import np_oracle
+    from kman_amd import shard
+
+    rd = shard.BytesReader(text)
+    specs = shard.shard_specs(rd, world, k)
+    keys, pos, base = [], [], 0
+    for sp in specs:
+        pre = b">\n" if sp.start > sp.h0 else b""
+        if sp.own_end > sp.start and sp.own_end > sp.h0:
+            own = sum(len(x) for _, x in np_oracle.parse_fasta(pre + text[sp.start:sp.own_end]))
+        else:
+            own = 0
+        if own:
+            kk, pp = np_oracle.stream_kmers(np_oracle.parse_fasta(pre + text[sp.start:sp.halo_end]), k)
+            m = (pp >> np.uint64(1)) < np.uint64(own)
+            keys.append(kk[m])
+            pos.append(pp[m] + np.uint64(2 * base))
+        base += own
+    return specs, np.concatenate(keys) if keys else np.zeros(0, np.uint64), \
+        np.concatenate(pos) if pos else np.zeros(0, np.uint64)
+
+
+def _texts():
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import inputs
+
+    lay = inputs.SynthLayout(60_000, 5, record_len=7_000, width=61)
+    return [inputs.messy_records(11, n_records=30, max_len=3000), inputs.messy_records(12, n_records=8, max_len=9000),
+            lay.read(0, lay.size), b"junk line\n\n>r1 x\nACGTACGTAC\r\nGGTT\n>r2\n\n>r3\nAC\nGT\nTTTTTTTT\n"]
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8, 17])
+@pytest.mark.parametrize("k", [2, 5, 21])
+def test_shards_cover_the_stream_exactly(world, k):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import np_oracle
+
+    for text in _texts():
+        specs, keys, pos = _shard_windows(text, world, k)
+        wk, wp = np_oracle.stream_kmers(np_oracle.parse_fasta(text), k)
+        np.testing.assert_array_equal(keys, wk)
+        np.testing.assert_array_equal(pos, wp)
+        assert specs[0].start == 0 and specs[-1].own_end == len(text)
+        for a, b in zip(specs, specs[1:]):
+            assert a.own_end == b.start and a.start <= a.own_end <= a.halo_end
+            c = b.start
+            assert c == len(text) or text[c - 1:c] == b"\n" or (text[c - 1:c] == b"\r" and text[c:c + 1] != b"\n")
+
+
+def test_synth_layout_reads_agree():
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import inputs
     import np_oracle
 
-    text = inputs.messy_records(100 + rank, n_records=30, max_len=6000) if rank % 2 else inputs.syn_numpy(150_000, 7 + rank, record_len=40_000)
-    keys, pos = np_oracle.stream_kmers(np_oracle.parse_fasta(text), k)
-    return keys, pos | (np.uint64(rank) << np.uint64(56))
+    lay = inputs.SynthLayout(10_000, 9, record_len=3_333, width=80)
+    t = lay.read(0, lay.size)
+    assert len(t) == lay.size
+    assert t == b"".join(lay.read(a, min(a + 777, lay.size)) for a in range(0, lay.size, 777))
+    recs = np_oracle.parse_fasta(t)
+    assert [n for n, _ in recs] == [b"syn0", b"syn1", b"syn2", b"syn3"]
+    assert sum(len(s) for _, s in recs) == 10_000 and all(len(s) <= 3_333 for _, s in recs)
+    assert set(b"".join(s for _, s in recs)) == set(b"ACGT")
 
 
-def _worker(rank, world, port, k, q):
+def _worker(rank, world, port, k, q, max_items, fail):
     import torch.distributed as dist
 
     sys.path.insert(0, ROOT)
@@ -80,20 +146,32 @@ def _worker(rank, world, port, k, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        import np_oracle
         from kman_amd import dist as kd
 
-        keys, pos = _shard_kmers(rank, k)
-        rk, rv, lut = kd.rehearse(keys, pos, k, world, rank, GlooComm(dist, world))
-        ck, cc = np_oracle.rle_count(rk)
-        uk, uv = np_oracle.rle_uniq(rk, rv)
-        q.put((rank, ck, cc, uk, uv, lut))
+        text = _texts()[2]
+        specs, keys, pos = _shard_windows(text, world, k)
+        # this rank's windows: those whose global base lies in its own bases
+        bases = np.cumsum([0] + [_own_bases(text, sp) for sp in specs])
+        m = ((pos >> np.uint64(1)) >= np.uint64(bases[rank])) & ((pos >> np.uint64(1)) < np.uint64(bases[rank + 1]))
+        ck, cc, R, cuts, redone = kd.rehearse(keys[m], k, world, rank, GlooComm(dist, world), int(bases[-1]),
+                                              max_round_items=max_items, fail=fail)
+        q.put((rank, ck, cc, R, list(cuts), redone))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("k", [5, 21])
-def test_two_rank_join_equals_single_process(k):
+def _own_bases(text, sp):
+    import np_oracle
+
+    pre = b">\n" if sp.start > sp.h0 else b""
+    if sp.own_end <= sp.start or sp.own_end <= sp.h0:
+        return 0
+    return sum(len(x) for _, x in np_oracle.parse_fasta(pre + text[sp.start:sp.own_end]))
+
+
+@pytest.mark.parametrize("k,max_items,fail", [(5, None, ()), (21, None, ()), (21, 9_000, ()),
+                                              (21, 9_000, ((1, 1),))])
+def test_two_rank_rounds_equal_single_process(k, max_items, fail):
     import multiprocessing as mp
 
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -103,59 +181,82 @@ def test_two_rank_join_equals_single_process(k):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, k, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, k, q, max_items, fail)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda x: x[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    # single-process reference over the union of shards
-    allk, allp = zip(*[_shard_kmers(r, k) for r in range(world)])
-    keys = np.concatenate(allk)
-    vals = np.concatenate(allp)
-    sk, sv = np_oracle.stable_sort(keys, vals)
-    wk, wc = np_oracle.rle_count(sk)
-    uk, uv = np_oracle.rle_uniq(sk, sv)
-    got_k = np.concatenate([r[1] for r in res])
-    got_c = np.concatenate([r[2] for r in res])
-    np.testing.assert_array_equal(got_k, wk)
-    np.testing.assert_array_equal(got_c, wc)
-    np.testing.assert_array_equal(np.concatenate([r[3] for r in res]), uk)
-    np.testing.assert_array_equal(np.concatenate([r[4] for r in res]), uv)
-    # prefix ranges are contiguous and in rank order
-    assert (np.diff(res[0][5].astype(np.int64)) >= 0).all()
+    keys, _ = np_oracle.stream_kmers(np_oracle.parse_fasta(_texts()[2]), k)
+    wk, wc = np_oracle.rle_count(np_oracle.stable_sort(keys)[0])
+    np.testing.assert_array_equal(np.concatenate([r[1] for r in res]), wk)
+    np.testing.assert_array_equal(np.concatenate([r[2] for r in res]), wc)
+    R = res[0][3]
+    assert all(r[3] == R and r[4] == res[0][4] for r in res), "ranks planned differently"
+    if max_items:
+        assert R >= 3
+    assert res[0][5] == res[1][5] == [r for (_, r) in fail]  # the fallback is agreed by both ranks
     if len(res[0][1]) and len(res[1][1]):
-        assert res[0][1].max() < res[1][1].min()
+        assert res[0][1].max() < res[1][1].min()  # rank order = key order
 
 
-def test_plan_is_balanced():
-    from kman_amd.dist import bucket_counts, plan_lut, recv_layout
-
-    rng = np.random.default_rng(3)
-    h = rng.integers(0, 1000, size=1 << 14).astype(np.uint64)
-    for world in (1, 2, 4, 8):
-        lut = plan_lut(h, world)
-        assert (np.diff(lut.astype(np.int64)) >= 0).all()
-        c = bucket_counts(h, lut, world)
-        assert int(c.sum()) == int(h.sum())
-        assert c.max() - c.min() <= 2 * h.max()
-    C = np.array([[1, 2], [3, 4]], dtype=np.uint64)
-    s, so, r, ro = recv_layout(C, 1)
-    assert list(s) == [3, 4] and list(so) == [0, 3] and list(r) == [2, 4] and list(ro) == [0, 2]
-
-
-def test_region_bucket_ranges():
-    """bucket_ranges: contiguous ranges covering the 256 buckets, ~1/G of the
-    k-mers each; within nb_max for uniform counts (skewed counts may exceed it:
-    the ranks then fall back together)."""
+def test_part_cuts_are_contiguous_and_balanced():
     from kman_amd import dist
 
     rng = np.random.default_rng(0)
-    for G in (1, 2, 3, 5, 8):
+    for parts in (1, 2, 3, 5, 8, 24, 64):
         g = rng.poisson(3_900_000, 256).astype(np.uint64)
-        b_lo, nb = dist.bucket_ranges(g, G)
-        assert nb.sum() == 256 and b_lo[0] == 0 and (b_lo[1:] == np.cumsum(nb)[:-1]).all()
-        assert (nb <= dist.nb_max(G)).all()
-        share = np.array([g[b_lo[q]:b_lo[q] + nb[q]].sum() for q in range(G)], np.float64) / g.sum()
-        assert np.abs(share - 1 / G).max() < 1.5 / 256 * G / G + 1e-9
+        cuts = dist.part_cuts(g, parts)
+        assert cuts[0] == 0 and cuts[-1] == 256 and (np.diff(cuts) >= 0).all()
+        share = np.array([g[cuts[p]:cuts[p + 1]].sum() for p in range(parts)], np.float64) / g.sum()
+        assert np.abs(share - 1 / parts).max() <= 1.5 / 256 + 1e-9
+
+
+def test_round_layouts_are_consistent():
+    from kman_amd import dist
+
+    rng = np.random.default_rng(1)
+    G, R = 3, 4
+    H = [rng.integers(0, 50, size=(256, 64)).astype(np.uint64) for _ in range(G)]
+    C = np.stack([h.sum(axis=1) for h in H])
+    cuts = dist.part_cuts(C.sum(axis=0), G * R)
+    send, recv = dist.round_sizes(C, cuts, G, R)
+    for r in range(R):
+        for q in range(G):
+            rtab, sc, so = dist.round_send(H[q], cuts, G, R, r)
+            assert sc.sum() == send[q, r]
+            kept = rtab != np.uint64(0xFFFFFFFFFFFFFFFF)
+            # kept regions tile [0, send) exactly, destination-major
+            base = rtab[kept].astype(np.int64)
+            cnt = H[q].reshape(-1)[kept].astype(np.int64)
+            assert (base[1:] == (base + cnt)[:-1]).all() and (len(base) == 0 or base[0] == 0)
+            lo, nb, counts, rc, ro = dist.round_recv(C, cuts, R, q, r)
+            assert rc.sum() == recv[q, r] and counts.shape == (G, nb)
+            assert rc[q] == sum(H[q][b].sum() for b in range(lo, lo + nb))
+    # every rank's rounds cover its buckets once; ranks in key order
+    owned = [[dist.part_of(cuts, R, q, r) for r in range(R)] for q in range(G)]
+    flat = [x for q in owned for x in q]
+    assert flat[0][0] == 0 and flat[-1][1] == 256 and all(a[1] == b[0] for a, b in zip(flat, flat[1:]))
+
+
+def test_config4_plan_fits_one_mi355x():
+    """BASELINE config 4: 100 GB FASTA, k = 21, 8 ranks -> 12.5 G bases (k-mers)
+    per rank.  The shard geometry is accepted and the rounds fit the HBM left
+    after the codes (12.5 GB) and the count output (12 B per received k-mer)."""
+    from kman_amd import _native as N
+    from kman_amd import dist
+
+    L = N.lib()
+    nbase = 12_500_000_000
+    assert L.kman_dshard_plan(nbase, nbase, 21, 0, N.KMAN_FINISH_COUNT) == N.KMAN_OK
+    G = 8
+    C = np.full((G, 256), nbase // 256, dtype=np.uint64)
+    hbm = 288 * 10**9
+    budget = int(0.85 * hbm) - nbase - 12 * (nbase + (1 << 20))
+    pl = dist.RoundPlanner(21, 0, N.KMAN_FINISH_COUNT, G, nbase)
+    R, cuts, a, b = pl.plan(C, budget)
+    assert a + b <= budget and 1 < R <= 8
+    for q in range(G):
+        for r in range(R):
+            assert pl.arenas(C, cuts, R, q, r) is not None

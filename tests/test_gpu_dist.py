@@ -25,7 +25,7 @@ def dev():
 @pytest.mark.parametrize("buckets", [1, 3, 8])
 def test_prefix_hist_and_partition(dev, n, buckets):
     from kman_amd import _native as N
-    from kman_amd.dist import bucket_counts, plan_lut
+    from kman_amd.dist import plan_lut
 
     L = N.lib()
     rng = np.random.default_rng(n + buckets)
@@ -43,8 +43,8 @@ def test_prefix_hist_and_partition(dev, n, buckets):
     want_h = np.bincount((keys >> np.uint64(28)).astype(np.int64), minlength=1 << 14)
     np.testing.assert_array_equal(h, want_h)
     lut = plan_lut(h, buckets)
-    dev.upload(dl, lut)
-    counts = bucket_counts(h, lut, buckets)
+    dev.upload(dl, lut.astype(np.uint8))
+    counts = np.bincount(lut, weights=h.astype(np.float64), minlength=buckets).astype(np.uint64)
     N.check(dev.ctx, L.kman_partition(dev.ctx, c_void_p(dk.ptr), c_void_p(dk2.ptr), c_void_p(dv.ptr),
                                       c_void_p(dv2.ptr), 8, n, c_void_p(dl.ptr), 28, buckets,
                                       counts.ctypes.data_as(c_void_p)), "partition")
@@ -56,23 +56,28 @@ def test_prefix_hist_and_partition(dev, n, buckets):
         b.free()
 
 
-@pytest.mark.parametrize("path", ["region", "split"])
+@pytest.mark.parametrize("path", ["region", "general"])
 @pytest.mark.parametrize("mode", ["count", "uniq"])
-def test_dist_pipeline_world1_equals_single(dev, mode, path):
-    import sys, os
+def test_dist_pipeline_world1_equals_single(dev, mode, path, tmp_path, oracle_bin):
+    """The RCCL pipeline at world size 1 (RCCL self-exchange): rows and the
+    emitted file equal the single-GPU path / the C oracle."""
+    import sys, os, subprocess
 
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
     import inputs
     import np_oracle
-    from kman_amd import dist
+    from kman_amd import dist, shard
 
     text = inputs.messy_records(7, n_records=40, max_len=20000)
-    p = dist.DistPipeline(dev, text, 13, mode, 1, 0, dist.unique_id(), path=path)
+    p = dist.DistPipeline(dev, shard.BytesReader(text), 13, mode, 1, 0, dist.unique_id(), path=path,
+                          max_round_items=40_000)
     try:
         for _ in range(2):
             p.step()
-            assert p.path == path  # RCCL world 1: no fallback
+            assert p.path == path and p.rounds >= 2
         keys, vals = p.results()
+        out = tmp_path / "o.txt"
+        p.comm.run(p.emit_gen(str(out)))
     finally:
         p.free()
     recs = np_oracle.parse_fasta(text)
@@ -86,3 +91,7 @@ def test_dist_pipeline_world1_equals_single(dev, mode, path):
         wk, wv = np_oracle.rle_uniq(sk, sp)
         np.testing.assert_array_equal(keys, wk)
         np.testing.assert_array_equal(vals, wv)
+    src = tmp_path / "in.fa"
+    src.write_bytes(text)
+    subprocess.run([oracle_bin, mode, str(src), str(tmp_path / "w.txt"), "13"], check=True)
+    assert out.read_bytes() == (tmp_path / "w.txt").read_bytes()

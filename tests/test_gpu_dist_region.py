@@ -1,14 +1,19 @@
-"""GPU parity of the multi-GPU region path (kman_dgroups_*, kman_amd/dist.py)
+"""GPU parity of the multi-GPU path over byte-range shards of ONE FASTA
+(kman_amd/shard.py, kman_amd/dist.py, kman_dshard_* / kman_dround_finish)
 with G simulated ranks in ONE process on one GPU (dist.SimGroup: one engine
 context per rank, host-side all-reduce / all-gather, device-to-device
-all-to-all).  The real run executes the same step generator with RCCL.
+all-to-all).  The real run executes the same step generators with RCCL.
 
 Bar: the ranks' outputs concatenated in rank order are bit-exact against the
-numpy restatement over all shards (np_oracle: stream_kmers per shard ->
-stable sort -> run-length count / uniq, seq.py:285-328, batch.py:156-168,
-join.py:95-130,244-285); uniq pos carry the source rank in bits 56-63."""
+numpy restatement over the whole file (np_oracle: parse -> stream_kmers ->
+stable sort -> run-length count / uniq, parsers.py:86-128, seq.py:285-328,
+batch.py:156-168, join.py:95-130,244-285); the emitted output file is
+byte-identical to the C oracle's `kmer count|uniq` output of the file."""
 
 from __future__ import annotations
+
+import os
+import subprocess
 
 import numpy as np
 import pytest
@@ -16,50 +21,240 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 
-def _shards(G, nb, seed0):
+def _texts():
     import inputs
 
-    return [inputs.syn_numpy(nb + 997 * r, seed0 + r, record_len=50_000) for r in range(G)]
+    lay = inputs.SynthLayout(400_000, 21, record_len=90_000, width=70)
+    return {"synth": lay.read(0, lay.size), "messy": inputs.messy_records(31, n_records=60, max_len=12_000)}
 
 
-def _oracle(texts, k, mode):
+def _oracle(text, k, mode, canonical=False):
     import np_oracle
 
-    keys, pos = [], []
-    for r, t in enumerate(texts):
-        kk, pp = np_oracle.stream_kmers(np_oracle.parse_fasta(t), k)
-        keys.append(kk)
-        pos.append(pp | np.uint64(r << 56))
-    keys, pos = np.concatenate(keys), np.concatenate(pos)
+    keys, pos = np_oracle.stream_kmers(np_oracle.parse_fasta(text), k, canonical=canonical)
     sk, sp = np_oracle.stable_sort(keys, pos)
     return np_oracle.rle_count(sk) if mode == "count" else np_oracle.rle_uniq(sk, sp)
+
+
+def _run(text, k, mode, G, **kw):
+    """G simulated ranks over one text, stepped twice (the resident buffers
+    are reused); returns the rank-ordered outputs of both steps (uniq pos
+    rebased to global base indices), the pipelines and the group."""
+    from kman_amd import dist, engine, shard
+
+    devs = [engine.Device(0) for _ in range(G)]
+    pipes = []
+    try:
+        rd = shard.BytesReader(text)
+        for r in range(G):
+            pipes.append(dist.DistPipeline(devs[r], rd, k, mode, G, r, None, **kw))
+            pipes[-1]._dev_owned = devs[r]
+        grp = dist.SimGroup(pipes)
+        outs = []
+        for _ in range(2):
+            grp.step()
+            keys = np.concatenate([p.results()[0] for p in pipes])
+            vals = np.concatenate([p.results()[1] for p in pipes])
+            if mode == "uniq":  # source-tagged pos -> global pos
+                src = (vals >> np.uint64(56)).astype(np.int64)
+                vals = (vals & np.uint64((1 << 56) - 1)) + (pipes[0].base_off[src] << np.uint64(1))
+            outs.append((keys, vals))
+        return outs, pipes, grp
+    except BaseException:
+        for p in pipes:
+            p.free()
+        for d in devs:
+            d.close()
+        raise
+
+
+def _close(pipes):
+    for p in pipes:
+        p.free()
+        p._dev_owned.close()
 
 
 @pytest.mark.parametrize("G", [1, 2, 3, 8])
 @pytest.mark.parametrize("mode", ["count", "uniq"])
 @pytest.mark.parametrize("k", [15, 21])
-def test_dist_region_matches_oracle(G, mode, k):
-    import np_oracle  # noqa: F401
-    from kman_amd import dist, engine
-
-    texts = _shards(G, 300_000, 10 * G + k)
-    devs = [engine.Device(0) for _ in range(G)]
-    pipes = []
+@pytest.mark.parametrize("name", ["synth", "messy"])
+def test_dist_shards_match_oracle(G, mode, k, name):
+    text = _texts()[name]
+    outs, pipes, _ = _run(text, k, mode, G)
     try:
-        nbq = max(sum(len(s) for _, s in __import__("np_oracle").parse_fasta(t)) for t in texts)
-        for r in range(G):
-            pipes.append(dist.DistPipeline(devs[r], texts[r], k, mode, G, r, None, n_bases_q=nbq))
         assert all(p.path == "region" for p in pipes)
-        for _ in range(2):  # twice: the resident buffers are reused
-            res = dist.SimGroup(pipes).step()
-            assert all(x is not None for x in res), "a rank fell back"
-            keys = np.concatenate([p.results()[0] for p in pipes])
-            vals = np.concatenate([p.results()[1] for p in pipes])
-            wk, wv = _oracle(texts, k, mode)
+        assert all(p.fallback_rounds == 0 for p in pipes)
+        wk, wv = _oracle(text, k, mode)
+        for keys, vals in outs:
             np.testing.assert_array_equal(keys, wk)
             np.testing.assert_array_equal(vals, wv)
     finally:
-        for p in pipes:
-            p.free()
-        for d in devs:
-            d.close()
+        _close(pipes)
+
+
+@pytest.mark.parametrize("G", [2, 8])
+@pytest.mark.parametrize("mode", ["count", "uniq"])
+def test_dist_streamed_rounds(G, mode):
+    """R >= 3 key rounds forced by a small per-round budget: each rank's
+    rounds append its key range in order."""
+    text = _texts()["synth"]
+    outs, pipes, _ = _run(text, 21, mode, G, max_round_items=120_000 // G)
+    try:
+        assert all(p.rounds >= 3 for p in pipes) and len({p.rounds for p in pipes}) == 1
+        wk, wv = _oracle(text, 21, mode)
+        for keys, vals in outs:
+            np.testing.assert_array_equal(keys, wk)
+            np.testing.assert_array_equal(vals, wv)
+    finally:
+        _close(pipes)
+
+
+def test_dist_wide_pass1b(monkeypatch):
+    """Pass 1b with 7 bits (the width config 4's 390 M-item buckets take)."""
+    monkeypatch.setenv("KMAN_DROUND_MIN_G", "7")
+    text = _texts()["synth"]
+    for mode in ("count", "uniq"):
+        outs, pipes, _ = _run(text, 21, mode, 3)
+        try:
+            wk, wv = _oracle(text, 21, mode)
+            np.testing.assert_array_equal(outs[0][0], wk)
+            np.testing.assert_array_equal(outs[0][1], wv)
+        finally:
+            _close(pipes)
+
+
+@pytest.mark.parametrize("G", [1, 8])
+def test_dist_canonical_count_and_hist(G):
+    """Config 5 across ranks: canonical counts + the all-reduced abundance
+    spectrum equal the single-GPU path and the oracle (canonical counts =
+    the `count -r` rows with key <= rc(key) for odd k, seq.py:274-282)."""
+    import inputs
+    from kman_amd import engine
+
+    text = inputs.grch38_like(5, n_bases=300_000)
+    outs, pipes, grp = _run(text, 21, "count", G, canonical=True)
+    try:
+        wk, wc = _oracle(text, 21, "count", canonical=True)
+        np.testing.assert_array_equal(outs[-1][0], wk)
+        np.testing.assert_array_equal(outs[-1][1], wc)
+        hs = grp.run(lambda p: p.hist_gen(1001))
+        want = np.bincount(np.minimum(wc.astype(np.int64), 1000), minlength=1001).astype(np.uint64)
+        want[0] = 0
+        for h in hs:
+            np.testing.assert_array_equal(h, want)
+        single = engine.abundance_hist(text, 21, canonical=True, nbins=1001, dev=pipes[0].dev)
+        np.testing.assert_array_equal(hs[0], single)
+    finally:
+        _close(pipes)
+
+
+def test_dist_region_overflow_redoes_the_round():
+    """A key repeated far more often than a region holds: that round is
+    redone through the general path on every rank, results stay exact."""
+    import inputs
+
+    rep = b"ACGTTGCAAGGCTTACGATCGATCGGATCC"
+    body = inputs.SynthLayout(200_000, 4, record_len=50_000).read(0, 10**9)
+    text = body + b">rep\n" + b"\n".join([rep * 2] * 30_000) + b"\n"
+    for mode in ("count", "uniq"):
+        outs, pipes, _ = _run(text, 21, mode, 2)
+        try:
+            assert sum(p.fallback_rounds for p in pipes) >= 2  # both ranks redid it
+            wk, wv = _oracle(text, 21, mode)
+            np.testing.assert_array_equal(outs[0][0], wk)
+            np.testing.assert_array_equal(outs[0][1], wv)
+        finally:
+            _close(pipes)
+
+
+def test_dist_general_path_k27():
+    """k > 25: the general path (key ranges, exchanged keys + pos)."""
+    text = _texts()["messy"]
+    for mode in ("count", "uniq"):
+        outs, pipes, _ = _run(text, 27, mode, 3)
+        try:
+            assert all(p.path == "general" for p in pipes)
+            wk, wv = _oracle(text, 27, mode)
+            np.testing.assert_array_equal(outs[0][0], wk)
+            np.testing.assert_array_equal(outs[0][1], wv)
+        finally:
+            _close(pipes)
+
+
+@pytest.mark.parametrize("mode", ["count", "uniq"])
+def test_dist_emit_matches_reference_bytes(mode, tmp_path, oracle_bin):
+    """The global output file written by the ranks at their offsets is the
+    reference's `kmer count|uniq` output of the whole file (C oracle, pinned
+    to the reference's own outputs in tests/golden)."""
+    text = _texts()["messy"]
+    src = tmp_path / "in.fa"
+    src.write_bytes(text)
+    want = tmp_path / "want.txt"
+    subprocess.run([oracle_bin, mode, str(src), str(want), "13"], check=True)
+    outs, pipes, grp = _run(text, 13, mode, 3)
+    try:
+        got = tmp_path / "got.txt"
+        grp.run(lambda p: p.emit_gen(str(got)))
+        assert got.read_bytes() == want.read_bytes()
+    finally:
+        _close(pipes)
+
+
+@pytest.mark.parametrize("chunk", [1000, 4096, 1 << 20])
+def test_chunked_loader_equals_parse(chunk):
+    from kman_amd import engine, shard
+
+    dev = engine.default_device()
+    for text in _texts().values():
+        a = engine.parse(dev, text)
+        b = shard.load_text(dev, text, chunk)
+        try:
+            assert a.n_bases == b.n_bases and a.names == b.names
+            np.testing.assert_array_equal(a.rec_seq, b.rec_seq)
+            ca = dev.download(a.codes, a.n_bases + 64, np.uint8)
+            cb = dev.download(b.codes, b.n_bases + 64, np.uint8)
+            np.testing.assert_array_equal(ca, cb)
+        finally:
+            a.free()
+            b.free()
+
+
+def test_pinned_chunked_loader(tmp_path):
+    """Async chunk copies from pinned memory (the pinned-host bench line)."""
+    from kman_amd import engine, shard
+
+    dev = engine.default_device()
+    text = _texts()["synth"]
+    rd = shard.PinnedReader(dev, text)
+    try:
+        sp = shard.shard_specs(rd, 1, 21)[0]
+        ld = shard.ShardLoader(dev, rd, sp, 21, chunk_bytes=50_000)
+        try:
+            for _ in range(2):
+                sh = ld.load()
+                a = engine.parse(dev, text)
+                try:
+                    np.testing.assert_array_equal(dev.download(sh.codes, sh.n_own, np.uint8),
+                                                  dev.download(a.codes, a.n_bases, np.uint8))
+                finally:
+                    a.free()
+        finally:
+            ld.free()
+    finally:
+        rd.free()
+
+
+def test_synth_device_matches_numpy():
+    import inputs
+    from kman_amd import engine, shard
+
+    dev = engine.default_device()
+    lay = inputs.SynthLayout(300_000, 77, record_len=100_003, width=80)
+    rd = shard.SynthReader(lay)
+    buf = dev.alloc(lay.size + 64)
+    try:
+        for lo, hi in ((0, lay.size), (5, 1000), (100_000, 200_017), (lay.size - 33, lay.size)):
+            rd.gen(dev, buf, lo, hi)
+            assert dev.download(buf, hi - lo, np.uint8).tobytes() == lay.read(lo, hi)
+    finally:
+        buf.free()

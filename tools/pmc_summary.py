@@ -42,6 +42,11 @@ for k, v in out.items():
     print("%-60s %3d  fetch %12.0f KiB  write %12.0f KiB  hbm/launch %8.3f GB" % (
         k[:60], v["launches"], v["fetch_kib"], v["write_kib"], v["hbm_bytes_per_launch"] / 1e9))
 if len(sys.argv) > 6:
+    # every kernel of this workload, for bench.py's roofline traffic fields
+    cur = dict(out)
+    cur["_meta"] = {"mode": sys.argv[4], "k": int(sys.argv[5]), "bases": int(sys.argv[6]), "tag": tag}
+    with open(os.path.join(ROOT, "profiles", "pmc_current.json"), "w") as fh:
+        json.dump(cur, fh, indent=1, sort_keys=True)
     # the bench's roofline kernel: the region path's digit pass (rg_pass), else
     # the LSD onesweep pass
     for name in ("rg_pass", "onesweep_pass"):
