@@ -359,6 +359,7 @@ def run_dist(args, world: int, rank: int, local: int):
                        "fasta_bytes": lay.size, "kmers_per_step": total // max(args.steps, 1), "k": args.k,
                        "mode": args.mode, "parallelism": "dp%d: top-8-bit bucket parts + RCCL all-to-all" % world,
                        "path": pipe.path, "rounds": pipe.rounds, "fallback_rounds": pipe.fallback_rounds,
+                       "memory_plan": getattr(pipe, "plan_info", None),
                        "stages_ms_per_step_rank0": stages},
             "roofline": {"kernel": "rg_pass (pass 1 after the exchange, rank 0)", "bound": "hbm", "achieved": ach,
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS if ach else None,

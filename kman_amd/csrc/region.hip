@@ -185,11 +185,14 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
 #pragma unroll
     for (int i = 0; i < SI; i++) key[i] = ib + i * 64 < tcnt ? skeys[ib + i * 64] : 0;
 #define XDIGIT(x) ((uint32_t)(((x) & keymask) >> shift))
+#define KEPT(d) (!EX || ((keep[(d) >> 5] >> ((d) & 31)) & 1u))
     if (BR) {
 #pragma unroll
         for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&thist[XDIGIT(key[i])], 1u) : 0u;
         __syncthreads();
-        if (threadIdx.x < RADIX) digit_publish(status + threadIdx.x, tile, first, thist[threadIdx.x], epoch);
+        // (EX: a digit not kept this round has no chain: nothing published)
+        if (threadIdx.x < RADIX && KEPT(threadIdx.x))
+            digit_publish(status + threadIdx.x, tile, first, thist[threadIdx.x], epoch);
     } else if (ATOMIC) {
 #pragma unroll
         for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&whist[w][XDIGIT(key[i])], 1u) : 0u;
@@ -236,14 +239,14 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     }
     {
         constexpr uint32_t TPD = NT / RADIX >= 4 ? 4 : (NT / RADIX >= 2 ? 2 : 1);
-        if (threadIdx.x < RADIX * TPD) {
+        if (threadIdx.x < RADIX * TPD && KEPT(threadIdx.x / TPD)) {
             const uint32_t d = threadIdx.x / TPD;
             const uint64_t excl =
                 (dbg & 1) ? 0ull  // timing ablation only: no look-back (wrong offsets)
                           : group_lookback<TPD>(status + d, tile, first, thist[d], epoch, err);
             if (threadIdx.x % TPD == 0) {
                 const uint64_t incl = excl + thist[d];
-                if (EX) {
+                if (EX) {  // (only kept digits get here)
                     // exact region: base from the table, size from rg_hist
                     const uint64_t rb = rtab[(uint64_t)d * RS + sgi];
                     const bool over = incl > cnt0[d * RS + sgi];
@@ -1332,6 +1335,7 @@ int make_shard_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t f
 
 struct RoundPlan {
     uint32_t K, Q, g, rest, G, nb;
+    uint32_t H;           // pass-1 chains per (bucket, source)
     bool rc;
     uint64_t C1s, C1;     // pass-1 sub-region / pass-1b region capacities
     uint64_t nsub, nreg;
@@ -1365,34 +1369,41 @@ int make_rplan(uint32_t k, uint32_t flags, int mode, uint32_t world, uint64_t n_
         }
         maxb = t > maxb ? t : maxb;
     }
-    // pass 1b bits: at least the source tag's ceil(log2 G), more until a final
-    // region expects <= 6144 items (the LDS finish holds FCAP = 8704)
-    uint32_t g = 1;
-    while ((1u << g) < world) g++;
+    // pass 1: H block-owned chains per (bucket, source), enough chains to
+    // fill the CUs (a round of few buckets on few ranks has few chains);
+    // pass 1b concatenates the G * H sub-regions of a (b, d): at most 64
+    d.H = 2;
+    while ((uint64_t)nb * world * d.H < 256 && world * d.H * 2 <= 64) d.H *= 2;
+    // pass 1b bits g: until a final region expects <= 6144 items (the LDS
+    // finish holds FCAP = 8704).  g = 0 (no pass 1b, the finish reads the
+    // pass-1 sub-regions) when one rank's 9-bit regions already fit: with one
+    // source and two chains (N > 1 needs pass 1b anyway, to tag each item with
+    // its source rank for uniq and to merge the ranks' sub-regions)
+    uint32_t g = 0;
     {
         const char *e = getenv("KMAN_DROUND_MIN_G");  // tests: the wide pass-1b digits of huge rounds
-        const uint32_t gm = e ? (uint32_t)atoi(e) : 0u;
-        g = gm > g && gm <= 9 ? gm : g;
+        g = e ? (uint32_t)atoi(e) : 0u;
+        g = g <= 9 ? g : 9;
     }
-    while (g < 9 && ((maxb >> 9) >> g) > 6144) g++;
+    if (g == 0 && (world * d.H > 2 || (maxb >> 9) > 7800)) g = 1;  // (7800: the single-GPU path's bound)
+    while (g > 0 && g < 9 && ((maxb >> 9) >> g) > 6144) g++;
     if (((maxb >> 9) >> g) > 7800) return KMAN_EFALLBACK;
     if (d.K < B1 + 9 + g + 1) return KMAN_EFALLBACK;
     d.g = g;
     d.rest = d.K - B1 - 9 - g;
-    // pass 1: two block-owned chains per (bucket, source), 512 digits
-    const uint64_t e1 = maxsb >> 10;
+    const uint64_t e1 = maxsb / (512ull * d.H);
     d.C1s = ceil_div(e1 + e1 / 2 + 256, 64) * 64;
-    if ((uint64_t)512 * world * 2 * d.C1s >= (1ull << 31)) return KMAN_EFALLBACK;  // (32-bit WC offsets)
+    if ((uint64_t)512 * world * d.H * d.C1s >= (1ull << 31)) return KMAN_EFALLBACK;  // (32-bit WC offsets)
     const uint64_t e2 = (maxb >> 9) >> g;
     const uint64_t c2 = ceil_div(e2 + e2 / 2 + 512, 64) * 64;
     d.C1 = c2 < (uint64_t)FCAP ? c2 : (uint64_t)FCAP;
-    d.nsub = (uint64_t)nb * 512 * world * 2;
+    d.nsub = (uint64_t)nb * 512 * world * d.H;
     d.nreg = (uint64_t)nb * 512 << g;
     d.off_c1 = d.nsub * d.C1s * 8;
     d.off_tab = ceil_div(d.off_c1 + d.nsub * 4, 64) * 64;
     d.a_bytes = d.off_tab + ceil_div((uint64_t)nb * world * 12 + 64, 64) * 64;
-    d.off_c2 = d.nreg * d.C1 * 8;
-    d.b_bytes = d.off_c2 + ceil_div(d.nreg * 4 + 64, 64) * 64;
+    d.off_c2 = g ? d.nreg * d.C1 * 8 : 0;
+    d.b_bytes = g ? d.off_c2 + ceil_div(d.nreg * 4 + 64, 64) * 64 : 64;
     *rp = d;
     return KMAN_OK;
 }
@@ -1538,7 +1549,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     HIP_TRY(ctx, hipMemcpyAsync(scnt, hn.data(), hn.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(c1, 0, d.nsub * 4, ctx->stream));
     uint32_t epoch, *counter;
-    // pass 1: by the 9 bits below the bucket, two chains per (b, src) into
+    // pass 1: by the 9 bits below the bucket, H chains per (b, src) into
     // sub-regions (b, d, src, h)
     {
         KMAN_TRY(kman_lookback_begin(ctx, 1, &epoch, &counter));
@@ -1550,7 +1561,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         pa.nbk = nb * G;
         pa.nsg = 1;
         pa.gsub = G;
-        pa.H = 2;
+        pa.H = d.H;
         pa.shift = d.Q + d.K - B1 - 9;
         pa.bits = 9;
         pa.out = r1;
@@ -1560,6 +1571,12 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         HIP_TRY(ctx, hipGetLastError());
     }
     KMAN_TRY(rg_check(ctx, "pass 1", c1, d.nsub));
+    if (d.g == 0) {
+        // one source, two chains: the finish reads the pass-1 sub-regions
+        FinishArgs f{r1, d.C1s, c1, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << 9, 0u, (uint32_t)d.nreg};
+        f.fsub = d.H;
+        KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, 0, nullptr));
+    } else {
     // (c2 may lie in the receive buffer: cleared only once pass 1 has read it)
     HIP_TRY(ctx, hipMemsetAsync(c2, 0, d.nreg * 4, ctx->stream));
     // pass 1b: per (b, d), its 2G sub-regions concatenated, by g more bits;
@@ -1573,13 +1590,13 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         pa.seg_cnt = c1;
         pa.stride = d.C1s;
         pa.nbk = nb * 512;
-        pa.nsg = 2 * G;
+        pa.nsg = d.H * G;
         pa.gsub = 1;
         pa.H = 1;
         pa.shift = d.Q + d.rest;
         pa.bits = d.g;
         pa.tag = mode == KMAN_FINISH_UNIQ;
-        pa.tag_div = 2;
+        pa.tag_div = d.H;
         pa.tag_shift = d.Q + d.rest + d.g;
         pa.tag_bits = 9;
         pa.out = r2;
@@ -1593,6 +1610,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         FinishArgs f{r2, d.C1, c2, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << (9 + d.g),
                      mode == KMAN_FINISH_UNIQ ? d.Q + d.rest + d.g : 0u, (uint32_t)d.nreg};
         KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, 0, nullptr));
+    }
     }
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small + 4, ctx->d_status + (d.nreg - 1), 8, hipMemcpyDeviceToHost, ctx->stream));
     uint32_t e;

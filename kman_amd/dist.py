@@ -454,6 +454,8 @@ class DistPipeline:
         out_bytes = (8 + self._vb(C)) * (tot if G == 1 else int(tot * 1.1 / G) + (1 << 20))
         R, cuts, a_need, b_need = pl.plan(C, max(1, self.budget - out_bytes), self.max_round_items)
         self.rounds = R
+        self.plan_info = {"budget_gb": self.budget / 1e9, "out_gb": out_bytes / 1e9, "arena_a_gb": a_need / 1e9,
+                          "arena_b_gb": b_need / 1e9, "rounds": R}
         _, recv = round_sizes(C, cuts, G, R)
         cap = int(recv[me].sum())
         vb = self._vb(C)
@@ -465,11 +467,15 @@ class DistPipeline:
                 A, B = self.arena_a.get(a_need), self.arena_b.get(b_need)
                 rtab, sc, so = round_send(H, cuts, G, R, r)
                 dev.upload(self.d_rtab, rtab)
+                # the send buffer is arena A; one rank extracts straight into
+                # its receive buffer B (no exchange at all)
                 N.check(ctx, L.kman_dshard_extract(ctx, c_void_p(sh.codes.ptr), sh.n_eff, self.n_bases_q, self.k,
                                                    self.flags, self.fmode, c_void_p(self.d_hist.ptr),
-                                                   c_void_p(self.d_rtab.ptr), c_void_p(A.ptr)), "kman_dshard_extract")
+                                                   c_void_p(self.d_rtab.ptr), c_void_p((A if G > 1 else B).ptr)),
+                        "kman_dshard_extract")
                 lo, nb, counts, rcnt, roff = round_recv(C, cuts, R, me, r)
-                yield ("alltoallv", (A.ptr, sc, so, B.ptr, rcnt, roff, 8))
+                if G > 1:
+                    yield ("alltoallv", (A.ptr, sc, so, B.ptr, rcnt, roff, 8))
                 got = c_uint64(0)
                 ret = L.kman_dround_finish(ctx, c_void_p(B.ptr), self.k, self.flags, self.fmode, G, self.n_bases_q,
                                            lo, nb, _u64p(np.ascontiguousarray(counts.reshape(-1))),
@@ -492,9 +498,10 @@ class DistPipeline:
         return self.n_local
 
     def _vb(self, C) -> int:
-        if self.mode == "uniq":
-            return 8
-        return 4 if int(np.asarray(C, np.uint64).sum()) <= 0xFFFFFFFF else 8
+        """Output value bytes: uniq pos are u64 (source rank in bits 56-63);
+        counts are u32 -- a region-path count is at most a region's size, and
+        a general round checks its receive size (_general_round)."""
+        return 8 if self.mode == "uniq" else 4
 
     def _prefix_hist(self) -> np.ndarray:
         """Top-8-bit bucket totals of the shard (general path)."""
@@ -521,6 +528,8 @@ class DistPipeline:
         uniq = self.mode == "uniq"
         send, recv = round_sizes(C, cuts, G, R)
         ns, nr = int(send[me, r]), int(recv[me, r])
+        if vb == 4 and int(recv[:, r].max()) > 0xFFFFFFFF:  # (every rank sees the same sizes)
+            raise NotImplementedError("a general round of more than 2^32 k-mers would need u64 counts")
         sk, rk, ak = (self.gen_bufs[i].get(8 * max(1, n)) for i, n in ((0, ns), (1, nr), (2, nr)))
         sp = rp = ap = None
         if uniq:
