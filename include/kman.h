@@ -300,6 +300,29 @@ int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_t k, uint32
 int kman_count_hist(kman_ctx *ctx, const void *d_counts, uint32_t count_bytes, uint64_t n, uint64_t *d_hist,
                     uint32_t nbins);
 
+/* k in 33..64 (Sequence.yield_kmers has no k limit, seq.py:285-328): keys
+ * as word pairs, hi = the first k - 32 bases (2(k-32) bits), lo = the last 32
+ * bases, both 2 bits per base MSB-first, so (hi, lo) in lexicographic order is
+ * the reference's str order.
+ *   kman_extract_wide  keys (+ pos) in stream order; d_hi = d_lo = NULL only
+ *                      counts (*n_kmers); flags KMAN_RC | KMAN_CANONICAL |
+ *                      KMAN_WANT_POS as kman_extract
+ *   kman_iota_u64      v[i] = i
+ *   kman_gather        dst[i] = src[idx[i]] (4 or 8 byte elements)
+ *   kman_rle_wide      count / uniq of (hi, lo) pairs sorted lexicographically
+ *                      (mode KMAN_FINISH_COUNT: d_ovals = group sizes; UNIQ:
+ *                      the pairs of groups of one with their d_vals payload)
+ * The sort is two stable kman_sort passes: by lo with an index payload, then
+ * by the gathered hi (an LSD sort over 2k bits); the host writers
+ * kman_format_*_wide print the pairs. */
+int kman_extract_wide(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                      uint64_t *d_hi, uint64_t *d_lo, void *d_pos, uint32_t pos_bytes, uint64_t cap,
+                      uint64_t *n_kmers);
+int kman_iota_u64(kman_ctx *ctx, uint64_t *d_v, uint64_t n);
+int kman_gather(kman_ctx *ctx, const void *d_src, const uint64_t *d_idx, uint64_t n, void *d_dst, uint32_t elem_bytes);
+int kman_rle_wide(kman_ctx *ctx, int mode, const uint64_t *d_hi, const uint64_t *d_lo, const void *d_vals,
+                  uint32_t val_bytes, uint64_t n, uint64_t *d_ohi, uint64_t *d_olo, void *d_ovals, uint64_t *n_out);
+
 /* Run-length count of sorted keys (join.py:95-130 + 266-285):
  * d_ukeys[j], d_counts[j] (u32 if count_bytes == 4 else u64). */
 int kman_rle_count(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint64_t *d_ukeys,
@@ -373,6 +396,12 @@ int kman_format_uniq(const uint64_t *keys, const void *pos, uint32_t pos_bytes, 
                      const uint64_t *rec_seq, uint64_t n_records, char *out, size_t cap,
                      size_t *used, int threads);
 
+int kman_format_count_wide(const uint64_t *hi, const uint64_t *lo, const void *counts, uint32_t count_bytes,
+                           uint64_t n, uint32_t k, char *out, size_t cap, size_t *used, int threads);
+int kman_format_uniq_wide(const uint64_t *hi, const uint64_t *lo, const void *pos, uint32_t pos_bytes, uint64_t n,
+                          uint32_t k, const char *names, const uint64_t *name_off, const uint64_t *rec_seq,
+                          uint64_t n_records, char *out, size_t cap, size_t *used, int threads);
+
 /* The same writers on the device: the output text is built in
  * HBM (d_out, 16-byte aligned) from device-resident results, so only the text
  * crosses PCIe.  Byte-identical to kman_format_count / kman_format_uniq.
@@ -384,6 +413,13 @@ int kman_format_count_dev(kman_ctx *ctx, const uint64_t *d_ukeys, const void *d_
 int kman_format_uniq_dev(kman_ctx *ctx, const uint64_t *d_keys, const void *d_pos, uint32_t pos_bytes, uint64_t n,
                          uint32_t k, const char *d_names, const uint64_t *d_name_off, const uint64_t *d_rec_seq,
                          uint64_t n_records, char *d_out, size_t cap, size_t *used);
+/* k in 33..64: the same writers over word-pair keys (kman_extract_wide). */
+int kman_format_count_wide_dev(kman_ctx *ctx, const uint64_t *d_hi, const uint64_t *d_lo, const void *d_counts,
+                               uint32_t count_bytes, uint64_t n, uint32_t k, char *d_out, size_t cap, size_t *used);
+int kman_format_uniq_wide_dev(kman_ctx *ctx, const uint64_t *d_hi, const uint64_t *d_lo, const void *d_pos,
+                              uint32_t pos_bytes, uint64_t n, uint32_t k, const char *d_names,
+                              const uint64_t *d_name_off, const uint64_t *d_rec_seq, uint64_t n_records, char *d_out,
+                              size_t cap, size_t *used);
 
 #ifdef __cplusplus
 }

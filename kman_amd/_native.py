@@ -152,6 +152,32 @@ SIGNATURES = {
     "kman_or_u64": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64]),
     "kman_widen_u32": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_uint64]),
     "kman_memcpy_d2d": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+    "kman_extract_wide": (
+        c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_uint32, c_uint64,
+                POINTER(c_uint64)],
+    ),
+    "kman_iota_u64": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "kman_gather": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, c_void_p, c_uint32]),
+    "kman_rle_wide": (
+        c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p,
+                POINTER(c_uint64)],
+    ),
+    "kman_format_count_wide": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_size_t, POINTER(c_size_t),
+                c_int],
+    ),
+    "kman_format_uniq_wide": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_uint64,
+                c_void_p, c_size_t, POINTER(c_size_t), c_int],
+    ),
+    "kman_format_count_wide_dev": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_size_t,
+                POINTER(c_size_t)],
+    ),
+    "kman_format_uniq_wide_dev": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p,
+                c_uint64, c_void_p, c_size_t, POINTER(c_size_t)],
+    ),
     "kman_rebase_pos": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_uint32]),
     "kman_synth_fasta": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32]),
     "kman_copy_h2d_async": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int]),

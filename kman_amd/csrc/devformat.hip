@@ -74,20 +74,30 @@ KMAN_DEV uint32_t put_seq(const S &s, uint32_t at, uint64_t key, uint32_t k) {
     return at;
 }
 
+// k > 32: the key is (hi, lo), the first k - 32 bases in hi
+template <typename S>
+KMAN_DEV uint32_t put_key(const S &s, uint32_t at, const uint64_t *hi, uint64_t khi, uint64_t key, uint32_t k) {
+    if (!hi) return put_seq(s, at, key, k);
+    at = put_seq(s, at, khi, k - 32);
+    return put_seq(s, at, key, 32);
+}
+
 struct CountRows {
     const uint64_t *keys;
     const void *vals;
     uint32_t vb, k;
+    const uint64_t *hi = nullptr;  // word-pair keys (k > 32)
     KMAN_DEV uint64_t val(uint64_t i) const {
         return vb == 4 ? ((const uint32_t *)vals)[i] : ((const uint64_t *)vals)[i];
     }
     struct Row {
-        uint64_t key, c;
+        uint64_t key, khi, c;
         uint32_t nd;
     };
     KMAN_DEV Row load(uint64_t i) const {
         Row r;
         r.key = keys[i];
+        r.khi = hi ? hi[i] : 0;
         r.c = val(i);
         r.nd = ndig(r.c);
         return r;
@@ -95,7 +105,7 @@ struct CountRows {
     KMAN_DEV uint32_t len(const Row &r) const { return k + 2 + r.nd; }
     template <typename S>
     KMAN_DEV uint32_t write(const S &s, uint32_t at, const Row &r) const {
-        at = put_seq(s, at, r.key, k);
+        at = put_key(s, at, hi, r.khi, r.key, k);
         s.put(at++, '\t');
         at = put_dec(s, at, r.c, r.nd);
         s.put(at++, '\n');
@@ -110,14 +120,16 @@ struct UniqRows {
     const uint8_t *names;
     const uint64_t *name_off, *rec_seq;
     uint64_t R;
+    const uint64_t *hi = nullptr;  // word-pair keys (k > 32)
     struct Row {
-        uint64_t key, st, noff;
+        uint64_t key, khi, st, noff;
         uint32_t nlen, nd0, nd1;
         bool minus;
     };
     KMAN_DEV Row load(uint64_t i) const {
         Row r;
         r.key = keys[i];
+        r.khi = hi ? hi[i] : 0;
         const uint64_t v = vb == 4 ? ((const uint32_t *)vals)[i] : ((const uint64_t *)vals)[i];
         const uint64_t g = v >> 1;
         r.minus = v & 1;
@@ -150,7 +162,7 @@ struct UniqRows {
         s.put(at++, ':');
         s.put(at++, r.minus ? '-' : '+');
         s.put(at++, '\n');
-        at = put_seq(s, at, r.key, k);
+        at = put_key(s, at, hi, r.khi, r.key, k);
         s.put(at++, '\n');
         return at;
     }
@@ -272,5 +284,28 @@ extern "C" int kman_format_uniq_dev(kman_ctx *ctx, const uint64_t *d_keys, const
     return run_format(ctx,
                       UniqRows{d_keys, d_pos, pos_bytes, k, reinterpret_cast<const uint8_t *>(d_names), d_name_off,
                                d_rec_seq, n_records},
+                      n, d_out, cap, used);
+}
+
+extern "C" int kman_format_count_wide_dev(kman_ctx *ctx, const uint64_t *d_hi, const uint64_t *d_lo,
+                                          const void *d_counts, uint32_t count_bytes, uint64_t n, uint32_t k,
+                                          char *d_out, size_t cap, size_t *used) {
+    if (!ctx || !used || (n && (!d_hi || !d_lo || !d_counts))) return KMAN_EINVAL;
+    if (k < 33 || k > 64) return kman_fail(ctx, KMAN_EINVAL, "k must be in [33, 64], got %u", k);
+    if (count_bytes != 4 && count_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "count_bytes must be 4 or 8");
+    return run_format(ctx, CountRows{d_lo, d_counts, count_bytes, k, d_hi}, n, d_out, cap, used);
+}
+
+extern "C" int kman_format_uniq_wide_dev(kman_ctx *ctx, const uint64_t *d_hi, const uint64_t *d_lo, const void *d_pos,
+                                         uint32_t pos_bytes, uint64_t n, uint32_t k, const char *d_names,
+                                         const uint64_t *d_name_off, const uint64_t *d_rec_seq, uint64_t n_records,
+                                         char *d_out, size_t cap, size_t *used) {
+    if (!ctx || !used || (n && (!d_hi || !d_lo || !d_pos || !d_name_off || !d_rec_seq || !n_records)))
+        return KMAN_EINVAL;
+    if (k < 33 || k > 64) return kman_fail(ctx, KMAN_EINVAL, "k must be in [33, 64], got %u", k);
+    if (pos_bytes != 4 && pos_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "pos_bytes must be 4 or 8");
+    return run_format(ctx,
+                      UniqRows{d_lo, d_pos, pos_bytes, k, reinterpret_cast<const uint8_t *>(d_names), d_name_off,
+                               d_rec_seq, n_records, d_hi},
                       n, d_out, cap, used);
 }

@@ -437,3 +437,148 @@ extern "C" int kman_debug_kmer_hist(kman_ctx *ctx, const uint8_t *d_codes, uint6
     if (!ctx || !n_kmers) return KMAN_EINVAL;
     return kman_kmer_hist(ctx, d_codes, n_bases, k, flags, lo_bit, 1, 1ull << 62, d_hist, n_kmers);
 }
+
+// ===================================================================== k > 32
+// Wide keys (k in 33..64; Sequence.yield_kmers has no k limit, seq.py:285-328):
+// key = hi (the first k - 32 bases, 2(k-32) bits) : lo (the last 32 bases),
+// MSB-first in each word, so (hi, lo) in lexicographic order == the
+// reference's str order.  Tiles of ET x WEI windows rolled from LDS-staged
+// codes (the 64-code halo covers k - 1 <= 63), compacted in stream order by a
+// decoupled look-back; hi == nullptr counts only.
+namespace {
+
+constexpr int WEI = 8;
+
+template <bool RC, bool CANON, typename P>
+__global__ __launch_bounds__(ET) void extract_wide_kernel(const uint8_t *__restrict__ codes, uint64_t n_bases,
+                                                          uint64_t n_tiles, int k, uint64_t *__restrict__ hi,
+                                                          uint64_t *__restrict__ lo, P *__restrict__ pos,
+                                                          uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
+                                                          uint32_t epoch, uint32_t *__restrict__ err, uint64_t cap) {
+    constexpr int TILE = ET * WEI;
+    constexpr bool HAS_POS = !std::is_same<P, NoPos>::value;
+    __shared__ __attribute__((aligned(16))) uint8_t scodes[TILE + 64];
+    __shared__ uint32_t lds_scan[ET / 64];
+    __shared__ uint64_t lds_base;
+    __shared__ uint32_t lds_tile;
+    const int kh = k - 32;
+    const uint64_t mh = kh >= 32 ? ~0ull : ((1ull << (2 * kh)) - 1);
+    for (;;) {
+        const int64_t tile = grab_tile(counter, &lds_tile);
+        if ((uint64_t)tile >= n_tiles) break;
+        const uint64_t tb = (uint64_t)tile * TILE;
+        stage_codes<ET, WEI>(codes, n_bases, tb, scodes);
+        __syncthreads();
+        const int base = threadIdx.x * WEI;
+        const uint64_t p0 = tb + (uint64_t)base;
+        uint64_t fh = 0, fl = 0, rh = 0, rl = 0;
+        uint32_t run = 0;
+        auto push = [&](uint32_t c) {
+            run = (c & 8) ? 0 : run;
+            run = (c & 4) ? 0 : run + 1;
+            fh = ((fh << 2) | (fl >> 62)) & mh;
+            fl = (fl << 2) | (c & 3);
+            rl = (rl >> 2) | (rh << 62);
+            rh = (rh >> 2) | ((uint64_t)(3 - (c & 3)) << (2 * kh - 2));
+        };
+        for (int q = 0; q < k - 1; q++) push(scodes[base + q]);
+        uint64_t oh[WEI][2], ol[WEI][2];
+        uint32_t valid = 0;
+#pragma unroll
+        for (int j = 0; j < WEI; j++) {
+            push(scodes[base + k - 1 + j]);
+            const bool ok = run >= (uint32_t)k && p0 + j < n_bases;
+            valid |= (uint32_t)ok << j;
+            if (CANON) {
+                const bool fwd = fh < rh || (fh == rh && fl <= rl);
+                oh[j][0] = fwd ? fh : rh;
+                ol[j][0] = fwd ? fl : rl;
+            } else {
+                oh[j][0] = fh;
+                ol[j][0] = fl;
+                oh[j][1] = rh;
+                ol[j][1] = rl;
+            }
+        }
+        constexpr uint32_t PER = RC && !CANON ? 2u : 1u;
+        uint32_t total;
+        const uint32_t off = block_exclusive_scan<ET>((uint32_t)__popc(valid) * PER, SumU32(), 0u, lds_scan, &total);
+        if (threadIdx.x < 64) {
+            const uint64_t b = wave_lookback<0>(status, tile, total, epoch, err);
+            if (threadIdx.x == 0) lds_base = b;
+        }
+        __syncthreads();
+        if (hi) {
+            uint64_t o = lds_base + off;
+#pragma unroll
+            for (int j = 0; j < WEI; j++) {
+                if (!((valid >> j) & 1u)) continue;
+#pragma unroll
+                for (uint32_t s = 0; s < PER; s++) {
+                    if (o < cap) {
+                        hi[o] = oh[j][s];
+                        lo[o] = ol[j][s];
+                        if constexpr (HAS_POS) pos[o] = (P)(((p0 + j) << 1) | s);
+                    }
+                    o++;
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+template <bool RC, bool CANON, typename P>
+int launch_wide(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k, uint64_t *hi, uint64_t *lo, P *pos,
+                uint64_t cap, uint64_t *n_out) {
+    const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * WEI);
+    uint32_t epoch, *counter;
+    KMAN_TRY(kman_lookback_begin(ctx, n_tiles, &epoch, &counter));
+    auto fn = extract_wide_kernel<RC, CANON, P>;
+    const int grid = kman_persistent_grid(ctx, (const void *)fn, ET, n_tiles);
+    {
+        KTimer kt_(ctx, "extract");
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(ET), 0, ctx->stream, codes, n_bases, n_tiles, k, hi, lo, pos,
+                           ctx->d_status, counter, epoch, ctx->d_err, cap);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    return kman_lookback_total(ctx, n_tiles, n_out);
+}
+
+template <typename P>
+int dispatch_wide(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k, uint32_t flags, uint64_t *hi,
+                  uint64_t *lo, P *pos, uint64_t cap, uint64_t *n_out) {
+    if (flags & KMAN_CANONICAL) return launch_wide<false, true, P>(ctx, codes, n_bases, k, hi, lo, pos, cap, n_out);
+    if (flags & KMAN_RC) return launch_wide<true, false, P>(ctx, codes, n_bases, k, hi, lo, pos, cap, n_out);
+    return launch_wide<false, false, P>(ctx, codes, n_bases, k, hi, lo, pos, cap, n_out);
+}
+
+}  // namespace
+
+extern "C" int kman_extract_wide(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                                 uint64_t *d_hi, uint64_t *d_lo, void *d_pos, uint32_t pos_bytes, uint64_t cap,
+                                 uint64_t *n_kmers) {
+    if (!ctx || !n_kmers) return KMAN_EINVAL;
+    if (k < 33 || k > 64) return kman_fail(ctx, KMAN_EINVAL, "kman_extract_wide: k must be in [33, 64], got %u", k);
+    const bool want_pos = flags & KMAN_WANT_POS;
+    if ((d_hi == nullptr) != (d_lo == nullptr)) return kman_fail(ctx, KMAN_EINVAL, "hi and lo go together");
+    if (want_pos && d_hi && pos_bytes != 4 && pos_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "pos_bytes must be 4 or 8");
+    if (want_pos && pos_bytes == 4 && (n_bases << 1) > 0xffffffffull)
+        return kman_fail(ctx, KMAN_EINVAL, "u32 pos payload cannot address %llu bases", (unsigned long long)n_bases);
+    if (((uintptr_t)d_codes & 15) != 0) return kman_fail(ctx, KMAN_EINVAL, "codes must be 16-byte aligned");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    *n_kmers = 0;
+    if (n_bases == 0) return KMAN_OK;
+    if (!want_pos || !d_hi)
+        KMAN_TRY(dispatch_wide<NoPos>(ctx, d_codes, n_bases, (int)k, flags, d_hi, d_lo, nullptr, cap, n_kmers));
+    else if (pos_bytes == 4)
+        KMAN_TRY(dispatch_wide<uint32_t>(ctx, d_codes, n_bases, (int)k, flags, d_hi, d_lo, (uint32_t *)d_pos, cap,
+                                         n_kmers));
+    else
+        KMAN_TRY(dispatch_wide<uint64_t>(ctx, d_codes, n_bases, (int)k, flags, d_hi, d_lo, (uint64_t *)d_pos, cap,
+                                         n_kmers));
+    if (d_hi && *n_kmers > cap)
+        return kman_fail(ctx, KMAN_ECAP, "%llu k-mers > capacity %llu", (unsigned long long)*n_kmers,
+                         (unsigned long long)cap);
+    return KMAN_OK;
+}

@@ -45,6 +45,12 @@ inline char *put_seq(char *p, uint64_t key, uint32_t k) {
     return p;
 }
 
+// k > 32: the first k - 32 bases in hi, the last 32 in lo
+inline char *put_seq_wide(char *p, uint64_t hi, uint64_t lo, uint32_t k) {
+    p = put_seq(p, hi, k - 32);
+    return put_seq(p, lo, 32);
+}
+
 inline uint64_t get_val(const void *a, uint32_t bytes, uint64_t i) {
     return bytes == 4 ? ((const uint32_t *)a)[i] : ((const uint64_t *)a)[i];
 }
@@ -100,7 +106,8 @@ struct Names {
 };
 
 int format_fasta_impl(const uint64_t *keys, const void *pos, uint32_t pos_bytes, uint64_t n, uint32_t k,
-                      const Names &nm, char *out, size_t cap, size_t *used, int threads) {
+                      const Names &nm, char *out, size_t cap, size_t *used, int threads,
+                      const uint64_t *hi = nullptr) {
     auto size_of = [&](uint64_t i) -> size_t {
         const uint64_t v = get_val(pos, pos_bytes, i);
         const uint64_t p = v >> 1;
@@ -125,7 +132,7 @@ int format_fasta_impl(const uint64_t *keys, const void *pos, uint32_t pos_bytes,
         *p++ = ':';
         *p++ = (v & 1) ? '-' : '+';
         *p++ = '\n';
-        p = put_seq(p, keys[i], k);
+        p = hi ? put_seq_wide(p, hi[i], keys[i], k) : put_seq(p, keys[i], k);
         *p++ = '\n';
         return p;
     };
@@ -156,4 +163,31 @@ extern "C" int kman_format_uniq(const uint64_t *keys, const void *pos, uint32_t 
     if (pos_bytes != 4 && pos_bytes != 8) return KMAN_EINVAL;
     Names nm{names, name_off, rec_seq, n_records};
     return format_fasta_impl(keys, pos, pos_bytes, n, k, nm, out, cap, used, threads);
+}
+
+// k in 33..64: keys as (hi, lo) word pairs (kman_extract_wide)
+extern "C" int kman_format_count_wide(const uint64_t *hi, const uint64_t *lo, const void *counts, uint32_t count_bytes,
+                                      uint64_t n, uint32_t k, char *out, size_t cap, size_t *used, int threads) {
+    if (!used || (n && (!hi || !lo || !counts)) || k < 33 || k > 64) return KMAN_EINVAL;
+    if (count_bytes != 4 && count_bytes != 8) return KMAN_EINVAL;
+    auto size_of = [&](uint64_t i) -> size_t { return k + 2 + ndigits(get_val(counts, count_bytes, i)); };
+    auto write_at = [&](uint64_t i, char *p) -> char * {
+        p = put_seq_wide(p, hi[i], lo[i], k);
+        *p++ = '\t';
+        p = put_u64(p, get_val(counts, count_bytes, i));
+        *p++ = '\n';
+        return p;
+    };
+    return run_sliced(n, out, cap, used, threads, size_of, write_at);
+}
+
+extern "C" int kman_format_uniq_wide(const uint64_t *hi, const uint64_t *lo, const void *pos, uint32_t pos_bytes,
+                                     uint64_t n, uint32_t k, const char *names, const uint64_t *name_off,
+                                     const uint64_t *rec_seq, uint64_t n_records, char *out, size_t cap, size_t *used,
+                                     int threads) {
+    if (!used || (n && (!hi || !lo || !pos || !name_off || !rec_seq || !n_records)) || k < 33 || k > 64)
+        return KMAN_EINVAL;
+    if (pos_bytes != 4 && pos_bytes != 8) return KMAN_EINVAL;
+    Names nm{names, name_off, rec_seq, n_records};
+    return format_fasta_impl(lo, pos, pos_bytes, n, k, nm, out, cap, used, threads, hi);
 }

@@ -105,6 +105,18 @@ __global__ void synth_kernel(uint8_t *__restrict__ out, uint64_t lo, uint64_t n,
     }
 }
 
+__global__ void iota_kernel(uint64_t *__restrict__ v, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        v[i] = i;
+}
+
+template <typename T>
+__global__ void gather_kernel(const T *__restrict__ src, const uint64_t *__restrict__ idx, uint64_t n,
+                              T *__restrict__ dst) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        dst[i] = src[idx[i]];
+}
+
 uint32_t grid_for(uint64_t n) {
     const uint64_t b = ceil_div(n, 256);
     return (uint32_t)(b < 8192 ? (b ? b : 1) : 8192);
@@ -182,5 +194,30 @@ extern "C" int kman_synth_fasta(kman_ctx *ctx, uint8_t *d_out, uint64_t byte_lo,
                        n_bytes, seed, (const SynthRec *)tab, n_records, line);
     HIP_TRY(ctx, hipGetLastError());
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return KMAN_OK;
+}
+
+extern "C" int kman_iota_u64(kman_ctx *ctx, uint64_t *d_v, uint64_t n) {
+    if (!ctx) return KMAN_EINVAL;
+    if (n == 0) return KMAN_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    hipLaunchKernelGGL(iota_kernel, dim3(grid_for(n)), dim3(256), 0, ctx->stream, d_v, n);
+    HIP_TRY(ctx, hipGetLastError());
+    return KMAN_OK;
+}
+
+extern "C" int kman_gather(kman_ctx *ctx, const void *d_src, const uint64_t *d_idx, uint64_t n, void *d_dst,
+                           uint32_t elem_bytes) {
+    if (!ctx) return KMAN_EINVAL;
+    if (elem_bytes != 4 && elem_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "elem_bytes must be 4 or 8");
+    if (n == 0) return KMAN_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (elem_bytes == 8)
+        hipLaunchKernelGGL(gather_kernel<uint64_t>, dim3(grid_for(n)), dim3(256), 0, ctx->stream,
+                           (const uint64_t *)d_src, d_idx, n, (uint64_t *)d_dst);
+    else
+        hipLaunchKernelGGL(gather_kernel<uint32_t>, dim3(grid_for(n)), dim3(256), 0, ctx->stream,
+                           (const uint32_t *)d_src, d_idx, n, (uint32_t *)d_dst);
+    HIP_TRY(ctx, hipGetLastError());
     return KMAN_OK;
 }

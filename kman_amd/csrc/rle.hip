@@ -217,6 +217,97 @@ __global__ __launch_bounds__(RT) void rle_uniq_kernel(const uint64_t *__restrict
     }
 }
 
+// Wide keys (k > 32): (hi, lo) pairs, sorted lexicographically; count or
+// uniq in one tile pass like the kernels above (keys read straight from HBM,
+// outputs written in place).  MODE 1: (hi, lo, group size); 2: the keys of
+// groups of one with their payload.
+template <int MODE, typename V>
+__global__ __launch_bounds__(RT) void rle_wide_kernel(const uint64_t *__restrict__ hi, const uint64_t *__restrict__ lo,
+                                                      const V *__restrict__ vals, uint64_t n,
+                                                      uint64_t *__restrict__ ohi, uint64_t *__restrict__ olo,
+                                                      V *__restrict__ ovals, uint64_t *__restrict__ st_sum,
+                                                      uint64_t *__restrict__ st_max, uint32_t *__restrict__ counter,
+                                                      uint32_t epoch, uint32_t *__restrict__ err) {
+    __shared__ uint32_t lds_scan[RT / 64];
+    __shared__ uint64_t lds_scan64[RT / 64];
+    __shared__ uint64_t lds_base, lds_head;
+    __shared__ uint32_t lds_tile;
+    const int64_t tile = grab_tile(counter, &lds_tile);
+    const uint64_t tb = (uint64_t)tile * RTILE;
+    const uint64_t t0 = tb + (uint64_t)threadIdx.x * RI;
+    uint64_t kh[RI + 2], kl[RI + 2];  // [0] = previous key, [RI + 1] = next key
+#pragma unroll
+    for (int j = 0; j < RI + 2; j++) {
+        const uint64_t i = t0 + j - 1;
+        const bool in = t0 + j >= 1 && i < n;
+        kh[j] = in ? hi[i] : ~0ull;
+        kl[j] = in ? lo[i] : ~0ull;
+    }
+    uint32_t heads = 0, tails = 0;
+#pragma unroll
+    for (int j = 1; j <= RI; j++) {
+        const uint64_t i = t0 + j - 1;
+        const bool in = i < n;
+        const bool dp = kh[j] != kh[j - 1] || kl[j] != kl[j - 1];
+        const bool dn = kh[j] != kh[j + 1] || kl[j] != kl[j + 1];
+        heads |= (uint32_t)(in && (i == 0 || dp)) << (j - 1);
+        tails |= (uint32_t)(in && (i + 1 == n || dn)) << (j - 1);
+    }
+    if constexpr (MODE == 2) {
+        const uint32_t single = heads & tails;
+        uint32_t tile_cnt;
+        const uint32_t off = block_exclusive_scan<RT>((uint32_t)__popc(single), SumU32(), 0u, lds_scan, &tile_cnt);
+        if (threadIdx.x < 64) {
+            const uint64_t b = wave_lookback<0>(st_sum, tile, tile_cnt, epoch, err);
+            if (threadIdx.x == 0) lds_base = b;
+        }
+        __syncthreads();
+        uint64_t o = lds_base + off;
+#pragma unroll
+        for (int j = 0; j < RI; j++) {
+            if ((single >> j) & 1u) {
+                ohi[o] = kh[j + 1];
+                olo[o] = kl[j + 1];
+                ovals[o] = vals[t0 + j];
+                o++;
+            }
+        }
+    } else {
+        const uint32_t nh = __popc(heads);
+        const uint64_t lh = heads ? t0 + (31 - __clz(heads)) + 1 : 0;
+        uint32_t tile_heads;
+        const uint32_t hoff = block_exclusive_scan<RT>(nh, SumU32(), 0u, lds_scan, &tile_heads);
+        uint64_t tile_lh;
+        const uint64_t lh_before = block_exclusive_scan<RT>(lh, MaxU64(), (uint64_t)0, lds_scan64, &tile_lh);
+        // does the tile start with a group head?
+        const bool first_is_head = tb == 0 || hi[tb] != hi[tb - 1] || lo[tb] != lo[tb - 1];
+        if (threadIdx.x < 64) {
+            const uint64_t b = wave_lookback<0>(st_sum, tile, tile_heads, epoch, err);
+            const uint64_t h = wave_lookback_lasthead(st_max, tile, tile_lh, !first_is_head, epoch, err);
+            if (threadIdx.x == 0) {
+                lds_base = b;
+                lds_head = h;
+            }
+        }
+        __syncthreads();
+        uint64_t cur_head = lh_before ? lh_before : lds_head;
+        uint64_t slot = lds_base + hoff;
+#pragma unroll
+        for (int j = 0; j < RI; j++) {
+            const uint64_t i = t0 + j;
+            if ((heads >> j) & 1u) {
+                cur_head = i + 1;
+                slot++;
+            }
+            if ((tails >> j) & 1u) {
+                ohi[slot - 1] = kh[j + 1];
+                olo[slot - 1] = kl[j + 1];
+                ovals[slot - 1] = (V)(i + 2 - cur_head);
+            }
+        }
+    }
+}
+
 }  // namespace
 
 extern "C" int kman_rle_count(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint64_t *d_ukeys, void *d_counts,
@@ -261,6 +352,36 @@ extern "C" int kman_rle_uniq(kman_ctx *ctx, const uint64_t *d_keys, const void *
         hipLaunchKernelGGL(rle_uniq_kernel<uint64_t>, dim3((uint32_t)T), dim3(RT), 0, ctx->stream, d_keys,
                            (const uint64_t *)d_vals, n, d_okeys, (uint64_t *)d_ovals, ctx->d_status, counter, epoch,
                            ctx->d_err);
+    HIP_TRY(ctx, hipGetLastError());
+    return kman_lookback_total(ctx, T, n_out);
+}
+
+extern "C" int kman_rle_wide(kman_ctx *ctx, int mode, const uint64_t *d_hi, const uint64_t *d_lo, const void *d_vals,
+                             uint32_t val_bytes, uint64_t n, uint64_t *d_ohi, uint64_t *d_olo, void *d_ovals,
+                             uint64_t *n_out) {
+    if (!ctx || !n_out) return KMAN_EINVAL;
+    if (mode != KMAN_FINISH_COUNT && mode != KMAN_FINISH_UNIQ) return kman_fail(ctx, KMAN_EINVAL, "bad mode");
+    if (val_bytes != 4 && val_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "val_bytes must be 4 or 8");
+    if (mode == KMAN_FINISH_COUNT && val_bytes == 4 && n > 0xffffffffull)
+        return kman_fail(ctx, KMAN_EINVAL, "u32 counts cannot hold groups of %llu keys", (unsigned long long)n);
+    *n_out = 0;
+    if (n == 0) return KMAN_OK;
+    if (!d_hi || !d_lo || !d_ohi || !d_olo || !d_ovals || (mode == KMAN_FINISH_UNIQ && !d_vals))
+        return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const uint64_t T = ceil_div(n, RTILE);
+    uint32_t epoch, *counter;
+    KMAN_TRY(kman_lookback_begin(ctx, 2 * T, &epoch, &counter));
+    KTimer kt_(ctx, mode == KMAN_FINISH_COUNT ? "rle_count" : "rle_uniq");
+#define KW(M, V)                                                                                                     \
+    hipLaunchKernelGGL((rle_wide_kernel<M, V>), dim3((uint32_t)T), dim3(RT), 0, ctx->stream, d_hi, d_lo,            \
+                       (const V *)d_vals, n, d_ohi, d_olo, (V *)d_ovals, ctx->d_status, ctx->d_status + T, counter, \
+                       epoch, ctx->d_err)
+    if (mode == KMAN_FINISH_COUNT && val_bytes == 4) KW(1, uint32_t);
+    else if (mode == KMAN_FINISH_COUNT) KW(1, uint64_t);
+    else if (val_bytes == 4) KW(2, uint32_t);
+    else KW(2, uint64_t);
+#undef KW
     HIP_TRY(ctx, hipGetLastError());
     return kman_lookback_total(ctx, T, n_out);
 }

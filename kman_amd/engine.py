@@ -31,7 +31,8 @@ import numpy as np
 
 from . import _native as N
 
-MAX_K = 32  # 2-bit keys in one u64 on the GPU path
+MAX_K = 32       # 2-bit keys in one u64 (the region / prefix-split paths)
+MAX_K_WIDE = 64  # (hi, lo) word-pair keys (kman_extract_wide + two sort passes)
 
 
 def host_threads() -> int:
@@ -263,18 +264,26 @@ def flags_for(rc: bool, want_pos: bool, canonical: bool = False) -> int:
 
 
 def count_kmers(p: Parsed, k: int, rc: bool, canonical: bool = False) -> int:
-    _check_k(k)
+    _check_k(k, wide=True)
     out = c_uint64(0)
+    if k > MAX_K:
+        N.check(p.dev.ctx, N.lib().kman_extract_wide(p.dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
+                                                     flags_for(rc, False, canonical), None, None, None, 0, 0,
+                                                     byref(out)), "kman_extract_wide")
+        return int(out.value)
     N.check(p.dev.ctx, N.lib().kman_count_kmers(p.dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
                                                  flags_for(rc, False, canonical), byref(out)), "kman_count_kmers")
     return int(out.value)
 
 
-def _check_k(k: int) -> None:
+def _check_k(k: int, wide: bool = False) -> None:
+    """batcher.py:477-478 (k <= 1 raises AssertionError); k > 32 only where
+    the word-pair path runs (count / uniq), k > 64 not on the GPU."""
     if k <= 1:
         raise AssertionError("k must be >= 1, got %d instead." % k)
-    if k > MAX_K:
-        raise NotImplementedError("k=%d: the MI355X path packs k-mers in 64-bit keys (k <= %d)" % (k, MAX_K))
+    if k > (MAX_K_WIDE if wide else MAX_K):
+        raise NotImplementedError("k=%d: this MI355X path packs k-mers in %s (k <= %d)"
+                                  % (k, "two 64-bit words" if wide else "64-bit keys", MAX_K_WIDE if wide else MAX_K))
 
 
 def extract(p: Parsed, k: int, rc: bool, want_pos: bool, canonical: bool = False) -> Kmers:
@@ -911,12 +920,101 @@ def _fits(p: Parsed, k: int, rc: bool, mode: str) -> bool:
     return need <= 0.85 * mem_info(p.dev)[0]
 
 
+@dataclass
+class WideResult:
+    """count / uniq rows of k > 32: keys as (hi, lo) word pairs."""
+
+    hi: DeviceBuffer
+    lo: DeviceBuffer
+    vals: DeviceBuffer
+    val_bytes: int
+    n: int
+    k: int
+    mode: str
+
+
+def wide_groups(p: Parsed, k: int, rc: bool, mode: str, canonical: bool = False) -> Optional[WideResult]:
+    """k in 33..64 (seq.py:285-328 has no k limit): kman_extract_wide (keys as
+    (hi, lo) + pos), two stable kman_sort passes -- by lo with an index
+    payload, then by the gathered hi -- (batch.py:156-168), kman_rle_wide
+    (join.py:95-130, 244-285).  None when the stream has no k-mers."""
+    _check_k(k, wide=True)
+    dev, L = p.dev, N.lib()
+    uniq = mode == "uniq"
+    n = count_kmers(p, k, rc, canonical)
+    if n == 0:
+        return None
+    bufs = []
+
+    def alloc(nb):
+        b = dev.alloc(max(nb, 8))
+        bufs.append(b)
+        return b
+
+    try:
+        hi, lo, pos = alloc(8 * n), alloc(8 * n), alloc(8 * n) if uniq else None
+        got = c_uint64(0)
+        N.check(dev.ctx, L.kman_extract_wide(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
+                                             flags_for(rc, uniq, canonical), c_void_p(hi.ptr), c_void_p(lo.ptr),
+                                             c_void_p(pos.ptr) if uniq else None, 8, n, byref(got)),
+                "kman_extract_wide")
+        assert int(got.value) == n
+        a, b, idx, idx2 = alloc(8 * n), alloc(8 * n), alloc(8 * n), alloc(8 * n)
+        res = c_int(0)
+
+        def stable_sort(keys, alt, vals, valt, bits):
+            N.check(dev.ctx, L.kman_sort(dev.ctx, c_void_p(keys.ptr), c_void_p(alt.ptr), c_void_p(vals.ptr),
+                                         c_void_p(valt.ptr), 8, n, bits, None, byref(res)), "kman_sort")
+            return (alt, valt, keys, vals) if res.value else (keys, vals, alt, valt)
+
+        # LSD over the 2k key bits: the low word first (index payload) ...
+        N.check(dev.ctx, L.kman_iota_u64(dev.ctx, c_void_p(idx.ptr), n), "iota")
+        lo_s, idx1, spare_k, spare_v = stable_sort(lo, a, idx, idx2, 64)
+        N.check(dev.ctx, L.kman_gather(dev.ctx, c_void_p(hi.ptr), c_void_p(idx1.ptr), n, c_void_p(spare_k.ptr), 8),
+                "gather")
+        # ... then the high word (stable: ties keep the low-word order)
+        perm = hi  # (hi is consumed: its gathered copy is in spare_k)
+        N.check(dev.ctx, L.kman_iota_u64(dev.ctx, c_void_p(perm.ptr), n), "iota")
+        hi_s, perm2, _, _ = stable_sort(spare_k, b, perm, spare_v, 2 * (k - 32))
+        lo_f = alloc(8 * n)
+        N.check(dev.ctx, L.kman_gather(dev.ctx, c_void_p(lo_s.ptr), c_void_p(perm2.ptr), n, c_void_p(lo_f.ptr), 8),
+                "gather")
+        vals = None
+        if uniq:
+            orig = alloc(8 * n)
+            N.check(dev.ctx, L.kman_gather(dev.ctx, c_void_p(idx1.ptr), c_void_p(perm2.ptr), n, c_void_p(orig.ptr), 8),
+                    "gather")
+            vals = alloc(8 * n)
+            N.check(dev.ctx, L.kman_gather(dev.ctx, c_void_p(pos.ptr), c_void_p(orig.ptr), n, c_void_p(vals.ptr), 8),
+                    "gather")
+        ohi, olo = dev.alloc(8 * n), dev.alloc(8 * n)
+        vb = 8 if uniq else (4 if n <= 0xFFFFFFFF else 8)
+        ov = dev.alloc(vb * n)
+        out = c_uint64(0)
+        try:
+            N.check(dev.ctx, L.kman_rle_wide(dev.ctx, N.KMAN_FINISH_UNIQ if uniq else N.KMAN_FINISH_COUNT,
+                                             c_void_p(hi_s.ptr), c_void_p(lo_f.ptr),
+                                             c_void_p(vals.ptr) if uniq else None, vb, n, c_void_p(ohi.ptr),
+                                             c_void_p(olo.ptr), c_void_p(ov.ptr), byref(out)), "kman_rle_wide")
+        except BaseException:
+            for x in (ohi, olo, ov):
+                x.free()
+            raise
+        return WideResult(ohi, olo, ov, vb, int(out.value), k, mode)
+    finally:
+        for x in bufs:
+            x.free()
+
+
 def join_groups(p: Parsed, k: int, rc: bool, mode: str, max_keys: Optional[int] = None):
     """The count / uniq result of the whole stream of p on the device, by the
     fastest path that takes it: the region path (kman_groups); the multi-batch
     join (RangedJoin) when the single-batch general path does not fit the
     free HBM or max_keys asks for it; else the general path (extract_sorted +
-    rle_*).  None when the stream has no k-mers."""
+    rle_*); k > 32: the word-pair path (wide_groups).  None when the stream
+    has no k-mers."""
+    if k > MAX_K:
+        return wide_groups(p, k, rc, mode)
     r = groups(p, k, rc, mode) if max_keys is None else None
     if r is None and (max_keys is not None or not _fits(p, k, rc, mode)):
         r = ranged_groups(p, k, rc, mode, max_keys)
@@ -934,8 +1032,53 @@ def join_groups(p: Parsed, k: int, rc: bool, mode: str, max_keys: Optional[int] 
 def free_result(r) -> None:
     if r is None:
         return
-    for b in ((r.ukeys, r.counts) if isinstance(r, CountResult) else (r.keys, r.pos)):
+    if isinstance(r, WideResult):
+        bs = (r.hi, r.lo, r.vals)
+    else:
+        bs = (r.ukeys, r.counts) if isinstance(r, CountResult) else (r.keys, r.pos)
+    for b in bs:
         b.free()
+
+
+def _emit_wide(p: Parsed, r: WideResult, sink=None):
+    """Word-pair rows as the reference's text: built on the device
+    (kman_format_*_wide_dev), or by the host writers (kman_format_*_wide)
+    with KMAN_HOST_FORMAT=1."""
+    dev, L = p.dev, N.lib()
+    if not host_format():
+        vb = r.val_bytes
+        if r.mode == "count":
+            def call(i0, m, d_out, cap, used):
+                return L.kman_format_count_wide_dev(dev.ctx, c_void_p(r.hi.ptr + 8 * i0), c_void_p(r.lo.ptr + 8 * i0),
+                                                    c_void_p(r.vals.ptr + vb * i0), vb, m, r.k, d_out, cap,
+                                                    byref(used))
+
+            return _format_dev(dev, r.n, r.k + 2 + 20, call, sink)
+        nm = DeviceNames(p)
+        try:
+            D = len(str(p.n_bases + r.k))
+
+            def call(i0, m, d_out, cap, used):
+                return L.kman_format_uniq_wide_dev(dev.ctx, c_void_p(r.hi.ptr + 8 * i0), c_void_p(r.lo.ptr + 8 * i0),
+                                                   c_void_p(r.vals.ptr + vb * i0), vb, m, r.k,
+                                                   c_void_p(nm.names.ptr), c_void_p(nm.off.ptr), c_void_p(nm.rec.ptr),
+                                                   nm.n_records, d_out, cap, byref(used))
+
+            return _format_dev(dev, r.n, 1 + nm.max_name + 1 + D + 1 + D + 3 + r.k + 1, call, sink)
+        finally:
+            nm.free()
+    hi = dev.download(r.hi, r.n, np.uint64)
+    lo = dev.download(r.lo, r.n, np.uint64)
+    vals = dev.download(r.vals, r.n, np.uint32 if r.val_bytes == 4 else np.uint64)
+    if r.mode == "count":
+        return _to(sink, _format(L.kman_format_count_wide, hi.ctypes.data_as(c_void_p), lo.ctypes.data_as(c_void_p),
+                                 vals.ctypes.data_as(c_void_p), r.val_bytes, r.n, r.k))
+    names = ctypes.create_string_buffer(p.names_blob, max(1, len(p.names_blob)))
+    off = np.ascontiguousarray(p.name_off, dtype=np.uint64)
+    rs = np.ascontiguousarray(p.rec_seq, dtype=np.uint64)
+    return _to(sink, _format(L.kman_format_uniq_wide, hi.ctypes.data_as(c_void_p), lo.ctypes.data_as(c_void_p),
+                             vals.ctypes.data_as(c_void_p), r.val_bytes, r.n, r.k, names, off.ctypes.data_as(c_void_p),
+                             rs.ctypes.data_as(c_void_p), p.n_records))
 
 
 def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = None,
@@ -944,7 +1087,7 @@ def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = No
     max_keys: run the multi-batch join with key ranges of at most that many
     k-mers (by default only when the single batch does not fit the HBM)."""
     dev = dev or default_device()
-    _check_k(k)
+    _check_k(k, wide=True)
     p = parse(dev, text)
     try:
         check_empty_names(p, k)
@@ -952,6 +1095,8 @@ def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = No
         if r is None:
             return b""
         try:
+            if isinstance(r, WideResult):
+                return _emit_wide(p, r)
             return emit_count(dev, r)
         finally:
             free_result(r)
@@ -964,7 +1109,7 @@ def uniq_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = Non
     """``kmer uniq`` output bytes for a FASTA text (UNIQUE mode); max_keys as
     in count_text."""
     dev = dev or default_device()
-    _check_k(k)
+    _check_k(k, wide=True)
     p = parse(dev, text)
     try:
         check_empty_names(p, k)
@@ -972,6 +1117,8 @@ def uniq_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = Non
         if r is None:
             return b""
         try:
+            if isinstance(r, WideResult):
+                return _emit_wide(p, r)
             return emit_uniq(p, r)
         finally:
             free_result(r)

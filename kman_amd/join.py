@@ -205,6 +205,8 @@ def join_bytes(batches: List[Batch], count: bool, sink=None):
         if r is None:
             return None if sink is not None else b""
         try:
+            if isinstance(r, engine.WideResult):
+                return engine._emit_wide(whole.parsed, r, sink)
             if count:
                 return engine.emit_count(whole.dev, r, sink)
             return engine.emit_uniq(whole.parsed, r, sink)

@@ -26,7 +26,7 @@ from . import engine
 
 class FastaSource:
     def __init__(self, dev: engine.Device, text: bytes, k: int, rc: bool):
-        engine._check_k(k)
+        engine._check_k(k, wide=True)
         self.dev, self.k, self.rc = dev, k, rc
         self.parsed = engine.parse(dev, text)
         engine.check_empty_names(self.parsed, k)
@@ -39,6 +39,7 @@ class FastaSource:
         place (sorts work on copies)."""
         km = self._km.get(want_pos) or (self._km.get(True) if not want_pos else None)
         if km is None:
+            engine._check_k(self.k)  # (k > 32: whole-stream count / uniq only, see engine.wide_groups)
             km = engine.extract(self.parsed, self.k, self.rc, want_pos=want_pos)
             self._km[want_pos] = km
         return km

@@ -33,7 +33,7 @@ def _ref_cases():
 
     with open(os.path.join(GOLDEN, "manifest.json")) as fh:
         cases = json.load(fh)["cases"]
-    return [c for c in cases if c["cmd"] == "count" and "-r" in c["flags"] and c["k"] % 2 == 1 and c["k"] <= 32
+    return [c for c in cases if c["cmd"] == "count" and "-r" in c["flags"] and c["k"] % 2 == 1 and c["k"] <= 64
             and os.path.isfile(os.path.join(GOLDEN, "ref_outputs", c["name"] + ".txt"))]
 
 
