@@ -171,9 +171,11 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
         uint32_t o = off;
 #pragma unroll
         for (int j = 0; j < EI; j++) {
-            const uint64_t tag = (uint64_t)((w0 + j) << 1) << kb;
+            // the tile-local (window << 1 | strand) above the key bits: only
+            // uniq items carry it (Q > 0, k <= 25); count items are the key
+            const uint64_t tag = Q ? (uint64_t)((w0 + j) << 1) << kb : 0ull;
             if ((vf >> j) & 1u) skeys[o++] = kf[j] | tag;
-            if (RC && ((vr >> j) & 1u)) skeys[o++] = kr[j] | tag | (1ull << kb);
+            if (RC && ((vr >> j) & 1u)) skeys[o++] = kr[j] | tag | (Q ? 1ull << kb : 0ull);
         }
     }
     __syncthreads();
@@ -270,10 +272,13 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
             const uint64_t kk = skeys[q];
             const uint32_t d = XDIGIT(kk);
             const uint64_t at = gexcl[d] + (q - lstart[d]);
-            const uint64_t f = kk >> kb;  // tile-local (window << 1 | strand)
-            const uint64_t win = wb + (f >> 1);
-            const uint64_t idx = RC ? ((win << 1) | (f & 1u)) : win;
-            const uint64_t v = Q ? (((kk & restmask) << Q) | idx) : (kk & restmask);
+            uint64_t v = kk & restmask;
+            if (Q) {
+                const uint64_t f = kk >> kb;  // tile-local (window << 1 | strand)
+                const uint64_t win = wb + (f >> 1);
+                const uint64_t idx = RC ? ((win << 1) | (f & 1u)) : win;
+                v = (v << Q) | idx;
+            }
             if (EX) {
                 if (gexcl[d] != ~0ull) out[at] = v;
             } else if (at < C0) {
@@ -661,14 +666,14 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
 // their pos ((window << 1) | strand).
 enum { RG_COUNT = 1, RG_UNIQ = 2 };
 
-template <int MODE, typename O, bool ATOMIC>
+template <int MODE, typename O, bool ATOMIC, bool PF = false>
 __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ in, uint64_t C1,
                                                 const uint32_t *__restrict__ cnt1, uint32_t Q, uint32_t rest,
                                                 uint32_t rc, uint64_t rbase, uint32_t tag_shift, uint32_t fsub,
                                                 uint64_t *__restrict__ okeys, O *__restrict__ ovals,
                                                 uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
                                                 uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg,
-                                                uint64_t *__restrict__ stp) {
+                                                uint64_t *__restrict__ stp, uint32_t nreg) {
     __shared__ __attribute__((aligned(16))) uint64_t s[FCAP];
     __shared__ uint32_t wh[FW][FWORD];  // per-wave digit counters, u16 pairs
     __shared__ uint32_t dstart[FRAD];
@@ -676,29 +681,56 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_out;
 
-    if (threadIdx.x == 0) s_tile = atomicAdd(counter, 1u);
-    __syncthreads();
-    const uint32_t r = s_tile;
     const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
-    // the region = fsub (1 or 2) sub-regions of capacity C1, concatenated
-    const uint32_t m0 = cnt1[(uint64_t)r * fsub];
-    const uint32_t m1 = fsub > 1 ? cnt1[(uint64_t)r * fsub + 1] : 0u;
-    uint32_t m = m0 + m1;
-    if (m > (uint32_t)FCAP) {  // (block-uniform) more than the LDS holds
-        if (t == 0) atomicOr(err, ERR_REGION);
-        m = 0;
-    }
-    RSTAMP(r, 0);
-    const uint64_t *src = in + (uint64_t)r * fsub * C1;
-    const uint64_t *src1 = src + C1 - m0;  // position p >= m0 of the region: src1[p]
     const uint64_t rmask = (1ull << rest) - 1;
     const uint32_t pw = (uint32_t)w * (FIPT * 64) + (uint32_t)lane;  // wave-striped positions
-    uint64_t x[FIPT];
+    // a region r = fsub (1 or 2) sub-regions of capacity C1, concatenated:
+    // position p < m0 at in[r * fsub * C1 + p], p >= m0 at .. + C1 - m0 + p
+    auto counts = [&](uint32_t rr, uint32_t &a0, uint32_t &a1) {
+        a0 = cnt1[(uint64_t)rr * fsub];
+        a1 = fsub > 1 ? cnt1[(uint64_t)rr * fsub + 1] : 0u;
+    };
+    auto load = [&](uint32_t rr, uint32_t a0, uint32_t mm, uint64_t (&v)[FIPT]) {
+        // (a uniform base and one 32-bit offset per item: few address VGPRs)
+        const uint64_t *src = in + (uint64_t)rr * fsub * C1;
+        const uint32_t skip = (uint32_t)C1 - a0;
 #pragma unroll
-    for (int i = 0; i < FIPT; i++) {
-        const uint32_t p = pw + i * 64;
-        x[i] = p < m ? (p < m0 ? src[p] : src1[p]) : 0;
+        for (int i = 0; i < FIPT; i++) {
+            const uint32_t p = pw + i * 64;
+            v[i] = p < mm ? src[p < a0 ? p : p + skip] : 0;
+        }
+    };
+    auto fit = [&](uint32_t a0, uint32_t a1) -> uint32_t {
+        const uint32_t mm = a0 + a1;
+        if (mm <= (uint32_t)FCAP) return mm;
+        if (t == 0) atomicOr(err, ERR_REGION);  // (block-uniform) more than the LDS holds
+        return 0u;
+    };
+    // PF (persistent blocks): a block walks regions in grab order; while it
+    // sorts region r the items of the next region rn are in flight to its
+    // registers and the counts of the one after (rnn) to its SGPRs, so HBM
+    // is read during the LDS work (the barriers wait on LDS only).  Regions
+    // are published in key order by the look-back; a block's smallest
+    // unpublished region is always its current one, so the walk cannot stall.
+    if (t == 0) s_tile = atomicAdd(counter, 1u);
+    __syncthreads();
+    uint32_t r = __builtin_amdgcn_readfirstlane(s_tile);
+    if (r >= nreg) return;
+    uint32_t m0, m1, rn = nreg, n0 = 0, n1 = 0;
+    counts(r, m0, m1);
+    uint32_t m = fit(m0, m1);
+    uint64_t x[FIPT];
+    load(r, m0, m, x);
+    if (PF) {
+        __syncthreads();  // (every read of s_tile above before it is reused)
+        if (t == 0) s_tile = atomicAdd(counter, 1u);
+        __syncthreads();
+        rn = __builtin_amdgcn_readfirstlane(s_tile);
+        if (rn < nreg) counts(rn, n0, n1);
     }
+    for (;;) {
+    RSTAMP(r, 0);
+    uint32_t rnn = nreg, nn0 = 0, nn1 = 0;
 
     // stable LSD passes of <= 9 bits.  Ranks: per-wave u16 counters packed two
     // to a word (a wave ranks <= 64 * FIPT items), same-word LDS atomics of one
@@ -776,15 +808,24 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
             if (pw + i * 64 < m) s[pw + i * 64] = x[i];
         __syncthreads();
     }
+    if (PF) {
+        // the next region's items are loaded now (x is dead: the sorted
+        // region is in LDS), arriving while this one is grouped and written
+        if (t == 0) s_tile = atomicAdd(counter, 1u);
+        if (rn < nreg) load(rn, n0, n0 + n1 <= (uint32_t)FCAP ? n0 + n1 : 0u, x);
+        __syncthreads();
+        rnn = __builtin_amdgcn_readfirstlane(s_tile);
+        if (rnn < nreg) counts(rnn, nn0, nn1);
+    }
 
     RSTAMP(r, 2);
     // ---- run-length pass (thread t: sorted positions t*FIPT ..)
     const uint32_t q0 = (uint32_t)t * FIPT;
-    uint64_t kv[FIPT];
     uint32_t heads = 0, tails = 0;
+#define RKEY(v) (((v) >> Q) & rmask)
+    uint64_t kv[FIPT];
 #pragma unroll
     for (int j = 0; j < FIPT; j++) kv[j] = q0 + j < m ? s[q0 + j] : 0;
-#define RKEY(v) (((v) >> Q) & rmask)
 #pragma unroll
     for (int j = 0; j < FIPT; j++) {
         const uint32_t q = q0 + j;
@@ -796,26 +837,14 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
             tails |= (uint32_t)e << j;
         }
     }
-    uint32_t emit = 0;
-    uint32_t cval[FIPT];
+    uint32_t emit = 0, lh_before = 0;
     if constexpr (MODE == RG_UNIQ) {
         emit = heads & tails;
     } else {
+        emit = tails;
         const uint32_t lh = heads ? q0 + (31 - __clz(heads)) + 1 : 0u;
-        const uint32_t lh_before = block_exclusive_scan<FT>(
+        lh_before = block_exclusive_scan<FT>(
             lh, [](uint32_t a, uint32_t b) { return a > b ? a : b; }, 0u, lds_scan, (uint32_t *)nullptr);
-        uint32_t cur = lh_before;  // head position + 1 of the open group
-#pragma unroll
-        for (int j = 0; j < FIPT; j++) {
-            const uint32_t q = q0 + j;
-            cval[j] = 0;
-            if (q >= m) continue;
-            if ((heads >> j) & 1u) cur = q + 1;
-            if ((tails >> j) & 1u) {
-                emit |= 1u << j;
-                cval[j] = q + 2 - cur;
-            }
-        }
     }
     const uint32_t ne = (uint32_t)__popc(emit);
     uint32_t total;
@@ -826,39 +855,52 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
         const uint64_t ob = wave_lookback<0>(status, r, total, epoch, err);
         if (lane == 0) s_out = ob;
     }
-    O ov[FIPT];
-    const uint64_t qmask = Q ? ((1ull << Q) - 1) : 0ull;
-    uint32_t o = off;
+    // the emitted rows compacted in LDS as one word each: the item itself
+    // (UNIQ: key rest + pos) or key rest | group size << rest (COUNT); every
+    // read of s above came before the scan's barriers
+    {
+        uint32_t o = off, cur = lh_before;  // head position + 1 of the open group
 #pragma unroll
-    for (int j = 0; j < FIPT; j++) {
-        if ((emit >> j) & 1u) {
-            if constexpr (MODE == RG_UNIQ) {
-                const uint64_t idx = kv[j] & qmask;
-                const uint64_t pos = rc ? idx : (idx << 1);
-                // N > 1: the source rank (tagged into the item by the pass after
-                // the exchange) in bits 56-63, as DistPipeline's payloads
-                ov[j] = (O)(tag_shift ? pos | (((kv[j] >> tag_shift) & 0x1ffull) << 56) : pos);
-            } else {
-                ov[j] = (O)cval[j];
-            }
-            s[o++] = ((uint64_t)(r + rbase) << rest) | RKEY(kv[j]);
+        for (int j = 0; j < FIPT; j++) {
+            const uint32_t q = q0 + j;
+            if (MODE != RG_UNIQ && ((heads >> j) & 1u)) cur = q + 1;
+            if ((emit >> j) & 1u)
+                s[o++] = MODE == RG_UNIQ ? kv[j] : (RKEY(kv[j]) | ((uint64_t)(q + 2 - cur) << rest));
         }
     }
-#undef RKEY
     __syncthreads();
     RSTAMP(r, 4);
     const uint64_t ob = s_out;
-    if (dbg & 2) return;  // timing ablation only: no output writes
-    for (uint32_t q = t; q < total; q += FT) okeys[ob + q] = s[q];
-    __syncthreads();
-    O *so = reinterpret_cast<O *>(s);
-    o = off;
-#pragma unroll
-    for (int j = 0; j < FIPT; j++)
-        if ((emit >> j) & 1u) so[o++] = ov[j];
-    __syncthreads();
-    for (uint32_t q = t; q < total; q += FT) ovals[ob + q] = so[q];
+    if (!(dbg & 2)) {  // (dbg & 2: timing ablation only, no output writes)
+        const uint64_t qmask = Q ? ((1ull << Q) - 1) : 0ull;
+        for (uint32_t q = t; q < total; q += FT) {
+            const uint64_t v = s[q];
+            okeys[ob + q] = ((uint64_t)(r + rbase) << rest) | RKEY(v);
+        }
+        for (uint32_t q = t; q < total; q += FT) {
+            const uint64_t v = s[q];
+            if constexpr (MODE == RG_UNIQ) {
+                const uint64_t idx = v & qmask;
+                const uint64_t pos = rc ? idx : (idx << 1);
+                // N > 1: the source rank (tagged into the item by the pass after
+                // the exchange) in bits 56-63, as DistPipeline's payloads
+                ovals[ob + q] = (O)(tag_shift ? pos | (((v >> tag_shift) & 0x1ffull) << 56) : pos);
+            } else {
+                ovals[ob + q] = (O)(v >> rest);
+            }
+        }
+    }
+#undef RKEY
     RSTAMP(r, 5);
+    if (!PF || rn >= nreg) break;
+    __syncthreads();  // (every read of s / s_out / s_tile above before the next region writes them)
+    r = rn;
+    m0 = n0;
+    m = fit(n0, n1);
+    rn = rnn;
+    n0 = nn0;
+    n1 = nn1;
+    }
 }
 
 struct RegionPlan {
@@ -880,8 +922,9 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     if (mode != KMAN_FINISH_COUNT && mode != KMAN_FINISH_UNIQ) return KMAN_EINVAL;
     if (k < 2 || k > 32) return KMAN_EINVAL;
     if (getenv("KMAN_NO_REGION")) return KMAN_EFALLBACK;
-    // k <= 25: the tile-local window index rides above the key bits in pass 0
-    if (k > 25 || n_bases == 0) return KMAN_EFALLBACK;
+    // uniq: k <= 25 (the tile-local window index rides above the key bits in
+    // pass 0); count items carry no index: k <= 32
+    if ((mode == KMAN_FINISH_UNIQ && k > 25) || n_bases == 0) return KMAN_EFALLBACK;
     RegionPlan p{};
     // canonical: one key per window, min(forward, reverse complement)
     p.canon = flags & KMAN_CANONICAL;
@@ -1008,17 +1051,30 @@ struct FinishArgs {
     uint32_t fsub = 1;  // sub-regions per region (cnt and in indexed per sub-region)
 };
 
+template <int MODE, typename O, bool ATOMIC, bool PF>
+void launch_finish_as(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ovals, uint32_t epoch,
+                      uint32_t *counter, uint32_t dbg, uint64_t *stp) {
+    const void *fn = (const void *)rg_finish<MODE, O, ATOMIC, PF>;
+    const uint32_t grid = PF ? (uint32_t)kman_persistent_grid(ctx, fn, FT, f.nreg) : f.nreg;
+    hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, PF>), dim3(grid), dim3(FT), 0, ctx->stream, f.in, f.C1, f.cnt, f.Q,
+                       f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status, counter, epoch,
+                       ctx->d_err, dbg, stp, f.nreg);
+}
+
+// one block per region; KMAN_RG_FIN=1: persistent blocks that prefetch the
+// next region while sorting this one (A/B only: the prefetch registers spill,
+// 11.1 vs 5.7 ms on the bench config)
 template <int MODE, typename O>
 void launch_finish(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ovals, uint32_t epoch,
                    uint32_t *counter, uint32_t dbg, uint64_t *stp) {
-    if (ctx->lds_atomic_ordered)
-        hipLaunchKernelGGL((rg_finish<MODE, O, true>), dim3(f.nreg), dim3(FT), 0, ctx->stream, f.in, f.C1, f.cnt, f.Q,
-                           f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status, counter,
-                           epoch, ctx->d_err, dbg, stp);
-    else
-        hipLaunchKernelGGL((rg_finish<MODE, O, false>), dim3(f.nreg), dim3(FT), 0, ctx->stream, f.in, f.C1, f.cnt,
-                           f.Q, f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status, counter,
-                           epoch, ctx->d_err, dbg, stp);
+    static const char *e = getenv("KMAN_RG_FIN");
+    const bool pf = e && atoi(e) != 0;
+    if (ctx->lds_atomic_ordered) {
+        if (pf) launch_finish_as<MODE, O, true, true>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
+        else launch_finish_as<MODE, O, true, false>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
+    } else {  // (the ballot ranks need the registers the prefetch would take)
+        launch_finish_as<MODE, O, false, false>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
+    }
 }
 
 int run_finish(kman_ctx *ctx, const FinishArgs &f, int mode, uint64_t *okeys, void *ovals, uint32_t oval_bytes,
@@ -1316,11 +1372,12 @@ int make_shard_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t f
     if (mode != KMAN_FINISH_COUNT && mode != KMAN_FINISH_UNIQ) return KMAN_EINVAL;
     if (k < 2 || k > 32 || n_bases_q < n_bases) return KMAN_EINVAL;
     if (getenv("KMAN_NO_REGION")) return KMAN_EFALLBACK;
-    if (k > 25) return KMAN_EFALLBACK;  // the tile-local window index rides above the key bits
+    if (mode == KMAN_FINISH_UNIQ && k > 25) return KMAN_EFALLBACK;  // (the tile-local window index above the key)
     RegionPlan p{};
     p.canon = flags & KMAN_CANONICAL;
     p.rc = (flags & KMAN_RC) && !p.canon;
     p.K = 2 * k;
+    if (p.K < B1 + 9 + 1) return KMAN_EFALLBACK;  // (the rounds' passes need 8 + 9 key bits and one more)
     p.W = n_bases * (p.rc ? 2 : 1);
     const uint64_t Wq = n_bases_q * (p.rc ? 2 : 1);
     p.Q = mode == KMAN_FINISH_UNIQ ? (bitlen(Wq - 1) ? bitlen(Wq - 1) : 1u) : 0u;

@@ -239,6 +239,36 @@ class RcclComm:
                 b.free()
 
 
+class LocalComm:
+    """One rank on its own (no RCCL): the collectives of a step generator are
+    identities and a general round's exchange is a device copy.  Serves the
+    single-GPU inputs outside kman_groups (local_groups)."""
+
+    def __init__(self, dev: engine.Device):
+        self.dev = dev
+
+    def run(self, gen):
+        try:
+            req = next(gen)
+            while True:
+                op, arg = req
+                if op == "allreduce":
+                    req = gen.send(np.asarray(arg, np.uint64).copy())
+                elif op == "allgather":
+                    req = gen.send(np.asarray(arg, np.uint64).reshape(1, -1).copy())
+                else:
+                    send, sc, so, recv, rc, ro, eb = arg
+                    if int(sc[0]):
+                        N.check(self.dev.ctx, N.lib().kman_memcpy_d2d(self.dev.ctx, c_void_p(recv), c_void_p(send),
+                                                                       eb * int(sc[0])), "d2d")
+                    req = gen.send(None)
+        except StopIteration as e:
+            return e.value
+
+    def free(self) -> None:
+        pass
+
+
 class SimGroup:
     """G ranks in ONE process on one GPU (tests): collectives computed on the
     host, the all-to-all as device-to-device copies."""
@@ -331,7 +361,7 @@ class DistPipeline:
     def __init__(self, dev: engine.Device, reader, k: int, mode: str, world: int, rank: int,
                  uid: Optional[bytes] = None, canonical: bool = False, rc: bool = False, path: str = "region",
                  max_round_items: Optional[int] = None, chunk_bytes: int = 256 << 20, reload: bool = False,
-                 mem_frac: float = 0.85):
+                 mem_frac: float = 0.85, shard: Optional[S.ShardCodes] = None, local: bool = False):
         engine._check_k(k)
         if mode not in ("count", "uniq"):
             raise ValueError(mode)
@@ -343,10 +373,16 @@ class DistPipeline:
         self.fmode = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
         self.flags = engine.flags_for(self.rc, mode == "uniq", canonical)
         self.reader = reader
-        self.spec = S.shard_specs(reader, world, k)[rank]
-        self.loader = S.ShardLoader(dev, reader, self.spec, k, chunk_bytes)
-        self.shard = self.loader.load()
-        self.comm = RcclComm(dev, world, rank, uid) if uid is not None else None
+        if shard is None:
+            self.spec = S.shard_specs(reader, world, k)[rank]
+            self.loader = S.ShardLoader(dev, reader, self.spec, k, chunk_bytes)
+            self.shard = self.loader.load()
+        else:  # an input already on the device (one rank: local_groups)
+            self.spec, self.loader, self.shard = shard.spec, None, shard
+        if uid is not None:
+            self.comm = RcclComm(dev, world, rank, uid)
+        else:
+            self.comm = LocalComm(dev) if local else None
         self.d_hist = dev.alloc(4 * NB * RS)
         self.d_rtab = dev.alloc(8 * NB * RS)
         self.d_small = dev.alloc(8 * 16384)  # prefix / abundance histograms
@@ -359,6 +395,17 @@ class DistPipeline:
         self.ready = False
         if self.comm is not None:
             self.comm.run(self.setup_gen())
+
+    def take_result(self):
+        """The output rows as an engine CountResult / UniqResult (uniq pos are
+        u64, source rank 0 on one rank); the buffers pass to the caller."""
+        ok_, ov_, vb = self._out
+        if self.mode == "uniq":
+            r = engine.UniqResult(ok_, ov_, 8, self.n_out, self.k)
+        else:
+            r = engine.CountResult(ok_, ov_, vb, self.n_out, self.k)
+        self.out_keys.buf = self.out_vals.buf = None
+        return r
 
     # ---------------------------------------------------------------- setup
     def setup_gen(self):
@@ -434,7 +481,7 @@ class DistPipeline:
         if not self.ready:
             yield from self.setup_gen()
         L, ctx, dev, sh = N.lib(), self.dev.ctx, self.dev, self.shard
-        if self.reload:
+        if self.reload and self.loader is not None:
             self.shard = sh = self.loader.load()
         G, me = self.world, self.rank
         # 1. (bucket, segment) counts of the shard, bucket totals all-gathered
@@ -670,7 +717,32 @@ class DistPipeline:
             self.comm = None
         for b in [self.d_hist, self.d_rtab, self.d_small, self.arena_a, self.arena_b, self.out_keys, self.out_vals] + self.gen_bufs:
             b.free()
-        self.loader.free()
+        if self.loader is not None:
+            self.loader.free()
+
+
+def local_groups(p: engine.Parsed, k: int, rc: bool, mode: str, canonical: bool = False,
+                 max_round_items: Optional[int] = None):
+    """Count / uniq of one parsed input on one GPU through the key rounds of
+    the multi-GPU path (shard histogram, exact extraction, per-bucket passes,
+    LDS finish; a round whose regions overflow is redone by key range): the
+    region-class kernels for the inputs kman_groups does not take -- more
+    k-mers than its region capacities, `-r` on large inputs, skewed keys.
+    None when the rounds do not take the input either (uniq with k > 25 or
+    more pos bits than an item holds)."""
+    flags = engine.flags_for(rc and not canonical, mode == "uniq", canonical)
+    fm = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
+    if k > engine.MAX_K or N.lib().kman_dshard_plan(p.n_bases, p.n_bases, k, flags, fm) != N.KMAN_OK:
+        return None
+    sh = S.ShardCodes(p.dev, S.ShardSpec(0, 0, 0, 0, 0), k, codes=p.codes, n_own=p.n_bases, n_eff=p.n_bases,
+                      names=list(p.names), rec_seq=np.asarray(p.rec_seq, dtype=np.uint64))
+    pipe = DistPipeline(p.dev, None, k, mode, 1, 0, None, canonical=canonical, rc=rc, shard=sh, local=True,
+                        max_round_items=max_round_items)
+    try:
+        pipe.step()
+        return pipe.take_result()
+    finally:
+        pipe.free()
 
 
 def unique_id() -> bytes:

@@ -865,6 +865,12 @@ def count_groups(p: Parsed, k: int, rc: bool = False, canonical: bool = False) -
     r = groups(p, k, rc, "count", canonical)
     if r is not None:
         return r
+    if p.n_bases:
+        from . import dist
+
+        r = dist.local_groups(p, k, rc, "count", canonical)
+        if r is not None:
+            return r
     km = extract_sorted(p, k, rc, want_pos=False, canonical=canonical)
     try:
         if km.n == 0:
@@ -1016,6 +1022,12 @@ def join_groups(p: Parsed, k: int, rc: bool, mode: str, max_keys: Optional[int] 
     if k > MAX_K:
         return wide_groups(p, k, rc, mode)
     r = groups(p, k, rc, mode) if max_keys is None else None
+    if r is None and max_keys is None and p.n_bases:
+        # outside kman_groups (too many k-mers for its regions, -r on large
+        # inputs, skewed keys): the key rounds of the multi-GPU path on one GPU
+        from . import dist
+
+        r = dist.local_groups(p, k, rc, mode)
     if r is None and (max_keys is not None or not _fits(p, k, rc, mode)):
         r = ranged_groups(p, k, rc, mode, max_keys)
     if r is None:

@@ -168,12 +168,14 @@ def test_dist_region_overflow_redoes_the_round():
 
 
 def test_dist_general_path_k27():
-    """k > 25: the general path (key ranges, exchanged keys + pos)."""
+    """k = 27: count items still fit the region rounds; uniq (window index +
+    key > 64 bits) and a forced path="general" take the general path (key
+    ranges, exchanged keys + pos)."""
     text = _texts()["messy"]
-    for mode in ("count", "uniq"):
-        outs, pipes, _ = _run(text, 27, mode, 3)
+    for mode, kw, want in (("count", {}, "region"), ("uniq", {}, "general"), ("count", {"path": "general"}, "general")):
+        outs, pipes, _ = _run(text, 27, mode, 3, **kw)
         try:
-            assert all(p.path == "general" for p in pipes)
+            assert all(p.path == want for p in pipes)
             wk, wv = _oracle(text, 27, mode)
             np.testing.assert_array_equal(outs[0][0], wk)
             np.testing.assert_array_equal(outs[0][1], wv)

@@ -10,6 +10,7 @@ size-independent properties and against the general path's count output."""
 
 from __future__ import annotations
 
+import os
 import ctypes
 from ctypes import byref, c_uint64
 
@@ -133,7 +134,8 @@ def test_groups_plan_domain():
     U, C = N.KMAN_FINISH_UNIQ, N.KMAN_FINISH_COUNT
     assert L.kman_groups_plan(1_000_000_000, 21, N.KMAN_WANT_POS, U, byref(wb)) == N.KMAN_OK and wb.value > 0
     assert L.kman_groups_plan(1_000_000_000, 21, 0, C, byref(wb)) == N.KMAN_OK
-    assert L.kman_groups_plan(1000, 31, 0, C, byref(wb)) == N.KMAN_EFALLBACK  # k > 25
+    assert L.kman_groups_plan(1000, 31, 0, C, byref(wb)) == N.KMAN_OK  # count items: k <= 32
+    assert L.kman_groups_plan(1000, 26, N.KMAN_WANT_POS, U, byref(wb)) == N.KMAN_EFALLBACK  # uniq: k <= 25
     assert L.kman_groups_plan(1000, 21, N.KMAN_CANONICAL, C, byref(wb)) == N.KMAN_OK  # canonical keys: in
     assert L.kman_groups_plan(1000, 4, 0, C, byref(wb)) == N.KMAN_EFALLBACK  # too few key bits
     assert L.kman_groups_plan(4_000_000_000, 21, 0, C, byref(wb)) == N.KMAN_EFALLBACK  # regions too full
@@ -227,3 +229,72 @@ def test_full_size_region(dev):
     assert int(np.sum(ck * cc.astype(np.uint64), dtype=np.uint64)) == int(np.sum(keys, dtype=np.uint64))
     del keys
     np.testing.assert_array_equal(ck[cc == 1], uk)
+
+
+@pytest.mark.parametrize("k", [26, 31, 32])
+@pytest.mark.parametrize("rc", [False, True])
+def test_groups_count_long_k(dev, golden_inputs, k, rc):
+    """Count items carry no window index, so the region path takes k up to
+    32 (config 3's k = 31) -- bit-exact vs np_oracle."""
+    for text in _texts(golden_inputs):
+        got = _groups(dev, text, k, rc, "count")
+        assert got is not None
+        want = _oracle(text, k, rc, "count")
+        np.testing.assert_array_equal(got[0], want[0])
+        np.testing.assert_array_equal(got[1].astype(np.uint64), want[1])
+
+
+@pytest.mark.parametrize("mode", ["count", "uniq"])
+@pytest.mark.parametrize("k,rc,canonical", [(21, False, False), (21, True, False), (31, False, False),
+                                            (21, False, True)])
+def test_local_rounds_match_oracle(dev, mode, k, rc, canonical):
+    """dist.local_groups: the key rounds of the multi-GPU path on one GPU
+    (the inputs kman_groups does not take), forced into >= 3 rounds."""
+    import inputs
+    import np_oracle
+    from kman_amd import dist, engine
+
+    if canonical and mode == "uniq":
+        pytest.skip("canonical keys are counted")
+    if mode == "uniq" and k > 25:
+        pytest.skip("uniq items hold the window index: k <= 25")
+    text = inputs.grch38_like(3, n_bases=250_000)
+    p = engine.parse(dev, text)
+    try:
+        r = dist.local_groups(p, k, rc, mode, canonical, max_round_items=60_000)
+        try:
+            keys = dev.download(r.ukeys if mode == "count" else r.keys, r.n, np.uint64)
+            vals = dev.download(r.counts if mode == "count" else r.pos, r.n,
+                                np.uint32 if (r.count_bytes if mode == "count" else r.pos_bytes) == 4 else np.uint64)
+        finally:
+            engine.free_result(r)
+    finally:
+        p.free()
+    kk, pp = np_oracle.stream_kmers(np_oracle.parse_fasta(text), k, rc=rc, canonical=canonical)
+    sk, sp = np_oracle.stable_sort(kk, pp)
+    wk, wv = np_oracle.rle_count(sk) if mode == "count" else np_oracle.rle_uniq(sk, sp)
+    np.testing.assert_array_equal(keys, wk)
+    np.testing.assert_array_equal(vals.astype(np.uint64), wv)
+
+
+def test_skewed_input_takes_the_rounds(dev):
+    """A repeat that overflows kman_groups' regions: count_text / uniq_text go
+    through the local key rounds (only the overflowing round redone by key
+    range) and stay byte-exact vs the C oracle."""
+    import subprocess
+    import tempfile
+
+    import inputs
+    from conftest import ROOT
+    from kman_amd import engine
+
+    rep = b"ACGTTGCAAGGCTTACGATCGATCGGATCC"
+    text = inputs.SynthLayout(150_000, 8, record_len=40_000).read(0, 10**9) + b">rep\n" + \
+        b"\n".join([rep * 2] * 20_000) + b"\n"
+    exe = os.path.join(ROOT, "oracle", "kman_oracle")
+    with tempfile.TemporaryDirectory() as d:
+        src = os.path.join(d, "in.fa")
+        open(src, "wb").write(text)
+        for cmd, fn in (("count", engine.count_text), ("uniq", engine.uniq_text)):
+            subprocess.run([exe, cmd, src, os.path.join(d, "w"), "21"], check=True)
+            assert fn(text, 21, dev=dev) == open(os.path.join(d, "w"), "rb").read()
