@@ -43,6 +43,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import time
 from ctypes import byref, c_int, c_uint64, c_void_p
 from typing import List, Optional, Tuple
 
@@ -392,6 +393,7 @@ class DistPipeline:
         self.n_local = self.n_out = self.n_recv = 0
         self.rounds = 0
         self.fallback_rounds = 0
+        self.phase_ms = {}
         self.ready = False
         if self.comm is not None:
             self.comm.run(self.setup_gen())
@@ -484,6 +486,16 @@ class DistPipeline:
         if self.reload and self.loader is not None:
             self.shard = sh = self.loader.load()
         G, me = self.world, self.rank
+        self.phase_ms = {}
+        tick = [time.perf_counter()]
+
+        def lap(tag):  # host-side phase times (KMAN_DIST_TIMES=1 synchronises after each phase)
+            if os.environ.get("KMAN_DIST_TIMES"):
+                dev.sync()
+            t = time.perf_counter()
+            self.phase_ms[tag] = self.phase_ms.get(tag, 0.0) + (t - tick[0]) * 1e3
+            tick[0] = t
+
         # 1. (bucket, segment) counts of the shard, bucket totals all-gathered
         H = np.zeros(NB * RS, np.uint32)
         if self.path == "region":
@@ -493,6 +505,7 @@ class DistPipeline:
             c_local = H.reshape(NB, RS).sum(axis=1).astype(np.uint64)
         else:
             c_local = self._prefix_hist()
+        lap("hist")
         C = yield ("allgather", c_local)
         self.n_local = int(c_local.sum())
         # 2. rounds
@@ -508,6 +521,7 @@ class DistPipeline:
         vb = self._vb(C)
         ok_, ov_ = self.out_keys.get(8 * max(cap, 1)), self.out_vals.get(vb * max(cap, 1))
         n_out = 0
+        lap("plan+alloc")
         self.fallback_rounds = 0
         for r in range(R):
             if self.path == "region":
@@ -521,8 +535,10 @@ class DistPipeline:
                                                    c_void_p(self.d_rtab.ptr), c_void_p((A if G > 1 else B).ptr)),
                         "kman_dshard_extract")
                 lo, nb, counts, rcnt, roff = round_recv(C, cuts, R, me, r)
+                lap("extract")
                 if G > 1:
                     yield ("alltoallv", (A.ptr, sc, so, B.ptr, rcnt, roff, 8))
+                    lap("exchange")
                 got = c_uint64(0)
                 ret = L.kman_dround_finish(ctx, c_void_p(B.ptr), self.k, self.flags, self.fmode, G, self.n_bases_q,
                                            lo, nb, _u64p(np.ascontiguousarray(counts.reshape(-1))),
@@ -532,6 +548,7 @@ class DistPipeline:
                 fb = 1 if ret == N.KMAN_EFALLBACK else 0
                 if not fb:
                     N.check(ctx, ret, "kman_dround_finish")
+                lap("finish")
                 f = yield ("allreduce", np.array([fb], np.uint64))
                 if int(f[0]) == 0:
                     n_out += int(got.value)
@@ -539,6 +556,7 @@ class DistPipeline:
                 self.fallback_rounds += 1
             # the general path for this round (every rank together)
             n_out += yield from self._general_round(C, cuts, R, r, ok_, ov_, n_out, vb)
+            lap("general_round")
         self.n_out = n_out
         self.n_recv = cap
         self._out = (ok_, ov_, vb)
@@ -736,13 +754,49 @@ def local_groups(p: engine.Parsed, k: int, rc: bool, mode: str, canonical: bool 
         return None
     sh = S.ShardCodes(p.dev, S.ShardSpec(0, 0, 0, 0, 0), k, codes=p.codes, n_own=p.n_bases, n_eff=p.n_bases,
                       names=list(p.names), rec_seq=np.asarray(p.rec_seq, dtype=np.uint64))
+    t0 = time.perf_counter()
     pipe = DistPipeline(p.dev, None, k, mode, 1, 0, None, canonical=canonical, rc=rc, shard=sh, local=True,
                         max_round_items=max_round_items)
     try:
+        t1 = time.perf_counter()
         pipe.step()
+        p.dev.sync()
+        t2 = time.perf_counter()
+        LAST_LOCAL.clear()
+        LAST_LOCAL.update(setup_ms=(t1 - t0) * 1e3, step_ms=(t2 - t1) * 1e3, rounds=pipe.rounds,
+                          fallback_rounds=pipe.fallback_rounds, plan=getattr(pipe, "plan_info", None),
+                          phases_ms=dict(pipe.phase_ms))
         return pipe.take_result()
     finally:
         pipe.free()
+
+
+class LocalRounds:
+    """local_groups with its buffers held across steps (tools/widebench.py
+    times the compute the way bench.py times ResidentPipeline): step() runs
+    the key rounds over the resident codes, result() views the rows."""
+
+    def __init__(self, p: engine.Parsed, k: int, rc: bool, mode: str, canonical: bool = False,
+                 max_round_items: Optional[int] = None):
+        sh = S.ShardCodes(p.dev, S.ShardSpec(0, 0, 0, 0, 0), k, codes=p.codes, n_own=p.n_bases, n_eff=p.n_bases,
+                          names=list(p.names), rec_seq=np.asarray(p.rec_seq, dtype=np.uint64))
+        self.pipe = DistPipeline(p.dev, None, k, mode, 1, 0, None, canonical=canonical, rc=rc, shard=sh, local=True,
+                                 max_round_items=max_round_items)
+
+    def step(self) -> int:
+        return self.pipe.step()
+
+    def result(self):
+        ok_, ov_, vb = self.pipe._out
+        if self.pipe.mode == "uniq":
+            return engine.UniqResult(ok_, ov_, 8, self.pipe.n_out, self.pipe.k)
+        return engine.CountResult(ok_, ov_, vb, self.pipe.n_out, self.pipe.k)
+
+    def free(self) -> None:
+        self.pipe.free()
+
+
+LAST_LOCAL: dict = {}  # the last local_groups call: rounds, fallbacks, host-side phase times (tools/widebench.py)
 
 
 def unique_id() -> bytes:

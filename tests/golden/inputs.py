@@ -173,8 +173,10 @@ def grch38_like(seed: int, n_bases: int = 1_000_000, n_records: int = 5, width: 
             chars[a:a + int(rng.integers(10, 500))] = ord("N")
         out.append(b">chr%d AC:CM0006%02d.2 gi:5688%02d LN:%d rl:Chromosome M5:x AS:GRCh38\n" % (r + 1, r, r, L))
         full = L // width
-        body = chars[:full * width].reshape(full, width)
-        out.append(b"\n".join(bytes(x) for x in body) + b"\n")
+        grid = np.empty((full, width + 1), dtype=np.uint8)
+        grid[:, :width] = chars[:full * width].reshape(full, width)
+        grid[:, width] = ord("\n")
+        out.append(grid.tobytes())
         if L > full * width:
             out.append(bytes(chars[full * width:]) + b"\n")
     return b"".join(out)
