@@ -495,16 +495,33 @@ def prefix_hist(p: Parsed, k: int, rc: bool) -> Tuple[np.ndarray, int]:
         h.free()
 
 
-def key_ranges(hist: np.ndarray, k: int, max_keys: int) -> List[Tuple[int, int, int]]:
+def key_ranges(hist: np.ndarray, k: int, max_keys: int, count=None) -> List[Tuple[int, int, int]]:
     """Consecutive top-8-bit prefixes grouped into key ranges of at most
     max_keys k-mers: [(key_lo, key_hi, n)] in key order, empty ranges dropped.
     The batches of a multi-batch join (join.py:63-130) cut by key instead of
-    by stream position: their n-way merge is then their concatenation."""
+    by stream position: their n-way merge is then their concatenation.  A
+    prefix holding more than max_keys k-mers (repeats, poly-A) is bisected
+    by key with count(lo, hi) -> k-mers in [lo, hi] until its pieces fit;
+    only one key value repeated more than max_keys times cannot be cut."""
     shift = max(0, 2 * k - 8)
     out, lo, acc = [], 0, 0
+
+    def split(a, b, c):
+        if c <= max_keys:
+            return [(a, b, c)] if c else []
+        if a == b or count is None:
+            raise MemoryError("%d k-mers in key range [%x, %x]: more than a batch of %d" % (c, a, b, max_keys))
+        m = (a + b) // 2
+        c0 = count(a, m)
+        return split(a, m, c0) + split(m + 1, b, c - c0)
+
     for b, c in enumerate(hist.tolist()):
         if c > max_keys:
-            raise MemoryError("%d k-mers share one 8-bit prefix: more than a batch of %d" % (c, max_keys))
+            if acc:
+                out.append((lo << shift, (b << shift) - 1, acc))
+            out.extend(split(b << shift, ((b + 1) << shift) - 1, c))
+            lo, acc = b + 1, 0
+            continue
         if acc and acc + c > max_keys:
             out.append((lo << shift, (b << shift) - 1, acc))
             lo, acc = b, 0
@@ -548,7 +565,7 @@ class RangedJoin:
             free, _ = mem_info(dev)
             max_keys = max(1 << 20, (int(free * 0.85) - (8 + self.vb) * n) // per_key)
         self.max_keys = int(max_keys)
-        self.ranges = key_ranges(hist, k, self.max_keys)
+        self.ranges = key_ranges(hist, k, self.max_keys, self._count_range)
         self.cap = max([r[2] for r in self.ranges] + [1])
         self.okeys = self._alloc(8 * max(n, 1))
         self.ovals = self._alloc(self.vb * max(n, 1))
@@ -557,6 +574,16 @@ class RangedJoin:
         self.pos_alt = self._alloc(self.pos_bytes * self.cap) if self.want_pos else None
         self.hbuf = self._alloc(8 * 256 * 8)
         self.n_out = 0
+
+    def _count_range(self, lo: int, hi: int) -> int:
+        """k-mers with keys in [lo, hi] (kman_extract_range with no capacity:
+        counted, nothing written)."""
+        got = c_uint64(0)
+        rc = N.lib().kman_extract_range(self.dev.ctx, c_void_p(self.p.codes.ptr), self.p.n_bases, self.k,
+                                        flags_for(self.rc, False), lo, hi, None, None, 4, 0, None, byref(got))
+        if rc not in (N.KMAN_OK, N.KMAN_ECAP):
+            N.check(self.dev.ctx, rc, "kman_extract_range")
+        return int(got.value)
 
     def _alloc(self, nbytes: int) -> DeviceBuffer:
         try:
@@ -572,8 +599,8 @@ class RangedJoin:
         each range into the output.  Returns the number of k-mers joined."""
         dev, L, k, p = self.dev, N.lib(), self.k, self.p
         hist, n = _prefix_hist_into(p, k, self.rc, self.phist)
-        ranges = key_ranges(hist, k, self.max_keys)
-        if n != self.n_kmers or any(r[2] > self.cap for r in ranges):
+        ranges = self.ranges
+        if n != self.n_kmers:
             raise RuntimeError("the stream changed under a planned RangedJoin")
         flags = flags_for(self.rc, self.want_pos)
         fmode = N.KMAN_FINISH_UNIQ if self.want_pos else N.KMAN_FINISH_COUNT
@@ -583,7 +610,7 @@ class RangedJoin:
         for lo_key, hi_key, nr in ranges:
             # the range's keys fill (hi - lo + 1) of the len(hist) prefixes:
             # segment bits as for a stream that dense over the whole key space
-            lo = split_bits(nr * len(hist) // (((hi_key - lo_key) >> shift) + 1), 2 * k)
+            lo = split_bits(nr * (1 << (2 * k)) // (hi_key - lo_key + 1), 2 * k)
             dev.memset(self.hbuf, 0, 8 * 256 * 8)
             got = c_uint64(0)
             N.check(dev.ctx, L.kman_extract_range(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,

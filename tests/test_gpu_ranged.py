@@ -177,3 +177,25 @@ def test_ranged_single_prefix_too_big(dev):
             engine.ranged_groups(p, 21, False, "count", max_keys=1000)
     finally:
         p.free()
+
+
+@pytest.mark.parametrize("mode", ["count", "uniq"])
+def test_ranged_heavy_prefix_is_bisected(dev, mode):
+    """A prefix bin larger than a batch (a poly-A run + a repeat) is cut by
+    key (kman_extract_range counts) instead of raising MemoryError."""
+    import inputs
+
+    from kman_amd import engine
+
+    text = inputs.syn_numpy(60_000, 5, record_len=20_000) + b">polyA\n" + b"A" * 5_000 + b"\n>rep\n" + \
+        b"AAAACAGGTAACCAGGTTTGA" * 400 + b"\n"
+    fn = engine.count_text if mode == "count" else engine.uniq_text
+    for k in (13, 21):
+        p = engine.parse(dev, text)
+        try:
+            h, _ = engine.prefix_hist(p, k, False)
+        finally:
+            p.free()
+        assert int(h.max()) > 5_000  # the AAAA.. bin is larger than a batch
+        got = fn(text, k, dev=dev, max_keys=5_000)
+        assert got == fn(text, k, dev=dev)  # the one-batch paths
