@@ -291,21 +291,36 @@ def _rendezvous(rank: int, world: int) -> bytes:
 
     if world == 1:
         return dist.unique_id()
-    path = os.path.join(tempfile.gettempdir(), "kman_rccl_id_%s_%s" % (os.environ.get("MASTER_PORT", "0"),
-                                                                      os.environ.get("TORCHELASTIC_RUN_ID", "")))
+    path = _uid_path()
     if rank == 0:
         uid = dist.unique_id()
         with open(path + ".tmp", "wb") as fh:
             fh.write(uid)
         os.replace(path + ".tmp", path)
         return uid
+    # (a file left by an earlier launch on the same port is older than this
+    # process: the ranks start together, rank 0 writes within seconds)
     t0 = time.time()
-    while not os.path.isfile(path):
+    while True:
+        try:
+            if os.path.getmtime(path) >= _START - 10:
+                break
+        except OSError:
+            pass
         if time.time() - t0 > 120:
             raise RuntimeError("no RCCL id from rank 0 at %s" % path)
         time.sleep(0.05)
+    time.sleep(0.05)
     with open(path, "rb") as fh:
         return fh.read()
+
+
+_START = time.time()
+
+
+def _uid_path() -> str:
+    return os.path.join(tempfile.gettempdir(), "kman_rccl_id_%s_%s_%s" % (
+        os.environ.get("MASTER_PORT", "0"), os.environ.get("TORCHELASTIC_RUN_ID", ""), os.environ.get("WORLD_SIZE", "1")))
 
 
 def run_dist(args, world: int, rank: int, local: int):
@@ -367,6 +382,12 @@ def run_dist(args, world: int, rank: int, local: int):
             "cpu_baseline": None,
         }
         print(json.dumps(out), flush=True)
+    comm.allreduce(np.zeros(1, np.uint64))  # every rank is done with the id file
+    if rank == 0 and world > 1:
+        try:
+            os.remove(_uid_path())
+        except OSError:
+            pass
     pipe.free()
     dev.close()
 
