@@ -328,6 +328,21 @@ int kman_rle_wide(kman_ctx *ctx, int mode, const uint64_t *d_hi, const uint64_t 
 int kman_rle_count(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint64_t *d_ukeys,
                    void *d_counts, uint32_t count_bytes, uint64_t *n_unique);
 
+/* n-way merge of runs each sorted by key (Crawler.do_records' heapq.merge
+ * over sorted batches, kmermaid/join.py:63-93): a tree of stable merge-path
+ * 2-way merges in run order, so equal keys keep run order, then in-run order.
+ * d_okeys / d_ovals get the merged total; d_tmp_* (same size) is scratch
+ * (unused for <= 2 runs).  val_bytes 0 (keys only), 4 or 8.
+ * kman_count_descents: number of i with keys[i] < keys[i-1] (0 = sorted). */
+typedef struct {
+    const uint64_t *keys;
+    const void *vals;
+    uint64_t n;
+} kman_run;
+int kman_merge_runs(kman_ctx *ctx, const kman_run *runs, int nruns, uint32_t val_bytes, uint64_t *d_okeys,
+                    void *d_ovals, uint64_t *d_tmp_keys, void *d_tmp_vals);
+int kman_count_descents(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint64_t *descents);
+
 /* Keys that occur exactly once, with their payload (join.py:244-263). */
 int kman_rle_uniq(kman_ctx *ctx, const uint64_t *d_keys, const void *d_vals, uint32_t val_bytes,
                   uint64_t n, uint64_t *d_okeys, void *d_ovals, uint64_t *n_out);
@@ -396,6 +411,13 @@ int kman_format_uniq(const uint64_t *keys, const void *pos, uint32_t pos_bytes, 
                      const uint64_t *rec_seq, uint64_t n_records, char *out, size_t cap,
                      size_t *used, int threads);
 
+/* uniq rows of a multi-source join (several FASTA inputs and reloaded batch
+ * files, join.py:63-93 + 244-263): pos are u64 global base indices over one
+ * merged record table; rec_kind[r] 0 = a FASTA record (header
+ * name:start-end:strand), 1 = a batch-file record printed by its title. */
+int kman_format_uniq_mixed(const uint64_t *keys, const uint64_t *pos, uint64_t n, uint32_t k, const char *names,
+                           const uint64_t *name_off, const uint64_t *rec_seq, const uint8_t *rec_kind,
+                           uint64_t n_records, char *out, size_t cap, size_t *used, int threads);
 int kman_format_count_wide(const uint64_t *hi, const uint64_t *lo, const void *counts, uint32_t count_bytes,
                            uint64_t n, uint32_t k, char *out, size_t cap, size_t *used, int threads);
 int kman_format_uniq_wide(const uint64_t *hi, const uint64_t *lo, const void *pos, uint32_t pos_bytes, uint64_t n,

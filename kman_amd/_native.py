@@ -46,6 +46,11 @@ class ParseInfo(ctypes.Structure):
     _fields_ = [("n_bases", c_uint64), ("n_records", c_uint64)]
 
 
+class Run(ctypes.Structure):
+    """kman_run: one sorted run for kman_merge_runs."""
+    _fields_ = [("keys", c_void_p), ("vals", c_void_p), ("n", c_uint64)]
+
+
 # name -> (restype, argtypes); every symbol include/kman.h declares
 SIGNATURES = {
     "kman_abi_version": (c_int, []),
@@ -178,6 +183,12 @@ SIGNATURES = {
         c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p,
                 c_uint64, c_void_p, c_size_t, POINTER(c_size_t)],
     ),
+    "kman_format_uniq_mixed": (
+        c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p,
+                c_size_t, POINTER(c_size_t), c_int],
+    ),
+    "kman_merge_runs": (c_int, [c_void_p, c_void_p, c_int, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "kman_count_descents": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
     "kman_rebase_pos": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_uint32]),
     "kman_synth_fasta": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32]),
     "kman_copy_h2d_async": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int]),

@@ -165,6 +165,50 @@ extern "C" int kman_format_uniq(const uint64_t *keys, const void *pos, uint32_t 
     return format_fasta_impl(keys, pos, pos_bytes, n, k, nm, out, cap, used, threads);
 }
 
+// uniq rows over several sources (a multi-source join: FASTA inputs and
+// reloaded batch files): one merged record table in global base indices;
+// rec_kind[r] = 0: a FASTA record (header name:start-end:strand), 1: a batch
+// file record whose title is the header as written (the k-mer's own
+// "ref:start-end:strand").
+extern "C" int kman_format_uniq_mixed(const uint64_t *keys, const uint64_t *pos, uint64_t n, uint32_t k,
+                                      const char *names, const uint64_t *name_off, const uint64_t *rec_seq,
+                                      const uint8_t *rec_kind, uint64_t n_records, char *out, size_t cap,
+                                      size_t *used, int threads) {
+    if (!used || (n && (!keys || !pos || !name_off || !rec_seq || !rec_kind || !n_records)) || k < 1 || k > 32)
+        return KMAN_EINVAL;
+    Names nm{names, name_off, rec_seq, n_records};
+    auto size_of = [&](uint64_t i) -> size_t {
+        const uint64_t g = pos[i] >> 1;
+        const uint64_t r = nm.find(g);
+        const size_t L = nm.off[r + 1] - nm.off[r];
+        if (rec_kind[r]) return 1 + L + 1 + k + 1;
+        const uint64_t st = g - nm.rec_seq[r];
+        return 1 + L + 1 + ndigits(st) + 1 + ndigits(st + k) + 2 + 1 + k + 1;
+    };
+    auto write_at = [&](uint64_t i, char *p) -> char * {
+        const uint64_t v = pos[i], g = v >> 1;
+        const uint64_t r = nm.find(g);
+        const uint64_t L = nm.off[r + 1] - nm.off[r];
+        *p++ = '>';
+        memcpy(p, nm.names + nm.off[r], L);
+        p += L;
+        if (!rec_kind[r]) {
+            const uint64_t st = g - nm.rec_seq[r];
+            *p++ = ':';
+            p = put_u64(p, st);
+            *p++ = '-';
+            p = put_u64(p, st + k);
+            *p++ = ':';
+            *p++ = (v & 1) ? '-' : '+';
+        }
+        *p++ = '\n';
+        p = put_seq(p, keys[i], k);
+        *p++ = '\n';
+        return p;
+    };
+    return run_sliced(n, out, cap, used, threads, size_of, write_at);
+}
+
 // k in 33..64: keys as (hi, lo) word pairs (kman_extract_wide)
 extern "C" int kman_format_count_wide(const uint64_t *hi, const uint64_t *lo, const void *counts, uint32_t count_bytes,
                                       uint64_t n, uint32_t k, char *out, size_t cap, size_t *used, int threads) {

@@ -16,6 +16,8 @@
 // uniq 8 B key read (+ payload of kept keys) + (8 + 4|8) B per kept key.
 #include "common.h"
 
+#include <vector>
+
 namespace {
 
 constexpr int RT = 256;
@@ -384,4 +386,139 @@ extern "C" int kman_rle_wide(kman_ctx *ctx, int mode, const uint64_t *d_hi, cons
 #undef KW
     HIP_TRY(ctx, hipGetLastError());
     return kman_lookback_total(ctx, T, n_out);
+}
+
+// ================================================================ merge
+// n-way merge of sorted runs (Crawler.do_records' heapq.merge over sorted
+// batches, kmermaid/join.py:63-93): a tree of stable 2-way merges (run order
+// kept, so ties go to the lower run index, then in-run order -- heapq.merge
+// over (key, batch) with batches in order).  Each 2-way merge is merge-path:
+// every thread finds where its MI outputs start on the merge path by a binary
+// search over the diagonal, then merges MI items.
+namespace {
+
+constexpr int MT = 256, MI = 8;
+
+template <typename V>
+__global__ __launch_bounds__(MT) void merge2_kernel(const uint64_t *__restrict__ ak, const V *__restrict__ av,
+                                                    uint64_t na, const uint64_t *__restrict__ bk,
+                                                    const V *__restrict__ bv, uint64_t nb,
+                                                    uint64_t *__restrict__ ok, V *__restrict__ ov) {
+    const uint64_t n = na + nb;
+    const uint64_t d = ((uint64_t)blockIdx.x * MT + threadIdx.x) * MI;
+    if (d >= n) return;
+    // i = A elements among the first d outputs (A first on ties)
+    uint64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (ak[mid] <= bk[d - 1 - mid]) lo = mid + 1;
+        else hi = mid;
+    }
+    uint64_t i = lo, j = d - lo;
+    const uint64_t e = d + MI < n ? d + MI : n;
+    for (uint64_t o = d; o < e; o++) {
+        const bool takeA = j >= nb || (i < na && ak[i] <= bk[j]);
+        if (takeA) {
+            ok[o] = ak[i];
+            if (av) ov[o] = av[i];
+            i++;
+        } else {
+            ok[o] = bk[j];
+            if (av) ov[o] = bv[j];
+            j++;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void descents_kernel(const uint64_t *__restrict__ k, uint64_t n,
+                                                       unsigned long long *__restrict__ out) {
+    uint32_t c = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x + 1; i < n; i += (uint64_t)gridDim.x * 256)
+        c += k[i] < k[i - 1];
+    if (c) atomicAdd(out, (unsigned long long)c);
+}
+
+}  // namespace
+
+extern "C" int kman_count_descents(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint64_t *descents) {
+    if (!ctx || !descents) return KMAN_EINVAL;
+    *descents = 0;
+    if (n < 2) return KMAN_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    void *scr;
+    KMAN_TRY(kman_scratch(ctx, 256, &scr));
+    HIP_TRY(ctx, hipMemsetAsync(scr, 0, 8, ctx->stream));
+    const uint64_t b = ceil_div(n, 256 * 16);
+    hipLaunchKernelGGL(descents_kernel, dim3((uint32_t)(b < 4096 ? b : 4096)), dim3(256), 0, ctx->stream, d_keys, n,
+                       (unsigned long long *)scr);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small, scr, 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    *descents = ctx->h_small[0];
+    return KMAN_OK;
+}
+
+extern "C" int kman_merge_runs(kman_ctx *ctx, const kman_run *runs, int nruns, uint32_t val_bytes,
+                               uint64_t *d_okeys, void *d_ovals, uint64_t *d_tmp_keys, void *d_tmp_vals) {
+    if (!ctx || nruns < 0 || (nruns && !runs)) return KMAN_EINVAL;
+    if (val_bytes != 0 && val_bytes != 4 && val_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "val_bytes 0, 4 or 8");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    struct R {
+        const uint64_t *k;
+        const void *v;
+        uint64_t n;
+    };
+    std::vector<R> cur;
+    uint64_t total = 0;
+    for (int r = 0; r < nruns; r++) {
+        cur.push_back({runs[r].keys, runs[r].vals, runs[r].n});
+        total += runs[r].n;
+    }
+    if (total == 0) return KMAN_OK;
+    if (!d_okeys || (val_bytes && !d_ovals)) return kman_fail(ctx, KMAN_EINVAL, "null output");
+    // levels of pairwise merges; the output of the last level must be d_okeys:
+    // levels alternate between (out, tmp) starting so that the last is out
+    int levels = 0;
+    for (size_t m = cur.size(); m > 1; m = (m + 1) / 2) levels++;
+    if (levels && (!d_tmp_keys || (val_bytes && !d_tmp_vals))) return kman_fail(ctx, KMAN_EINVAL, "null scratch");
+    KTimer kt_(ctx, "merge");
+    for (int lv = 0; lv < levels; lv++) {
+        const bool to_out = ((levels - 1 - lv) & 1) == 0;
+        uint64_t *dk = to_out ? d_okeys : d_tmp_keys;
+        char *dv = (char *)(to_out ? d_ovals : d_tmp_vals);
+        std::vector<R> nxt;
+        uint64_t at = 0;
+        for (size_t p = 0; p < cur.size(); p += 2) {
+            const R a = cur[p];
+            const R b = p + 1 < cur.size() ? cur[p + 1] : R{nullptr, nullptr, 0};
+            const uint64_t n = a.n + b.n;
+            uint64_t *ok = dk + at;
+            void *ov = val_bytes ? (void *)(dv + (size_t)val_bytes * at) : nullptr;
+            if (n) {
+                const uint64_t th = ceil_div(n, (uint64_t)MI);
+                const dim3 g((uint32_t)ceil_div(th, (uint64_t)MT));
+                if (val_bytes == 8)
+                    hipLaunchKernelGGL(merge2_kernel<uint64_t>, g, dim3(MT), 0, ctx->stream, a.k, (const uint64_t *)a.v,
+                                       a.n, b.k, (const uint64_t *)b.v, b.n, ok, (uint64_t *)ov);
+                else if (val_bytes == 4)
+                    hipLaunchKernelGGL(merge2_kernel<uint32_t>, g, dim3(MT), 0, ctx->stream, a.k, (const uint32_t *)a.v,
+                                       a.n, b.k, (const uint32_t *)b.v, b.n, ok, (uint32_t *)ov);
+                else
+                    hipLaunchKernelGGL(merge2_kernel<uint32_t>, g, dim3(MT), 0, ctx->stream, a.k, (const uint32_t *)nullptr,
+                                       a.n, b.k, (const uint32_t *)nullptr, b.n, ok, (uint32_t *)nullptr);
+                HIP_TRY(ctx, hipGetLastError());
+            }
+            nxt.push_back({ok, ov, n});
+            at += n;
+        }
+        cur.swap(nxt);
+    }
+    if (levels == 0) {  // one run: a copy
+        HIP_TRY(ctx, hipMemcpyAsync(d_okeys, cur[0].k, 8 * total, hipMemcpyDeviceToDevice, ctx->stream));
+        if (val_bytes)
+            HIP_TRY(ctx, hipMemcpyAsync(d_ovals, cur[0].v, (size_t)val_bytes * total, hipMemcpyDeviceToDevice,
+                                        ctx->stream));
+    }
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    return kman_check_device_error(ctx);
 }

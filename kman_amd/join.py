@@ -231,12 +231,58 @@ def join_bytes(batches: List[Batch], count: bool, sink=None):
             r.pos.free()
     finally:
         km.free()
-    if not tagged:
-        return engine._to(sink, srcs[0].format_fasta(keys, pos))
-    out = []
-    for key, p in zip(keys.tolist(), pos.tolist()):
-        out.append(">%s\n%s\n" % (srcs[p >> 56].header(p & ((1 << 56) - 1)), engine.decode_key(key, k)))
-    return engine._to(sink, "".join(out).encode("utf-8", "surrogateescape"))
+    return engine._to(sink, format_sources(keys, pos, k, srcs, tagged))
+
+
+def format_sources(keys: np.ndarray, pos: np.ndarray, k: int, srcs, tagged: bool) -> bytes:
+    """uniq rows whose pos point into one or several sources (FastaSource /
+    BatchFileSource): one merged record table in global base indices, printed
+    by the host writer kman_format_uniq_mixed (no per-row Python)."""
+    import ctypes
+    from ctypes import byref, c_size_t, c_void_p
+
+    from . import _native as N
+
+    names, rec_seq, kind, base = [], [], [], []
+    at = 0
+    for s in srcs:
+        base.append(at)
+        p = s.parsed
+        if p is None:
+            continue
+        if hasattr(s, "titles"):  # a reloaded batch file: the title is the header
+            names += [t.encode("utf-8", "surrogateescape") for t in s.titles]
+            kind += [1] * p.n_records
+        else:
+            names += list(p.names)
+            kind += [0] * p.n_records
+        rec_seq += (np.asarray(p.rec_seq, dtype=np.uint64) + np.uint64(at)).tolist()
+        at += p.n_bases
+    pos = np.asarray(pos, dtype=np.uint64)
+    if tagged:
+        src = (pos >> np.uint64(56)).astype(np.int64)
+        pos = (pos & np.uint64((1 << 56) - 1)) + (np.asarray(base, dtype=np.uint64)[src] << np.uint64(1))
+    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    pos = np.ascontiguousarray(pos, dtype=np.uint64)
+    blob = b"".join(names)
+    off = np.zeros(len(names) + 1, dtype=np.uint64)
+    if names:
+        off[1:] = np.cumsum([len(x) for x in names], dtype=np.uint64)
+    rs = np.asarray(rec_seq, dtype=np.uint64)
+    kd = np.asarray(kind, dtype=np.uint8)
+    nb = ctypes.create_string_buffer(blob, max(1, len(blob)))
+    L = N.lib()
+    args = (keys.ctypes.data_as(c_void_p), pos.ctypes.data_as(c_void_p), len(keys), k, nb,
+            off.ctypes.data_as(c_void_p), rs.ctypes.data_as(c_void_p), kd.ctypes.data_as(c_void_p), len(names))
+    used = c_size_t(0)
+    rc = L.kman_format_uniq_mixed(*args, None, 0, byref(used), engine.host_threads())
+    if rc not in (N.KMAN_OK, N.KMAN_ECAP):
+        raise RuntimeError("kman_format_uniq_mixed failed (%d)" % rc)
+    buf = ctypes.create_string_buffer(max(1, used.value))
+    rc = L.kman_format_uniq_mixed(*args, buf, used.value, byref(used), engine.host_threads())
+    if rc != N.KMAN_OK:
+        raise RuntimeError("kman_format_uniq_mixed failed (%d)" % rc)
+    return buf.raw[:used.value]
 
 
 class KJoinerThreading(KJoiner):

@@ -111,10 +111,9 @@ class BatchFileSource:
         return self.titles[self.parsed.record_of(int(pos) >> 1)]
 
     def format_fasta(self, keys: np.ndarray, pos: np.ndarray) -> bytes:
-        out = []
-        for key, p in zip(keys.tolist(), pos.tolist()):
-            out.append(">%s\n%s\n" % (self.header(p), engine.decode_key(key, self.k)))
-        return "".join(out).encode("utf-8", "surrogateescape")
+        from .join import format_sources
+
+        return format_sources(keys, pos, self.k, [self], False)
 
     def free(self) -> None:
         if self._km is not None:
@@ -261,5 +260,46 @@ def gather_sorted(entries, want_pos: bool):
                 N.check(dev.ctx, L.kman_widen_u32(dev.ctx, c_void_p(km.pos.ptr + 4 * s),
                                                    c_void_p(out.pos.ptr + 8 * at), m, tag), "widen")
         at += m
+    if all(isinstance(s, BatchFileSource) for s, _, _ in entries) and _merge_sorted_runs(out, entries, dev):
+        return out, srcs, tagged
     _sort(out, dev, 2 * k)
     return out, srcs, tagged
+
+
+def _merge_sorted_runs(out: engine.Kmers, entries, dev: engine.Device) -> bool:
+    """Batch files written by `kmer batch` are each sorted: their union is
+    merged (kman_merge_runs, the device form of Crawler.do_records'
+    heapq.merge, join.py:63-93) instead of sorted; equal keys keep batch
+    order, then in-batch order, as the heap merge does.  False (nothing
+    changed) when a run is not sorted after all -- the caller sorts."""
+    L = N.lib()
+    runs, at = [], 0
+    for _, s, e in entries:
+        m = e - s
+        if m <= 0:
+            continue
+        d = ctypes.c_uint64(0)
+        N.check(dev.ctx, L.kman_count_descents(dev.ctx, c_void_p(out.keys.ptr + 8 * at), m, byref(d)), "descents")
+        if d.value:
+            return False
+        runs.append(N.Run(out.keys.ptr + 8 * at, out.pos.ptr + out.pos_bytes * at if out.pos else None, m))
+        at += m
+    if len(runs) < 2:
+        out.sorted = True
+        return True
+    pb = out.pos_bytes if out.pos else 0
+    tk = dev.alloc(8 * max(at, 1))
+    tv = dev.alloc(pb * max(at, 1)) if pb else None
+    try:
+        arr = (N.Run * len(runs))(*runs)
+        N.check(dev.ctx, L.kman_merge_runs(dev.ctx, arr, len(runs), pb, c_void_p(out.alt.ptr),
+                                           c_void_p(out.pos_alt.ptr) if pb else None, c_void_p(tk.ptr),
+                                           c_void_p(tv.ptr) if tv else None), "kman_merge_runs")
+    finally:
+        tk.free()
+        if tv is not None:
+            tv.free()
+    out.keys, out.alt = out.alt, out.keys
+    out.pos, out.pos_alt = out.pos_alt, out.pos
+    out.sorted = True
+    return True

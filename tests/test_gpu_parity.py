@@ -478,3 +478,47 @@ def test_wide_keys_match_oracle(dev, k, rc, canonical):
             assert vals.tolist() == want_v
     finally:
         p.free()
+
+
+@pytest.mark.parametrize("nruns", [1, 2, 3, 7, 16])
+@pytest.mark.parametrize("vb", [0, 4, 8])
+def test_merge_runs_is_a_stable_merge(dev, nruns, vb):
+    """kman_merge_runs == heapq.merge over the sorted runs in run order
+    (join.py:63-93): equal keys keep run order, then in-run order."""
+    import ctypes
+    from ctypes import c_void_p
+
+    from kman_amd import _native as N
+
+    rng = np.random.default_rng(nruns * 10 + vb)
+    runs = [np.sort(rng.integers(0, 300, size=int(rng.integers(0, 5000)), dtype=np.uint64)) for _ in range(nruns)]
+    vals = [np.arange(len(r), dtype=np.uint64) + np.uint64(i << 40) for i, r in enumerate(runs)]
+    keys = np.concatenate(runs)
+    allv = np.concatenate(vals)
+    n = len(keys)
+    dt = np.uint32 if vb == 4 else np.uint64
+    dk, dv = dev.alloc(8 * max(n, 1)), dev.alloc(8 * max(n, 1))
+    ok, ov, tk, tv = (dev.alloc(8 * max(n, 1)) for _ in range(4))
+    try:
+        if n:
+            dev.upload(dk, keys)
+            dev.upload(dv, allv.astype(dt) if vb else allv)
+        rr, at = [], 0
+        for r in runs:
+            rr.append(N.Run(dk.ptr + 8 * at, (dv.ptr + vb * at) if vb else None, len(r)))
+            at += len(r)
+        arr = (N.Run * nruns)(*rr)
+        N.check(dev.ctx, N.lib().kman_merge_runs(dev.ctx, arr, nruns, vb, c_void_p(ok.ptr),
+                                                 c_void_p(ov.ptr) if vb else None, c_void_p(tk.ptr),
+                                                 c_void_p(tv.ptr) if vb else None), "merge")
+        # heapq.merge over (key, run, index) == a stable sort of the concatenation
+        order = np.argsort(keys, kind="stable")
+        np.testing.assert_array_equal(dev.download(ok, n, np.uint64), keys[order])
+        if vb:
+            np.testing.assert_array_equal(dev.download(ov, n, dt), allv.astype(dt)[order])
+        d = ctypes.c_uint64(0)
+        N.check(dev.ctx, N.lib().kman_count_descents(dev.ctx, c_void_p(dk.ptr), n, ctypes.byref(d)), "descents")
+        assert d.value == (0 if nruns == 1 else int((keys[1:] < keys[:-1]).sum()))
+    finally:
+        for b in (dk, dv, ok, ov, tk, tv):
+            b.free()
