@@ -4,6 +4,7 @@
 // not ACGT, bit 3 record start).
 #pragma once
 #include "common.h"
+#include "rollfast.h"
 
 namespace {
 
@@ -64,9 +65,10 @@ KMAN_DEV void stage_codes(const uint8_t *__restrict__ codes, uint64_t n_bases, u
     store_codes<NT, EI>(cv, codes, n_bases, tb, s);
 }
 
-// Roll the EI windows starting at s[base .. base+EI) (k from LDS bytes).
+// Roll the EI windows starting at s[base .. base+EI) (k from LDS bytes), one
+// base at a time (kept for A/B timing: make EXTRA=-DKMAN_ROLL_SEQ).
 template <int EI, bool CANON>
-KMAN_DEV uint32_t roll(const uint8_t *s, int base, int k, uint64_t mask, uint64_t p0, uint64_t n_bases,
+KMAN_DEV uint32_t roll_seq(const uint8_t *s, int base, int k, uint64_t mask, uint64_t p0, uint64_t n_bases,
                        uint64_t (&kf)[EI], uint64_t (&kr)[EI]) {
     uint64_t f = 0, r = 0;
     uint32_t run = 0;
@@ -96,6 +98,18 @@ KMAN_DEV uint32_t roll(const uint8_t *s, int base, int k, uint64_t mask, uint64_
         valid |= (uint32_t)(run >= (uint32_t)k && p0 + j < n_bases) << j;
     }
     return valid;
+}
+
+// The same windows bit-parallel (rollfast.h): aligned 32-bit LDS reads packed
+// four codes per multiply, each window a funnel shift of the packed stream.
+template <int EI, bool CANON>
+KMAN_DEV uint32_t roll(const uint8_t *s, int base, int k, uint64_t mask, uint64_t p0, uint64_t n_bases,
+                       uint64_t (&kf)[EI], uint64_t (&kr)[EI]) {
+#ifdef KMAN_ROLL_SEQ
+    return roll_seq<EI, CANON>(s, base, k, mask, p0, n_bases, kf, kr);
+#else
+    return roll_fast<EI, CANON>(s, base, k, mask, p0, n_bases, kf, kr);
+#endif
 }
 
 }  // namespace

@@ -290,6 +290,161 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
 #undef XDIGIT
 }
 
+// ------------------------------------------------- pass 0, owned chains
+// The same extraction with block-owned position chains: chain c (one of S)
+// is a contiguous run of seg_tiles tiles that one 1024-thread block walks in
+// order, carrying each digit's running count in LDS, into region (d, c) of
+// capacity C0 (digit d's region is d * S * C0 items after digit 0's).  No
+// tile waits on another block (no status words, no look-back), and each
+// digit's last partial 128-byte line stays in LDS until a later tile of the
+// chain completes it, so only whole lines leave the CU (rg_pass's write
+// combining).  The next tile's codes load into registers behind this tile's
+// rank and stores.  Rank by one block-wide LDS atomic per item (unstable
+// inside a tile, as rg_extract<BR>).
+template <int NT, int EI, bool RC, bool CANON = false, int WL = 16>
+__global__ __launch_bounds__(NT, NT == 256 ? 4 : 1024 / NT) void rg_xown(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
+                                                   uint32_t Q, uint64_t *__restrict__ out, uint64_t C0, uint32_t S,
+                                                   uint32_t seg_tiles, uint32_t n_tiles,
+                                                   uint32_t *__restrict__ cnt0, uint32_t *__restrict__ counter,
+                                                   uint32_t *__restrict__ err, uint64_t *__restrict__ stp) {
+    constexpr int NWAVE = NT / 64;
+    constexpr int WIN = NT * EI;
+    constexpr int TILE = WIN * (RC ? 2 : 1);
+    constexpr int SI = TILE / NT;
+    static_assert(WIN + 64 <= TILE * 8 && NT >= RADIX, "codes fit in the key staging area; a thread per digit");
+    __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
+    __shared__ uint64_t wcb[RADIX][WL];  // the pending items of digit d at wcb[d][pos % WL]
+    __shared__ uint64_t qpar[RADIX];     // (q bound of the whole-line items << 32) | rel. index of tile item 0
+    __shared__ uint32_t thist[RADIX];
+    __shared__ uint32_t lstart[RADIX];
+    __shared__ uint32_t run[RADIX];
+    __shared__ uint32_t lds_scan[NWAVE];
+    __shared__ uint32_t lds_tile;
+    const int lane = lane_id();
+    const int w = threadIdx.x >> 6;
+    const uint32_t kb = 2u * (uint32_t)k;
+    const uint32_t shift = kb - B1;
+    const uint64_t keymask = kb >= 64 ? ~0ull : ((1ull << kb) - 1);
+    const uint64_t restmask = (1ull << shift) - 1;
+    const uint32_t dstride = S * (uint32_t)C0;  // (the host keeps RADIX * S * C0 < 2^32)
+    uint8_t *scodes = reinterpret_cast<uint8_t *>(skeys);
+    const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
+    for (;;) {
+        const uint32_t c = (uint32_t)grab_tile(counter, &lds_tile);
+        if (c >= S) break;
+        const uint32_t ta = c * seg_tiles;
+        const uint32_t tb = ta + seg_tiles < n_tiles ? ta + seg_tiles : n_tiles;
+        uint64_t *const obase0 = out + (uint64_t)c * C0;
+        if (threadIdx.x < RADIX) run[threadIdx.x] = 0;
+        CodeVecs<NT, EI> cv;
+        if (ta < tb) load_codes<NT, EI>(codes, n_bases, (uint64_t)ta * WIN, cv);
+        for (uint32_t t = ta; t < tb; t++) {
+            const uint64_t wb = (uint64_t)t * WIN;
+            RSTAMP(t, 0);
+            if (threadIdx.x < RADIX) thist[threadIdx.x] = 0;
+            store_codes<NT, EI>(cv, codes, n_bases, wb, scodes);
+            __syncthreads();
+            RSTAMP(t, 1);
+            uint64_t kf[EI], kr[EI];
+            const uint32_t w0 = threadIdx.x * EI;
+            const uint32_t valid = roll<EI, CANON>(scodes, w0, k, keymask, wb + w0, n_bases, kf, kr);
+            // the next tile's codes, behind this tile's work
+            RSTAMP(t, 2);
+            if (t + 1 < tb) load_codes<NT, EI>(codes, n_bases, wb + WIN, cv);
+            uint32_t tcnt;
+            const uint32_t off = block_exclusive_scan<NT>((uint32_t)(__popc(valid) * (RC ? 2 : 1)), SumU32(), 0u,
+                                                          lds_scan, &tcnt);
+            {
+                uint32_t o = off;
+#pragma unroll
+                for (int j = 0; j < EI; j++) {
+                    // the tile-local (window << 1 | strand) above the key bits
+                    // (uniq items only: Q > 0, k <= 25)
+                    const uint64_t tag = Q ? (uint64_t)((w0 + j) << 1) << kb : 0ull;
+                    if ((valid >> j) & 1u) {
+                        skeys[o++] = kf[j] | tag;
+                        if (RC) skeys[o++] = kr[j] | tag | (Q ? 1ull << kb : 0ull);
+                    }
+                }
+            }
+            __syncthreads();
+            RSTAMP(t, 3);
+#define XDIGIT(x) ((uint32_t)(((x) & keymask) >> shift))
+            uint64_t key[SI];
+            uint32_t rank[SI];
+#pragma unroll
+            for (int i = 0; i < SI; i++) key[i] = ib + i * 64 < tcnt ? skeys[ib + i * 64] : 0;
+#pragma unroll
+            for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&thist[XDIGIT(key[i])], 1u) : 0u;
+            __syncthreads();
+            const uint32_t ls = block_exclusive_scan<NT>(threadIdx.x < RADIX ? thist[threadIdx.x] : 0u, SumU32(), 0u,
+                                                         lds_scan, (uint32_t *)nullptr);
+            if (threadIdx.x < RADIX) lstart[threadIdx.x] = ls;
+            __syncthreads();
+            RSTAMP(t, 4);
+#pragma unroll
+            for (int i = 0; i < SI; i++)
+                if (ib + i * 64 < tcnt) skeys[lstart[XDIGIT(key[i])] + rank[i]] = key[i];
+            __syncthreads();
+            RSTAMP(t, 5);
+            // a digit whose partial line completes in this tile: its pending
+            // items go out first, 16 lanes per digit
+#pragma unroll
+            for (uint32_t d = threadIdx.x / WL; d < (uint32_t)RADIX; d += NT / WL) {
+                const uint32_t j = threadIdx.x & (WL - 1u), rn = run[d], p = rn & (WL - 1u);
+                if (j < p && ((rn + thist[d]) / WL) > (rn / WL) && rn - p + j < C0)
+                    obase0[d * dstride + rn - p + j] = wcb[d][j];
+            }
+            if (threadIdx.x < RADIX) {
+                // tile item q of digit d goes to position q + off in its
+                // region; whole lines end at fe; positions >= C0 are dropped
+                // (the overflow flag turns the call into KMAN_EFALLBACK)
+                const uint32_t d = threadIdx.x, rn = run[d], off2 = rn - lstart[d];
+                const int32_t fe = (int32_t)((rn + thist[d]) & ~(WL - 1u));
+                const int32_t qlim = (fe < (int32_t)C0 ? fe : (int32_t)C0) - (int32_t)off2;
+                qpar[d] = ((uint64_t)(uint32_t)qlim << 32) | (d * dstride + off2);
+            }
+            __syncthreads();
+            RSTAMP(t, 6);
+#pragma unroll
+            for (int rr = 0; rr < SI; rr++) {
+                const uint32_t q = threadIdx.x + rr * NT;
+                if (q < tcnt) {
+                    const uint64_t kk = skeys[q];
+                    const uint32_t d = XDIGIT(kk);
+                    uint64_t v = kk & restmask;
+                    if (Q) {
+                        const uint64_t f = kk >> kb;  // tile-local (window << 1 | strand)
+                        const uint64_t win = wb + (f >> 1);
+                        v = (v << Q) | (RC ? ((win << 1) | (f & 1u)) : win);
+                    }
+                    const uint64_t qp = qpar[d];
+                    const uint32_t rel = (uint32_t)qp + q;
+                    if ((int32_t)q < (int32_t)(qp >> 32)) obase0[rel] = v;
+                    else wcb[d][rel & (WL - 1u)] = v;
+                }
+            }
+#undef XDIGIT
+            __syncthreads();  // every read of run[] and skeys above before their updates
+            RSTAMP(t, 7);
+            if (threadIdx.x < RADIX) run[threadIdx.x] += thist[threadIdx.x];
+        }
+        __syncthreads();
+        // the chain's last partial lines and its final region counts
+#pragma unroll
+        for (uint32_t d = threadIdx.x / WL; d < (uint32_t)RADIX; d += NT / WL) {
+            const uint32_t j = threadIdx.x & (WL - 1u), rn = run[d], p = rn & (WL - 1u);
+            if (j < p && rn - p + j < C0) obase0[d * dstride + rn - p + j] = wcb[d][j];
+        }
+        if (threadIdx.x < RADIX) {
+            const uint32_t d = threadIdx.x;
+            if (run[d] > C0) atomicOr(err, ERR_REGION);
+            cnt0[d * S + c] = run[d] < C0 ? run[d] : (uint32_t)C0;
+        }
+        __syncthreads();  // (run and wcb are the next chain's)
+    }
+}
+
 // ---------------------------------------------------------------- pass 1
 // One tile of bucket b's items (cid round robin over the buckets; the RS
 // regions (b, *) read as one concatenated sequence, so each bucket is its own
@@ -331,12 +486,14 @@ struct PassArgs {
 // BR: rank by one block-wide LDS atomic per item (no per-wave counters: the
 // order of equal digits inside a tile is then not stable, which the finish
 // does not need -- it sorts every remaining key bit and compares keys only).
-template <bool ATOMIC, int NT, int SI, bool PF, bool WC = false, bool BR = false>
+// NSG > 64 (the owned-chain pass 0's S <= NSG segments per bucket): each
+// item finds its segment in an LDS prefix table instead of the lanes' ballots.
+template <bool ATOMIC, int NT, int SI, bool PF, bool WC = false, bool BR = false, int NSG = 64>
 __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
                                                  uint32_t *__restrict__ err, uint32_t dbg,
                                                  uint64_t *__restrict__ stp) {
     constexpr int TILE = NT * SI, NWAVE = NT / 64;
-    static_assert(NT >= R1 && 64 * SI <= 65535, "a thread per digit; u16 wave counters");
+    static_assert(NT >= R1 && 64 * SI <= 65535 && (NSG <= 64 || NSG <= NT), "a thread per digit / segment; u16 wave counters");
     __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
     __shared__ uint64_t wcb[WC ? R1 : 1][16];  // WC: the pending items of digit d at wcb[d][pos % 16]
     // WC, per digit for the store loop: qpar[d] = (q bound of the whole-line
@@ -351,6 +508,7 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
     __shared__ uint32_t lds_scan[NWAVE];
     __shared__ uint32_t s_items;
     __shared__ uint32_t lds_tile;
+    __shared__ uint32_t spre[NSG > 64 ? NSG + 1 : 1];  // NSG > 64: items before segment s
     const uint32_t shift = pa.shift, bits = pa.bits, nsg = pa.nsg, H = pa.H;
     const uint64_t C1 = pa.C1;
     const int lane = lane_id();
@@ -369,9 +527,19 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
         const uint32_t b = ch / H, h = ch % H;
         // every wave: the bucket's segment prefixes (lane s: items before
         // segment s; segments >= nsg empty) and bases, in registers
-        uint32_t spre_l;
-        uint64_t sbase_l;
-        {
+        uint32_t spre_l = 0;
+        uint64_t sbase_l = 0;
+        if (NSG > 64) {
+            const uint32_t t = threadIdx.x;
+            const uint32_t c = t < nsg ? pa.seg_cnt[(uint64_t)b * nsg + t] : 0u;
+            uint32_t tot;
+            const uint32_t ex = block_exclusive_scan<NT>(c, SumU32(), 0u, lds_scan, &tot);
+            if (t < (uint32_t)NSG) spre[t] = ex;
+            if (t == 0) {
+                spre[NSG] = tot;
+                s_items = tot;
+            }
+        } else {
             const uint32_t sgl = (uint32_t)lane;
             const uint64_t gi = (uint64_t)b * nsg + sgl;
             const uint32_t c = sgl < nsg ? pa.seg_cnt[gi] : 0u;
@@ -405,6 +573,30 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
             const uint32_t nn = items - tt0 < (uint32_t)TILE ? items - tt0 : (uint32_t)TILE;
 #pragma unroll
             for (int i = 0; i < (SI + 3) / 4; i++) sgp[i] = 0;
+            if constexpr (NSG > 64) {
+                // the first row's segment by binary search (largest s with
+                // spre[s] <= li), then forward past the (rare) boundaries
+                const uint32_t lf = tt0 + (uint32_t)w * (SI * 64) + (uint32_t)lane;
+                uint32_t lo = 0, hi = NSG;
+#pragma unroll
+                for (int it = 0; (1 << it) < NSG; it++) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (spre[mid] <= lf) lo = mid;
+                    else hi = mid;
+                }
+                uint32_t sg = lo, po = spre[lo], nx = spre[lo + 1];
+#pragma unroll
+                for (int i = 0; i < SI; i++) {
+                    const uint32_t li = lf + (uint32_t)i * 64;
+                    while (li >= nx && sg + 1 < (uint32_t)NSG) {
+                        sg++;
+                        po = nx;
+                        nx = spre[sg + 1];
+                    }
+                    key[i] = ib + i * 64 < nn ? pa.in[((uint64_t)b * nsg + sg) * pa.stride + (li - po)] : 0;
+                }
+                return;
+            }
 #pragma unroll
             for (int i = 0; i < SI; i++) {
                 const uint32_t li0 = tt0 + (uint32_t)w * (SI * 64) + (uint32_t)i * 64;
@@ -913,6 +1105,9 @@ struct RegionPlan {
     uint64_t C1h;        // pass-1 sub-region capacity
     uint32_t n_tiles0, seg_tiles, maxt1;
     uint32_t ei;         // windows per thread of pass 0
+    bool own;            // pass 0 = rg_xown (S block-owned chains), else rg_extract (RS look-back segments)
+    uint32_t xnt;        // rg_xown block size
+    uint32_t S;          // pass-0 segments (chains)
     uint64_t off_r1, off_c0, off_c1, off_lim, bytes;
 };
 
@@ -942,6 +1137,26 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     p.B2 = b2;
     p.rest = p.K - B1 - b2;
     {
+        // KMAN_RG_OWN=1: pass 0 by block-owned chains (rg_xown; A/B only --
+        // exact HBM traffic, 9.15 GB vs 14.3 for the config-2 step, but 4.9 ms
+        // at 256 threads (5.4 at 512 or 1024) vs 3.7 for rg_extract)
+        const char *e = getenv("KMAN_RG_OWN");
+        p.own = e && atoi(e) != 0;
+    }
+    if (p.own) {
+        // 1024 threads x 8 windows (4 with -r); up to 256 chains (one per
+        // CU), each at least 4 tiles long
+        const char *e = getenv("KMAN_RG_XNT");  // 512 / 1024: two / one block per CU (A/B timing)
+        p.xnt = e && atoi(e) == 1024 ? 1024u : (e && atoi(e) == 512 ? 512u : 256u);
+        p.ei = p.rc ? 4u : 8u;
+        const uint64_t win = (uint64_t)p.xnt * p.ei;
+        p.n_tiles0 = (uint32_t)ceil_div(n_bases, win);
+        const uint64_t smax = 256ull * (1024 / p.xnt);  // the resident blocks
+        uint64_t s = ceil_div(p.n_tiles0, 4);
+        s = s < 1 ? 1 : (s > smax ? smax : s);
+        p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, s);
+        p.S = (uint32_t)ceil_div(p.n_tiles0, p.seg_tiles);
+    } else {
         // windows per thread: 12 (6 with -r: two items per window) makes
         // 6144-item tiles, 53 KiB of LDS, three blocks per CU: 3.92 ms vs 4.77
         // with the 16-window tiles (two blocks per CU) and 4.63 with 8
@@ -951,12 +1166,16 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
         const int ei = e ? atoi(e) : 12;
         if (p.rc) p.ei = ei == 16 ? 8u : 6u;  // two windows per item slot
         else p.ei = ei == 16 ? 16u : (ei == 8 && !p.canon ? 8u : 12u);
+        const uint64_t win = (uint64_t)RT * p.ei;
+        p.n_tiles0 = (uint32_t)ceil_div(n_bases, win);
+        p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, RS);
+        p.S = RS;
     }
-    const uint64_t win = (uint64_t)RT * p.ei;
-    p.n_tiles0 = (uint32_t)ceil_div(n_bases, win);
-    p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, RS);
-    const uint64_t e0 = p.W / ((uint64_t)RADIX * RS);
-    p.C0 = ceil_div(e0 + e0 / 2 + 256, 64) * 64;
+    const uint64_t e0 = p.W / ((uint64_t)RADIX * p.S);
+    // (owned chains are longer than the look-back segments of small inputs:
+    // a 1024-item floor keeps a local repeat inside a region)
+    p.C0 = ceil_div(e0 + e0 / 2 + (p.own ? 1024 : 256), 64) * 64;
+    if ((uint64_t)RADIX * p.S * p.C0 >= (1ull << 32)) return KMAN_EFALLBACK;  // (32-bit item indices)
     const uint64_t e1 = p.W >> (B1 + b2);
     uint64_t c1 = ceil_div(e1 + e1 / 2 + 512, 64) * 64;
     p.C1 = c1 < (uint64_t)FCAP ? c1 : (uint64_t)FCAP;
@@ -968,11 +1187,11 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
         p.H = e && atoi(e) == 1 ? 1u : 2u;
     }
     p.C1h = p.C1;  // either half may hold most of a region (position-skewed repeats)
-    p.maxt1 = (uint32_t)ceil_div((uint64_t)(RS / p.H) * p.C0, T1);
+    p.maxt1 = (uint32_t)ceil_div((uint64_t)ceil_div(p.S, p.H) * p.C0, T1);
     const uint64_t nreg = 1ull << (B1 + b2);
-    p.off_r1 = (uint64_t)RADIX * RS * p.C0 * 8;
+    p.off_r1 = (uint64_t)RADIX * p.S * p.C0 * 8;
     p.off_c0 = p.off_r1 + nreg * p.H * p.C1h * 8;
-    p.off_c1 = p.off_c0 + (uint64_t)RADIX * RS * 4;
+    p.off_c1 = p.off_c0 + (uint64_t)RADIX * p.S * 4;
     p.off_lim = p.off_c1 + nreg * p.H * 4;
     p.bytes = p.off_lim + 64;
     *pl = p;
@@ -1007,6 +1226,13 @@ void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32
 // 4 4.29, 5 3.78, 6 4.69; later boxes: 5 3.49-3.58 with per-digit store
 // parameters, 3.54 with 32-bit relative output indices (7: 3.56).
 void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
+    if (pa.nsg > 64) {  // the owned-chain pass 0's segments (<= 1024, no seg_base, no tag): shape 5
+        const void *fn = (const void *)rg_pass<true, 1024, 8, true, true, true, 1024>;
+        const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, 1024, (uint64_t)pa.nbk * pa.H);
+        hipLaunchKernelGGL((rg_pass<true, 1024, 8, true, true, true, 1024>), dim3(grid), dim3(1024), 0, ctx->stream,
+                           pa, counter, ctx->d_err, dbg, stp);
+        return;
+    }
     const char *e = getenv("KMAN_RG_PASS");
     const int shape = e ? atoi(e) : 5;
     if (pa.bits <= 4 && shape >= 3) {
@@ -1112,8 +1338,35 @@ void launch_extract(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, ui
                            ctx->d_err, dbg, stp);
 }
 
+template <int EI, bool RC, bool CANON = false>
+void launch_xown(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
+                 uint64_t *r0, uint32_t *c0, uint32_t *counter, uint64_t *stp) {
+    if (p.xnt == 256) {  // four blocks per CU, write combining in 64-byte lines
+        const void *fn = (const void *)rg_xown<256, EI, RC, CANON, 8>;
+        const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, 256, p.S);
+        hipLaunchKernelGGL((rg_xown<256, EI, RC, CANON, 8>), dim3(grid), dim3(256), 0, ctx->stream, codes, n_bases,
+                           (int)k, p.Q, r0, p.C0, p.S, p.seg_tiles, p.n_tiles0, c0, counter, ctx->d_err, stp);
+    } else if (p.xnt == 1024) {
+        const void *fn = (const void *)rg_xown<1024, EI, RC, CANON>;
+        const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, 1024, p.S);
+        hipLaunchKernelGGL((rg_xown<1024, EI, RC, CANON>), dim3(grid), dim3(1024), 0, ctx->stream, codes, n_bases,
+                           (int)k, p.Q, r0, p.C0, p.S, p.seg_tiles, p.n_tiles0, c0, counter, ctx->d_err, stp);
+    } else {
+        const void *fn = (const void *)rg_xown<512, EI, RC, CANON>;
+        const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, 512, p.S);
+        hipLaunchKernelGGL((rg_xown<512, EI, RC, CANON>), dim3(grid), dim3(512), 0, ctx->stream, codes, n_bases,
+                           (int)k, p.Q, r0, p.C0, p.S, p.seg_tiles, p.n_tiles0, c0, counter, ctx->d_err, stp);
+    }
+}
+
 void launch_extract_any(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                         uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
+    if (p.own) {
+        if (p.canon) launch_xown<8, false, true>(ctx, p, codes, n_bases, k, r0, c0, counter, stp);
+        else if (p.rc) launch_xown<4, true>(ctx, p, codes, n_bases, k, r0, c0, counter, stp);
+        else launch_xown<8, false>(ctx, p, codes, n_bases, k, r0, c0, counter, stp);
+        return;
+    }
     if (p.canon && p.ei == 12) launch_extract<12, false, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
     else if (p.canon) launch_extract<16, false, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
     else if (p.rc && p.ei == 6) launch_extract<6, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
@@ -1201,7 +1454,7 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
         }
     uint32_t epoch, *counter;
     // pass 0: extraction by the top 8 bits
-    KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
+    KMAN_TRY(kman_lookback_begin(ctx, p.own ? 1 : (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
     {
         KTimer kt_(ctx, "region_extract");
         launch_extract_any(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter, dbg >> 8, stamps[0]);
@@ -1217,7 +1470,7 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
         pa.seg_cnt = c0;
         pa.stride = p.C0;
         pa.nbk = RADIX;
-        pa.nsg = RS;
+        pa.nsg = p.S;
         pa.gsub = 1;
         pa.H = p.H;
         pa.shift = p.Q + p.rest;
@@ -1239,7 +1492,7 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
     uint64_t *h = ctx->h_small;
     HIP_TRY(ctx, hipMemcpyAsync(h + 4, ctx->d_status + (nreg - 1), 8, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(h + 8, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
-    std::vector<uint32_t> hc(RADIX * RS);
+    std::vector<uint32_t> hc((size_t)RADIX * p.S);
     HIP_TRY(ctx, hipMemcpyAsync(hc.data(), c0, hc.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     uint32_t e;

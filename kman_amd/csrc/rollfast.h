@@ -1,0 +1,81 @@
+// rollfast.h — the windows of kmer.h's roll() computed bit-parallel: the
+// thread's code bytes are read as aligned 32-bit words and packed four at a
+// time (one multiply each) into 2-bit streams, so a window's key is a funnel
+// shift of the packed stream instead of k - 1 + EI dependent steps.
+//
+// Semantics (Sequence.yield_kmers, kmermaid/seq.py:285-328, on the codes of
+// kman_parse_fasta: bits 0-1 base, bit 2 not ACGT, bit 3 record start):
+// window j covers codes [base + j, base + j + k); it is valid when none of its
+// k codes is not-ACGT, no code after its first starts a record, and its start
+// p0 + j < n_bases.  kf = forward key (first base most significant), kr =
+// reverse complement; CANON: kf = min(forward, reverse complement).
+//
+// Host-compilable (tests/test_rollfast.py checks it against a per-base roll).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define KMAN_RF_HD __host__ __device__ __forceinline__
+#else
+#define KMAN_RF_HD static inline
+#endif
+
+// bytes b0..b3 of x (b0 least significant), low 2 bits each, first byte in
+// the top pair (BE) or bottom pair (LE); bit `bit` of each byte (4 bits, b0 at
+// bit 0).  The multiplies place each field at its target bits with no carry
+// into them from the cross terms below (every cross term sits >= 2 bits lower).
+KMAN_RF_HD uint32_t rf_be8(uint32_t x) { return ((x & 0x03030303u) * 0x40100401u) >> 24; }
+KMAN_RF_HD uint32_t rf_le8(uint32_t x) { return (((x & 0x03030303u) * 0x00041041u) >> 18) & 0xffu; }
+KMAN_RF_HD uint32_t rf_bit4(uint32_t x, int bit) {
+    return ((((x >> bit) & 0x01010101u) * 0x00204081u) >> 21) & 0xfu;
+}
+
+template <int EI, bool CANON>
+KMAN_RF_HD uint32_t roll_fast(const uint8_t *s, int base, int k, uint64_t mask, uint64_t p0, uint64_t n_bases,
+                              uint64_t (&kf)[EI], uint64_t (&kr)[EI]) {
+    // words covering (base & 3) + k - 1 + EI codes for any k <= 32
+    constexpr int NW = (3 + 31 + EI + 3) / 4;
+    static_assert(NW <= 16, "at most 64 codes");
+    const int b4 = base & ~3, dl = base & 3;
+    uint32_t w[NW];
+#pragma unroll
+    for (int i = 0; i < NW; i++) w[i] = *reinterpret_cast<const uint32_t *>(s + b4 + 4 * i);
+    // code c (0 .. 4 * NW) of the thread's words: BE stream be0:be1 (code 0 at
+    // the top of be0), LE stream le0:le1 (code 0 at the bottom of le0); the
+    // not-ACGT and record-start flags, one bit per code
+    uint32_t be[2 * ((NW + 3) / 4)], le[2 * ((NW + 3) / 4)];
+#pragma unroll
+    for (int i = 0; i < 2 * ((NW + 3) / 4); i++) be[i] = le[i] = 0;
+    uint64_t inv = 0, rst = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        be[i / 4] |= rf_be8(w[i]) << (24 - 8 * (i % 4));
+        le[i / 4] |= rf_le8(w[i]) << (8 * (i % 4));
+        inv |= (uint64_t)rf_bit4(w[i], 2) << (4 * i);
+        rst |= (uint64_t)rf_bit4(w[i], 3) << (4 * i);
+    }
+    const uint64_t be0 = ((uint64_t)be[0] << 32) | be[1];
+    const uint64_t be1 = NW > 8 ? ((uint64_t)be[2] << 32) | be[3] : 0ull;
+    const uint64_t le0 = ((uint64_t)le[1] << 32) | le[0];
+    const uint64_t le1 = NW > 8 ? ((uint64_t)le[3] << 32) | le[2] : 0ull;
+    const uint64_t km = (k >= 64) ? ~0ull : ((1ull << k) - 1);
+    const int ksh = 64 - 2 * k;
+    uint32_t valid = 0;
+#pragma unroll
+    for (int j = 0; j < EI; j++) {
+        const int o = dl + j;  // < 32
+        const uint64_t t = o ? (be0 << (2 * o)) | (be1 >> (64 - 2 * o)) : be0;
+        const uint64_t fwd = t >> ksh;
+        const uint64_t u = o ? (le0 >> (2 * o)) | (le1 << (64 - 2 * o)) : le0;
+        const uint64_t rc = (u & mask) ^ mask;
+        if (CANON) {
+            kf[j] = fwd < rc ? fwd : rc;
+        } else {
+            kf[j] = fwd;
+            kr[j] = rc;
+        }
+        const bool ok = !((inv >> o) & km) && !((rst >> (o + 1)) & (km >> 1)) && p0 + j < n_bases;
+        valid |= (uint32_t)ok << j;
+    }
+    return valid;
+}

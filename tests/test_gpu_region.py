@@ -298,3 +298,20 @@ def test_skewed_input_takes_the_rounds(dev):
         for cmd, fn in (("count", engine.count_text), ("uniq", engine.uniq_text)):
             subprocess.run([exe, cmd, src, os.path.join(d, "w"), "21"], check=True)
             assert fn(text, 21, dev=dev) == open(os.path.join(d, "w"), "rb").read()
+
+
+@pytest.mark.parametrize("xnt", ["256", "512"])
+@pytest.mark.parametrize("k,rc,mode", [(21, False, "count"), (21, False, "uniq"), (13, True, "uniq"),
+                                       (25, True, "count"), (31, False, "count")])
+def test_groups_owned_pass0(dev, golden_inputs, monkeypatch, xnt, k, rc, mode):
+    """The opt-in pass 0 by block-owned chains (KMAN_RG_OWN=1: rg_xown, no
+    look-back, write-combined lines) gives the same rows as the oracle."""
+    monkeypatch.setenv("KMAN_RG_OWN", "1")
+    monkeypatch.setenv("KMAN_RG_XNT", xnt)
+    for text in _texts(golden_inputs):
+        got = _groups(dev, text, k, rc, mode)
+        if got is None:
+            continue
+        want = _oracle(text, k, rc, mode)
+        np.testing.assert_array_equal(got[0], want[0])
+        np.testing.assert_array_equal(got[1].astype(np.uint64), want[1])
