@@ -64,6 +64,7 @@ extern "C" {
 #define KMAN_ECOMM (-6)    /* RCCL error */
 #define KMAN_ECAP (-7)     /* output capacity too small; *needed reports the size */
 #define KMAN_EFALLBACK (-8) /* kman_groups: input outside the region path; use the general path */
+#define KMAN_EPARTIAL (-9)  /* kman_dround_finish: some key ranges left out (kman_dround_failed) */
 
 /* kman_extract flags */
 #define KMAN_RC 1u          /* also emit reverse complements (kmer -r, seq.py:274-282) */
@@ -173,6 +174,12 @@ int kman_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32
 int kman_extract_range(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
                        uint64_t key_lo, uint64_t key_hi, uint64_t *d_keys, void *d_pos, uint32_t pos_bytes,
                        uint64_t cap, uint64_t *d_hist, uint64_t *n_kmers);
+/* The same for the keys whose top map_bits bits p have d_map[p] == map_val
+ * (d_map: 2^map_bits bytes): the key ranges a round left out
+ * (kman_dround_failed), each destination's in one pass. */
+int kman_extract_marked(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                        const uint8_t *d_map, uint32_t map_bits, uint32_t map_val, uint64_t *d_keys, void *d_pos,
+                        uint32_t pos_bytes, uint64_t cap, uint64_t *n_kmers);
 /* Histogram of the top 8 key bits of the stream (256 u64 into d_hist256) and
  * the k-mer count; flags: KMAN_RC (not KMAN_CANONICAL). */
 int kman_kmer_prefix_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
@@ -273,7 +280,8 @@ int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_
  *                        counts[src * nb + j] = items of bucket b_lo + j from
  *                        src) -> the round's count / uniq rows, ascending
  *                        (uniq pos u64 with the source rank in bits 56-63);
- *                        KMAN_EFALLBACK on a region overflow (skewed keys).
+ *                        KMAN_EPARTIAL when regions overflowed (skewed
+ *                        keys): their key ranges are left out (below).
  *                        d_a (>= a_bytes) may be the send buffer, d_b (>=
  *                        b_bytes) may be d_recv itself.
  * A rank's rounds emit its key range in order; the ranks' outputs in rank
@@ -290,6 +298,14 @@ int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_t k, uint32
                        uint64_t n_bases_q, uint32_t b_lo, uint32_t nb, const uint64_t *counts, void *d_a,
                        uint64_t a_bytes, void *d_b, uint64_t b_bytes, uint64_t *d_okeys, void *d_ovals,
                        uint32_t oval_bytes, uint64_t *n_out);
+/* After kman_dround_finish returned KMAN_EPARTIAL: regions that overflowed a
+ * capacity (a key repeated far beyond its region's share) emitted nothing,
+ * the other *n_out rows are in place in key order.  kman_dround_failed gives
+ * the left-out key ranges as [lo, hi] pairs (2 u64 each, ascending, merged;
+ * *n = ranges; NULL ranges: count only) for the caller to redo through
+ * kman_extract_marked + kman_sort_range + kman_finish and merge in
+ * (kman_merge_runs). */
+int kman_dround_failed(kman_ctx *ctx, uint64_t *ranges, uint64_t cap, uint64_t *n);
 
 /* Abundance spectrum of a count output (BASELINE config 5; not
  * in the reference): d_hist[c] = number of distinct k-mers seen c times, the

@@ -28,6 +28,7 @@ KMAN_ETIMEOUT = -5
 KMAN_ECOMM = -6
 KMAN_ECAP = -7
 KMAN_EFALLBACK = -8
+KMAN_EPARTIAL = -9
 
 KMAN_RC = 1
 KMAN_WANT_POS = 2
@@ -134,6 +135,12 @@ SIGNATURES = {
         c_int,
         [c_void_p, c_void_p, c_uint32, c_uint32, c_int, c_uint32, c_uint64, c_uint32, c_uint32, c_void_p, c_void_p,
          c_uint64, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, POINTER(c_uint64)],
+    ),
+    "kman_dround_failed": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
+    "kman_extract_marked": (
+        c_int,
+        [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_uint32,
+         c_uint64, POINTER(c_uint64)],
     ),
     "kman_count_hist": (c_int, [c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_uint32]),
     "kman_rle_count": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, POINTER(c_uint64)]),

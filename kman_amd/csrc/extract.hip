@@ -44,7 +44,9 @@ __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__
                                                      P *__restrict__ pos, uint64_t *__restrict__ status,
                                                      uint32_t *__restrict__ counter, uint32_t epoch,
                                                      uint32_t *__restrict__ err, uint64_t *__restrict__ hist,
-                                                     Plan plan, uint64_t key_lo, uint64_t key_hi, uint64_t cap) {
+                                                     Plan plan, uint64_t key_lo, uint64_t key_hi, uint64_t cap,
+                                                     const uint8_t *__restrict__ pmap, uint32_t pshift,
+                                                     uint32_t pval) {
     constexpr int TILE = ET * EI;
     constexpr int KPT = RC && !CANON ? 2 * EI : EI;  // keys per thread, max
     constexpr int MAXKEYS = ET * KPT;
@@ -69,12 +71,23 @@ __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__
         uint64_t kf[EI], kr[EI];
         const uint64_t p0 = tb + (uint64_t)threadIdx.x * EI;
         const uint32_t valid = roll<EI, CANON>(scodes, threadIdx.x * EI, k, mask, p0, n_bases, kf, kr);
-        // keys inside [key_lo, key_hi] only (kman_extract_range; the full range otherwise)
+        // keys inside [key_lo, key_hi] only (kman_extract_range; the full range
+        // otherwise), or with pmap[key >> pshift] == pval (kman_extract_marked)
         uint32_t vf = 0, vr = 0;
+        if (pmap) {
 #pragma unroll
-        for (int j = 0; j < EI; j++) {
-            vf |= (uint32_t)(kf[j] >= key_lo && kf[j] <= key_hi) << j;
-            if (RC && !CANON) vr |= (uint32_t)(kr[j] >= key_lo && kr[j] <= key_hi) << j;
+            for (int j = 0; j < EI; j++) {
+                if ((valid >> j) & 1u) {
+                    vf |= (uint32_t)(pmap[kf[j] >> pshift] == pval) << j;
+                    if (RC && !CANON) vr |= (uint32_t)(pmap[kr[j] >> pshift] == pval) << j;
+                }
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < EI; j++) {
+                vf |= (uint32_t)(kf[j] >= key_lo && kf[j] <= key_hi) << j;
+                if (RC && !CANON) vr |= (uint32_t)(kr[j] >= key_lo && kr[j] <= key_hi) << j;
+            }
         }
         vf &= valid;
         vr &= valid;
@@ -252,7 +265,8 @@ __global__ __launch_bounds__(ET) void kmer_hist_kernel(const uint8_t *__restrict
 
 template <int EI, bool RC, bool CANON, typename P>
 int launch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k, uint64_t *keys, P *pos,
-                   uint64_t *hist, const Plan &plan, uint64_t klo, uint64_t khi, uint64_t cap) {
+                   uint64_t *hist, const Plan &plan, uint64_t klo, uint64_t khi, uint64_t cap, const uint8_t *pmap,
+                   uint32_t pshift, uint32_t pval) {
     const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * EI);
     uint32_t epoch, *counter;
     KMAN_TRY(kman_lookback_begin(ctx, n_tiles, &epoch, &counter));
@@ -260,19 +274,23 @@ int launch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k,
     const int grid = kman_persistent_grid(ctx, (const void *)fn, ET, n_tiles);
     KTimer kt_(ctx, "extract");
     hipLaunchKernelGGL(fn, dim3(grid), dim3(ET), 0, ctx->stream, codes, n_bases, n_tiles, k, keys, pos,
-                       ctx->d_status, counter, epoch, ctx->d_err, hist, plan, klo, khi, cap);
+                       ctx->d_status, counter, epoch, ctx->d_err, hist, plan, klo, khi, cap, pmap, pshift, pval);
     HIP_TRY(ctx, hipGetLastError());
     return KMAN_OK;
 }
 
 template <typename P>
 int dispatch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k, uint32_t flags, uint64_t *keys,
-                     P *pos, uint64_t *hist, const Plan &plan, uint64_t klo, uint64_t khi, uint64_t cap) {
+                     P *pos, uint64_t *hist, const Plan &plan, uint64_t klo, uint64_t khi, uint64_t cap,
+                     const uint8_t *pmap, uint32_t pshift, uint32_t pval) {
     if (flags & KMAN_CANONICAL)
-        return launch_extract<16, false, true, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap);
+        return launch_extract<16, false, true, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap, pmap,
+                                                  pshift, pval);
     if (flags & KMAN_RC)
-        return launch_extract<8, true, false, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap);
-    return launch_extract<16, false, false, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap);
+        return launch_extract<8, true, false, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap, pmap,
+                                                 pshift, pval);
+    return launch_extract<16, false, false, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap, pmap,
+                                               pshift, pval);
 }
 
 }  // namespace
@@ -306,10 +324,12 @@ extern "C" int kman_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_ba
                               n_kmers);
 }
 
-extern "C" int kman_extract_range(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
-                                  uint64_t key_lo, uint64_t key_hi, uint64_t *d_keys, void *d_pos, uint32_t pos_bytes,
-                                  uint64_t cap, uint64_t *d_hist, uint64_t *n_kmers) {
-    const bool ranged = key_lo != 0 || key_hi != ~0ull;
+namespace {
+int extract_filtered(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                     uint64_t key_lo, uint64_t key_hi, const uint8_t *pmap, uint32_t pshift, uint32_t pval,
+                     uint64_t *d_keys, void *d_pos, uint32_t pos_bytes, uint64_t cap, uint64_t *d_hist,
+                     uint64_t *n_kmers) {
+    const bool ranged = key_lo != 0 || key_hi != ~0ull || pmap;
     if (!ctx || !n_kmers) return KMAN_EINVAL;
     if (k < 2 || k > 32) return kman_fail(ctx, KMAN_EINVAL, "k must be in [2, 32] on the GPU path, got %u", k);
     const bool want_pos = flags & KMAN_WANT_POS;
@@ -347,13 +367,13 @@ extern "C" int kman_extract_range(kman_ctx *ctx, const uint8_t *d_codes, uint64_
     }
     if (!want_pos) {
         KMAN_TRY(dispatch_extract<NoPos>(ctx, d_codes, n_bases, (int)k, flags, d_keys, nullptr, d_hist, plan, key_lo,
-                                         key_hi, cap));
+                                         key_hi, cap, pmap, pshift, pval));
     } else if (pos_bytes == 4) {
         KMAN_TRY(dispatch_extract<uint32_t>(ctx, d_codes, n_bases, (int)k, flags, d_keys, (uint32_t *)d_pos, d_hist,
-                                            plan, key_lo, key_hi, cap));
+                                            plan, key_lo, key_hi, cap, pmap, pshift, pval));
     } else {
         KMAN_TRY(dispatch_extract<uint64_t>(ctx, d_codes, n_bases, (int)k, flags, d_keys, (uint64_t *)d_pos, d_hist,
-                                            plan, key_lo, key_hi, cap));
+                                            plan, key_lo, key_hi, cap, pmap, pshift, pval));
     }
     // the last tile's inclusive prefix is the number of k-mers written
     const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * ((flags & KMAN_RC) && !(flags & KMAN_CANONICAL) ? 8 : 16));
@@ -362,6 +382,25 @@ extern "C" int kman_extract_range(kman_ctx *ctx, const uint8_t *d_codes, uint64_
         return kman_fail(ctx, KMAN_ECAP, "key range holds %llu keys > capacity %llu", (unsigned long long)*n_kmers,
                          (unsigned long long)cap);
     return KMAN_OK;
+}
+}  // namespace
+
+extern "C" int kman_extract_range(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                                  uint64_t key_lo, uint64_t key_hi, uint64_t *d_keys, void *d_pos, uint32_t pos_bytes,
+                                  uint64_t cap, uint64_t *d_hist, uint64_t *n_kmers) {
+    return extract_filtered(ctx, d_codes, n_bases, k, flags, key_lo, key_hi, nullptr, 0, 0, d_keys, d_pos, pos_bytes,
+                            cap, d_hist, n_kmers);
+}
+
+extern "C" int kman_extract_marked(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k,
+                                   uint32_t flags, const uint8_t *d_map, uint32_t map_bits, uint32_t map_val,
+                                   uint64_t *d_keys, void *d_pos, uint32_t pos_bytes, uint64_t cap,
+                                   uint64_t *n_kmers) {
+    if (!ctx || !n_kmers) return KMAN_EINVAL;
+    if (!d_map || map_bits == 0 || map_bits > 2 * k || map_bits > 30)
+        return kman_fail(ctx, KMAN_EINVAL, "kman_extract_marked: map of %u key bits (k = %u)", map_bits, k);
+    return extract_filtered(ctx, d_codes, n_bases, k, flags, 0, ~0ull, d_map, 2 * k - map_bits, map_val, d_keys,
+                            d_pos, pos_bytes, cap, nullptr, n_kmers);
 }
 
 // top-8-bit histogram of the stream's keys (the k-mer count is its sum): the

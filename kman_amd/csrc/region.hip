@@ -475,6 +475,11 @@ struct PassArgs {
     uint64_t *out;
     uint64_t C1;
     uint32_t *cnt1;
+    // optional: a sub-region that overflows C1 flags the finish regions
+    // [(sub / fail_div) << fail_shift, +2^fail_shift) in fail[] (the round
+    // path then leaves them out and redoes only their keys)
+    uint8_t *fail;
+    uint32_t fail_div, fail_shift;
 };
 
 // NT threads x SI items per tile: (512, 16) runs two blocks per CU, (1024, 8)
@@ -842,7 +847,13 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
         }
         if (threadIdx.x < R1) {
             const uint32_t d = threadIdx.x;
-            if (run[d] > C1) atomicOr(err, ERR_REGION);
+            if (run[d] > C1 && d < radix) {
+                atomicOr(err, ERR_REGION);
+                if (pa.fail) {
+                    const uint64_t f0 = (SUBREG(d) / pa.fail_div) << pa.fail_shift;
+                    for (uint64_t f = 0; f < (1ull << pa.fail_shift); f++) pa.fail[f0 + f] = 1;
+                }
+            }
             if (d < radix) pa.cnt1[SUBREG(d)] = run[d] < C1 ? run[d] : (uint32_t)C1;
         }
 #undef SUBREG
@@ -865,7 +876,8 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
                                                 uint64_t *__restrict__ okeys, O *__restrict__ ovals,
                                                 uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
                                                 uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg,
-                                                uint64_t *__restrict__ stp, uint32_t nreg) {
+                                                uint64_t *__restrict__ stp, uint32_t nreg,
+                                                uint8_t *__restrict__ freg) {
     __shared__ __attribute__((aligned(16))) uint64_t s[FCAP];
     __shared__ uint32_t wh[FW][FWORD];  // per-wave digit counters, u16 pairs
     __shared__ uint32_t dstart[FRAD];
@@ -892,10 +904,16 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
             v[i] = p < mm ? src[p < a0 ? p : p + skip] : 0;
         }
     };
-    auto fit = [&](uint32_t a0, uint32_t a1) -> uint32_t {
+    // freg (the round path): a region flagged by a pass (a sub-region
+    // overflowed) or here (more than the LDS holds) emits nothing
+    auto fit = [&](uint32_t rr, uint32_t a0, uint32_t a1) -> uint32_t {
         const uint32_t mm = a0 + a1;
+        if (freg && freg[rr]) return 0u;  // (block-uniform)
         if (mm <= (uint32_t)FCAP) return mm;
-        if (t == 0) atomicOr(err, ERR_REGION);  // (block-uniform) more than the LDS holds
+        if (t == 0) {
+            atomicOr(err, ERR_REGION);  // (block-uniform) more than the LDS holds
+            if (freg) freg[rr] = 1;
+        }
         return 0u;
     };
     // PF (persistent blocks): a block walks regions in grab order; while it
@@ -910,7 +928,7 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
     if (r >= nreg) return;
     uint32_t m0, m1, rn = nreg, n0 = 0, n1 = 0;
     counts(r, m0, m1);
-    uint32_t m = fit(m0, m1);
+    uint32_t m = fit(r, m0, m1);
     uint64_t x[FIPT];
     load(r, m0, m, x);
     if (PF) {
@@ -1004,7 +1022,7 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
         // the next region's items are loaded now (x is dead: the sorted
         // region is in LDS), arriving while this one is grouped and written
         if (t == 0) s_tile = atomicAdd(counter, 1u);
-        if (rn < nreg) load(rn, n0, n0 + n1 <= (uint32_t)FCAP ? n0 + n1 : 0u, x);
+        if (rn < nreg) load(rn, n0, n0 + n1 <= (uint32_t)FCAP && !(freg && freg[rn]) ? n0 + n1 : 0u, x);
         __syncthreads();
         rnn = __builtin_amdgcn_readfirstlane(s_tile);
         if (rnn < nreg) counts(rnn, nn0, nn1);
@@ -1088,7 +1106,7 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
     __syncthreads();  // (every read of s / s_out / s_tile above before the next region writes them)
     r = rn;
     m0 = n0;
-    m = fit(n0, n1);
+    m = fit(r, n0, n1);
     rn = rnn;
     n0 = nn0;
     n1 = nn1;
@@ -1275,6 +1293,7 @@ struct FinishArgs {
     uint32_t tag_shift;
     uint32_t nreg;
     uint32_t fsub = 1;  // sub-regions per region (cnt and in indexed per sub-region)
+    uint8_t *freg = nullptr;  // per-region overflow flags (the round path), else null
 };
 
 template <int MODE, typename O, bool ATOMIC, bool PF>
@@ -1284,7 +1303,7 @@ void launch_finish_as(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void 
     const uint32_t grid = PF ? (uint32_t)kman_persistent_grid(ctx, fn, FT, f.nreg) : f.nreg;
     hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, PF>), dim3(grid), dim3(FT), 0, ctx->stream, f.in, f.C1, f.cnt, f.Q,
                        f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status, counter, epoch,
-                       ctx->d_err, dbg, stp, f.nreg);
+                       ctx->d_err, dbg, stp, f.nreg, f.freg);
 }
 
 // one block per region; KMAN_RG_FIN=1: persistent blocks that prefetch the
@@ -1649,8 +1668,9 @@ struct RoundPlan {
     bool rc;
     uint64_t C1s, C1;     // pass-1 sub-region / pass-1b region capacities
     uint64_t nsub, nreg;
-    // arena A: r1 | c1 | pass-1 segment bases (u64) + counts (u32); arena B: r2 | c2
-    uint64_t off_c1, off_tab, a_bytes, off_c2, b_bytes;
+    // arena A: r1 | c1 | pass-1 segment bases (u64) + counts (u32) | region
+    // overflow flags (u8); arena B: r2 | c2
+    uint64_t off_c1, off_tab, off_fail, a_bytes, off_c2, b_bytes;
 };
 
 // counts[src * nb + j] = items of bucket b_lo + j from rank src
@@ -1711,7 +1731,8 @@ int make_rplan(uint32_t k, uint32_t flags, int mode, uint32_t world, uint64_t n_
     d.nreg = (uint64_t)nb * 512 << g;
     d.off_c1 = d.nsub * d.C1s * 8;
     d.off_tab = ceil_div(d.off_c1 + d.nsub * 4, 64) * 64;
-    d.a_bytes = d.off_tab + ceil_div((uint64_t)nb * world * 12 + 64, 64) * 64;
+    d.off_fail = d.off_tab + ceil_div((uint64_t)nb * world * 12 + 64, 64) * 64;
+    d.a_bytes = d.off_fail + ceil_div(d.nreg + 64, 64) * 64;
     d.off_c2 = g ? d.nreg * d.C1 * 8 : 0;
     d.b_bytes = g ? d.off_c2 + ceil_div(d.nreg * 4 + 64, 64) * 64 : 64;
     *rp = d;
@@ -1842,7 +1863,9 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     uint32_t *scnt = (uint32_t *)(sbase + (uint64_t)nb * world);
     uint64_t *r2 = (uint64_t *)wb;
     uint32_t *c2 = (uint32_t *)(wb + d.off_c2);
+    uint8_t *freg = (uint8_t *)(wa + d.off_fail);
     const uint32_t G = world;
+    ctx->failed.clear();
     // pass-1 segments: bucket (b, src) = one contiguous run of src's chunk
     std::vector<uint64_t> hb((size_t)nb * G);
     std::vector<uint32_t> hn((size_t)nb * G);
@@ -1858,6 +1881,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     HIP_TRY(ctx, hipMemcpyAsync(sbase, hb.data(), hb.size() * 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(scnt, hn.data(), hn.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(c1, 0, d.nsub * 4, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(freg, 0, d.nreg, ctx->stream));
     uint32_t epoch, *counter;
     // pass 1: by the 9 bits below the bucket, H chains per (b, src) into
     // sub-regions (b, d, src, h)
@@ -1877,6 +1901,9 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         pa.out = r1;
         pa.C1 = d.C1s;
         pa.cnt1 = c1;
+        pa.fail = freg;  // sub-region (b, d, src, h) -> regions ((b, d) << g) + *
+        pa.fail_div = G * d.H;
+        pa.fail_shift = d.g;
         launch_pass(ctx, pa, counter, 0, nullptr);
         HIP_TRY(ctx, hipGetLastError());
     }
@@ -1885,6 +1912,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         // one source, two chains: the finish reads the pass-1 sub-regions
         FinishArgs f{r1, d.C1s, c1, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << 9, 0u, (uint32_t)d.nreg};
         f.fsub = d.H;
+        f.freg = freg;
         KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, 0, nullptr));
     } else {
     // (c2 may lie in the receive buffer: cleared only once pass 1 has read it)
@@ -1912,6 +1940,9 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         pa.out = r2;
         pa.C1 = d.C1;
         pa.cnt1 = c2;
+        pa.fail = freg;
+        pa.fail_div = 1;
+        pa.fail_shift = 0;
         launch_pass(ctx, pa, counter, 0, nullptr);
         HIP_TRY(ctx, hipGetLastError());
     }
@@ -1919,17 +1950,45 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     {
         FinishArgs f{r2, d.C1, c2, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << (9 + d.g),
                      mode == KMAN_FINISH_UNIQ ? d.Q + d.rest + d.g : 0u, (uint32_t)d.nreg};
+        f.freg = freg;
         KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, 0, nullptr));
     }
     }
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small + 4, ctx->d_status + (d.nreg - 1), 8, hipMemcpyDeviceToHost, ctx->stream));
     uint32_t e;
     KMAN_TRY(read_err(ctx, &e));  // synchronises
-    if (e) return KMAN_EFALLBACK;  // a region overflowed (skewed keys): outputs invalid
     const uint64_t wd = ctx->h_small[4];
     if (((wd >> 56) & 63u) != ctx->epoch || (wd >> 62) != ST_INCL)
         return kman_fail(ctx, KMAN_EHIP, "region output total not published");
     *n_out = wd & ST_VMASK;
+    if (!e) return KMAN_OK;
+    // regions that overflowed a capacity (skewed keys: repeats) emitted
+    // nothing; the rows of every other region are in place, in key order.
+    // Their key ranges, merged, for the caller to redo (kman_dround_failed)
+    std::vector<uint8_t> hf(d.nreg);
+    HIP_TRY(ctx, hipMemcpy(hf.data(), freg, d.nreg, hipMemcpyDeviceToHost));
+    const uint64_t rbase = (uint64_t)b_lo << (9 + d.g);
+    const uint64_t top = d.rest >= 64 ? ~0ull : ((1ull << d.rest) - 1);
+    for (uint64_t r = 0; r < d.nreg; r++) {
+        if (!hf[r]) continue;
+        const uint64_t lo = (rbase + r) << d.rest, hi = lo | top;
+        if (!ctx->failed.empty() && ctx->failed.back() + 1 == lo) ctx->failed.back() = hi;
+        else {
+            ctx->failed.push_back(lo);
+            ctx->failed.push_back(hi);
+        }
+    }
+    if (ctx->failed.empty())  // (an overflow that flagged no region: not expected)
+        return kman_fail(ctx, KMAN_EHIP, "kman_dround_finish: overflow without a flagged region");
+    return KMAN_EPARTIAL;
+}
+
+extern "C" int kman_dround_failed(kman_ctx *ctx, uint64_t *ranges, uint64_t cap, uint64_t *n) {
+    if (!ctx || !n) return KMAN_EINVAL;
+    *n = ctx->failed.size() / 2;
+    if (!ranges) return KMAN_OK;
+    if (cap < *n) return KMAN_ECAP;
+    memcpy(ranges, ctx->failed.data(), ctx->failed.size() * 8);
     return KMAN_OK;
 }
 

@@ -392,9 +392,11 @@ extern "C" int kman_rle_wide(kman_ctx *ctx, int mode, const uint64_t *d_hi, cons
 // n-way merge of sorted runs (Crawler.do_records' heapq.merge over sorted
 // batches, kmermaid/join.py:63-93): a tree of stable 2-way merges (run order
 // kept, so ties go to the lower run index, then in-run order -- heapq.merge
-// over (key, batch) with batches in order).  Each 2-way merge is merge-path:
-// every thread finds where its MI outputs start on the merge path by a binary
-// search over the diagonal, then merges MI items.
+// over (key, batch) with batches in order).  Each 2-way merge is merge-path
+// in tiles: a block's MT * MI outputs start at its diagonal's split (two
+// binary searches in HBM), its A and B slices are loaded coalesced into LDS,
+// each thread merges MI outputs from LDS (its own diagonal searched there),
+// and the tile is staged back through LDS and stored coalesced.
 namespace {
 
 constexpr int MT = 256, MI = 8;
@@ -404,29 +406,67 @@ __global__ __launch_bounds__(MT) void merge2_kernel(const uint64_t *__restrict__
                                                     uint64_t na, const uint64_t *__restrict__ bk,
                                                     const V *__restrict__ bv, uint64_t nb,
                                                     uint64_t *__restrict__ ok, V *__restrict__ ov) {
+    constexpr int TILE = MT * MI;
+    __shared__ uint64_t sk[TILE];
+    __shared__ V sv[TILE];
+    __shared__ uint64_t split[2];
     const uint64_t n = na + nb;
-    const uint64_t d = ((uint64_t)blockIdx.x * MT + threadIdx.x) * MI;
-    if (d >= n) return;
-    // i = A elements among the first d outputs (A first on ties)
-    uint64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+    const uint64_t t0 = (uint64_t)blockIdx.x * TILE;
+    if (t0 >= n) return;  // (block-uniform)
+    const uint64_t t1 = t0 + TILE < n ? t0 + TILE : n;
+    // A elements among the first d outputs (A first on ties), d = t0 and t1
+    if (threadIdx.x < 2) {
+        const uint64_t d = threadIdx.x ? t1 : t0;
+        uint64_t lo = d > nb ? d - nb : 0, hi = d < na ? d : na;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (ak[mid] <= bk[d - 1 - mid]) lo = mid + 1;
+            else hi = mid;
+        }
+        split[threadIdx.x] = lo;
+    }
+    __syncthreads();
+    const uint64_t a0 = split[0], b0 = t0 - a0;
+    const uint32_t nA = (uint32_t)(split[1] - a0), nt = (uint32_t)(t1 - t0), nB = nt - nA;
+    for (uint32_t q = threadIdx.x; q < nt; q += MT) {
+        const bool isA = q < nA;
+        sk[q] = isA ? ak[a0 + q] : bk[b0 + (q - nA)];
+        if (av) sv[q] = isA ? av[a0 + q] : bv[b0 + (q - nA)];
+    }
+    __syncthreads();
+    const uint32_t d = threadIdx.x * MI < nt ? threadIdx.x * MI : nt;
+    uint32_t lo = d > nB ? d - nB : 0, hi = d < nA ? d : nA;
     while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        if (ak[mid] <= bk[d - 1 - mid]) lo = mid + 1;
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sk[mid] <= sk[nA + d - 1 - mid]) lo = mid + 1;
         else hi = mid;
     }
-    uint64_t i = lo, j = d - lo;
-    const uint64_t e = d + MI < n ? d + MI : n;
-    for (uint64_t o = d; o < e; o++) {
-        const bool takeA = j >= nb || (i < na && ak[i] <= bk[j]);
-        if (takeA) {
-            ok[o] = ak[i];
-            if (av) ov[o] = av[i];
-            i++;
-        } else {
-            ok[o] = bk[j];
-            if (av) ov[o] = bv[j];
-            j++;
+    uint32_t i = lo, j = d - lo;
+    uint64_t rk[MI];
+    V rv[MI];
+#pragma unroll
+    for (int o = 0; o < MI; o++) {
+        if (d + o < nt) {
+            const bool takeA = j >= nB || (i < nA && sk[i] <= sk[nA + j]);
+            const uint32_t src = takeA ? i : nA + j;
+            rk[o] = sk[src];
+            if (av) rv[o] = sv[src];
+            i += takeA;
+            j += !takeA;
         }
+    }
+    __syncthreads();  // every LDS read above before the outputs overwrite it
+#pragma unroll
+    for (int o = 0; o < MI; o++) {
+        if (d + o < nt) {
+            sk[d + o] = rk[o];
+            if (av) sv[d + o] = rv[o];
+        }
+    }
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < nt; q += MT) {
+        ok[t0 + q] = sk[q];
+        if (av) ov[t0 + q] = sv[q];
     }
 }
 
@@ -480,7 +520,8 @@ extern "C" int kman_merge_runs(kman_ctx *ctx, const kman_run *runs, int nruns, u
     // levels alternate between (out, tmp) starting so that the last is out
     int levels = 0;
     for (size_t m = cur.size(); m > 1; m = (m + 1) / 2) levels++;
-    if (levels && (!d_tmp_keys || (val_bytes && !d_tmp_vals))) return kman_fail(ctx, KMAN_EINVAL, "null scratch");
+    // (one level -- two runs -- writes d_okeys directly: no scratch)
+    if (levels > 1 && (!d_tmp_keys || (val_bytes && !d_tmp_vals))) return kman_fail(ctx, KMAN_EINVAL, "null scratch");
     KTimer kt_(ctx, "merge");
     for (int lv = 0; lv < levels; lv++) {
         const bool to_out = ((levels - 1 - lv) & 1) == 0;
@@ -495,8 +536,7 @@ extern "C" int kman_merge_runs(kman_ctx *ctx, const kman_run *runs, int nruns, u
             uint64_t *ok = dk + at;
             void *ov = val_bytes ? (void *)(dv + (size_t)val_bytes * at) : nullptr;
             if (n) {
-                const uint64_t th = ceil_div(n, (uint64_t)MI);
-                const dim3 g((uint32_t)ceil_div(th, (uint64_t)MT));
+                const dim3 g((uint32_t)ceil_div(n, (uint64_t)MT * MI));
                 if (val_bytes == 8)
                     hipLaunchKernelGGL(merge2_kernel<uint64_t>, g, dim3(MT), 0, ctx->stream, a.k, (const uint64_t *)a.v,
                                        a.n, b.k, (const uint64_t *)b.v, b.n, ok, (uint64_t *)ov);

@@ -390,9 +390,12 @@ class DistPipeline:
         self.arena_a, self.arena_b = _Grow(dev), _Grow(dev)
         self.out_keys, self.out_vals = _Grow(dev), _Grow(dev)
         self.gen_bufs = [_Grow(dev) for _ in range(6)]  # general path: send/recv keys, pos, alt keys, alt pos
+        self.part_bufs = [_Grow(dev), _Grow(dev), _Grow(dev)]  # the redone key ranges' rows (keys, values), map
         self.n_local = self.n_out = self.n_recv = 0
         self.rounds = 0
         self.fallback_rounds = 0
+        self.partial_rounds = 0
+        self.redone_kmers = 0
         self.phase_ms = {}
         self.ready = False
         if self.comm is not None:
@@ -523,6 +526,8 @@ class DistPipeline:
         n_out = 0
         lap("plan+alloc")
         self.fallback_rounds = 0
+        self.partial_rounds = 0
+        self.redone_kmers = 0
         for r in range(R):
             if self.path == "region":
                 A, B = self.arena_a.get(a_need), self.arena_b.get(b_need)
@@ -546,12 +551,22 @@ class DistPipeline:
                                            c_void_p(ok_.ptr + 8 * n_out), c_void_p(ov_.ptr + vb * n_out), vb,
                                            byref(got))
                 fb = 1 if ret == N.KMAN_EFALLBACK else 0
-                if not fb:
+                part = 1 if ret == N.KMAN_EPARTIAL else 0
+                if not fb and not part:
                     N.check(ctx, ret, "kman_dround_finish")
                 lap("finish")
-                f = yield ("allreduce", np.array([fb], np.uint64))
-                if int(f[0]) == 0:
+                f = yield ("allreduce", np.array([fb, part], np.uint64))
+                if int(f[0]) == 0 and int(f[1]) == 0:
                     n_out += int(got.value)
+                    continue
+                if int(f[0]) == 0:
+                    # regions overflowed (a repeat far beyond its region's
+                    # share): the other rows are in place, only the left-out
+                    # key ranges go through the general path, merged in
+                    self.partial_rounds += 1
+                    mine = self._failed_ranges() if part else np.zeros((0, 2), np.uint64)
+                    n_out += yield from self._redo_ranges(mine, int(got.value), A, B, ok_, ov_, n_out, vb)
+                    lap("partial_redo")
                     continue
                 self.fallback_rounds += 1
             # the general path for this round (every rank together)
@@ -561,6 +576,161 @@ class DistPipeline:
         self.n_recv = cap
         self._out = (ok_, ov_, vb)
         return self.n_local
+
+    def _failed_ranges(self) -> np.ndarray:
+        """[lo, hi] key ranges the last kman_dround_finish left out."""
+        L, ctx = N.lib(), self.dev.ctx
+        n = c_uint64(0)
+        N.check(ctx, L.kman_dround_failed(ctx, None, 0, byref(n)), "kman_dround_failed")
+        out = np.zeros((int(n.value), 2), np.uint64)
+        if n.value:
+            N.check(ctx, L.kman_dround_failed(ctx, out.ctypes.data_as(c_void_p), n.value, byref(n)),
+                    "kman_dround_failed")
+        return out
+
+    def _redo_ranges(self, mine: np.ndarray, n_region: int, A, B, ok_, ov_, n_out: int, vb: int):
+        """The key ranges each rank's round finish left out (mine: this
+        rank's), through the general path: every rank extracts the k-mers of
+        each destination's ranges (kman_extract_marked), one exchange, then the
+        destination sorts (kman_sort_range) and groups (kman_finish) them and
+        merges the rows with its n_region region rows at ok_/ov_[n_out]
+        (kman_merge_runs: the ranges are disjoint).  Generator; returns the
+        rows now at n_out."""
+        L, ctx, dev, sh = N.lib(), self.dev.ctx, self.dev, self.shard
+        G, me, k = self.world, self.rank, self.k
+        uniq = self.mode == "uniq"
+        tick = [time.perf_counter()]
+
+        def lap(tag):  # (KMAN_DIST_TIMES=1: host-side phase times of the redo, synchronised)
+            if os.environ.get("KMAN_DIST_TIMES"):
+                dev.sync()
+                t = time.perf_counter()
+                self.phase_ms["redo_" + tag] = self.phase_ms.get("redo_" + tag, 0.0) + (t - tick[0]) * 1e3
+                tick[0] = t
+
+        cnt = yield ("allgather", np.array([len(mine)], np.uint64))
+        cnt = np.asarray(cnt, np.uint64).reshape(G)
+        m = max(1, int(cnt.max()))
+        pad = np.zeros(2 * m, np.uint64)
+        pad[:2 * len(mine)] = np.asarray(mine, np.uint64).reshape(-1)
+        allr = np.asarray((yield ("allgather", pad)), np.uint64).reshape(G, 2 * m)
+        ranges = [allr[q, :2 * int(cnt[q])].reshape(-1, 2) for q in range(G)]
+        # destination map over key prefixes (map[p] = q + 1: prefix p is in
+        # one of q's ranges), so each destination's k-mers come out in one
+        # pass (kman_extract_marked) however many ranges it has
+        K = 2 * k
+        pbits = 1
+        for q in range(G):
+            for lo, hi in ranges[q]:
+                lo, end = int(lo), int(hi) + 1
+                s_ = min((lo & -lo).bit_length() - 1 if lo else K, (end & -end).bit_length() - 1 if end < (1 << K) else K)
+                pbits = max(pbits, K - s_)
+        if pbits > 24:
+            raise NotImplementedError("left-out key ranges finer than 24 key bits")
+        sh_ = K - pbits
+        pmap = np.zeros(1 << pbits, np.uint8)
+        for q in range(G):
+            for lo, hi in ranges[q]:
+                pmap[int(lo) >> sh_:(int(hi) >> sh_) + 1] = q + 1
+        d_map = self.part_bufs[2].get(len(pmap))
+        dev.upload(d_map, pmap)
+        flags = engine.flags_for(self.rc, uniq, self.canonical)
+
+        def marked(q, keys_ptr, pos_ptr, cap):
+            got = c_uint64(0)
+            rc_ = L.kman_extract_marked(ctx, c_void_p(sh.codes.ptr), sh.n_eff, k, flags, c_void_p(d_map.ptr), pbits,
+                                        q + 1, c_void_p(keys_ptr) if keys_ptr else None,
+                                        c_void_p(pos_ptr) if pos_ptr else None, 8, cap, byref(got))
+            if rc_ not in (N.KMAN_OK, N.KMAN_ECAP) or (cap and rc_ != N.KMAN_OK):
+                N.check(ctx, rc_, "kman_extract_marked")
+            return int(got.value)
+
+        lap("map")
+        # the send buffers are the round's arenas (free once its finish is
+        # done): each destination's k-mers extracted straight in, the count
+        # coming back with them; only if they do not fit, counted first
+        ecap = min(A.nbytes, B.nbytes if uniq else A.nbytes) // 8
+        sc = np.zeros(G, np.uint64)
+        at = 0
+        sk, sp = A, (B if uniq else None)
+        fits = True
+        for q in range(G):
+            if not len(ranges[q]):
+                continue
+            got = c_uint64(0)
+            rc_ = L.kman_extract_marked(ctx, c_void_p(sh.codes.ptr), sh.n_eff, k, flags, c_void_p(d_map.ptr), pbits,
+                                        q + 1, c_void_p(A.ptr + 8 * at), c_void_p(B.ptr + 8 * at) if uniq else None,
+                                        8, max(0, ecap - at), byref(got))
+            if rc_ == N.KMAN_ECAP:
+                fits = False
+                break
+            N.check(ctx, rc_, "kman_extract_marked")
+            sc[q] = int(got.value)
+            at += int(got.value)
+        if not fits:  # (more than the arenas hold: counted, then extracted into grown buffers)
+            sc = np.array([marked(q, 0, 0, 0) if len(ranges[q]) else 0 for q in range(G)], np.uint64)
+            ns = int(sc.sum())
+            sk = self.gen_bufs[0].get(8 * max(1, ns))
+            sp = self.gen_bufs[3].get(8 * max(1, ns)) if uniq else None
+            at = 0
+            for q in range(G):
+                want = int(sc[q])
+                if want and marked(q, sk.ptr + 8 * at, sp.ptr + 8 * at if uniq else 0, want) != want:
+                    raise RuntimeError("rank %d: rank %d's left-out k-mers changed between passes" % (me, q))
+                at += want
+        if uniq:
+            at = 0
+            for q in range(G):
+                if sc[q]:
+                    N.check(ctx, L.kman_or_u64(ctx, c_void_p(sp.ptr + 8 * at), int(sc[q]), me << RANK_SHIFT), "tag")
+                at += int(sc[q])
+        lap("extract")
+        sent = np.asarray((yield ("allgather", sc)), np.uint64).reshape(G, G)  # sent[src, dst]
+        rcnt = sent[:, me].copy()
+        roff = np.concatenate([[0], np.cumsum(rcnt)[:-1]]).astype(np.uint64)
+        so = np.concatenate([[0], np.cumsum(sc)[:-1]]).astype(np.uint64)
+        nr = int(rcnt.sum())
+        self.redone_kmers += nr
+        if vb == 4 and nr > 0xFFFFFFFF:
+            raise NotImplementedError("a redone key range of more than 2^32 k-mers would need u64 counts")
+        rk, ak = (self.gen_bufs[i].get(8 * max(1, nr)) for i in (1, 2))
+        rp = ap = None
+        if uniq:
+            rp, ap = (self.gen_bufs[i].get(8 * max(1, nr)) for i in (4, 5))
+        yield ("alltoallv", (sk.ptr, sc, so, rk.ptr, rcnt, roff, 8))
+        if uniq:
+            yield ("alltoallv", (sp.ptr, sc, so, rp.ptr, rcnt, roff, 8))
+        lap("exchange")
+        n_gen = 0
+        gk, gv = self.part_bufs[0].get(8 * max(1, nr)), self.part_bufs[1].get(vb * max(1, nr))
+        if nr:
+            res = c_int(0)
+            lo_bit = engine.split_bits(nr, 2 * k)
+            vbytes = 8 if uniq else 0
+            N.check(ctx, L.kman_sort_range(ctx, c_void_p(rk.ptr), c_void_p(ak.ptr), c_void_p(rp.ptr) if uniq else None,
+                                           c_void_p(ap.ptr) if uniq else None, vbytes, nr, lo_bit, 2 * k, None,
+                                           byref(res)), "kman_sort_range")
+            keys, alt = (ak, rk) if res.value else (rk, ak)
+            pos, palt = ((ap, rp) if res.value else (rp, ap)) if uniq else (None, None)
+            lap("sort")
+            out = c_uint64(0)
+            N.check(ctx, L.kman_finish(ctx, c_void_p(keys.ptr), c_void_p(alt.ptr), c_void_p(pos.ptr) if uniq else None,
+                                       c_void_p(palt.ptr) if uniq else None, vbytes, nr, 2 * k, lo_bit, self.fmode,
+                                       c_void_p(gk.ptr), c_void_p(gv.ptr), vb, byref(out)), "kman_finish")
+            n_gen = int(out.value)
+            lap("finish")
+        if n_gen:
+            # the region rows move to the (now free) round arenas, then the two
+            # sorted, key-disjoint runs merge back into place
+            N.check(ctx, L.kman_memcpy_d2d(ctx, c_void_p(A.ptr), c_void_p(ok_.ptr + 8 * n_out), 8 * n_region), "copy")
+            N.check(ctx, L.kman_memcpy_d2d(ctx, c_void_p(B.ptr), c_void_p(ov_.ptr + vb * n_out), vb * n_region),
+                    "copy")
+            runs = (N.Run * 2)(N.Run(c_void_p(A.ptr), c_void_p(B.ptr), n_region),
+                               N.Run(c_void_p(gk.ptr), c_void_p(gv.ptr), n_gen))
+            N.check(ctx, L.kman_merge_runs(ctx, runs, 2, vb, c_void_p(ok_.ptr + 8 * n_out),
+                                           c_void_p(ov_.ptr + vb * n_out), None, None), "kman_merge_runs")
+            lap("merge")
+        return n_region + n_gen
 
     def _vb(self, C) -> int:
         """Output value bytes: uniq pos are u64 (source rank in bits 56-63);
@@ -733,7 +903,8 @@ class DistPipeline:
         if self.comm is not None:
             self.comm.free()
             self.comm = None
-        for b in [self.d_hist, self.d_rtab, self.d_small, self.arena_a, self.arena_b, self.out_keys, self.out_vals] + self.gen_bufs:
+        for b in ([self.d_hist, self.d_rtab, self.d_small, self.arena_a, self.arena_b, self.out_keys, self.out_vals]
+                  + self.gen_bufs + self.part_bufs):
             b.free()
         if self.loader is not None:
             self.loader.free()
@@ -764,7 +935,8 @@ def local_groups(p: engine.Parsed, k: int, rc: bool, mode: str, canonical: bool 
         t2 = time.perf_counter()
         LAST_LOCAL.clear()
         LAST_LOCAL.update(setup_ms=(t1 - t0) * 1e3, step_ms=(t2 - t1) * 1e3, rounds=pipe.rounds,
-                          fallback_rounds=pipe.fallback_rounds, plan=getattr(pipe, "plan_info", None),
+                          fallback_rounds=pipe.fallback_rounds, partial_rounds=pipe.partial_rounds,
+                          redone_kmers=pipe.redone_kmers, plan=getattr(pipe, "plan_info", None),
                           phases_ms=dict(pipe.phase_ms))
         return pipe.take_result()
     finally:
