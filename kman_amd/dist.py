@@ -592,7 +592,8 @@ class DistPipeline:
         """The key ranges each rank's round finish left out (mine: this
         rank's), through the general path: every rank extracts the k-mers of
         each destination's ranges (kman_extract_marked), one exchange, then the
-        destination sorts (kman_sort_range) and groups (kman_finish) them and
+        destination sorts (kman_sort_range, every key bit) and groups them
+        (kman_rle_count / kman_rle_uniq) and
         merges the rows with its n_region region rows at ok_/ov_[n_out]
         (kman_merge_runs: the ranges are disjoint).  Generator; returns the
         rows now at n_out."""
@@ -704,19 +705,25 @@ class DistPipeline:
         n_gen = 0
         gk, gv = self.part_bufs[0].get(8 * max(1, nr)), self.part_bufs[1].get(vb * max(1, nr))
         if nr:
+            # a full-key sort, then run-length: these ranges are where keys
+            # repeat far beyond a region's share, so equal-prefix segments are
+            # huge (kman_finish would re-sort them through its big-segment
+            # path) while the sort's passes do not care
             res = c_int(0)
-            lo_bit = engine.split_bits(nr, 2 * k)
             vbytes = 8 if uniq else 0
             N.check(ctx, L.kman_sort_range(ctx, c_void_p(rk.ptr), c_void_p(ak.ptr), c_void_p(rp.ptr) if uniq else None,
-                                           c_void_p(ap.ptr) if uniq else None, vbytes, nr, lo_bit, 2 * k, None,
+                                           c_void_p(ap.ptr) if uniq else None, vbytes, nr, 0, 2 * k, None,
                                            byref(res)), "kman_sort_range")
-            keys, alt = (ak, rk) if res.value else (rk, ak)
-            pos, palt = ((ap, rp) if res.value else (rp, ap)) if uniq else (None, None)
+            keys = ak if res.value else rk
+            pos = (ap if res.value else rp) if uniq else None
             lap("sort")
             out = c_uint64(0)
-            N.check(ctx, L.kman_finish(ctx, c_void_p(keys.ptr), c_void_p(alt.ptr), c_void_p(pos.ptr) if uniq else None,
-                                       c_void_p(palt.ptr) if uniq else None, vbytes, nr, 2 * k, lo_bit, self.fmode,
-                                       c_void_p(gk.ptr), c_void_p(gv.ptr), vb, byref(out)), "kman_finish")
+            if uniq:
+                N.check(ctx, L.kman_rle_uniq(ctx, c_void_p(keys.ptr), c_void_p(pos.ptr), 8, nr, c_void_p(gk.ptr),
+                                             c_void_p(gv.ptr), byref(out)), "kman_rle_uniq")
+            else:
+                N.check(ctx, L.kman_rle_count(ctx, c_void_p(keys.ptr), nr, c_void_p(gk.ptr), c_void_p(gv.ptr), vb,
+                                              byref(out)), "kman_rle_count")
             n_gen = int(out.value)
             lap("finish")
         if n_gen:
@@ -725,6 +732,7 @@ class DistPipeline:
             N.check(ctx, L.kman_memcpy_d2d(ctx, c_void_p(A.ptr), c_void_p(ok_.ptr + 8 * n_out), 8 * n_region), "copy")
             N.check(ctx, L.kman_memcpy_d2d(ctx, c_void_p(B.ptr), c_void_p(ov_.ptr + vb * n_out), vb * n_region),
                     "copy")
+            lap("copy")
             runs = (N.Run * 2)(N.Run(c_void_p(A.ptr), c_void_p(B.ptr), n_region),
                                N.Run(c_void_p(gk.ptr), c_void_p(gv.ptr), n_gen))
             N.check(ctx, L.kman_merge_runs(ctx, runs, 2, vb, c_void_p(ok_.ptr + 8 * n_out),
