@@ -113,7 +113,11 @@ def pmc_traffic(kernel: str, mode: str, k: int, bases: int):
     meta = d.get("_meta", {})
     if meta.get("mode") != mode or meta.get("k") != k or meta.get("bases") != bases:
         return None
-    hits = [v for n, v in d.items() if n != "_meta" and n.startswith(kernel)]
+    # (summary names are rocprofv3's: "void rg_finish<2, unsigned int, true, false>")
+    def base(n):
+        return n.replace("void ", "", 1).split("<")[0].split("(")[0]
+
+    hits = [v for n, v in d.items() if n != "_meta" and base(n) == kernel]
     return max(hits, key=lambda v: v["launches"])["hbm_bytes_per_launch"] if hits else None
 
 
@@ -374,6 +378,7 @@ def run_dist(args, world: int, rank: int, local: int):
                        "fasta_bytes": lay.size, "kmers_per_step": total // max(args.steps, 1), "k": args.k,
                        "mode": args.mode, "parallelism": "dp%d: top-8-bit bucket parts + RCCL all-to-all" % world,
                        "path": pipe.path, "rounds": pipe.rounds, "fallback_rounds": pipe.fallback_rounds,
+                       "partial_rounds": pipe.partial_rounds,
                        "memory_plan": getattr(pipe, "plan_info", None),
                        "stages_ms_per_step_rank0": stages},
             "roofline": {"kernel": "rg_pass (pass 1 after the exchange, rank 0)", "bound": "hbm", "achieved": ach,
