@@ -225,6 +225,41 @@ KMAN_DEV void load_chunk(const uint8_t *text, uint64_t n, uint64_t pos, Chunk &c
     ch.hdr = hdr;
 }
 
+// The fast path alone (plain sequence text, a full chunk): false when the
+// chunk needs load_chunk (then its whole tile goes to the SLOW kernels).
+// Kept apart so the common kernels carry none of the general path's registers.
+KMAN_DEV bool load_chunk_fast(const uint8_t *text, uint64_t n, uint64_t pos, Chunk &ch) {
+    ch.cnt = pos < n ? (int)((n - pos) < (uint64_t)PB ? (n - pos) : (uint64_t)PB) : 0;
+    if (ch.cnt != PB) return false;
+    const uint4 *p = reinterpret_cast<const uint4 *>(text + pos);
+#pragma unroll
+    for (int v = 0; v < PB / 16; v++) {
+        const uint4 x = p[v];
+        ch.w[4 * v + 0] = x.x;
+        ch.w[4 * v + 1] = x.y;
+        ch.w[4 * v + 2] = x.z;
+        ch.w[4 * v + 3] = x.w;
+    }
+    const uint32_t prev = pos == 0 ? '\n' : text[pos - 1];
+    uint32_t spec = 0;
+    uint64_t nl = 0;
+#pragma unroll
+    for (int v = 0; v < PB / 4; v++) {
+        const uint32_t w = ch.w[v];
+        const uint32_t znl = eq_bytes(w, '\n');
+        const uint32_t lt21 = ~((w & 0x7f7f7f7fu) + 0x5f5f5f5fu) & ~w & 0x80808080u;
+        spec |= (lt21 & ~znl) | eq_bytes(w, '>');
+        nl |= (uint64_t)hibits4(znl) << (4 * v);
+    }
+    if (spec) return false;
+    const uint64_t ls0 = (prev == '\n' || (prev == '\r' && !(nl & 1ull))) ? 1ull : 0ull;
+    ch.ls = (nl << 1) | ls0;
+    ch.hls = 0;
+    ch.keep = ~nl;
+    ch.hdr = 0;
+    return true;
+}
+
 // content bytes that land in the cleaned sequence, per incoming state
 struct Emit {
     uint64_t lead;  // bytes before the first line start (kept iff incoming SEQ)
@@ -269,14 +304,26 @@ KMAN_DEV Xf chunk_xf(const Chunk &ch) {
     return x;
 }
 
-// (PT, 3): three waves per SIMD (168 VGPRs, a few spilled) instead of the two
-// that 179 VGPRs allow: 0.85 -> 0.69 ms per launch on 1 GB of text
+// Two variants over every tile: !SLOW handles the tiles of plain sequence
+// text (every chunk on the fast path) and flags the others (pad = 1); SLOW
+// handles only the flagged ones, with the general per-byte path ((PT, 3):
+// three waves per SIMD, 168 VGPRs, a few spilled).
+template <bool SLOW>
 __global__ __launch_bounds__(PT, 3) void parse_reduce(const uint8_t *__restrict__ text, uint64_t n,
                                                    Xf64 *__restrict__ tiles) {
     __shared__ Xf lds[PT / 64];
+    if (SLOW && tiles[blockIdx.x].pad == 0) return;  // (block-uniform) done by the fast variant
     const uint64_t pos = (uint64_t)blockIdx.x * PTILE + (uint64_t)threadIdx.x * PB;
     Chunk ch;
-    load_chunk(text, n, pos, ch);
+    if (SLOW) {
+        load_chunk(text, n, pos, ch);
+    } else {
+        const bool fast = load_chunk_fast(text, n, pos, ch);
+        if (__syncthreads_or(!fast)) {  // (block-uniform) a tile for the SLOW variant
+            if (threadIdx.x == 0) tiles[blockIdx.x].pad = 1;
+            return;
+        }
+    }
     Xf x = chunk_xf(ch);
     Xf id;
     id.outs = XF_ID_OUTS;
@@ -287,7 +334,7 @@ __global__ __launch_bounds__(PT, 3) void parse_reduce(const uint8_t *__restrict_
     if (threadIdx.x == 0) {
         Xf64 t;
         t.outs = tot.outs;
-        t.pad = 0;
+        t.pad = SLOW ? 1u : 0u;  // (keeps the flag for parse_emit)
         for (int s = 0; s < 3; s++) t.kept[s] = tot.kept[s];
         t.nhdr = tot.nhdr;
         tiles[blockIdx.x] = t;
@@ -340,15 +387,20 @@ __global__ __launch_bounds__(SCAN_T) void parse_scan_top(const Xf64 *__restrict_
     }
 }
 
+// the same split: tiles flagged by parse_reduce<false> (tiles[].pad) take SLOW
+template <bool SLOW>
 __global__ __launch_bounds__(PT, 3) void parse_emit(const uint8_t *__restrict__ text, uint64_t n,
+                                                 const Xf64 *__restrict__ tiles,
                                                  const Xf64 *__restrict__ local, const Xf64 *__restrict__ bpre,
                                                  uint8_t *__restrict__ codes, uint64_t code_off, uint32_t s0,
                                                  uint64_t *__restrict__ rec_hdr, uint64_t *__restrict__ rec_seq) {
     __shared__ Xf lds[PT / 64];
     __shared__ __attribute__((aligned(16))) uint8_t stage[PTILE + 32];
+    if ((tiles[blockIdx.x].pad != 0) != SLOW) return;  // (block-uniform) the other variant's tile
     const uint64_t pos = (uint64_t)blockIdx.x * PTILE + (uint64_t)threadIdx.x * PB;
     Chunk ch;
-    load_chunk(text, n, pos, ch);
+    if (SLOW) load_chunk(text, n, pos, ch);
+    else (void)load_chunk_fast(text, n, pos, ch);
     const Xf x = chunk_xf(ch);
     Xf id;
     id.outs = XF_ID_OUTS;
@@ -458,7 +510,9 @@ extern "C" int kman_parse_fasta_at(kman_ctx *ctx, const uint8_t *d_text, uint64_
     Xf64 *d_bpre = (Xf64 *)((char *)scr + 2 * xf_bytes + nb_bytes);
     uint64_t *d_info = (uint64_t *)((char *)scr + 2 * xf_bytes + 2 * nb_bytes);
     { KTimer kt_(ctx, "parse");
-    hipLaunchKernelGGL(parse_reduce, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf);
+    HIP_TRY(ctx, hipMemsetAsync(d_xf, 0, T * sizeof(Xf64), ctx->stream));  // (pad = 0: not flagged)
+    hipLaunchKernelGGL(parse_reduce<false>, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf);
+    hipLaunchKernelGGL(parse_reduce<true>, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf);
     hipLaunchKernelGGL(parse_scan_blocks, dim3((uint32_t)NB), dim3(SCAN_T), 0, ctx->stream, d_xf, T, d_local, d_btot);
     hipLaunchKernelGGL(parse_scan_top, dim3(1), dim3(SCAN_T), 0, ctx->stream, d_btot, NB, d_bpre, d_info, s0); }
     HIP_TRY(ctx, hipGetLastError());
@@ -471,8 +525,10 @@ extern "C" int kman_parse_fasta_at(kman_ctx *ctx, const uint8_t *d_text, uint64_
         return kman_fail(ctx, KMAN_ECAP, "record capacity %llu < %llu", (unsigned long long)rec_cap,
                          (unsigned long long)info->n_records);
     { KTimer kt_(ctx, "parse");
-    hipLaunchKernelGGL(parse_emit, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_local, d_bpre, d_codes,
-                       code_off, s0, d_rec_hdr, d_rec_seq);
+    hipLaunchKernelGGL(parse_emit<false>, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf, d_local,
+                       d_bpre, d_codes, code_off, s0, d_rec_hdr, d_rec_seq);
+    hipLaunchKernelGGL(parse_emit<true>, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf, d_local,
+                       d_bpre, d_codes, code_off, s0, d_rec_hdr, d_rec_seq);
     const uint64_t R = info->n_records;
     if (R)
         hipLaunchKernelGGL(mark_records, dim3((uint32_t)ceil_div(R, 256)), dim3(256), 0, ctx->stream, d_codes,
