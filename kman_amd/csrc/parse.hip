@@ -304,23 +304,28 @@ KMAN_DEV Xf chunk_xf(const Chunk &ch) {
     return x;
 }
 
-// Two variants over every tile: !SLOW handles the tiles of plain sequence
-// text (every chunk on the fast path) and flags the others (pad = 1); SLOW
-// handles only the flagged ones, with the general per-byte path ((PT, 3):
-// three waves per SIMD, 168 VGPRs, a few spilled).
+// Two variants: !SLOW, one block per tile, handles the tiles of plain
+// sequence text (every chunk on the fast path) and lists the others (pad = 1,
+// slow[1 + i]; slow[0] = how many); SLOW walks only that list with the general
+// per-byte path ((PT, 3): three waves per SIMD, 168 VGPRs, a few spilled).
 template <bool SLOW>
 __global__ __launch_bounds__(PT, 3) void parse_reduce(const uint8_t *__restrict__ text, uint64_t n,
-                                                   Xf64 *__restrict__ tiles) {
+                                                   Xf64 *__restrict__ tiles, uint32_t *__restrict__ slow) {
     __shared__ Xf lds[PT / 64];
-    if (SLOW && tiles[blockIdx.x].pad == 0) return;  // (block-uniform) done by the fast variant
-    const uint64_t pos = (uint64_t)blockIdx.x * PTILE + (uint64_t)threadIdx.x * PB;
+    const uint32_t nit = SLOW ? slow[0] : 1u;
+    for (uint32_t it = SLOW ? blockIdx.x : 0u; it < nit; it += SLOW ? gridDim.x : 1u) {
+    const uint32_t tb = SLOW ? slow[1 + it] : blockIdx.x;
+    const uint64_t pos = (uint64_t)tb * PTILE + (uint64_t)threadIdx.x * PB;
     Chunk ch;
     if (SLOW) {
         load_chunk(text, n, pos, ch);
     } else {
         const bool fast = load_chunk_fast(text, n, pos, ch);
         if (__syncthreads_or(!fast)) {  // (block-uniform) a tile for the SLOW variant
-            if (threadIdx.x == 0) tiles[blockIdx.x].pad = 1;
+            if (threadIdx.x == 0) {
+                tiles[tb].pad = 1;
+                slow[1 + atomicAdd(&slow[0], 1u)] = tb;
+            }
             return;
         }
     }
@@ -337,7 +342,9 @@ __global__ __launch_bounds__(PT, 3) void parse_reduce(const uint8_t *__restrict_
         t.pad = SLOW ? 1u : 0u;  // (keeps the flag for parse_emit)
         for (int s = 0; s < 3; s++) t.kept[s] = tot.kept[s];
         t.nhdr = tot.nhdr;
-        tiles[blockIdx.x] = t;
+        tiles[tb] = t;
+    }
+    __syncthreads();  // (lds is the next listed tile's)
     }
 }
 
@@ -387,17 +394,20 @@ __global__ __launch_bounds__(SCAN_T) void parse_scan_top(const Xf64 *__restrict_
     }
 }
 
-// the same split: tiles flagged by parse_reduce<false> (tiles[].pad) take SLOW
+// the same split: the tiles parse_reduce<false> listed take SLOW
 template <bool SLOW>
 __global__ __launch_bounds__(PT, 3) void parse_emit(const uint8_t *__restrict__ text, uint64_t n,
-                                                 const Xf64 *__restrict__ tiles,
+                                                 const Xf64 *__restrict__ tiles, const uint32_t *__restrict__ slow,
                                                  const Xf64 *__restrict__ local, const Xf64 *__restrict__ bpre,
                                                  uint8_t *__restrict__ codes, uint64_t code_off, uint32_t s0,
                                                  uint64_t *__restrict__ rec_hdr, uint64_t *__restrict__ rec_seq) {
     __shared__ Xf lds[PT / 64];
     __shared__ __attribute__((aligned(16))) uint8_t stage[PTILE + 32];
-    if ((tiles[blockIdx.x].pad != 0) != SLOW) return;  // (block-uniform) the other variant's tile
-    const uint64_t pos = (uint64_t)blockIdx.x * PTILE + (uint64_t)threadIdx.x * PB;
+    const uint32_t nit = SLOW ? slow[0] : 1u;
+    for (uint32_t it = SLOW ? blockIdx.x : 0u; it < nit; it += SLOW ? gridDim.x : 1u) {
+    const uint32_t tb = SLOW ? slow[1 + it] : blockIdx.x;
+    if (!SLOW && tiles[tb].pad != 0) return;  // (block-uniform) a listed tile
+    const uint64_t pos = (uint64_t)tb * PTILE + (uint64_t)threadIdx.x * PB;
     Chunk ch;
     if (SLOW) load_chunk(text, n, pos, ch);
     else (void)load_chunk_fast(text, n, pos, ch);
@@ -411,7 +421,7 @@ __global__ __launch_bounds__(PT, 3) void parse_emit(const uint8_t *__restrict__ 
     // the concrete state entering this tile: the file prefix applied to PRE
     TileIn ti;
     {
-        const Xf64 p = ComposeXf64()(bpre[blockIdx.x / SCAN_T], local[blockIdx.x]);
+        const Xf64 p = ComposeXf64()(bpre[tb / SCAN_T], local[tb]);
         ti.state = xf_out(p.outs, s0);
         ti.kept = s0 == S_PRE ? p.kept[S_PRE] : p.kept[S_SEQ];
         ti.nhdr = p.nhdr;
@@ -438,7 +448,41 @@ __global__ __launch_bounds__(PT, 3) void parse_emit(const uint8_t *__restrict__ 
 #pragma unroll
     for (int v = 0; v < PB / 4; v++) cw[v] = codes4(ch.w[v]);
     uint32_t lk = al + lk0;
-    if (em == ~0ull) {
+    if (!SLOW && __popcll(~em) <= 8) {
+        // the chunk's kept codes compacted in registers (each dropped byte --
+        // a newline, mostly -- shifts the bytes above it down), then written
+        // as whole LDS words, bytewise only where a word is shared with the
+        // neighbouring chunks: 17 word stores instead of 64 byte stores
+        // whose lanes, 64 bytes apart, all hit a few banks
+        uint64_t rmv = ~em;
+        while (rmv) {
+            const int p = 63 - __clzll((unsigned long long)rmv);
+            rmv &= ~(1ull << p);
+            const int q = p >> 2;
+            const uint32_t lowm = (1u << (8 * (p & 3))) - 1u;
+#pragma unroll
+            for (int i = 0; i < PB / 4; i++) {
+                const uint32_t nxt = i + 1 < PB / 4 ? cw[i + 1] : 0u;
+                const uint32_t sh = (cw[i] >> 8) | (nxt << 24);
+                cw[i] = i < q ? cw[i] : (i == q ? ((cw[i] & lowm) | (sh & ~lowm)) : sh);
+            }
+        }
+        const uint32_t e = lk + (uint32_t)__popcll(em), sa = lk & 3u, a0 = lk >> 2;
+        uint32_t *st32 = reinterpret_cast<uint32_t *>(stage);
+#pragma unroll
+        for (int j = 0; j <= PB / 4; j++) {
+            const uint32_t lo = j ? cw[j - 1] : 0u, hi = j < PB / 4 ? cw[j] : 0u;
+            const uint32_t word = sa ? ((hi << (8 * sa)) | (lo >> (32 - 8 * sa))) : hi;
+            const uint32_t wb = 4 * (a0 + (uint32_t)j);
+            const uint32_t b0 = wb > lk ? wb : lk, b1 = wb + 4 < e ? wb + 4 : e;
+            if (b0 >= b1) continue;
+            if (b0 == wb && b1 == wb + 4) {
+                st32[a0 + j] = word;
+            } else {
+                for (uint32_t b = b0; b < b1; b++) stage[b] = (uint8_t)(word >> (8 * (b - wb)));
+            }
+        }
+    } else if (em == ~0ull) {
 #pragma unroll
         for (int i = 0; i < PB; i++) stage[lk + i] = (uint8_t)byte_at(cw, i);
     } else {
@@ -461,6 +505,8 @@ __global__ __launch_bounds__(PT, 3) void parse_emit(const uint8_t *__restrict__ 
             for (uint32_t b = b0; b < b0 + 16; b++)
                 if (b >= al && b < end) dst[b] = stage[b];
         }
+    }
+    __syncthreads();  // (lds and stage are the next listed tile's)
     }
 }
 
@@ -503,16 +549,20 @@ extern "C" int kman_parse_fasta_at(kman_ctx *ctx, const uint8_t *d_text, uint64_
     const size_t xf_bytes = ((T * sizeof(Xf64)) + 255) & ~size_t(255);
     const size_t nb_bytes = ((NB * sizeof(Xf64)) + 255) & ~size_t(255);
     void *scr;
-    KMAN_TRY(kman_scratch(ctx, 2 * xf_bytes + 2 * nb_bytes + 256, &scr));
+    const size_t sl_bytes = ((4 * (T + 1)) + 255) & ~size_t(255);
+    KMAN_TRY(kman_scratch(ctx, 2 * xf_bytes + 2 * nb_bytes + 256 + sl_bytes, &scr));
     Xf64 *d_xf = (Xf64 *)scr;
     Xf64 *d_local = (Xf64 *)((char *)scr + xf_bytes);
     Xf64 *d_btot = (Xf64 *)((char *)scr + 2 * xf_bytes);
     Xf64 *d_bpre = (Xf64 *)((char *)scr + 2 * xf_bytes + nb_bytes);
     uint64_t *d_info = (uint64_t *)((char *)scr + 2 * xf_bytes + 2 * nb_bytes);
+    uint32_t *d_slow = (uint32_t *)((char *)scr + 2 * xf_bytes + 2 * nb_bytes + 256);  // [count, tiles...]
+    const uint32_t gslow = (uint32_t)(T < 2048 ? T : 2048);  // (blocks walking the listed tiles)
     { KTimer kt_(ctx, "parse");
-    HIP_TRY(ctx, hipMemsetAsync(d_xf, 0, T * sizeof(Xf64), ctx->stream));  // (pad = 0: not flagged)
-    hipLaunchKernelGGL(parse_reduce<false>, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf);
-    hipLaunchKernelGGL(parse_reduce<true>, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf);
+    HIP_TRY(ctx, hipMemsetAsync(d_xf, 0, T * sizeof(Xf64), ctx->stream));  // (pad = 0: not listed)
+    HIP_TRY(ctx, hipMemsetAsync(d_slow, 0, 4, ctx->stream));
+    hipLaunchKernelGGL(parse_reduce<false>, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf, d_slow);
+    hipLaunchKernelGGL(parse_reduce<true>, dim3(gslow), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf, d_slow);
     hipLaunchKernelGGL(parse_scan_blocks, dim3((uint32_t)NB), dim3(SCAN_T), 0, ctx->stream, d_xf, T, d_local, d_btot);
     hipLaunchKernelGGL(parse_scan_top, dim3(1), dim3(SCAN_T), 0, ctx->stream, d_btot, NB, d_bpre, d_info, s0); }
     HIP_TRY(ctx, hipGetLastError());
@@ -525,10 +575,10 @@ extern "C" int kman_parse_fasta_at(kman_ctx *ctx, const uint8_t *d_text, uint64_
         return kman_fail(ctx, KMAN_ECAP, "record capacity %llu < %llu", (unsigned long long)rec_cap,
                          (unsigned long long)info->n_records);
     { KTimer kt_(ctx, "parse");
-    hipLaunchKernelGGL(parse_emit<false>, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf, d_local,
-                       d_bpre, d_codes, code_off, s0, d_rec_hdr, d_rec_seq);
-    hipLaunchKernelGGL(parse_emit<true>, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf, d_local,
-                       d_bpre, d_codes, code_off, s0, d_rec_hdr, d_rec_seq);
+    hipLaunchKernelGGL(parse_emit<false>, dim3((uint32_t)T), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf, d_slow,
+                       d_local, d_bpre, d_codes, code_off, s0, d_rec_hdr, d_rec_seq);
+    hipLaunchKernelGGL(parse_emit<true>, dim3(gslow), dim3(PT), 0, ctx->stream, d_text, n_bytes, d_xf, d_slow,
+                       d_local, d_bpre, d_codes, code_off, s0, d_rec_hdr, d_rec_seq);
     const uint64_t R = info->n_records;
     if (R)
         hipLaunchKernelGGL(mark_records, dim3((uint32_t)ceil_div(R, 256)), dim3(256), 0, ctx->stream, d_codes,

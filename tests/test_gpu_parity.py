@@ -49,6 +49,36 @@ def _messy(seed):
     return inputs.messy_records(seed, n_records=60, max_len=20000)
 
 
+@pytest.mark.parametrize("width", [1, 3, 4, 7, 8, 13, 31, 60, 63, 64, 65, 80, 127, 1000])
+def test_parse_fast_tiles_match_oracle(dev, width):
+    """Plain sequence text (the fast parse kernels: newline bytes dropped by
+    in-register compaction, whole-word LDS staging) at every line width
+    around the 4-byte words and 64-byte chunks, upper / lower case and N runs,
+    records long enough that most 16 KiB tiles hold no header."""
+    import np_oracle
+    from kman_amd import engine
+
+    rng = np.random.default_rng(width)
+    parts = []
+    for r in range(5):
+        n = int(rng.integers(20_000, 90_000))
+        seq = rng.choice(np.frombuffer(b"ACGTacgtN", np.uint8), n, p=[.24, .24, .24, .24, .01, .01, .01, .005, .005])
+        body = seq.tobytes()
+        lines = [body[i:i + width] for i in range(0, n, width)]
+        parts.append(b">rec%d some description\n" % r + b"\n".join(lines) + b"\n")
+    text = b"".join(parts)
+    recs = np_oracle.parse_fasta(text)
+    codes_ref, rec_seq_ref = np_oracle.codes_of(recs)
+    p = engine.parse(dev, text)
+    try:
+        assert p.n_records == len(recs) and p.n_bases == len(codes_ref)
+        got = dev.download(p.codes, p.n_bases + 64, np.uint8)
+        np.testing.assert_array_equal(got[: p.n_bases], codes_ref)
+        np.testing.assert_array_equal(p.rec_seq, rec_seq_ref)
+    finally:
+        p.free()
+
+
 @pytest.mark.parametrize("idx", range(len(WEIRD) + 3))
 def test_parse_matches_oracle(dev, golden_inputs, idx):
     import np_oracle
