@@ -124,6 +124,36 @@ def round_sizes(C: np.ndarray, cuts: np.ndarray, G: int, R: int):
     return send, recv
 
 
+def gather_ranges(cnt: np.ndarray, allr: np.ndarray, G: int) -> List[np.ndarray]:
+    """Each destination's left-out [lo, hi] key ranges from the all-gathered
+    range counts (cnt[q]) and zero-padded range arrays (allr[q])."""
+    cnt = np.asarray(cnt, np.uint64).reshape(G)
+    allr = np.asarray(allr, np.uint64).reshape(G, -1)
+    return [allr[q, :2 * int(cnt[q])].reshape(-1, 2) for q in range(G)]
+
+
+def redo_map(ranges: List[np.ndarray], key_bits: int, max_bits: int = 24) -> Tuple[int, np.ndarray]:
+    """(pbits, map): map[p] = q + 1 when the keys with top pbits bits p lie in
+    one of destination q's left-out ranges (0 elsewhere); pbits is the
+    coarsest prefix length at which every range is whole."""
+    K = key_bits
+    pbits = 1
+    for rq in ranges:
+        for lo, hi in rq:
+            lo, end = int(lo), int(hi) + 1
+            a = (lo & -lo).bit_length() - 1 if lo else K
+            b = (end & -end).bit_length() - 1 if end < (1 << K) else K
+            pbits = max(pbits, K - min(a, b))
+    if pbits > max_bits:
+        raise NotImplementedError("left-out key ranges finer than %d key bits" % max_bits)
+    sh = K - pbits
+    pmap = np.zeros(1 << pbits, np.uint8)
+    for q, rq in enumerate(ranges):
+        for lo, hi in rq:
+            pmap[int(lo) >> sh:(int(hi) >> sh) + 1] = q + 1
+    return pbits, pmap
+
+
 def _u64p(a: np.ndarray):
     return a.ctypes.data_as(c_void_p)
 
@@ -614,25 +644,11 @@ class DistPipeline:
         m = max(1, int(cnt.max()))
         pad = np.zeros(2 * m, np.uint64)
         pad[:2 * len(mine)] = np.asarray(mine, np.uint64).reshape(-1)
-        allr = np.asarray((yield ("allgather", pad)), np.uint64).reshape(G, 2 * m)
-        ranges = [allr[q, :2 * int(cnt[q])].reshape(-1, 2) for q in range(G)]
-        # destination map over key prefixes (map[p] = q + 1: prefix p is in
-        # one of q's ranges), so each destination's k-mers come out in one
-        # pass (kman_extract_marked) however many ranges it has
-        K = 2 * k
-        pbits = 1
-        for q in range(G):
-            for lo, hi in ranges[q]:
-                lo, end = int(lo), int(hi) + 1
-                s_ = min((lo & -lo).bit_length() - 1 if lo else K, (end & -end).bit_length() - 1 if end < (1 << K) else K)
-                pbits = max(pbits, K - s_)
-        if pbits > 24:
-            raise NotImplementedError("left-out key ranges finer than 24 key bits")
-        sh_ = K - pbits
-        pmap = np.zeros(1 << pbits, np.uint8)
-        for q in range(G):
-            for lo, hi in ranges[q]:
-                pmap[int(lo) >> sh_:(int(hi) >> sh_) + 1] = q + 1
+        allr = yield ("allgather", pad)
+        ranges = gather_ranges(cnt, allr, G)
+        # destination map over key prefixes, so each destination's k-mers
+        # come out in one pass (kman_extract_marked) however many ranges it has
+        pbits, pmap = redo_map(ranges, 2 * k)
         d_map = self.part_bufs[2].get(len(pmap))
         dev.upload(d_map, pmap)
         flags = engine.flags_for(self.rc, uniq, self.canonical)
@@ -1001,10 +1017,12 @@ def rehearse(keys: np.ndarray, k: int, world: int, rank: int, comm, n_bases_q: i
     RoundPlanner, per round the items of the round's buckets sent
     destination-major as round_send lays them out, one all-to-all, the finish
     by numpy; `fail` = {(rank, round)} raises a region overflow there, agreed
-    by an all-reduce exactly like the device path (the round is then redone as
-    a general round: the same keys by key range).  comm: allgather(a) ->
-    flat array, allreduce(a), alltoallv(list) -> list.  Returns (keys,
-    counts, R, cuts, rounds_redone)."""
+    by an all-reduce exactly like the device path: that rank's first bucket of
+    the round is left out of its rows (as KMAN_EPARTIAL leaves overflowing
+    regions out), the ranges all-gathered, every rank sends each destination
+    its k-mers under redo_map, the destination merges them in (the device
+    path's _redo_ranges).  comm: allgather(a) -> flat array, allreduce(a),
+    alltoallv(list) -> list.  Returns (keys, counts, R, cuts, rounds_redone)."""
     shift = max(0, 2 * k - 8)
     keys = np.asarray(keys, dtype=np.uint64)
     b = (keys >> np.uint64(shift)).astype(np.int64)
@@ -1024,21 +1042,29 @@ def rehearse(keys: np.ndarray, k: int, world: int, rank: int, comm, n_bases_q: i
         got = comm.alltoallv(parts)
         _, _, _, rc, _ = round_recv(C, cuts, R, rank, r)
         assert [len(g) for g in got] == rc.tolist(), "receive sizes disagree with the all-gathered counts"
-        f = comm.allreduce(np.array([1 if (rank, r) in fail else 0], np.uint64))
-        if int(f[0]):
-            redone.append(r)
-            # general round: destination q gets the key range of part (q, r)
-            parts = []
-            for q in range(world):
-                ql, qh = part_of(cuts, R, q, r)
-                sel = (keys >= np.uint64(ql << shift)) & (keys < np.uint64(qh << shift)) if qh > ql else np.zeros(
-                    len(keys), bool)
-                if qh == NB and qh > ql:
-                    sel = keys >= np.uint64(ql << shift)
-                parts.append(keys[sel])
-            got = comm.alltoallv(parts)
         rk = np.sort(np.concatenate(got)) if got else np.zeros(0, np.uint64)
+        mine = np.zeros((0, 2), np.uint64)
+        if (rank, r) in fail:
+            ql, qh = part_of(cuts, R, rank, r)
+            if qh > ql:  # the part's first bucket overflowed
+                mine = np.array([[ql << shift, ((ql + 1) << shift) - 1]], np.uint64)
+        for lo, hi in mine:  # its rows are left out
+            rk = rk[(rk < lo) | (rk > hi)]
         u, c = np.unique(rk, return_counts=True)
+        f = comm.allreduce(np.array([0, len(mine)], np.uint64))
+        if int(f[1]):
+            redone.append(r)
+            cnt = comm.allgather(np.array([len(mine)], np.uint64))
+            m = max(1, int(np.asarray(cnt).max()))
+            pad = np.zeros(2 * m, np.uint64)
+            pad[:2 * len(mine)] = mine.reshape(-1)
+            ranges = gather_ranges(cnt, comm.allgather(pad), world)
+            pbits, pmap = redo_map(ranges, 2 * k)
+            dest = pmap[(keys >> np.uint64(2 * k - pbits)).astype(np.int64)].astype(np.int64) - 1
+            got = comm.alltoallv([keys[dest == q] for q in range(world)])
+            gk, gc = np.unique(np.concatenate(got) if got else np.zeros(0, np.uint64), return_counts=True)
+            o = np.argsort(np.concatenate([u, gk]), kind="stable")  # key-disjoint runs merged
+            u, c = np.concatenate([u, gk])[o], np.concatenate([c, gc])[o]
         outk.append(u)
         outc.append(c.astype(np.uint64))
     return (np.concatenate(outk) if outk else np.zeros(0, np.uint64),
