@@ -99,7 +99,9 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 // region (b, s) is written at rtab[b * RS + s] (exact sizes from rg_hist, in
 // cnt0, which is then read-only); buckets with rtab == ~0 are not kept this
 // round, and their windows are dropped before the rank (keep bitmap).
-template <int EI, bool RC, bool ATOMIC, bool CANON = false, bool BR = false, bool EX = false>
+// NS: position segments (look-back chains); RS for the shard path (EX), more
+// for kman_groups (shorter chains, pass 1 finds segments in an LDS table)
+template <int EI, bool RC, bool ATOMIC, bool CANON = false, bool BR = false, bool EX = false, int NS = RS>
 __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI == 8 ? 8 : 4)))) void rg_extract(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
                                                  uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
                                                  uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ cnt0,
@@ -122,7 +124,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     __shared__ uint32_t keep[EX ? RADIX / 32 : 1];
 
     const uint32_t cid = (uint32_t)grab_tile(counter, &lds_tile);
-    const uint32_t sgi = cid % RS, jj = cid / RS;
+    const uint32_t sgi = cid % NS, jj = cid / NS;
     const uint32_t t0 = sgi * seg_tiles;
     const uint32_t t1 = t0 + seg_tiles < n_tiles ? t0 + seg_tiles : n_tiles;
     if (t0 + jj >= t1) return;  // (block-uniform) past a segment's end
@@ -257,7 +259,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
                 } else {
                     gexcl[d] = excl;
                     if (incl > C0) atomicOr(err, ERR_REGION);
-                    if (tile == (int64_t)t1 - 1) cnt0[d * RS + sgi] = (uint32_t)(incl < C0 ? incl : C0);
+                    if (tile == (int64_t)t1 - 1) cnt0[d * NS + sgi] = (uint32_t)(incl < C0 ? incl : C0);
                 }
             }
         }
@@ -282,7 +284,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
             if (EX) {
                 if (gexcl[d] != ~0ull) out[at] = v;
             } else if (at < C0) {
-                out[((uint64_t)d * RS + sgi) * C0 + at] = v;
+                out[((uint64_t)d * NS + sgi) * C0 + at] = v;
             }
         }
     }
@@ -1186,8 +1188,13 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
         else p.ei = ei == 16 ? 16u : (ei == 8 && !p.canon ? 8u : 12u);
         const uint64_t win = (uint64_t)RT * p.ei;
         p.n_tiles0 = (uint32_t)ceil_div(n_bases, win);
-        p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, RS);
-        p.S = RS;
+        // RS = 64 look-back chains (KMAN_RG_NS=128 / 256: shorter chains, A/B
+        // only -- rg_extract 3.80-3.93 ms either way, and rg_pass finding its
+        // segments in an LDS table is slower: 3.71-3.82 vs 3.46-3.55 ms)
+        const char *e2 = getenv("KMAN_RG_NS");
+        const uint32_t ns = e2 && (atoi(e2) == 128 || atoi(e2) == 256) ? (uint32_t)atoi(e2) : (uint32_t)RS;
+        p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, ns);
+        p.S = ns;
     }
     const uint64_t e0 = p.W / ((uint64_t)RADIX * p.S);
     // (owned chains are longer than the look-back segments of small inputs:
@@ -1338,15 +1345,25 @@ int run_finish(kman_ctx *ctx, const FinishArgs &f, int mode, uint64_t *okeys, vo
     return KMAN_OK;
 }
 
+template <int EI, bool RC, bool CANON, int NS>
+void launch_extract_ns(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
+                       uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
+    hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS>), dim3(NS * p.seg_tiles), dim3(RT), 0,
+                       ctx->stream, codes, n_bases, (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status,
+                       counter, epoch, ctx->d_err, dbg, stp);
+}
+
 template <int EI, bool RC, bool CANON = false>
 void launch_extract(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                     uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     const uint32_t grid = RS * p.seg_tiles;
-    const char *e = getenv("KMAN_RG_EXTRACT");  // 1 (default): block-wide rank; 0: stable per-wave rank
-    if (!e || atoi(e) != 0)
-        hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true>), dim3(grid), dim3(RT), 0, ctx->stream, codes,
-                           n_bases, (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch,
-                           ctx->d_err, dbg, stp);
+    const char *e = getenv("KMAN_RG_EXTRACT");  // 1 (default): block-wide rank; 0: stable per-wave rank (RS chains)
+    if (p.S == 256)
+        launch_extract_ns<EI, RC, CANON, 256>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
+    else if (p.S == 128)
+        launch_extract_ns<EI, RC, CANON, 128>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
+    else if (!e || atoi(e) != 0)
+        launch_extract_ns<EI, RC, CANON, RS>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
     else if (ctx->lds_atomic_ordered)
         hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON>), dim3(grid), dim3(RT), 0, ctx->stream, codes, n_bases,
                            (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch,
