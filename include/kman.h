@@ -359,6 +359,25 @@ int kman_merge_runs(kman_ctx *ctx, const kman_run *runs, int nruns, uint32_t val
                     void *d_ovals, uint64_t *d_tmp_keys, void *d_tmp_vals);
 int kman_count_descents(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint64_t *descents);
 
+/* Abundance vectors, KJoiner VEC_COUNT / VEC_COUNT_MASKED (join.py:288-335 ->
+ * AbundanceVector.add_count, abundance.py:103-130; the reference's base-class
+ * call raises NotImplementedError, so these are its evident semantics): over
+ * a key-sorted, stream-stable array with pos payloads ((window << 1) | strand,
+ * tagged with the source in bits 56-63 when `tagged`), write d_vec[index] =
+ * the size of the item's key run (masked = 0), or (masked = 1) the run's
+ * items in other records, only when the run spans several records.  index =
+ * pos, or src_base[pos >> 56] + (pos & (2^56 - 1)) when tagged.  Masked:
+ * rec_start (nrec ascending, index space) and rec_id (the record identity,
+ * one per distinct name) give each item's record.  d_vec (u32) is zeroed by
+ * the caller; entries never written stay 0. */
+int kman_vec_fill(kman_ctx *ctx, const uint64_t *d_keys, const void *d_pos, uint32_t pos_bytes, uint64_t n,
+                  int masked, const uint64_t *d_src_base, uint32_t tagged, const uint64_t *d_rec_start,
+                  const uint32_t *d_rec_id, uint64_t nrec, uint32_t *d_vec);
+/* Host: one vector as text, "%d\n" per entry v[0], v[stride], .. (n entries;
+ * AbundanceVector.write_to, abundance.py:151-168); out NULL: size only. */
+int kman_format_vector(const uint32_t *v, uint64_t n, uint64_t stride, char *out, size_t cap, size_t *used,
+                       int threads);
+
 /* Keys that occur exactly once, with their payload (join.py:244-263). */
 int kman_rle_uniq(kman_ctx *ctx, const uint64_t *d_keys, const void *d_vals, uint32_t val_bytes,
                   uint64_t n, uint64_t *d_okeys, void *d_ovals, uint64_t *n_out);

@@ -196,6 +196,12 @@ SIGNATURES = {
     ),
     "kman_merge_runs": (c_int, [c_void_p, c_void_p, c_int, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kman_count_descents": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
+    "kman_format_vector": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p, c_size_t, POINTER(c_size_t), c_int]),
+    "kman_vec_fill": (
+        c_int,
+        [c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_int, c_void_p, c_uint32, c_void_p, c_void_p, c_uint64,
+         c_void_p],
+    ),
     "kman_rebase_pos": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_uint32]),
     "kman_synth_fasta": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32]),
     "kman_copy_h2d_async": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int]),

@@ -156,6 +156,20 @@ extern "C" int kman_format_count(const uint64_t *ukeys, const void *counts, uint
     return run_sliced(n, out, cap, used, threads, size_of, write_at);
 }
 
+// one abundance vector as text, "%d\n" per entry (AbundanceVector.write_to,
+// abundance.py:151-168, after its "# k=%d" line): entries v[0], v[stride], ..
+extern "C" int kman_format_vector(const uint32_t *v, uint64_t n, uint64_t stride, char *out, size_t cap,
+                                  size_t *used, int threads) {
+    if (!used || (n && !v) || stride == 0) return KMAN_EINVAL;
+    auto size_of = [&](uint64_t i) -> size_t { return ndigits(v[i * stride]) + 1; };
+    auto write_at = [&](uint64_t i, char *p) -> char * {
+        p = put_u64(p, v[i * stride]);
+        *p++ = '\n';
+        return p;
+    };
+    return run_sliced(n, out, cap, used, threads, size_of, write_at);
+}
+
 extern "C" int kman_format_uniq(const uint64_t *keys, const void *pos, uint32_t pos_bytes, uint64_t n, uint32_t k,
                                 const char *names, const uint64_t *name_off, const uint64_t *rec_seq,
                                 uint64_t n_records, char *out, size_t cap, size_t *used, int threads) {

@@ -480,6 +480,120 @@ __global__ __launch_bounds__(256) void descents_kernel(const uint64_t *__restric
 
 }  // namespace
 
+// ================================================================ vectors
+// VEC_COUNT / VEC_COUNT_MASKED (KJoiner.join_vector_count[_masked],
+// kmermaid/join.py:288-335 -> AbundanceVector.add_count, abundance.py:103-130):
+// one thread per item of a key-sorted, stream-stable array; its key run (and,
+// MASKED, the sub-run of its record) found by galloping + binary search, so
+// runs of any length cost O(log run) per item.
+namespace {
+
+template <typename F>
+KMAN_DEV uint64_t run_first(uint64_t i, F same) {  // smallest j <= i with same(j) (same: an interval around i)
+    uint64_t good = i, step = 1;
+    int64_t bad = -1;
+    for (;;) {
+        if (good < step) break;
+        const uint64_t c = good - step;
+        if (same(c)) {
+            good = c;
+            step <<= 1;
+        } else {
+            bad = (int64_t)c;
+            break;
+        }
+    }
+    while ((int64_t)good - bad > 1) {
+        const uint64_t mid = (uint64_t)((bad + (int64_t)good) / 2);
+        if (same(mid)) good = mid;
+        else bad = (int64_t)mid;
+    }
+    return good;
+}
+
+template <typename F>
+KMAN_DEV uint64_t run_last(uint64_t i, uint64_t n, F same) {  // largest j >= i with same(j)
+    uint64_t good = i, step = 1, bad = n;
+    for (;;) {
+        if (good + step >= n) break;
+        const uint64_t c = good + step;
+        if (same(c)) {
+            good = c;
+            step <<= 1;
+        } else {
+            bad = c;
+            break;
+        }
+    }
+    while (bad - good > 1) {
+        const uint64_t mid = good + (bad - good) / 2;
+        if (same(mid)) good = mid;
+        else bad = mid;
+    }
+    return good;
+}
+
+template <typename P>
+__global__ __launch_bounds__(256) void vec_fill_kernel(const uint64_t *__restrict__ keys, const P *__restrict__ pos,
+                                                       uint64_t n, int masked, const uint64_t *__restrict__ src_base,
+                                                       uint32_t tagged, const uint64_t *__restrict__ rec_start,
+                                                       const uint32_t *__restrict__ rec_id, uint64_t nrec,
+                                                       uint32_t *__restrict__ vec) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    auto index = [&](uint64_t j) -> uint64_t {
+        const uint64_t p = (uint64_t)pos[j];
+        return tagged ? src_base[p >> 56] + (p & ((1ull << 56) - 1)) : p;
+    };
+    auto record = [&](uint64_t j) -> uint32_t {  // the record identity of item j (last rec_start <= index)
+        const uint64_t x = index(j);
+        uint64_t lo = 0, hi = nrec;  // first rec_start > x
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (rec_start[mid] <= x) lo = mid + 1;
+            else hi = mid;
+        }
+        return rec_id[lo ? lo - 1 : 0];
+    };
+    const uint64_t key = keys[i];
+    auto same_key = [&](uint64_t j) { return keys[j] == key; };
+    const uint64_t a = run_first(i, same_key), b = run_last(i, n, same_key);
+    const uint64_t cnt = b - a + 1;
+    uint64_t v = cnt;
+    if (masked) {
+        // occurrences in other records (the run's records are contiguous:
+        // stream order inside the run); nothing when it has one record only
+        const uint32_t me = record(i);
+        auto same_rec = [&](uint64_t j) { return keys[j] == key && record(j) == me; };
+        const uint64_t sa = run_first(i, same_rec), sb = run_last(i, n, same_rec);
+        v = cnt - (sb - sa + 1);
+        if (v == 0) return;
+    }
+    vec[index(i)] = (uint32_t)(v < 0xffffffffull ? v : 0xffffffffull);
+}
+
+}  // namespace
+
+extern "C" int kman_vec_fill(kman_ctx *ctx, const uint64_t *d_keys, const void *d_pos, uint32_t pos_bytes, uint64_t n,
+                             int masked, const uint64_t *d_src_base, uint32_t tagged, const uint64_t *d_rec_start,
+                             const uint32_t *d_rec_id, uint64_t nrec, uint32_t *d_vec) {
+    if (!ctx || (pos_bytes != 4 && pos_bytes != 8)) return KMAN_EINVAL;
+    if (n == 0) return KMAN_OK;
+    if (!d_keys || !d_pos || !d_vec || (tagged && !d_src_base) || (masked && (!d_rec_start || !d_rec_id || !nrec)))
+        return kman_fail(ctx, KMAN_EINVAL, "kman_vec_fill: null buffer");
+    if (tagged && pos_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "tagged pos are u64");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const dim3 g((uint32_t)ceil_div(n, 256));
+    if (pos_bytes == 8)
+        hipLaunchKernelGGL(vec_fill_kernel<uint64_t>, g, dim3(256), 0, ctx->stream, d_keys, (const uint64_t *)d_pos, n,
+                           masked, d_src_base, tagged, d_rec_start, d_rec_id, nrec, d_vec);
+    else
+        hipLaunchKernelGGL(vec_fill_kernel<uint32_t>, g, dim3(256), 0, ctx->stream, d_keys, (const uint32_t *)d_pos, n,
+                           masked, d_src_base, tagged, d_rec_start, d_rec_id, nrec, d_vec);
+    HIP_TRY(ctx, hipGetLastError());
+    return KMAN_OK;
+}
+
 extern "C" int kman_count_descents(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint64_t *descents) {
     if (!ctx || !descents) return KMAN_EINVAL;
     *descents = 0;

@@ -13,13 +13,22 @@ Outputs do not depend on how the stream was cut into batches (verified on
 the reference), so batches that come from one FastaBatcher run
 are joined as the whole device-resident stream without materialising them.
 
-VEC_COUNT / VEC_COUNT_MASKED: the reference always raises
-NotImplementedError from its abstract abundance vector (abundance.py:60,123);
-they are out of this path's scope and raise the same way here.
+VEC_COUNT / VEC_COUNT_MASKED (join.py:288-335): the reference's
+AbundanceVector.add_count first calls its abstract base (abundance.py:60,123),
+which raises NotImplementedError, so its join never gets past the first
+k-mer.  Here they do what the code around that call evidently means
+(abundance.py:103-168): one vector per (record, strand) indexed by window
+start, holding the k-mer's count (VEC_COUNT) or its occurrences in other
+records when it occurs in more than one (VEC_COUNT_MASKED), written as
+``<out>/<ref>___<strand>.gz`` = "# k=<k>" + one count per line.  The counts
+come from one device sort + kman_vec_fill; tests/test_gpu_vectors.py checks
+them against a restatement of that code (parity unpinned: the reference
+never produces a vector).
 """
 
 from __future__ import annotations
 
+import gzip
 import logging
 import os
 import tempfile
@@ -176,11 +185,10 @@ class KJoiner:
 
     def join(self, batches: List[Batch], outpath: str) -> None:
         """Join batches into ``outpath`` on the GPU (join.py:376-391)."""
-        if self.mode.name.startswith("VEC_"):
-            raise NotImplementedError(
-                "abundance vectors (VEC_*) are out of this engine's scope; the reference raises the same "
-                "NotImplementedError (kmermaid/abundance.py:60,123)")
         print("Joining...")
+        if self.mode.name.startswith("VEC_"):
+            join_vectors(batches, self.mode == self.MODE.VEC_COUNT_MASKED, outpath)
+            return
         with open(outpath, "wb") as OH:
             join_bytes(batches, self.mode == self.MODE.SEQ_COUNT, sink=OH)
 
@@ -232,6 +240,95 @@ def join_bytes(batches: List[Batch], count: bool, sink=None):
     finally:
         km.free()
     return engine._to(sink, format_sources(keys, pos, k, srcs, tagged))
+
+
+def join_vectors(batches: List[Batch], masked: bool, outpath: str) -> None:
+    """Abundance vectors of the joined batches (module docstring): the union
+    sorted on the device (gather_sorted), each item's count (or masked count)
+    written at its (source, window, strand) slot by kman_vec_fill, then one
+    gzip file per (record, strand) that received a count, its vector running
+    to the last such window (AbundanceVector.add_ref grows it to pos + 1)."""
+    import ctypes
+    from ctypes import byref, c_size_t, c_void_p
+
+    from . import _native as N
+    from .source import FastaSource, gather_sorted
+
+    dirpath = os.path.splitext(outpath)[0]
+    entries = _entries(batches)
+    if not entries:
+        logging.error("nothing to crawl")  # join.py:110; then write_to with no vectors
+        if os.path.isfile(dirpath):
+            raise AssertionError
+        print('Writing output in "%s"' % dirpath)
+        os.makedirs(dirpath, exist_ok=True)
+        return
+    if os.path.isfile(dirpath):
+        raise AssertionError
+    if not all(isinstance(e[0], FastaSource) for e in entries):
+        raise NotImplementedError("abundance vectors of reloaded batch files (-B)")
+    km, srcs, tagged = gather_sorted(entries, want_pos=True)
+    dev, k, L = srcs[0].dev, srcs[0].k, N.lib()
+    base = np.concatenate([[0], np.cumsum([2 * s.parsed.n_bases for s in srcs])]).astype(np.uint64)
+    total = int(base[-1])
+    # record identity = record name (SequenceCoords.from_str: ref); two
+    # records of one name would share a vector and collide in add_count
+    names, rec_start, rec_end = [], [], []
+    for si, s in enumerate(srcs):
+        p = s.parsed
+        rs = np.asarray(p.rec_seq, dtype=np.uint64)
+        ends = np.append(rs[1:], np.uint64(p.n_bases))
+        names += list(p.names)
+        rec_start.append(base[si] + 2 * rs)
+        rec_end.append(base[si] + 2 * ends)
+    if len(set(names)) != len(names):
+        raise AssertionError("abundance vectors need distinct record names (one vector per ref:strand)")
+    rec_start = np.concatenate(rec_start).astype(np.uint64)
+    rec_end = np.concatenate(rec_end).astype(np.uint64)
+    rec_id = np.arange(len(names), dtype=np.uint32)
+    bufs = []
+    try:
+        vec = dev.alloc(4 * max(total, 1))
+        bufs.append(vec)
+        dev.memset(vec, 0, 4 * max(total, 1))
+        d_base, d_rs, d_id = dev.alloc(8 * len(base)), dev.alloc(8 * max(1, len(rec_start))), dev.alloc(
+            4 * max(1, len(rec_id)))
+        bufs += [d_base, d_rs, d_id]
+        dev.upload(d_base, base)
+        dev.upload(d_rs, rec_start)
+        dev.upload(d_id, rec_id)
+        N.check(dev.ctx, L.kman_vec_fill(dev.ctx, c_void_p(km.keys.ptr), c_void_p(km.pos.ptr), km.pos_bytes, km.n,
+                                         1 if masked else 0, c_void_p(d_base.ptr), 1 if tagged else 0,
+                                         c_void_p(d_rs.ptr), c_void_p(d_id.ptr), len(rec_start), c_void_p(vec.ptr)),
+                "kman_vec_fill")
+        v = dev.download(vec, total, np.uint32)
+    finally:
+        km.free()
+        for b in bufs:
+            b.free()
+    print('Writing output in "%s"' % dirpath)  # abundance.py:160
+    os.makedirs(dirpath, exist_ok=True)
+    for r, name in enumerate(names):
+        for strand in (0, 1):
+            sl = v[int(rec_start[r]) + strand:int(rec_end[r]):2]
+            nz = np.flatnonzero(sl)
+            if not len(nz):
+                continue  # no add_count for this ref:strand: no vector, no file
+            n = int(nz[-1]) + 1
+            arr = np.ascontiguousarray(sl[:n])
+            used = c_size_t(0)
+            rc = L.kman_format_vector(arr.ctypes.data_as(c_void_p), n, 1, None, 0, byref(used), engine.host_threads())
+            if rc not in (N.KMAN_OK, N.KMAN_ECAP):
+                raise RuntimeError("kman_format_vector failed (%d)" % rc)
+            buf = ctypes.create_string_buffer(max(1, used.value))
+            rc = L.kman_format_vector(arr.ctypes.data_as(c_void_p), n, 1, buf, used.value, byref(used),
+                                      engine.host_threads())
+            if rc != N.KMAN_OK:
+                raise RuntimeError("kman_format_vector failed (%d)" % rc)
+            ref = name.decode("utf-8", "surrogateescape")
+            with gzip.open(os.path.join(dirpath, "%s___%s.gz" % (ref, "+-"[strand])), "wb") as OH:
+                OH.write(b"# k=%d\n" % k)
+                OH.write(buf.raw[:used.value])
 
 
 def format_sources(keys: np.ndarray, pos: np.ndarray, k: int, srcs, tagged: bool) -> bytes:

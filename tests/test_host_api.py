@@ -117,7 +117,7 @@ def test_batcher_validation(tmp_path):
         load_batches(str(empty))
 
 
-def test_joiner_modes():
+def test_joiner_modes(tmp_path):
     from kman_amd.join import KJoiner, KJoinerThreading
 
     j = KJoinerThreading()
@@ -127,5 +127,10 @@ def test_joiner_modes():
     with pytest.raises(AssertionError):
         j.batch_size = 1
     j.batch_size = 4
-    with pytest.raises(NotImplementedError):
-        KJoiner(KJoiner.MODE.VEC_COUNT).join([], "/dev/null")
+    # abundance vectors of nothing: the output directory (extension dropped),
+    # no vector files (AbundanceVector.write_to over an empty crawl)
+    KJoiner(KJoiner.MODE.VEC_COUNT).join([], str(tmp_path / "vec.out"))
+    assert (tmp_path / "vec").is_dir() and not list((tmp_path / "vec").iterdir())
+    (tmp_path / "file").write_text("")
+    with pytest.raises(AssertionError):  # the directory path is a file
+        KJoiner(KJoiner.MODE.VEC_COUNT_MASKED).join([], str(tmp_path / "file.txt"))
