@@ -284,7 +284,7 @@ def run_single(args):
             out["cpu_baseline"] = cpu_baseline(args.k, args.mode)
         except Exception as e:  # reported, never fatal to the GPU number
             out["cpu_baseline"] = {"error": repr(e)}
-    print(json.dumps(out), flush=True)
+    emit(out)
     dev.close()
 
 
@@ -386,7 +386,7 @@ def run_dist(args, world: int, rank: int, local: int):
                          "traffic": None, "avg_launch_ms": avg * 1e3},
             "cpu_baseline": None,
         }
-        print(json.dumps(out), flush=True)
+        emit(out)
     comm.allreduce(np.zeros(1, np.uint64))  # every rank is done with the id file
     if rank == 0 and world > 1:
         try:
@@ -397,7 +397,25 @@ def run_dist(args, world: int, rank: int, local: int):
     dev.close()
 
 
+_RESULT_FD = None  # stdout as the driver sees it (main() points fd 1 at stderr)
+
+
+def emit(out: dict) -> None:
+    """The ONE JSON line, on the real stdout: libraries (RCCL prints a
+    version banner at communicator init) only ever see fd 1 -> stderr."""
+    line = (json.dumps(out) + "\n").encode()
+    if _RESULT_FD is None:
+        sys.stdout.write(line.decode())
+        sys.stdout.flush()
+    else:
+        os.write(_RESULT_FD, line)
+
+
 def main() -> None:
+    global _RESULT_FD
+    sys.stdout.flush()
+    _RESULT_FD = os.dup(1)
+    os.dup2(2, 1)  # everything else printed to fd 1 (ours or a library's) goes to stderr
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
