@@ -101,7 +101,8 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 // round, and their windows are dropped before the rank (keep bitmap).
 // NS: position segments (look-back chains); RS for the shard path (EX), more
 // for kman_groups (shorter chains, pass 1 finds segments in an LDS table)
-template <int EI, bool RC, bool ATOMIC, bool CANON = false, bool BR = false, bool EX = false, int NS = RS>
+template <int EI, bool RC, bool ATOMIC, bool CANON = false, bool BR = false, bool EX = false, int NS = RS,
+          int XLB = LB>
 __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI == 8 ? 8 : 4)))) void rg_extract(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
                                                  uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
                                                  uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ cnt0,
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
             const uint32_t d = threadIdx.x / TPD;
             const uint64_t excl =
                 (dbg & 1) ? 0ull  // timing ablation only: no look-back (wrong offsets)
-                          : group_lookback<TPD>(status + d, tile, first, thist[d], epoch, err);
+                          : group_lookback<TPD, XLB>(status + d, tile, first, thist[d], epoch, err);
             if (threadIdx.x % TPD == 0) {
                 const uint64_t incl = excl + thist[d];
                 if (EX) {  // (only kept digits get here)
@@ -1345,10 +1346,25 @@ int run_finish(kman_ctx *ctx, const FinishArgs &f, int mode, uint64_t *okeys, vo
     return KMAN_OK;
 }
 
-template <int EI, bool RC, bool CANON, int NS>
+// XLB: predecessor status words per lane and look-back round -- each round
+// loads 2 * XLB words per digit (a 2 KB row per word), so the wide rounds of
+// the sort passes (LB = 8) cost rg_extract 4.6 GB of status reads per launch
+// (PMC: FETCH 2.27 GB raw, 8 GB of items out): 1 word per lane reads 2.6x
+// less at the same speed (3.69-3.73 vs 3.77-3.86 ms; KMAN_RG_XLB=2/4/8 for A/B)
+template <int EI, bool RC, bool CANON, int NS, int XLB = 1>
 void launch_extract_ns(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                        uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
-    hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS>), dim3(NS * p.seg_tiles), dim3(RT), 0,
+    if (NS == RS && XLB == 1) {
+        static const char *e = getenv("KMAN_RG_XLB");
+        const int x = e ? atoi(e) : 1;
+        if (x == 2) return launch_extract_ns<EI, RC, CANON, NS, 2>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter,
+                                                                    dbg, stp);
+        if (x == 4) return launch_extract_ns<EI, RC, CANON, NS, 4>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter,
+                                                                    dbg, stp);
+        if (x == 8) return launch_extract_ns<EI, RC, CANON, NS, 8>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter,
+                                                                    dbg, stp);
+    }
+    hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS, XLB>), dim3(NS * p.seg_tiles), dim3(RT), 0,
                        ctx->stream, codes, n_bases, (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status,
                        counter, epoch, ctx->d_err, dbg, stp);
 }
@@ -1781,7 +1797,7 @@ template <int EI, bool RC, bool CANON>
 void launch_extract_ex(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                        uint64_t *out, uint32_t *cnt, const uint64_t *rtab, uint32_t epoch, uint32_t *counter) {
     const uint32_t grid = RS * p.seg_tiles;
-    hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, true>), dim3(grid), dim3(RT), 0, ctx->stream, codes,
+    hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, true, RS, 1>), dim3(grid), dim3(RT), 0, ctx->stream, codes,
                        n_bases, (int)k, p.Q, out, (uint64_t)0, p.seg_tiles, p.n_tiles0, cnt, ctx->d_status, counter,
                        epoch, ctx->d_err, 0u, nullptr, rtab);
 }
