@@ -872,8 +872,12 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
 // their pos ((window << 1) | strand).
 enum { RG_COUNT = 1, RG_UNIQ = 2 };
 
-template <int MODE, typename O, bool ATOMIC, bool PF = false>
-__global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ in, uint64_t C1,
+// DB: persistent 1024-thread blocks (one per CU) with two LDS region
+// buffers: while region r is sorted in one, region r + 1 streams into the
+// other by direct global -> LDS loads (global_load_lds_dwordx4: no registers
+// held, unlike PF), so the region loads hide behind the LDS work.
+template <int MODE, typename O, bool ATOMIC, bool PF = false, bool DB = false>
+__global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : 4) void rg_finish(const uint64_t *__restrict__ in, uint64_t C1,
                                                 const uint32_t *__restrict__ cnt1, uint32_t Q, uint32_t rest,
                                                 uint32_t rc, uint64_t rbase, uint32_t tag_shift, uint32_t fsub,
                                                 uint64_t *__restrict__ okeys, O *__restrict__ ovals,
@@ -881,30 +885,58 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
                                                 uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg,
                                                 uint64_t *__restrict__ stp, uint32_t nreg,
                                                 uint8_t *__restrict__ freg) {
-    __shared__ __attribute__((aligned(16))) uint64_t s[FCAP];
-    __shared__ uint32_t wh[FW][FWORD];  // per-wave digit counters, u16 pairs
+    constexpr int NT = DB ? 1024 : FT, NW_ = NT / 64;
+    constexpr int IPT = DB ? (FCAP + 1023) / 1024 : FIPT;  // items per thread (DB: 9 x 1024 >= FCAP)
+    constexpr int SCAP = DB ? FCAP + 2 : FCAP;  // (DB: + the alignment holes of two odd sub-regions)
+    __shared__ __attribute__((aligned(16))) uint64_t sb[DB ? 2 : 1][SCAP];
+    __shared__ uint32_t wh[NW_][FWORD];  // per-wave digit counters, u16 pairs
     __shared__ uint32_t dstart[FRAD];
-    __shared__ uint32_t lds_scan[FW];
+    __shared__ uint32_t lds_scan[NW_];
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_out;
+    uint32_t cur = 0;
+    uint64_t *s = sb[0];
 
     const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
     const uint64_t rmask = (1ull << rest) - 1;
-    const uint32_t pw = (uint32_t)w * (FIPT * 64) + (uint32_t)lane;  // wave-striped positions
+    const uint32_t pw = (uint32_t)w * (IPT * 64) + (uint32_t)lane;  // wave-striped positions
     // a region r = fsub (1 or 2) sub-regions of capacity C1, concatenated:
     // position p < m0 at in[r * fsub * C1 + p], p >= m0 at .. + C1 - m0 + p
     auto counts = [&](uint32_t rr, uint32_t &a0, uint32_t &a1) {
         a0 = cnt1[(uint64_t)rr * fsub];
         a1 = fsub > 1 ? cnt1[(uint64_t)rr * fsub + 1] : 0u;
     };
-    auto load = [&](uint32_t rr, uint32_t a0, uint32_t mm, uint64_t (&v)[FIPT]) {
+    auto load = [&](uint32_t rr, uint32_t a0, uint32_t mm, uint64_t (&v)[IPT]) {
         // (a uniform base and one 32-bit offset per item: few address VGPRs)
         const uint64_t *src = in + (uint64_t)rr * fsub * C1;
         const uint32_t skip = (uint32_t)C1 - a0;
 #pragma unroll
-        for (int i = 0; i < FIPT; i++) {
+        for (int i = 0; i < IPT; i++) {
             const uint32_t p = pw + i * 64;
             v[i] = p < mm ? src[p < a0 ? p : p + skip] : 0;
+        }
+    };
+    // DB: region rr's items into an LDS buffer in 16-byte chunks, one per
+    // lane (a wave's 64 chunks land contiguously at the M0 base): sub-region
+    // 1 starts at the even slot after sub-region 0 (a hole when a0 is odd;
+    // reading one item past an odd count stays inside the capacity C1)
+    auto dma = [&](uint32_t rr, uint32_t a0, uint32_t a1, uint64_t *dst) {
+        const uint64_t *src0 = in + (uint64_t)rr * fsub * C1, *src1 = src0 + C1;
+        const uint32_t c0 = (a0 + 1) >> 1, ctot = c0 + ((a1 + 1) >> 1);
+        for (uint32_t cb = (uint32_t)w * 64; cb < ctot; cb += NT) {  // (wave-uniform)
+            const uint32_t c = cb + (uint32_t)lane;
+            if (c < ctot) {
+                const uint64_t *g = c < c0 ? src0 + 2 * c : src1 + 2 * (c - c0);
+                __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)(dst + 2 * cb), 16, 0, 0);
+            }
+        }
+    };
+    auto from_lds = [&](uint32_t a0, uint32_t mm, uint64_t (&v)[IPT]) {
+        const uint32_t hole = a0 & 1u;
+#pragma unroll
+        for (int i = 0; i < IPT; i++) {
+            const uint32_t p = pw + i * 64;
+            v[i] = p < mm ? s[p + (p >= a0 ? hole : 0u)] : 0;
         }
     };
     // freg (the round path): a region flagged by a pass (a sub-region
@@ -932,8 +964,22 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
     uint32_t m0, m1, rn = nreg, n0 = 0, n1 = 0;
     counts(r, m0, m1);
     uint32_t m = fit(r, m0, m1);
-    uint64_t x[FIPT];
-    load(r, m0, m, x);
+    uint64_t x[IPT];
+    if (DB) {
+        if (m) dma(r, m0, m1, sb[0]);
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        from_lds(m0, m, x);
+        if (t == 0) s_tile = atomicAdd(counter, 1u);
+        __syncthreads();
+        rn = __builtin_amdgcn_readfirstlane(s_tile);
+        if (rn < nreg) {
+            counts(rn, n0, n1);
+            if (fit(rn, n0, n1)) dma(rn, n0, n1, sb[1]);
+        }
+    } else {
+        load(r, m0, m, x);
+    }
     if (PF) {
         __syncthreads();  // (every read of s_tile above before it is reused)
         if (t == 0) s_tile = atomicAdd(counter, 1u);
@@ -959,9 +1005,9 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
 #pragma unroll
         for (int q = 0; q < FWORD / 64; q++) wh[w][lane + 64 * q] = 0;
         __builtin_amdgcn_wave_barrier();
-        uint32_t rk[FIPT];
+        uint32_t rk[IPT];
 #pragma unroll
-        for (int i = 0; i < FIPT; i++) {
+        for (int i = 0; i < IPT; i++) {
             const bool valid = pw + i * 64 < m;
             const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
             const uint32_t hs = (d & 1u) * 16u;
@@ -988,21 +1034,21 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
         uint32_t tlo = 0, thi = 0;
         if (t < FWORD) {
 #pragma unroll
-            for (int ww = 0; ww < FW; ww++) {
+            for (int ww = 0; ww < NW_; ww++) {
                 const uint32_t c = wh[ww][t];
                 wh[ww][t] = tlo | (thi << 16);
                 tlo += c & 0xffffu;
                 thi += c >> 16;
             }
         }
-        const uint32_t ls = block_exclusive_scan<FT>(tlo + thi, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
+        const uint32_t ls = block_exclusive_scan<NT>(tlo + thi, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
         if (t < FWORD) {
             dstart[2 * t] = ls;
             dstart[2 * t + 1] = ls + tlo;
         }
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < FIPT; i++) {
+        for (int i = 0; i < IPT; i++) {
             if (pw + i * 64 < m) {
                 const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
                 s[dstart[d] + ((wh[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rk[i]] = x[i];
@@ -1011,13 +1057,13 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
         __syncthreads();
         if (p + 1 < np) {
 #pragma unroll
-            for (int i = 0; i < FIPT; i++)
+            for (int i = 0; i < IPT; i++)
                 if (pw + i * 64 < m) x[i] = s[pw + i * 64];
         }
     }
     if (np == 0) {
 #pragma unroll
-        for (int i = 0; i < FIPT; i++)
+        for (int i = 0; i < IPT; i++)
             if (pw + i * 64 < m) s[pw + i * 64] = x[i];
         __syncthreads();
     }
@@ -1033,19 +1079,19 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
 
     RSTAMP(r, 2);
     // ---- run-length pass (thread t: sorted positions t*FIPT ..)
-    const uint32_t q0 = (uint32_t)t * FIPT;
+    const uint32_t q0 = (uint32_t)t * IPT;
     uint32_t heads = 0, tails = 0;
 #define RKEY(v) (((v) >> Q) & rmask)
-    uint64_t kv[FIPT];
+    uint64_t kv[IPT];
 #pragma unroll
-    for (int j = 0; j < FIPT; j++) kv[j] = q0 + j < m ? s[q0 + j] : 0;
+    for (int j = 0; j < IPT; j++) kv[j] = q0 + j < m ? s[q0 + j] : 0;
 #pragma unroll
-    for (int j = 0; j < FIPT; j++) {
+    for (int j = 0; j < IPT; j++) {
         const uint32_t q = q0 + j;
         if (q < m) {
             const uint64_t kq = RKEY(kv[j]);
             const bool h = q == 0 || kq != RKEY(j ? kv[j - 1] : s[q - 1]);
-            const bool e = q + 1 == m || kq != RKEY(j + 1 < FIPT ? kv[j + 1] : s[q + 1]);
+            const bool e = q + 1 == m || kq != RKEY(j + 1 < IPT ? kv[j + 1] : s[q + 1]);
             heads |= (uint32_t)h << j;
             tails |= (uint32_t)e << j;
         }
@@ -1056,12 +1102,12 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
     } else {
         emit = tails;
         const uint32_t lh = heads ? q0 + (31 - __clz(heads)) + 1 : 0u;
-        lh_before = block_exclusive_scan<FT>(
+        lh_before = block_exclusive_scan<NT>(
             lh, [](uint32_t a, uint32_t b) { return a > b ? a : b; }, 0u, lds_scan, (uint32_t *)nullptr);
     }
     const uint32_t ne = (uint32_t)__popc(emit);
     uint32_t total;
-    const uint32_t off = block_exclusive_scan<FT>(ne, SumU32(), 0u, lds_scan, &total);
+    const uint32_t off = block_exclusive_scan<NT>(ne, SumU32(), 0u, lds_scan, &total);
     // (the scan's barriers ordered every read of s above before the writes below)
     RSTAMP(r, 3);
     if (w == 0) {
@@ -1074,7 +1120,7 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
     {
         uint32_t o = off, cur = lh_before;  // head position + 1 of the open group
 #pragma unroll
-        for (int j = 0; j < FIPT; j++) {
+        for (int j = 0; j < IPT; j++) {
             const uint32_t q = q0 + j;
             if (MODE != RG_UNIQ && ((heads >> j) & 1u)) cur = q + 1;
             if ((emit >> j) & 1u)
@@ -1086,11 +1132,11 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
     const uint64_t ob = s_out;
     if (!(dbg & 2)) {  // (dbg & 2: timing ablation only, no output writes)
         const uint64_t qmask = Q ? ((1ull << Q) - 1) : 0ull;
-        for (uint32_t q = t; q < total; q += FT) {
+        for (uint32_t q = t; q < total; q += NT) {
             const uint64_t v = s[q];
             okeys[ob + q] = ((uint64_t)(r + rbase) << rest) | RKEY(v);
         }
-        for (uint32_t q = t; q < total; q += FT) {
+        for (uint32_t q = t; q < total; q += NT) {
             const uint64_t v = s[q];
             if constexpr (MODE == RG_UNIQ) {
                 const uint64_t idx = v & qmask;
@@ -1105,8 +1151,28 @@ __global__ __launch_bounds__(FT, 4) void rg_finish(const uint64_t *__restrict__ 
     }
 #undef RKEY
     RSTAMP(r, 5);
-    if (!PF || rn >= nreg) break;
+    if (!(PF || DB) || rn >= nreg) break;
     __syncthreads();  // (every read of s / s_out / s_tile above before the next region writes them)
+    if (DB) {
+        // region rn has landed in the other buffer (vmcnt: every load and
+        // store of this wave; the barrier: every wave's chunks)
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        cur ^= 1u;
+        s = sb[cur];
+        r = rn;
+        m0 = n0;
+        m = fit(r, n0, n1);
+        from_lds(m0, m, x);
+        if (t == 0) s_tile = atomicAdd(counter, 1u);
+        __syncthreads();
+        rn = __builtin_amdgcn_readfirstlane(s_tile);
+        if (rn < nreg) {
+            counts(rn, n0, n1);
+            if (fit(rn, n0, n1)) dma(rn, n0, n1, sb[cur ^ 1u]);
+        }
+        continue;
+    }
     r = rn;
     m0 = n0;
     m = fit(r, n0, n1);
@@ -1304,26 +1370,33 @@ struct FinishArgs {
     uint8_t *freg = nullptr;  // per-region overflow flags (the round path), else null
 };
 
-template <int MODE, typename O, bool ATOMIC, bool PF>
+template <int MODE, typename O, bool ATOMIC, bool PF, bool DB = false>
 void launch_finish_as(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ovals, uint32_t epoch,
                       uint32_t *counter, uint32_t dbg, uint64_t *stp) {
-    const void *fn = (const void *)rg_finish<MODE, O, ATOMIC, PF>;
-    const uint32_t grid = PF ? (uint32_t)kman_persistent_grid(ctx, fn, FT, f.nreg) : f.nreg;
-    hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, PF>), dim3(grid), dim3(FT), 0, ctx->stream, f.in, f.C1, f.cnt, f.Q,
+    const void *fn = (const void *)rg_finish<MODE, O, ATOMIC, PF, DB>;
+    constexpr int NT = DB ? 1024 : FT;
+    const uint32_t grid = PF || DB ? (uint32_t)kman_persistent_grid(ctx, fn, NT, f.nreg) : f.nreg;
+    hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, PF, DB>), dim3(grid), dim3(NT), 0, ctx->stream, f.in, f.C1, f.cnt, f.Q,
                        f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status, counter, epoch,
                        ctx->d_err, dbg, stp, f.nreg, f.freg);
 }
 
 // one block per region; KMAN_RG_FIN=1: persistent blocks that prefetch the
 // next region while sorting this one (A/B only: the prefetch registers spill,
-// 11.1 vs 5.7 ms on the bench config)
+// 11.1 vs 5.7 ms on the bench config); KMAN_RG_FIN=2: persistent 1024-thread
+// blocks, the next region streamed into a second LDS buffer by direct
+// global -> LDS loads (no registers held; parity green) -- 11.1-11.2 ms too:
+// with one block per CU the sort's barriers are exposed, where two blocks
+// per CU interleave them, so the loads were never the bound
 template <int MODE, typename O>
 void launch_finish(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ovals, uint32_t epoch,
                    uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     static const char *e = getenv("KMAN_RG_FIN");
-    const bool pf = e && atoi(e) != 0;
+    const bool pf = e && atoi(e) == 1;
+    const bool db = e && atoi(e) == 2;
     if (ctx->lds_atomic_ordered) {
-        if (pf) launch_finish_as<MODE, O, true, true>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
+        if (db) launch_finish_as<MODE, O, true, false, true>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
+        else if (pf) launch_finish_as<MODE, O, true, true>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
         else launch_finish_as<MODE, O, true, false>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
     } else {  // (the ballot ranks need the registers the prefetch would take)
         launch_finish_as<MODE, O, false, false>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
