@@ -176,6 +176,26 @@ def test_dist_region_overflow_redoes_only_its_keys(G):
             _close(pipes)
 
 
+@pytest.mark.parametrize("G", [1, 3])
+def test_dist_overflow_redo_canonical_and_rc(G):
+    """The partial redo with canonical keys (config 5's count) and with -r
+    uniq: left-out ranges of min(fwd, rc) keys, and of both strands."""
+    import inputs
+
+    rep = b"TTGACCATGACCGATTACAGATTGGC"
+    body = inputs.SynthLayout(150_000, 6, record_len=40_000).read(0, 10**9)
+    text = body + b">sat\n" + b"\n".join([rep * 3] * 20_000) + b"\n"
+    outs, pipes, _ = _run(text, 21, "count", G, canonical=True)
+    try:
+        assert sum(p.partial_rounds for p in pipes) >= 1
+        wk, wc = _oracle(text, 21, "count", canonical=True)
+        for o in outs:
+            np.testing.assert_array_equal(o[0], wk)
+            np.testing.assert_array_equal(o[1], wc)
+    finally:
+        _close(pipes)
+
+
 def test_dist_general_path_k27():
     """k = 27: count items still fit the region rounds; uniq (window index +
     key > 64 bits) and a forced path="general" take the general path (key
