@@ -387,12 +387,16 @@ class DistPipeline:
     min(fwd, rc) (config 5).  path: "region" (default; per-round fallback to
     the general path) or "general".  max_round_items: force more rounds
     (tests).  reload: re-upload + re-parse the shard in every step (the
-    pinned-host benchmark line)."""
+    pinned-host benchmark line); reparse: keep the shard's text in HBM and
+    parse it in every step (a shard of one chunk: the benchmark's step then
+    covers parse + histogram + rounds, as the single-GPU step covers parse +
+    join)."""
 
     def __init__(self, dev: engine.Device, reader, k: int, mode: str, world: int, rank: int,
                  uid: Optional[bytes] = None, canonical: bool = False, rc: bool = False, path: str = "region",
                  max_round_items: Optional[int] = None, chunk_bytes: int = 256 << 20, reload: bool = False,
-                 mem_frac: float = 0.85, shard: Optional[S.ShardCodes] = None, local: bool = False):
+                 mem_frac: float = 0.85, shard: Optional[S.ShardCodes] = None, local: bool = False,
+                 reparse: bool = False):
         engine._check_k(k)
         if mode not in ("count", "uniq"):
             raise ValueError(mode)
@@ -401,12 +405,13 @@ class DistPipeline:
         self.dev, self.k, self.mode, self.world, self.rank = dev, k, mode, world, rank
         self.canonical, self.rc = canonical, rc and not canonical
         self.path, self.max_round_items, self.reload, self.mem_frac = path, max_round_items, reload, mem_frac
+        self.reparse = reparse
         self.fmode = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
         self.flags = engine.flags_for(self.rc, mode == "uniq", canonical)
         self.reader = reader
         if shard is None:
             self.spec = S.shard_specs(reader, world, k)[rank]
-            self.loader = S.ShardLoader(dev, reader, self.spec, k, chunk_bytes)
+            self.loader = S.ShardLoader(dev, reader, self.spec, k, chunk_bytes, resident=reparse)
             self.shard = self.loader.load()
         else:  # an input already on the device (one rank: local_groups)
             self.spec, self.loader, self.shard = shard.spec, None, shard
@@ -516,7 +521,7 @@ class DistPipeline:
         if not self.ready:
             yield from self.setup_gen()
         L, ctx, dev, sh = N.lib(), self.dev.ctx, self.dev, self.shard
-        if self.reload and self.loader is not None:
+        if (self.reload or self.reparse) and self.loader is not None:
             self.shard = sh = self.loader.load()
         G, me = self.world, self.rank
         self.phase_ms = {}
