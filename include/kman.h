@@ -404,6 +404,15 @@ int kman_allreduce_u64(kman_ctx *ctx, uint64_t *d_buf, uint64_t n);
 int kman_allgather_u64(kman_ctx *ctx, const uint64_t *d_send, uint64_t *d_recv, uint64_t n);
 int kman_alltoallv(kman_ctx *ctx, const void *d_send, const uint64_t *send_counts, const uint64_t *send_offsets,
                    void *d_recv, const uint64_t *recv_counts, const uint64_t *recv_offsets, uint32_t elem_bytes);
+/* The same on the context's communication stream, ordered after the work
+ * queued so far on its compute stream; completion recorded in event `slot`
+ * (0..7).  kman_comm_wait makes the compute stream wait for it: an exchange
+ * overlaps the compute on the parts already received (DistPipeline's
+ * overlapped rounds). */
+int kman_alltoallv_async(kman_ctx *ctx, const void *d_send, const uint64_t *send_counts,
+                         const uint64_t *send_offsets, void *d_recv, const uint64_t *recv_counts,
+                         const uint64_t *recv_offsets, uint32_t elem_bytes, int slot);
+int kman_comm_wait(kman_ctx *ctx, int slot);
 int kman_partition(kman_ctx *ctx, const uint64_t *d_keys, uint64_t *d_keys_out, const void *d_vals,
                    void *d_vals_out, uint32_t val_bytes, uint64_t n, const uint8_t *d_lut, uint32_t lut_shift,
                    uint32_t nbuckets, const uint64_t *bucket_counts);

@@ -155,6 +155,10 @@ SIGNATURES = {
     "kman_allreduce_u64": (c_int, [c_void_p, c_void_p, c_uint64]),
     "kman_allgather_u64": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64]),
     "kman_alltoallv": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32]),
+    "kman_alltoallv_async": (
+        c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_int],
+    ),
+    "kman_comm_wait": (c_int, [c_void_p, c_int]),
     "kman_partition": (
         c_int,
         [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_void_p, c_uint32, c_uint32,

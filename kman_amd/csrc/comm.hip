@@ -106,9 +106,10 @@ extern "C" int kman_allgather_u64(kman_ctx *ctx, const uint64_t *d_send, uint64_
 
 // All-to-all-v of elem_bytes elements: send_counts/offsets and
 // recv_counts/offsets are host arrays of nranks elements (in elements).
-extern "C" int kman_alltoallv(kman_ctx *ctx, const void *d_send, const uint64_t *send_counts,
-                              const uint64_t *send_offsets, void *d_recv, const uint64_t *recv_counts,
-                              const uint64_t *recv_offsets, uint32_t elem_bytes) {
+namespace {
+int alltoallv_on(kman_ctx *ctx, hipStream_t st, const void *d_send, const uint64_t *send_counts,
+                 const uint64_t *send_offsets, void *d_recv, const uint64_t *recv_counts,
+                 const uint64_t *recv_offsets, uint32_t elem_bytes) {
     if (!ctx || !send_counts || !send_offsets || !recv_counts || !recv_offsets) return KMAN_EINVAL;
     if (elem_bytes != 4 && elem_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "elem_bytes must be 4 or 8");
     Comm *c = comm_of(ctx);
@@ -130,17 +131,53 @@ extern "C" int kman_alltoallv(kman_ctx *ctx, const void *d_send, const uint64_t 
             const uint64_t o = r * CH;
             if (send_counts[p] > o) {
                 const uint64_t n = send_counts[p] - o < CH ? send_counts[p] - o : CH;
-                NCCL_TRY(ctx, ncclSend((const char *)d_send + (send_offsets[p] + o) * elem_bytes, n, t, p, c->comm,
-                                       ctx->stream));
+                NCCL_TRY(ctx, ncclSend((const char *)d_send + (send_offsets[p] + o) * elem_bytes, n, t, p, c->comm, st));
             }
             if (recv_counts[p] > o) {
                 const uint64_t n = recv_counts[p] - o < CH ? recv_counts[p] - o : CH;
-                NCCL_TRY(ctx, ncclRecv((char *)d_recv + (recv_offsets[p] + o) * elem_bytes, n, t, p, c->comm,
-                                       ctx->stream));
+                NCCL_TRY(ctx, ncclRecv((char *)d_recv + (recv_offsets[p] + o) * elem_bytes, n, t, p, c->comm, st));
             }
         }
         NCCL_TRY(ctx, ncclGroupEnd());
     }
+    return KMAN_OK;
+}
+}  // namespace
+
+extern "C" int kman_alltoallv(kman_ctx *ctx, const void *d_send, const uint64_t *send_counts,
+                              const uint64_t *send_offsets, void *d_recv, const uint64_t *recv_counts,
+                              const uint64_t *recv_offsets, uint32_t elem_bytes) {
+    if (!ctx) return KMAN_EINVAL;
+    return alltoallv_on(ctx, ctx->stream, d_send, send_counts, send_offsets, d_recv, recv_counts, recv_offsets,
+                        elem_bytes);
+}
+
+// The same on the context's communication stream, after the work already
+// queued on its compute stream (which produced d_send); completion is
+// recorded in event `slot` (0..7) for kman_comm_wait.  The compute stream
+// keeps going meanwhile: the exchange of one part overlaps the work on the
+// parts already received.
+extern "C" int kman_alltoallv_async(kman_ctx *ctx, const void *d_send, const uint64_t *send_counts,
+                                    const uint64_t *send_offsets, void *d_recv, const uint64_t *recv_counts,
+                                    const uint64_t *recv_offsets, uint32_t elem_bytes, int slot) {
+    if (!ctx || slot < 0 || slot >= 8) return KMAN_EINVAL;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (!ctx->comm_stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->comm_stream, hipStreamNonBlocking));
+    if (!ctx->comm_pre) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->comm_pre, hipEventDisableTiming));
+    if (!ctx->comm_ev[slot]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->comm_ev[slot], hipEventDisableTiming));
+    HIP_TRY(ctx, hipEventRecord(ctx->comm_pre, ctx->stream));
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->comm_stream, ctx->comm_pre, 0));
+    KMAN_TRY(alltoallv_on(ctx, ctx->comm_stream, d_send, send_counts, send_offsets, d_recv, recv_counts, recv_offsets,
+                          elem_bytes));
+    HIP_TRY(ctx, hipEventRecord(ctx->comm_ev[slot], ctx->comm_stream));
+    return KMAN_OK;
+}
+
+// the compute stream waits for the exchange recorded in `slot`
+extern "C" int kman_comm_wait(kman_ctx *ctx, int slot) {
+    if (!ctx || slot < 0 || slot >= 8) return KMAN_EINVAL;
+    if (!ctx->comm_ev[slot]) return KMAN_OK;
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->comm_ev[slot], 0));
     return KMAN_OK;
 }
 

@@ -52,6 +52,10 @@ struct kman_ctx {
     // H2D copies that overlap the work of `stream` (chunked FASTA uploads)
     hipStream_t copy_stream = nullptr;
     hipEvent_t copy_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // all-to-alls that overlap the work of `stream` (kman_alltoallv_async)
+    hipStream_t comm_stream = nullptr;
+    hipEvent_t comm_pre = nullptr;
+    hipEvent_t comm_ev[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     // key ranges [lo, hi] (pairs) that the last kman_dround_finish left out
     // (KMAN_EPARTIAL): regions that overflowed a capacity
     std::vector<uint64_t> failed;

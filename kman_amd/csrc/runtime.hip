@@ -270,6 +270,13 @@ void kman_destroy(kman_ctx *ctx) {
     }
     for (auto e : ctx->copy_ev)
         if (e) (void)hipEventDestroy(e);
+    if (ctx->comm_stream) {
+        (void)hipStreamSynchronize(ctx->comm_stream);
+        (void)hipStreamDestroy(ctx->comm_stream);
+    }
+    if (ctx->comm_pre) (void)hipEventDestroy(ctx->comm_pre);
+    for (auto e : ctx->comm_ev)
+        if (e) (void)hipEventDestroy(e);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

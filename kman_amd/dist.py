@@ -111,6 +111,27 @@ def round_recv(C: np.ndarray, cuts: np.ndarray, R: int, rank: int, r: int):
     return lo, hi - lo, counts, rc, ro
 
 
+def round_pieces(C: np.ndarray, cuts: np.ndarray, G: int, R: int, r: int, S: int) -> List[List[int]]:
+    """Each destination's part of round r cut into S pieces of about equal
+    k-mers (every rank derives the same cuts from the all-gathered bucket
+    totals C [G, 256]): bounds[q] = S + 1 bucket indices."""
+    tot = np.asarray(C, dtype=np.uint64).reshape(G, NB).sum(axis=0).astype(np.float64)
+    out = []
+    for q in range(G):
+        lo, hi = part_of(cuts, R, q, r)
+        b = [lo]
+        if hi > lo:
+            cum = np.cumsum(tot[lo:hi])
+            for s_ in range(1, S):
+                j = lo + int(np.searchsorted(cum, cum[-1] * s_ / S, side="left")) + 1
+                b.append(min(max(j, b[-1]), hi))
+        else:
+            b += [lo] * (S - 1)
+        b.append(hi)
+        out.append(b)
+    return out
+
+
 def round_sizes(C: np.ndarray, cuts: np.ndarray, G: int, R: int):
     """send[q, r] / recv[q, r] items of every rank and round."""
     C = np.asarray(C, dtype=np.uint64)
@@ -247,6 +268,12 @@ class RcclComm:
         N.check(self.dev.ctx, N.lib().kman_alltoallv(self.dev.ctx, c_void_p(send), _u64p(sc), _u64p(so),
                                                       c_void_p(recv), _u64p(rc), _u64p(ro), eb), "alltoallv")
 
+    def alltoallv_async(self, send, sc, so, recv, rc, ro, eb, slot) -> None:
+        sc, so, rc, ro = (np.ascontiguousarray(x, np.uint64) for x in (sc, so, rc, ro))
+        N.check(self.dev.ctx, N.lib().kman_alltoallv_async(self.dev.ctx, c_void_p(send), _u64p(sc), _u64p(so),
+                                                            c_void_p(recv), _u64p(rc), _u64p(ro), eb, slot),
+                "alltoallv_async")
+
     def run(self, gen):
         """Drive this rank's generator to its result."""
         try:
@@ -257,6 +284,12 @@ class RcclComm:
                     req = gen.send(self.allreduce(arg))
                 elif op == "allgather":
                     req = gen.send(self.allgather(arg))
+                elif op == "alltoallv_async":
+                    self.alltoallv_async(*arg)
+                    req = gen.send(None)
+                elif op == "comm_wait":
+                    N.check(self.dev.ctx, N.lib().kman_comm_wait(self.dev.ctx, int(arg)), "kman_comm_wait")
+                    req = gen.send(None)
                 else:
                     self.alltoallv(*arg)
                     req = gen.send(None)
@@ -287,8 +320,10 @@ class LocalComm:
                     req = gen.send(np.asarray(arg, np.uint64).copy())
                 elif op == "allgather":
                     req = gen.send(np.asarray(arg, np.uint64).reshape(1, -1).copy())
-                else:
-                    send, sc, so, recv, rc, ro, eb = arg
+                elif op == "comm_wait":
+                    req = gen.send(None)
+                else:  # alltoallv (async: the same copy, in stream order)
+                    send, sc, so, recv, rc, ro, eb = arg[:7]
                     if int(sc[0]):
                         N.check(self.dev.ctx, N.lib().kman_memcpy_d2d(self.dev.ctx, c_void_p(recv), c_void_p(send),
                                                                        eb * int(sc[0])), "d2d")
@@ -328,11 +363,13 @@ class SimGroup:
             elif op == "allgather":
                 mat = np.stack([np.asarray(reqs[i][1], np.uint64) for i in live])
                 outs = [mat.copy() for _ in live]
-            else:
+            elif op == "comm_wait":
+                outs = [None for _ in live]
+            else:  # alltoallv (async: done right away, which any later wait allows)
                 L = N.lib()
                 for dst in live:
                     pd = self.pipes[dst]
-                    _, _, _, recv, rcnt, roff, eb = reqs[dst][1]
+                    _, _, _, recv, rcnt, roff, eb = reqs[dst][1][:7]
                     for src in live:
                         send, scnt, soff = reqs[src][1][:3]
                         c = int(scnt[dst])
@@ -396,7 +433,7 @@ class DistPipeline:
                  uid: Optional[bytes] = None, canonical: bool = False, rc: bool = False, path: str = "region",
                  max_round_items: Optional[int] = None, chunk_bytes: int = 256 << 20, reload: bool = False,
                  mem_frac: float = 0.85, shard: Optional[S.ShardCodes] = None, local: bool = False,
-                 reparse: bool = False):
+                 reparse: bool = False, overlap: Optional[bool] = None):
         engine._check_k(k)
         if mode not in ("count", "uniq"):
             raise ValueError(mode)
@@ -406,6 +443,12 @@ class DistPipeline:
         self.canonical, self.rc = canonical, rc and not canonical
         self.path, self.max_round_items, self.reload, self.mem_frac = path, max_round_items, reload, mem_frac
         self.reparse = reparse
+        # overlapped rounds (round_pieces): default on for several ranks;
+        # KMAN_DIST_OVERLAP=0/1 overrides (A/B), tests force it on one rank
+        env = os.environ.get("KMAN_DIST_OVERLAP")
+        self.overlap = (env != "0") if env is not None else (overlap if overlap is not None else world > 1)
+        self.pieces = 4
+        self.overlapped_rounds = 0
         self.fmode = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
         self.flags = engine.flags_for(self.rc, mode == "uniq", canonical)
         self.reader = reader
@@ -563,7 +606,18 @@ class DistPipeline:
         self.fallback_rounds = 0
         self.partial_rounds = 0
         self.redone_kmers = 0
+        self.overlapped_rounds = 0
+        # overlapped rounds need two more scratch arenas (a piece's a and b)
+        S_ = self.pieces
+        use_ov = (self.path == "region" and self.overlap and R == 1
+                  and (a_need + b_need) * (1 + 2.0 / S_) + out_bytes <= self.budget)
         for r in range(R):
+            if use_ov:
+                got_ = yield from self._overlapped_round(C, cuts, R, r, H, c_local, a_need, b_need, ok_, ov_, n_out, vb)
+                if got_ is not None:
+                    n_out = got_
+                    lap("round")
+                    continue
             if self.path == "region":
                 A, B = self.arena_a.get(a_need), self.arena_b.get(b_need)
                 rtab, sc, so = round_send(H, cuts, G, R, r)
@@ -611,6 +665,89 @@ class DistPipeline:
         self.n_recv = cap
         self._out = (ok_, ov_, vb)
         return self.n_local
+
+    def _overlapped_round(self, C, cuts, R, r, H, c_local, a_need, b_need, ok_, ov_, n_out, vb):
+        """Round r with its exchange overlapped: one extraction (destination-
+        major, as round_send lays it out), then each destination's part cut
+        into S pieces (round_pieces); all S all-to-alls are queued on the
+        communication stream at once, and piece s's passes + finish
+        (kman_dround_finish over its buckets, into two scratch arenas of its
+        own) wait only for exchange s -- so exchange s + 1 runs while piece s
+        is sorted.  Regions that overflow are redone once every piece is in
+        (_redo_ranges: the send and receive arenas are free then).
+        Generator; returns the new n_out, or None when a piece's plan does
+        not fit (every rank then runs the round the sequential way)."""
+        L, ctx, sh = N.lib(), self.dev.ctx, self.shard
+        G, me, S_ = self.world, self.rank, self.pieces
+        C = np.asarray(C, np.uint64).reshape(G, NB)
+        bounds = round_pieces(C, cuts, G, R, r, S_)
+        my = bounds[me]
+        plans, bad = [], 0
+        a2 = b2 = 64
+        for s_ in range(S_):
+            b0, b1 = my[s_], my[s_ + 1]
+            cnt = np.ascontiguousarray(C[:, b0:b1])
+            a, b = c_uint64(0), c_uint64(0)
+            if b1 > b0:
+                ret = L.kman_dround_plan(self.k, self.flags, self.fmode, G, self.n_bases_q, b1 - b0,
+                                         _u64p(cnt.reshape(-1)), byref(a), byref(b))
+                bad |= ret != N.KMAN_OK
+            plans.append(cnt)
+            a2, b2 = max(a2, int(a.value)), max(b2, int(b.value))
+        f = yield ("allreduce", np.array([bad], np.uint64))
+        if int(f[0]):
+            return None
+        self.overlapped_rounds += 1
+        # arenas: A = the send buffer, B = the receive buffer (all pieces),
+        # a2 / b2 = a piece's scratch (gen_bufs[1], [2]: free outside a general round)
+        rtab, sc, so = round_send(H, cuts, G, R, r)
+        _, _, _, rcnt, _ = round_recv(C, cuts, R, me, r)
+        A = self.arena_a.get(max(a_need, 8 * int(sc.sum()), 64))
+        B = self.arena_b.get(max(b_need, 8 * int(rcnt.sum()), 64))
+        A2, B2 = self.gen_bufs[1].get(a2), self.gen_bufs[2].get(b2)
+        self.dev.upload(self.d_rtab, rtab)
+        N.check(ctx, L.kman_dshard_extract(ctx, c_void_p(sh.codes.ptr), sh.n_eff, self.n_bases_q, self.k, self.flags,
+                                           self.fmode, c_void_p(self.d_hist.ptr), c_void_p(self.d_rtab.ptr),
+                                           c_void_p(A.ptr)), "kman_dshard_extract")
+        cl = np.asarray(c_local, np.uint64)
+        at = 0
+        recv_at = []
+        for s_ in range(S_):
+            ssc = np.zeros(G, np.uint64)
+            sso = np.zeros(G, np.uint64)
+            for q in range(G):
+                lo_q = part_of(cuts, R, q, r)[0]
+                b0, b1 = bounds[q][s_], bounds[q][s_ + 1]
+                ssc[q] = cl[b0:b1].sum()
+                sso[q] = so[q] + cl[lo_q:b0].sum()
+            rc_s = plans[s_].sum(axis=1).astype(np.uint64)
+            ro_s = (np.concatenate([[0], np.cumsum(rc_s)[:-1]]) + at).astype(np.uint64)
+            recv_at.append(at)
+            at += int(rc_s.sum())
+            yield ("alltoallv_async", (A.ptr, ssc, sso, B.ptr, rc_s, ro_s, 8, s_))
+        start, mine = n_out, []
+        for s_ in range(S_):
+            yield ("comm_wait", s_)
+            b0, b1 = my[s_], my[s_ + 1]
+            if b1 <= b0:
+                continue
+            got = c_uint64(0)
+            ret = L.kman_dround_finish(ctx, c_void_p(B.ptr + 8 * recv_at[s_]), self.k, self.flags, self.fmode, G,
+                                       self.n_bases_q, b0, b1 - b0, _u64p(plans[s_].reshape(-1)),
+                                       c_void_p(A2.ptr), A2.nbytes, c_void_p(B2.ptr), B2.nbytes,
+                                       c_void_p(ok_.ptr + 8 * n_out), c_void_p(ov_.ptr + vb * n_out), vb, byref(got))
+            if ret == N.KMAN_EPARTIAL:
+                mine.append(self._failed_ranges())
+            elif ret != N.KMAN_OK:
+                N.check(ctx, ret, "kman_dround_finish")
+            n_out += int(got.value)
+        f = yield ("allreduce", np.array([0, len(mine)], np.uint64))
+        if int(f[1]):
+            self.partial_rounds += 1
+            mine = np.concatenate(mine) if mine else np.zeros((0, 2), np.uint64)
+            rows = yield from self._redo_ranges(mine, n_out - start, A, B, ok_, ov_, start, vb)
+            n_out = start + rows
+        return n_out
 
     def _failed_ranges(self) -> np.ndarray:
         """[lo, hi] key ranges the last kman_dround_finish left out."""

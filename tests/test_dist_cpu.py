@@ -262,3 +262,30 @@ def test_config4_plan_fits_one_mi355x():
     for q in range(G):
         for r in range(R):
             assert pl.arenas(C, cuts, R, q, r) is not None
+
+
+@pytest.mark.parametrize("G,S", [(1, 4), (2, 4), (3, 2), (8, 4)])
+def test_round_pieces_partition_each_part(G, S):
+    """The overlapped rounds' pieces (dist.round_pieces): each destination's
+    part cut into S contiguous, ordered bucket ranges that cover it exactly,
+    the same on every rank, of about equal k-mers."""
+    from kman_amd import dist
+
+    rng = np.random.default_rng(G * 10 + S)
+    C = rng.integers(0, 50_000, size=(G, 256)).astype(np.uint64)
+    C[:, 17] += 2_000_000  # one heavy bucket
+    pl = dist.RoundPlanner(21, 0, 1, G, 10**9)
+    R, cuts, _, _ = pl.plan(C, 1 << 40)
+    for r in range(R):
+        bounds = dist.round_pieces(C, cuts, G, R, r, S)
+        assert len(bounds) == G
+        tot = C.sum(axis=0).astype(np.int64)
+        for q in range(G):
+            lo, hi = dist.part_of(cuts, R, q, r)
+            b = bounds[q]
+            assert len(b) == S + 1 and b[0] == lo and b[-1] == hi
+            assert all(x <= y for x, y in zip(b, b[1:]))
+            if hi - lo >= S and tot[lo:hi].sum():
+                sizes = [tot[x:y].sum() for x, y in zip(b, b[1:])]
+                # no piece above its share plus one bucket
+                assert max(sizes) <= tot[lo:hi].sum() / S + tot[lo:hi].max()
