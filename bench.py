@@ -12,8 +12,9 @@ the FASTA bytes already resident in HBM:
 leaving the (k-mer, pos) rows device-resident.  ``value`` is that rate.
 Reported beside it:
   * ``pinned_host``: the same step starting from pinned host bytes: chunked
-    H2D copies on a copy stream overlapping the parse of the previous chunk
-    (shard.StreamedPipeline), plus the plain H2D time of the text;
+    H2D copies on a copy stream overlapping the parse and the first region
+    pass of the previous chunk (shard.StreamedPipeline), beside the serial
+    variant and the plain H2D time of the text;
   * ``output``: device text formatting and the file write of a bounded
     slice of the rows, as rates and as ms extrapolated to all rows;
   * ``file_to_file``: the CLI (`kmer count`) on a bounded FASTA file;
@@ -265,23 +266,28 @@ def run_single(args):
             _copy()
             h2d = time.perf_counter() - t0
             buf.free()
-            sp_ = shard.StreamedPipeline(dev, rd, args.k, args.mode, chunk_bytes=args.chunk_mb << 20)
-            for _ in range(args.warmup):
-                sp_.step()
-            dev.sync()
-            t0 = time.perf_counter()
-            n = 0
-            for _ in range(args.steps):
-                n += sp_.step()
-            dev.sync()
-            el = time.perf_counter() - t0
-            sp_.free()
-            out["pinned_host"] = {"value": n / el, "unit": "k-mers/s", "ms_per_step": el / args.steps * 1e3,
+            lines = {}
+            for ov in (True, False):
+                sp_ = shard.StreamedPipeline(dev, rd, args.k, args.mode, chunk_bytes=args.chunk_mb << 20, overlap=ov)
+                for _ in range(args.warmup):
+                    sp_.step()
+                dev.sync()
+                t0 = time.perf_counter()
+                n = 0
+                for _ in range(args.steps):
+                    n += sp_.step()
+                dev.sync()
+                lines[ov] = (n / (time.perf_counter() - t0), (time.perf_counter() - t0) / args.steps * 1e3)
+                sp_.free()
+            out["pinned_host"] = {"value": lines[True][0], "unit": "k-mers/s", "ms_per_step": lines[True][1],
+                                  "serial_value": lines[False][0], "serial_ms_per_step": lines[False][1],
                                   "h2d_ms": h2d * 1e3, "h2d_gbs": rd.size / h2d / 1e9, "chunk_mb": args.chunk_mb,
-                                  "note": "step from pinned host bytes: %d MiB chunks copied on a copy stream behind "
-                                          "the parse of the previous chunk, then the region path (which needs "
-                                          "the whole stream: copy + compute, not overlapped); h2d_ms = one warm "
-                                          "async copy of the whole text on the copy stream" % args.chunk_mb}
+                                  "note": "step from pinned host bytes: %d MiB chunks copied on a copy stream; the "
+                                          "parse and the region path's first pass (kman_groups_begin / _extract) "
+                                          "of chunk i run behind the copy of chunk i + 1, pass 1 + finish after "
+                                          "the last chunk (kman_groups_end); serial_* = the whole load, then "
+                                          "kman_groups; h2d_ms = one warm async copy of the whole text on the "
+                                          "copy stream" % args.chunk_mb}
         except Exception as e:
             out["pinned_host"] = {"error": repr(e)}
         finally:

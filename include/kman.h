@@ -110,7 +110,9 @@ int kman_memset(kman_ctx *ctx, void *dst, int value, size_t bytes);
 /* Chunked uploads that overlap the context's work: kman_copy_h2d_async
  * enqueues a copy (from pinned memory for real overlap) on the context's copy
  * stream and marks event `slot` (0..3); kman_copy_wait makes the work stream
- * wait for that event; kman_copy_sync drains the copy stream. */
+ * wait for that event; kman_copy_sync drains the copy stream.  The copy does
+ * not wait for the work stream: a caller reusing a destination that queued
+ * work still reads synchronises first (kman_sync). */
 int kman_copy_h2d_async(kman_ctx *ctx, void *dst, const void *src, size_t bytes, int slot);
 int kman_copy_wait(kman_ctx *ctx, int slot);
 int kman_copy_sync(kman_ctx *ctx);
@@ -255,6 +257,28 @@ int kman_groups_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, uin
 int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags, int mode,
                 void *d_work, uint64_t work_bytes, uint64_t *d_okeys, void *d_ovals, uint32_t oval_bytes,
                 uint64_t *n_kmers, uint64_t *n_out);
+
+/* kman_groups in three calls, so that its first pass (the extraction) runs
+ * while the FASTA is still arriving (the reference reads and extracts one
+ * record at a time, batcher.py:454-470 -> seq.py:285-328):
+ *   kman_groups_begin    plans, clears the work area and opens the pass;
+ *                        *n_tiles tiles, tile t reads codes
+ *                        [t * tile_bases, (t + 1) * tile_bases + 64)
+ *                        (*n_tiles = 0: the pass runs whole at the end)
+ *   kman_groups_extract  extracts tiles up to tile_hi (exclusive) once their
+ *                        codes are final; call in increasing tile_hi
+ *   kman_groups_end      extracts the rest, then as kman_groups
+ * Every call takes the arguments kman_groups takes (n_bases = the final
+ * total); no other call of this ctx that uses look-back status words (the
+ * general extraction, sorts, other kman_groups) may come in between.  The
+ * result equals kman_groups'. */
+int kman_groups_begin(kman_ctx *ctx, uint64_t n_bases, uint32_t k, uint32_t flags, int mode, void *d_work,
+                      uint64_t work_bytes, uint32_t *n_tiles, uint64_t *tile_bases);
+int kman_groups_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                        int mode, void *d_work, uint64_t work_bytes, uint32_t tile_hi);
+int kman_groups_end(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags, int mode,
+                    void *d_work, uint64_t work_bytes, uint64_t *d_okeys, void *d_ovals, uint32_t oval_bytes,
+                    uint64_t *n_kmers, uint64_t *n_out);
 
 /* kman_groups across G ranks, in key rounds (one process per GPU over RCCL;
  * kman_amd/dist.py runs the collectives in between).  Rank q

@@ -123,6 +123,19 @@ SIGNATURES = {
         [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_int, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32,
          POINTER(c_uint64), POINTER(c_uint64)],
     ),
+    "kman_groups_begin": (
+        c_int,
+        [c_void_p, c_uint64, c_uint32, c_uint32, c_int, c_void_p, c_uint64, POINTER(c_uint32), POINTER(c_uint64)],
+    ),
+    "kman_groups_extract": (
+        c_int,
+        [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_int, c_void_p, c_uint64, c_uint32],
+    ),
+    "kman_groups_end": (
+        c_int,
+        [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_int, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32,
+         POINTER(c_uint64), POINTER(c_uint64)],
+    ),
     "kman_dshard_plan": (c_int, [c_uint64, c_uint64, c_uint32, c_uint32, c_int]),
     "kman_dshard_hist": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_uint32, c_uint32, c_int, c_void_p, c_void_p]),
     "kman_dshard_extract": (

@@ -59,6 +59,11 @@ struct kman_ctx {
     // key ranges [lo, hi] (pairs) that the last kman_dround_finish left out
     // (KMAN_EPARTIAL): regions that overflowed a capacity
     std::vector<uint64_t> failed;
+    // kman_groups_begin .. kman_groups_end: pass 0 by tile ranges as the
+    // codes arrive (the look-back epoch it runs in, the next tile)
+    uint32_t grp_epoch = 0;
+    uint32_t grp_next = 0;
+    uint32_t grp_tiles = 0;
 };
 
 // RAII launch timer: records an event pair around the launches in its scope.

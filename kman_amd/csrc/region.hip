@@ -101,8 +101,14 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 // round, and their windows are dropped before the rank (keep bitmap).
 // NS: position segments (look-back chains); RS for the shard path (EX), more
 // for kman_groups (shorter chains, pass 1 finds segments in an LDS table)
+// IL (kman_groups): interleaved chains -- tile t is step t / NS of chain
+// t % NS (status words chain-major), so any prefix of the stream spreads over
+// every chain and pass 0 can run in consecutive launches over tile ranges as
+// the codes arrive (kman_groups_extract): the epoch's ticket counter carries
+// on from one launch to the next, and a launch of n blocks takes the next n
+// tiles in stream order.
 template <int EI, bool RC, bool ATOMIC, bool CANON = false, bool BR = false, bool EX = false, int NS = RS,
-          int XLB = LB>
+          int XLB = LB, bool IL = false>
 __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI == 8 ? 8 : 4)))) void rg_extract(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
                                                  uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
                                                  uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ cnt0,
@@ -125,12 +131,28 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     __shared__ uint32_t keep[EX ? RADIX / 32 : 1];
 
     const uint32_t cid = (uint32_t)grab_tile(counter, &lds_tile);
-    const uint32_t sgi = cid % NS, jj = cid / NS;
-    const uint32_t t0 = sgi * seg_tiles;
-    const uint32_t t1 = t0 + seg_tiles < n_tiles ? t0 + seg_tiles : n_tiles;
-    if (t0 + jj >= t1) return;  // (block-uniform) past a segment's end
-    const int64_t tile = (int64_t)t0 + jj;
-    const int64_t first = t0;
+    uint32_t sgi, jj;
+    int64_t tile, first, stile;  // data tile; the chain's first status slot; this tile's status slot
+    bool last;                   // the chain's last tile
+    if (IL) {
+        tile = cid;
+        if (tile >= (int64_t)n_tiles) return;  // (block-uniform)
+        sgi = (uint32_t)(tile % NS);
+        jj = (uint32_t)(tile / NS);
+        first = (int64_t)sgi * seg_tiles;
+        stile = first + jj;
+        last = tile + NS >= (int64_t)n_tiles;
+    } else {
+        sgi = cid % NS;
+        jj = cid / NS;
+        const uint32_t t0 = sgi * seg_tiles;
+        const uint32_t t1 = t0 + seg_tiles < n_tiles ? t0 + seg_tiles : n_tiles;
+        if (t0 + jj >= t1) return;  // (block-uniform) past a segment's end
+        tile = (int64_t)t0 + jj;
+        first = t0;
+        stile = tile;
+        last = tile == (int64_t)t1 - 1;
+    }
     RSTAMP(tile, 0);
     const int lane = lane_id();
     const int w = threadIdx.x >> 6;
@@ -197,7 +219,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
         __syncthreads();
         // (EX: a digit not kept this round has no chain: nothing published)
         if (threadIdx.x < RADIX && KEPT(threadIdx.x))
-            digit_publish(status + threadIdx.x, tile, first, thist[threadIdx.x], epoch);
+            digit_publish(status + threadIdx.x, stile, first, thist[threadIdx.x], epoch);
     } else if (ATOMIC) {
 #pragma unroll
         for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&whist[w][XDIGIT(key[i])], 1u) : 0u;
@@ -207,14 +229,14 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
 #pragma unroll
             for (int ww = 0; ww < NWAVE; ww++) c += whist[ww][threadIdx.x];
             thist[threadIdx.x] = c;
-            digit_publish(status + threadIdx.x, tile, first, c, epoch);
+            digit_publish(status + threadIdx.x, stile, first, c, epoch);
         }
     } else {
 #pragma unroll
         for (int i = 0; i < SI; i++)
             if (ib + i * 64 < tcnt) atomicAdd(&thist[XDIGIT(key[i])], 1u);
         __syncthreads();
-        if (threadIdx.x < RADIX) digit_publish(status + threadIdx.x, tile, first, thist[threadIdx.x], epoch);
+        if (threadIdx.x < RADIX) digit_publish(status + threadIdx.x, stile, first, thist[threadIdx.x], epoch);
 #pragma unroll
         for (int i = 0; i < SI; i++) rank[i] = ballot_rank(whist[w], XDIGIT(key[i]), ib + i * 64 < tcnt, B1);
     }
@@ -248,7 +270,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
             const uint32_t d = threadIdx.x / TPD;
             const uint64_t excl =
                 (dbg & 1) ? 0ull  // timing ablation only: no look-back (wrong offsets)
-                          : group_lookback<TPD, XLB>(status + d, tile, first, thist[d], epoch, err);
+                          : group_lookback<TPD, XLB>(status + d, stile, first, thist[d], epoch, err);
             if (threadIdx.x % TPD == 0) {
                 const uint64_t incl = excl + thist[d];
                 if (EX) {  // (only kept digits get here)
@@ -260,7 +282,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
                 } else {
                     gexcl[d] = excl;
                     if (incl > C0) atomicOr(err, ERR_REGION);
-                    if (tile == (int64_t)t1 - 1) cnt0[d * NS + sgi] = (uint32_t)(incl < C0 ? incl : C0);
+                    if (last) cnt0[d * NS + sgi] = (uint32_t)(incl < C0 ? incl : C0);
                 }
             }
         }
@@ -1426,16 +1448,25 @@ int run_finish(kman_ctx *ctx, const FinishArgs &f, int mode, uint64_t *okeys, vo
 // less at the same speed (3.69-3.73 vs 3.77-3.86 ms; KMAN_RG_XLB=2/4/8 for A/B)
 template <int EI, bool RC, bool CANON, int NS, int XLB = 1>
 void launch_extract_ns(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
-                       uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
+                       uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp,
+                       uint32_t n_launch) {
     if (NS == RS && XLB == 1) {
         static const char *e = getenv("KMAN_RG_XLB");
         const int x = e ? atoi(e) : 1;
         if (x == 2) return launch_extract_ns<EI, RC, CANON, NS, 2>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter,
-                                                                    dbg, stp);
+                                                                    dbg, stp, n_launch);
         if (x == 4) return launch_extract_ns<EI, RC, CANON, NS, 4>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter,
-                                                                    dbg, stp);
+                                                                    dbg, stp, n_launch);
         if (x == 8) return launch_extract_ns<EI, RC, CANON, NS, 8>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter,
-                                                                    dbg, stp);
+                                                                    dbg, stp, n_launch);
+    }
+    static const bool il_env = getenv("KMAN_RG_IL") && atoi(getenv("KMAN_RG_IL")) != 0;
+    if (n_launch || il_env) {  // interleaved chains, tile = block ticket (a tile range per launch)
+        hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS, XLB, true>),
+                           dim3(n_launch ? n_launch : p.n_tiles0), dim3(RT), 0, ctx->stream, codes, n_bases, (int)k,
+                           p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch, ctx->d_err, dbg,
+                           stp, nullptr);
+        return;
     }
     hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS, XLB>), dim3(NS * p.seg_tiles), dim3(RT), 0,
                        ctx->stream, codes, n_bases, (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status,
@@ -1444,15 +1475,19 @@ void launch_extract_ns(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes,
 
 template <int EI, bool RC, bool CANON = false>
 void launch_extract(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
-                    uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
+                    uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp,
+                    uint32_t n_launch) {
     const uint32_t grid = RS * p.seg_tiles;
     const char *e = getenv("KMAN_RG_EXTRACT");  // 1 (default): block-wide rank; 0: stable per-wave rank (RS chains)
     if (p.S == 256)
-        launch_extract_ns<EI, RC, CANON, 256>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
+        launch_extract_ns<EI, RC, CANON, 256>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp,
+                                               n_launch);
     else if (p.S == 128)
-        launch_extract_ns<EI, RC, CANON, 128>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
-    else if (!e || atoi(e) != 0)
-        launch_extract_ns<EI, RC, CANON, RS>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
+        launch_extract_ns<EI, RC, CANON, 128>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp,
+                                               n_launch);
+    else if (!e || atoi(e) != 0 || n_launch)
+        launch_extract_ns<EI, RC, CANON, RS>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp,
+                                               n_launch);
     else if (ctx->lds_atomic_ordered)
         hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON>), dim3(grid), dim3(RT), 0, ctx->stream, codes, n_bases,
                            (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch,
@@ -1484,21 +1519,24 @@ void launch_xown(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint6
     }
 }
 
+// n_launch > 0: the next n_launch tiles of pass 0 (interleaved chains; the
+// epoch's ticket counter carries the tile across launches)
 void launch_extract_any(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
-                        uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
+                        uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp,
+                        uint32_t n_launch = 0) {
     if (p.own) {
         if (p.canon) launch_xown<8, false, true>(ctx, p, codes, n_bases, k, r0, c0, counter, stp);
         else if (p.rc) launch_xown<4, true>(ctx, p, codes, n_bases, k, r0, c0, counter, stp);
         else launch_xown<8, false>(ctx, p, codes, n_bases, k, r0, c0, counter, stp);
         return;
     }
-    if (p.canon && p.ei == 12) launch_extract<12, false, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
-    else if (p.canon) launch_extract<16, false, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
-    else if (p.rc && p.ei == 6) launch_extract<6, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
-    else if (p.rc) launch_extract<8, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
-    else if (p.ei == 12) launch_extract<12, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
-    else if (p.ei == 8) launch_extract<8, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
-    else launch_extract<16, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp);
+    if (p.canon && p.ei == 12) launch_extract<12, false, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
+    else if (p.canon) launch_extract<16, false, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
+    else if (p.rc && p.ei == 6) launch_extract<6, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
+    else if (p.rc) launch_extract<8, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
+    else if (p.ei == 12) launch_extract<12, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
+    else if (p.ei == 8) launch_extract<8, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
+    else launch_extract<16, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
 }
 
 // mean phase durations (us) per kernel from the stamp rows; frees the buffers
@@ -1544,55 +1582,58 @@ extern "C" int kman_groups_plan(uint64_t n_bases, uint32_t k, uint32_t flags, in
     return rc;
 }
 
-extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
-                           int mode, void *d_work, uint64_t work_bytes, uint64_t *d_okeys, void *d_ovals,
-                           uint32_t oval_bytes, uint64_t *n_kmers, uint64_t *n_out) {
-    if (!ctx || !n_kmers || !n_out) return KMAN_EINVAL;
-    *n_kmers = 0;
-    *n_out = 0;
+namespace {
+
+// one kman_groups call: the plan and the work-area carve-up
+struct GroupsCall {
     RegionPlan p;
+    uint64_t *r0, *r1;
+    uint32_t *c0, *c1;
+    uint32_t nreg;
+};
+
+int groups_setup(kman_ctx *ctx, uint64_t n_bases, uint32_t k, uint32_t flags, int mode, void *d_work,
+                 uint64_t work_bytes, GroupsCall *g) {
+    RegionPlan &p = g->p;
     const int prc = make_plan(n_bases, k, flags, mode, &p);
     if (prc == KMAN_EINVAL) return kman_fail(ctx, KMAN_EINVAL, "kman_groups: bad mode or k");
     if (prc != KMAN_OK) return prc;
-    if (!d_codes || !d_work || !d_okeys || !d_ovals) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    if (!d_work) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
     if (work_bytes < p.bytes)
         return kman_fail(ctx, KMAN_ECAP, "work area %llu < %llu bytes", (unsigned long long)work_bytes,
                          (unsigned long long)p.bytes);
-    if (oval_bytes != 4 && oval_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "oval_bytes must be 4 or 8");
-    if (oval_bytes == 4 && mode == KMAN_FINISH_UNIQ && (p.rc ? p.W : 2 * p.W) - 1 > 0xffffffffull)
-        return kman_fail(ctx, KMAN_EINVAL, "u32 pos cannot address %llu bases", (unsigned long long)n_bases);
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    const char *dbg_env = getenv("KMAN_RG_DBG");  // timing ablations (tools/regionbench.py)
-    const uint32_t dbg = dbg_env ? (uint32_t)atoi(dbg_env) : 0u;
-    uint64_t *r0 = (uint64_t *)d_work;
-    uint64_t *r1 = (uint64_t *)((char *)d_work + p.off_r1);
-    uint32_t *c0 = (uint32_t *)((char *)d_work + p.off_c0);
-    uint32_t *c1 = (uint32_t *)((char *)d_work + p.off_c1);
-    const uint32_t nreg = 1u << (B1 + p.B2);
-    HIP_TRY(ctx, hipMemsetAsync(c0, 0, p.bytes - p.off_c0, ctx->stream));
-    uint64_t *stamps[3] = {nullptr, nullptr, nullptr};
-    const uint64_t stamp_rows[3] = {p.n_tiles0, (uint64_t)p.maxt1 * RADIX, nreg};
-    if (getenv("KMAN_RG_STAMPS"))
-        for (int q = 0; q < 3; q++) {
-            HIP_TRY(ctx, hipMalloc((void **)&stamps[q], stamp_rows[q] * 64));
-            HIP_TRY(ctx, hipMemsetAsync(stamps[q], 0, stamp_rows[q] * 64, ctx->stream));
-        }
+    g->r0 = (uint64_t *)d_work;
+    g->r1 = (uint64_t *)((char *)d_work + p.off_r1);
+    g->c0 = (uint32_t *)((char *)d_work + p.off_c0);
+    g->c1 = (uint32_t *)((char *)d_work + p.off_c1);
+    g->nreg = 1u << (B1 + p.B2);
+    return KMAN_OK;
+}
+
+int groups_outputs_ok(kman_ctx *ctx, const GroupsCall &g, int mode, const void *d_okeys, const void *d_ovals,
+                      uint32_t oval_bytes, uint64_t n_bases) {
+    if (!d_okeys || !d_ovals) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    if (oval_bytes != 4 && oval_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "oval_bytes must be 4 or 8");
+    if (oval_bytes == 4 && mode == KMAN_FINISH_UNIQ && (g.p.rc ? g.p.W : 2 * g.p.W) - 1 > 0xffffffffull)
+        return kman_fail(ctx, KMAN_EINVAL, "u32 pos cannot address %llu bases", (unsigned long long)n_bases);
+    return KMAN_OK;
+}
+
+// pass 1 (per bucket, by the next B2 bits), the finish (one block per
+// region) and the results: output count (the last region's inclusive),
+// region-0 counts (k-mers), error word
+int groups_tail(kman_ctx *ctx, const GroupsCall &g, int mode, uint64_t *d_okeys, void *d_ovals, uint32_t oval_bytes,
+                uint32_t dbg, uint64_t **stamps, const uint64_t *stamp_rows, uint64_t *n_kmers, uint64_t *n_out) {
+    const RegionPlan &p = g.p;
     uint32_t epoch, *counter;
-    // pass 0: extraction by the top 8 bits
-    KMAN_TRY(kman_lookback_begin(ctx, p.own ? 1 : (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
-    {
-        KTimer kt_(ctx, "region_extract");
-        launch_extract_any(ctx, p, d_codes, n_bases, k, r0, c0, epoch, counter, dbg >> 8, stamps[0]);
-        HIP_TRY(ctx, hipGetLastError());
-    }
-    // pass 1: per bucket, by the next B2 bits (H block-owned chains per bucket)
     KMAN_TRY(kman_lookback_begin(ctx, 1, &epoch, &counter));  // (the chain counter only)
     {
         KTimer kt_(ctx, "region_pass");
         PassArgs pa{};
-        pa.in = r0;
+        pa.in = g.r0;
         pa.seg_base = nullptr;
-        pa.seg_cnt = c0;
+        pa.seg_cnt = g.c0;
         pa.stride = p.C0;
         pa.nbk = RADIX;
         pa.nsg = p.S;
@@ -1600,25 +1641,23 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
         pa.H = p.H;
         pa.shift = p.Q + p.rest;
         pa.bits = p.B2;
-        pa.out = r1;
+        pa.out = g.r1;
         pa.C1 = p.C1h;
-        pa.cnt1 = c1;
+        pa.cnt1 = g.c1;
         launch_pass(ctx, pa, counter, dbg >> 4, stamps[1]);
         HIP_TRY(ctx, hipGetLastError());
     }
-    // finish: one block per region
     {
-        FinishArgs f{r1, p.C1h, c1, p.Q, p.rest, (uint32_t)p.rc, 0, 0, nreg};
+        FinishArgs f{g.r1, p.C1h, g.c1, p.Q, p.rest, (uint32_t)p.rc, 0, 0, g.nreg};
         f.fsub = p.H;
         KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, dbg & 15, stamps[2]));
     }
     if (stamps[0]) KMAN_TRY(report_stamps(ctx, stamps, stamp_rows));
-    // results: output count (last region's inclusive), region-0 counts (k-mers), error word
     uint64_t *h = ctx->h_small;
-    HIP_TRY(ctx, hipMemcpyAsync(h + 4, ctx->d_status + (nreg - 1), 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(h + 4, ctx->d_status + (g.nreg - 1), 8, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(h + 8, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
     std::vector<uint32_t> hc((size_t)RADIX * p.S);
-    HIP_TRY(ctx, hipMemcpyAsync(hc.data(), c0, hc.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(hc.data(), g.c0, hc.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     uint32_t e;
     memcpy(&e, h + 8, 4);
@@ -1636,6 +1675,114 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
     *n_kmers = nk;
     *n_out = wd & ST_VMASK;
     return KMAN_OK;
+}
+
+}  // namespace
+
+extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                           int mode, void *d_work, uint64_t work_bytes, uint64_t *d_okeys, void *d_ovals,
+                           uint32_t oval_bytes, uint64_t *n_kmers, uint64_t *n_out) {
+    if (!ctx || !n_kmers || !n_out) return KMAN_EINVAL;
+    *n_kmers = 0;
+    *n_out = 0;
+    GroupsCall g;
+    KMAN_TRY(groups_setup(ctx, n_bases, k, flags, mode, d_work, work_bytes, &g));
+    if (!d_codes) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    KMAN_TRY(groups_outputs_ok(ctx, g, mode, d_okeys, d_ovals, oval_bytes, n_bases));
+    const RegionPlan &p = g.p;
+    const char *dbg_env = getenv("KMAN_RG_DBG");  // timing ablations (tools/regionbench.py)
+    const uint32_t dbg = dbg_env ? (uint32_t)atoi(dbg_env) : 0u;
+    HIP_TRY(ctx, hipMemsetAsync(g.c0, 0, p.bytes - p.off_c0, ctx->stream));
+    uint64_t *stamps[3] = {nullptr, nullptr, nullptr};
+    const uint64_t stamp_rows[3] = {p.n_tiles0, (uint64_t)p.maxt1 * RADIX, g.nreg};
+    if (getenv("KMAN_RG_STAMPS"))
+        for (int q = 0; q < 3; q++) {
+            HIP_TRY(ctx, hipMalloc((void **)&stamps[q], stamp_rows[q] * 64));
+            HIP_TRY(ctx, hipMemsetAsync(stamps[q], 0, stamp_rows[q] * 64, ctx->stream));
+        }
+    uint32_t epoch, *counter;
+    // pass 0: extraction by the top 8 bits
+    KMAN_TRY(kman_lookback_begin(ctx, p.own ? 1 : (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
+    {
+        KTimer kt_(ctx, "region_extract");
+        launch_extract_any(ctx, p, d_codes, n_bases, k, g.r0, g.c0, epoch, counter, dbg >> 8, stamps[0]);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    return groups_tail(ctx, g, mode, d_okeys, d_ovals, oval_bytes, dbg, stamps, stamp_rows, n_kmers, n_out);
+}
+
+extern "C" int kman_groups_begin(kman_ctx *ctx, uint64_t n_bases, uint32_t k, uint32_t flags, int mode,
+                                 void *d_work, uint64_t work_bytes, uint32_t *n_tiles, uint64_t *tile_bases) {
+    if (!ctx || !n_tiles || !tile_bases) return KMAN_EINVAL;
+    *n_tiles = 0;
+    *tile_bases = 0;
+    GroupsCall g;
+    KMAN_TRY(groups_setup(ctx, n_bases, k, flags, mode, d_work, work_bytes, &g));
+    const RegionPlan &p = g.p;
+    HIP_TRY(ctx, hipMemsetAsync(g.c0, 0, p.bytes - p.off_c0, ctx->stream));
+    uint32_t epoch, *counter;
+    KMAN_TRY(kman_lookback_begin(ctx, p.own ? 1 : (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
+    ctx->grp_epoch = epoch;
+    ctx->grp_next = 0;
+    ctx->grp_tiles = p.n_tiles0;
+    // (the opt-in owned pass 0 walks whole chains: it runs at kman_groups_end)
+    *n_tiles = p.own ? 0u : p.n_tiles0;
+    *tile_bases = p.own ? 0u : (uint64_t)RT * p.ei;
+    return KMAN_OK;
+}
+
+namespace {
+int groups_extract_to(kman_ctx *ctx, const GroupsCall &g, const uint8_t *d_codes, uint64_t n_bases, uint32_t k,
+                      uint32_t tile_hi) {
+    const RegionPlan &p = g.p;
+    if (ctx->grp_epoch == 0 || ctx->grp_epoch != ctx->epoch || ctx->grp_tiles != p.n_tiles0)
+        return kman_fail(ctx, KMAN_EINVAL, "kman_groups_extract: no kman_groups_begin of this input before it, or "
+                                           "another look-back call in between");
+    if (!d_codes) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    if (tile_hi > p.n_tiles0) tile_hi = p.n_tiles0;
+    uint32_t *counter = ctx->d_counters + ctx->grp_epoch;
+    if (p.own) {
+        if (tile_hi < p.n_tiles0 || ctx->grp_next) return KMAN_OK;
+        KTimer kt_(ctx, "region_extract");
+        launch_extract_any(ctx, p, d_codes, n_bases, k, g.r0, g.c0, ctx->grp_epoch, counter, 0, nullptr);
+        HIP_TRY(ctx, hipGetLastError());
+        ctx->grp_next = p.n_tiles0;
+        return KMAN_OK;
+    }
+    if (tile_hi <= ctx->grp_next) return KMAN_OK;
+    {
+        KTimer kt_(ctx, "region_extract");
+        launch_extract_any(ctx, p, d_codes, n_bases, k, g.r0, g.c0, ctx->grp_epoch, counter, 0, nullptr,
+                           tile_hi - ctx->grp_next);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    ctx->grp_next = tile_hi;
+    return KMAN_OK;
+}
+}  // namespace
+
+extern "C" int kman_groups_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k,
+                                   uint32_t flags, int mode, void *d_work, uint64_t work_bytes, uint32_t tile_hi) {
+    if (!ctx) return KMAN_EINVAL;
+    GroupsCall g;
+    KMAN_TRY(groups_setup(ctx, n_bases, k, flags, mode, d_work, work_bytes, &g));
+    return groups_extract_to(ctx, g, d_codes, n_bases, k, tile_hi);
+}
+
+extern "C" int kman_groups_end(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                               int mode, void *d_work, uint64_t work_bytes, uint64_t *d_okeys, void *d_ovals,
+                               uint32_t oval_bytes, uint64_t *n_kmers, uint64_t *n_out) {
+    if (!ctx || !n_kmers || !n_out) return KMAN_EINVAL;
+    *n_kmers = 0;
+    *n_out = 0;
+    GroupsCall g;
+    KMAN_TRY(groups_setup(ctx, n_bases, k, flags, mode, d_work, work_bytes, &g));
+    KMAN_TRY(groups_outputs_ok(ctx, g, mode, d_okeys, d_ovals, oval_bytes, n_bases));
+    KMAN_TRY(groups_extract_to(ctx, g, d_codes, n_bases, k, g.p.n_tiles0));
+    ctx->grp_epoch = 0;
+    uint64_t *stamps[3] = {nullptr, nullptr, nullptr};
+    const uint64_t stamp_rows[3] = {0, 0, 0};
+    return groups_tail(ctx, g, mode, d_okeys, d_ovals, oval_bytes, 0, stamps, stamp_rows, n_kmers, n_out);
 }
 
 namespace {

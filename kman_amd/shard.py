@@ -289,9 +289,11 @@ class ShardLoader:
         c = self.dev.download(self.shard.codes, 1, np.uint8, offset=at)
         self.dev.upload(self.shard.codes, c | np.uint8(8), offset=at)
 
-    def load(self) -> ShardCodes:
+    def load(self, on_chunk=None) -> ShardCodes:
         """Upload + parse every chunk (the next chunk's copy behind the
-        current parse), then the halo; seal the codes after k-1 halo bases."""
+        current parse), then the halo; seal the codes after k-1 halo bases.
+        on_chunk(n) runs after each chunk's parse, when the codes below n are
+        final (kman_groups_extract queues work behind the next copy)."""
         sh, sp, dev = self.shard, self.spec, self.dev
         n, hdrs, seqs = 0, [], []
         cuts = self.cuts
@@ -302,7 +304,9 @@ class ShardLoader:
         for i, (lo, hi) in enumerate(pieces):
             slot = i & 1
             if i + 1 < len(pieces):
-                self._stage(slot ^ 1, *pieces[i + 1])  # (the parse of chunk i - 1 has finished: it synchronises)
+                if i:  # the parse of chunk i - 1 (slot ^ 1) may still run: the copy must not overwrite its text
+                    dev.sync()
+                self._stage(slot ^ 1, *pieces[i + 1])
             if not keep:
                 self._wait(slot)
             m, h, s = self._parse(slot, lo, hi, n)
@@ -311,6 +315,8 @@ class ShardLoader:
             n += m
             hdrs += h
             seqs += s
+            if on_chunk is not None and i + 1 < len(pieces):
+                on_chunk(n)
         sh.n_own = n
         halo = 0
         if sp.halo_end > sp.own_end:
@@ -362,14 +368,17 @@ def load_text(dev: engine.Device, text: bytes, chunk_bytes: int = 256 << 20) -> 
 class StreamedPipeline:
     """``kmer count|uniq`` of a FASTA held in (pinned) host memory, as the
     reference's CLI runs it from its input bytes: every step uploads the text
-    in chunks -- each chunk's copy on the copy stream behind the parse of the
-    previous one -- and runs the region path (kman_groups) on the codes,
-    leaving the result device-resident (bench.py's pinned-host line)."""
+    in chunks -- each chunk's copy on the copy stream behind the parse and
+    (overlap) the region path's first pass over the previous one -- and
+    finishes the region path (kman_groups) on the codes, leaving the result
+    device-resident (bench.py's pinned-host line)."""
 
-    def __init__(self, dev: engine.Device, reader, k: int, mode: str = "uniq", chunk_bytes: int = 128 << 20):
-        self.dev, self.k, self.mode = dev, k, mode
+    def __init__(self, dev: engine.Device, reader, k: int, mode: str = "uniq", chunk_bytes: int = 128 << 20,
+                 overlap: bool = True):
+        self.dev, self.k, self.mode, self.overlap = dev, k, mode, overlap
         self.loader = ShardLoader(dev, reader, shard_specs(reader, 1, k)[0], k, chunk_bytes)
         sh = self.loader.load()
+        self.n_bases = sh.n_own
         self.m = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
         self.flags = engine.flags_for(False, mode == "uniq")
         wb = ctypes.c_uint64(0)
@@ -382,12 +391,36 @@ class StreamedPipeline:
         self.n_kmers = self.n_out = 0
 
     def step(self) -> int:
-        sh = self.loader.load()
+        """One pass from the host bytes: with `overlap`, kman_groups' first
+        pass runs chunk by chunk (kman_groups_begin / _extract / _end) behind
+        the copies of the following chunks; else kman_groups after the load."""
+        L, ctx = N.lib(), self.dev.ctx
         nk, no = ctypes.c_uint64(0), ctypes.c_uint64(0)
-        L = N.lib()
-        N.check(self.dev.ctx, L.kman_groups(self.dev.ctx, c_void_p(sh.codes.ptr), sh.n_own, self.k, self.flags, self.m,
-                                            c_void_p(self.work.ptr), self.work_bytes, c_void_p(self.out_keys.ptr),
-                                            c_void_p(self.out_vals.ptr), self.vb, byref(nk), byref(no)), "kman_groups")
+        work = (c_void_p(self.work.ptr), self.work_bytes)
+        if not self.overlap:
+            sh = self.loader.load()
+            N.check(ctx, L.kman_groups(ctx, c_void_p(sh.codes.ptr), sh.n_own, self.k, self.flags, self.m, *work,
+                                       c_void_p(self.out_keys.ptr), c_void_p(self.out_vals.ptr), self.vb, byref(nk),
+                                       byref(no)), "kman_groups")
+        else:
+            n_all = self.n_bases
+            codes = c_void_p(self.loader.shard.codes.ptr)
+            nt, tb = ctypes.c_uint32(0), ctypes.c_uint64(0)
+            N.check(ctx, L.kman_groups_begin(ctx, n_all, self.k, self.flags, self.m, *work, byref(nt), byref(tb)),
+                    "kman_groups_begin")
+            width = int(tb.value)
+
+            def on_chunk(n: int) -> None:
+                if width and n >= 64 + width:  # tile t reads codes below (t + 1) * width + 64
+                    N.check(ctx, L.kman_groups_extract(ctx, codes, n_all, self.k, self.flags, self.m, *work,
+                                                       (n - 64) // width), "kman_groups_extract")
+
+            sh = self.loader.load(on_chunk)
+            if sh.n_own != n_all:
+                raise RuntimeError("the input changed size (%d -> %d bases)" % (n_all, sh.n_own))
+            N.check(ctx, L.kman_groups_end(ctx, codes, n_all, self.k, self.flags, self.m, *work,
+                                           c_void_p(self.out_keys.ptr), c_void_p(self.out_vals.ptr), self.vb,
+                                           byref(nk), byref(no)), "kman_groups_end")
         self.n_kmers, self.n_out = int(nk.value), int(no.value)
         return self.n_kmers
 

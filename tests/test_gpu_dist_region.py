@@ -289,3 +289,66 @@ def test_synth_device_matches_numpy():
             assert dev.download(buf, hi - lo, np.uint8).tobytes() == lay.read(lo, hi)
     finally:
         buf.free()
+
+
+@pytest.mark.parametrize("mode,k", [("count", 21), ("uniq", 13), ("count", 31)])
+def test_streamed_overlap_matches_oracle(mode, k):
+    """kman_groups_begin / _extract (one call per parsed chunk, behind the
+    next chunk's copy) / _end give kman_groups' rows (StreamedPipeline with
+    and without the overlap), bit-exact against np_oracle; stepped twice."""
+    import inputs
+
+    from kman_amd import engine, shard
+
+    dev = engine.default_device()
+    text = inputs.syn_numpy(3_000_000, 11, record_len=700_000, width=61) + _texts()["messy"]
+    want = _oracle(text, k, mode)
+    rd = shard.PinnedReader(dev, text)
+    try:
+        for ov in (True, False):
+            sp = shard.StreamedPipeline(dev, rd, k, mode, chunk_bytes=333_333, overlap=ov)
+            try:
+                for _ in range(2):
+                    sp.step()
+                    keys = dev.download(sp.out_keys, sp.n_out, np.uint64)
+                    vals = dev.download(sp.out_vals, sp.n_out, np.uint32).astype(np.uint64)
+                    np.testing.assert_array_equal(keys, want[0])
+                    np.testing.assert_array_equal(vals, want[1].astype(np.uint64))
+            finally:
+                sp.free()
+    finally:
+        rd.free()
+
+
+def test_groups_extract_needs_begin():
+    """kman_groups_extract without its kman_groups_begin (or after another
+    look-back call) is refused, not run against stale status words."""
+    from ctypes import byref, c_uint32, c_uint64, c_void_p
+
+    from kman_amd import _native as N
+    from kman_amd import engine
+
+    dev = engine.default_device()
+    L = N.lib()
+    n, k, flags, m = 1 << 20, 21, 0, N.KMAN_FINISH_COUNT
+    wb = c_uint64(0)
+    N.check(dev.ctx, L.kman_groups_plan(n, k, flags, m, byref(wb)), "plan")
+    work, codes = dev.alloc(int(wb.value)), dev.alloc(n + 128)
+    ok, ov = dev.alloc(8 * n), dev.alloc(4 * n)
+    try:
+        rng = np.random.default_rng(5)
+        dev.upload(codes, np.concatenate([rng.integers(0, 4, n, dtype=np.uint8), np.full(128, 4, np.uint8)]))
+        args = (n, k, flags, m, c_void_p(work.ptr), wb.value)
+        nt, tb = c_uint32(0), c_uint64(0)
+        N.check(dev.ctx, L.kman_groups_begin(dev.ctx, *args, byref(nt), byref(tb)), "begin")
+        assert nt.value > 1 and tb.value > 0
+        N.check(dev.ctx, L.kman_groups_extract(dev.ctx, c_void_p(codes.ptr), *args, 1), "extract")
+        nk, no = c_uint64(), c_uint64()
+        N.check(dev.ctx, L.kman_groups_end(dev.ctx, c_void_p(codes.ptr), *args, c_void_p(ok.ptr), c_void_p(ov.ptr), 4,
+                                           byref(nk), byref(no)), "end")
+        assert nk.value == n - k + 1
+        # the pass is closed: a further extract has no begin
+        assert L.kman_groups_extract(dev.ctx, c_void_p(codes.ptr), *args, 2) == N.KMAN_EINVAL
+    finally:
+        for b in (work, codes, ok, ov):
+            b.free()
