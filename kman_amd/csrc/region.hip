@@ -899,8 +899,11 @@ enum { RG_COUNT = 1, RG_UNIQ = 2 };
 // buffers: while region r is sorted in one, region r + 1 streams into the
 // other by direct global -> LDS loads (global_load_lds_dwordx4: no registers
 // held, unlike PF), so the region loads hide behind the LDS work.
-template <int MODE, typename O, bool ATOMIC, bool PF = false, bool DB = false>
-__global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : 4) void rg_finish(const uint64_t *__restrict__ in, uint64_t C1,
+// T = uint32_t (count mode, rest <= 32 bits, no tag): items held as their
+// key rest in 4 bytes, half the LDS (three blocks per CU); rows staged in two
+// rounds (keys, then counts)
+template <int MODE, typename O, bool ATOMIC, bool PF = false, bool DB = false, typename T = uint64_t>
+__global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) void rg_finish(const uint64_t *__restrict__ in, uint64_t C1,
                                                 const uint32_t *__restrict__ cnt1, uint32_t Q, uint32_t rest,
                                                 uint32_t rc, uint64_t rbase, uint32_t tag_shift, uint32_t fsub,
                                                 uint64_t *__restrict__ okeys, O *__restrict__ ovals,
@@ -911,14 +914,16 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : 4) void rg_finish(const ui
     constexpr int NT = DB ? 1024 : FT, NW_ = NT / 64;
     constexpr int IPT = DB ? (FCAP + 1023) / 1024 : FIPT;  // items per thread (DB: 9 x 1024 >= FCAP)
     constexpr int SCAP = DB ? FCAP + 2 : FCAP;  // (DB: + the alignment holes of two odd sub-regions)
-    __shared__ __attribute__((aligned(16))) uint64_t sb[DB ? 2 : 1][SCAP];
+    constexpr bool NARROW = sizeof(T) == 4;
+    static_assert(!NARROW || (MODE == RG_COUNT && !DB && !PF), "narrow items: count mode, one region per block");
+    __shared__ __attribute__((aligned(16))) T sb[DB ? 2 : 1][SCAP];
     __shared__ uint32_t wh[NW_][FWORD];  // per-wave digit counters, u16 pairs
     __shared__ uint32_t dstart[FRAD];
     __shared__ uint32_t lds_scan[NW_];
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_out;
     uint32_t cur = 0;
-    uint64_t *s = sb[0];
+    T *s = sb[0];
 
     const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
     const uint64_t rmask = (1ull << rest) - 1;
@@ -929,21 +934,22 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : 4) void rg_finish(const ui
         a0 = cnt1[(uint64_t)rr * fsub];
         a1 = fsub > 1 ? cnt1[(uint64_t)rr * fsub + 1] : 0u;
     };
-    auto load = [&](uint32_t rr, uint32_t a0, uint32_t mm, uint64_t (&v)[IPT]) {
+    auto load = [&](uint32_t rr, uint32_t a0, uint32_t mm, T (&v)[IPT]) {
         // (a uniform base and one 32-bit offset per item: few address VGPRs)
         const uint64_t *src = in + (uint64_t)rr * fsub * C1;
         const uint32_t skip = (uint32_t)C1 - a0;
 #pragma unroll
         for (int i = 0; i < IPT; i++) {
             const uint32_t p = pw + i * 64;
-            v[i] = p < mm ? src[p < a0 ? p : p + skip] : 0;
+            v[i] = p < mm ? (T)src[p < a0 ? p : p + skip] : (T)0;
         }
     };
     // DB: region rr's items into an LDS buffer in 16-byte chunks, one per
     // lane (a wave's 64 chunks land contiguously at the M0 base): sub-region
     // 1 starts at the even slot after sub-region 0 (a hole when a0 is odd;
     // reading one item past an odd count stays inside the capacity C1)
-    auto dma = [&](uint32_t rr, uint32_t a0, uint32_t a1, uint64_t *dst) {
+    auto dma = [&](uint32_t rr, uint32_t a0, uint32_t a1, T *dst_) {
+        uint64_t *dst = reinterpret_cast<uint64_t *>(dst_);  // (DB: T is the u64 item)
         const uint64_t *src0 = in + (uint64_t)rr * fsub * C1, *src1 = src0 + C1;
         const uint32_t c0 = (a0 + 1) >> 1, ctot = c0 + ((a1 + 1) >> 1);
         for (uint32_t cb = (uint32_t)w * 64; cb < ctot; cb += NT) {  // (wave-uniform)
@@ -954,7 +960,7 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : 4) void rg_finish(const ui
             }
         }
     };
-    auto from_lds = [&](uint32_t a0, uint32_t mm, uint64_t (&v)[IPT]) {
+    auto from_lds = [&](uint32_t a0, uint32_t mm, T (&v)[IPT]) {
         const uint32_t hole = a0 & 1u;
 #pragma unroll
         for (int i = 0; i < IPT; i++) {
@@ -987,7 +993,7 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : 4) void rg_finish(const ui
     uint32_t m0, m1, rn = nreg, n0 = 0, n1 = 0;
     counts(r, m0, m1);
     uint32_t m = fit(r, m0, m1);
-    uint64_t x[IPT];
+    T x[IPT];
     if (DB) {
         if (m) dma(r, m0, m1, sb[0]);
         __builtin_amdgcn_s_waitcnt(0);
@@ -1105,7 +1111,7 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : 4) void rg_finish(const ui
     const uint32_t q0 = (uint32_t)t * IPT;
     uint32_t heads = 0, tails = 0;
 #define RKEY(v) (((v) >> Q) & rmask)
-    uint64_t kv[IPT];
+    T kv[IPT];
 #pragma unroll
     for (int j = 0; j < IPT; j++) kv[j] = q0 + j < m ? s[q0 + j] : 0;
 #pragma unroll
@@ -1139,17 +1145,23 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : 4) void rg_finish(const ui
     }
     // the emitted rows compacted in LDS as one word each: the item itself
     // (UNIQ: key rest + pos) or key rest | group size << rest (COUNT); every
-    // read of s above came before the scan's barriers
-    {
+    // read of s above came before the scan's barriers.  NARROW: the key
+    // rests, then (after they are written) the group sizes
+    auto stage = [&](bool sizes) {
         uint32_t o = off, cur = lh_before;  // head position + 1 of the open group
 #pragma unroll
         for (int j = 0; j < IPT; j++) {
             const uint32_t q = q0 + j;
             if (MODE != RG_UNIQ && ((heads >> j) & 1u)) cur = q + 1;
-            if ((emit >> j) & 1u)
-                s[o++] = MODE == RG_UNIQ ? kv[j] : (RKEY(kv[j]) | ((uint64_t)(q + 2 - cur) << rest));
+            if ((emit >> j) & 1u) {
+                if constexpr (NARROW)
+                    s[o++] = sizes ? (T)(q + 2 - cur) : kv[j];
+                else
+                    s[o++] = MODE == RG_UNIQ ? kv[j] : (T)(RKEY(kv[j]) | ((uint64_t)(q + 2 - cur) << rest));
+            }
         }
-    }
+    };
+    stage(false);
     __syncthreads();
     RSTAMP(r, 4);
     const uint64_t ob = s_out;
@@ -1159,6 +1171,11 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : 4) void rg_finish(const ui
             const uint64_t v = s[q];
             okeys[ob + q] = ((uint64_t)(r + rbase) << rest) | RKEY(v);
         }
+        if constexpr (NARROW) {
+            __syncthreads();  // (every key read before the sizes overwrite them)
+            stage(true);
+            __syncthreads();
+        }
         for (uint32_t q = t; q < total; q += NT) {
             const uint64_t v = s[q];
             if constexpr (MODE == RG_UNIQ) {
@@ -1167,6 +1184,8 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : 4) void rg_finish(const ui
                 // N > 1: the source rank (tagged into the item by the pass after
                 // the exchange) in bits 56-63, as DistPipeline's payloads
                 ovals[ob + q] = (O)(tag_shift ? pos | (((v >> tag_shift) & 0x1ffull) << 56) : pos);
+            } else if constexpr (NARROW) {
+                ovals[ob + q] = (O)v;
             } else {
                 ovals[ob + q] = (O)(v >> rest);
             }
@@ -1393,13 +1412,13 @@ struct FinishArgs {
     uint8_t *freg = nullptr;  // per-region overflow flags (the round path), else null
 };
 
-template <int MODE, typename O, bool ATOMIC, bool PF, bool DB = false>
+template <int MODE, typename O, bool ATOMIC, bool PF, bool DB = false, typename T = uint64_t>
 void launch_finish_as(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ovals, uint32_t epoch,
                       uint32_t *counter, uint32_t dbg, uint64_t *stp) {
-    const void *fn = (const void *)rg_finish<MODE, O, ATOMIC, PF, DB>;
+    const void *fn = (const void *)rg_finish<MODE, O, ATOMIC, PF, DB, T>;
     constexpr int NT = DB ? 1024 : FT;
     const uint32_t grid = PF || DB ? (uint32_t)kman_persistent_grid(ctx, fn, NT, f.nreg) : f.nreg;
-    hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, PF, DB>), dim3(grid), dim3(NT), 0, ctx->stream, f.in, f.C1, f.cnt, f.Q,
+    hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, PF, DB, T>), dim3(grid), dim3(NT), 0, ctx->stream, f.in, f.C1, f.cnt, f.Q,
                        f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status, counter, epoch,
                        ctx->d_err, dbg, stp, f.nreg, f.freg);
 }
@@ -1417,6 +1436,20 @@ void launch_finish(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ov
     static const char *e = getenv("KMAN_RG_FIN");
     const bool pf = e && atoi(e) == 1;
     const bool db = e && atoi(e) == 2;
+    // count rows whose key rest fits 32 bits: 4-byte items in LDS
+    // (KMAN_RG_NARROW=0: the 8-byte items, for A/B)
+    static const char *en = getenv("KMAN_RG_NARROW");
+    if constexpr (MODE == RG_COUNT) {
+        if (!pf && !db && f.rest <= 32 && f.Q == 0 && f.tag_shift == 0 && !(en && atoi(en) == 0)) {
+            if (ctx->lds_atomic_ordered)
+                launch_finish_as<MODE, O, true, false, false, uint32_t>(ctx, f, okeys, ovals, epoch, counter, dbg,
+                                                                        stp);
+            else
+                launch_finish_as<MODE, O, false, false, false, uint32_t>(ctx, f, okeys, ovals, epoch, counter, dbg,
+                                                                         stp);
+            return;
+        }
+    }
     if (ctx->lds_atomic_ordered) {
         if (db) launch_finish_as<MODE, O, true, false, true>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
         else if (pf) launch_finish_as<MODE, O, true, true>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
