@@ -415,6 +415,13 @@ class _Grow:
             self.buf = None
 
 
+class _View:
+    """A window [ptr, ptr + nbytes) of a buffer owned elsewhere."""
+
+    def __init__(self, ptr: int, nbytes: int):
+        self.ptr, self.nbytes = ptr, nbytes
+
+
 class DistPipeline:
     """One rank of the multi-GPU join (bench.py, CLI, tests).
 
@@ -427,13 +434,16 @@ class DistPipeline:
     pinned-host benchmark line); reparse: keep the shard's text in HBM and
     parse it in every step (a shard of one chunk: the benchmark's step then
     covers parse + histogram + rounds, as the single-GPU step covers parse +
-    join)."""
+    join).  ordered=False: the rows are wanted only as a multiset (the
+    abundance spectrum, config 5), so a partial redo appends the redone key
+    ranges' rows after the region rows instead of merging them into key
+    order (no copy, no merge pass)."""
 
     def __init__(self, dev: engine.Device, reader, k: int, mode: str, world: int, rank: int,
                  uid: Optional[bytes] = None, canonical: bool = False, rc: bool = False, path: str = "region",
                  max_round_items: Optional[int] = None, chunk_bytes: int = 256 << 20, reload: bool = False,
                  mem_frac: float = 0.85, shard: Optional[S.ShardCodes] = None, local: bool = False,
-                 reparse: bool = False, overlap: Optional[bool] = None):
+                 reparse: bool = False, overlap: Optional[bool] = None, ordered: bool = True):
         engine._check_k(k)
         if mode not in ("count", "uniq"):
             raise ValueError(mode)
@@ -442,7 +452,7 @@ class DistPipeline:
         self.dev, self.k, self.mode, self.world, self.rank = dev, k, mode, world, rank
         self.canonical, self.rc = canonical, rc and not canonical
         self.path, self.max_round_items, self.reload, self.mem_frac = path, max_round_items, reload, mem_frac
-        self.reparse = reparse
+        self.reparse, self.ordered = reparse, ordered
         # overlapped rounds (round_pieces): default on for several ranks;
         # KMAN_DIST_OVERLAP=0/1 overrides (A/B), tests force it on one rank
         env = os.environ.get("KMAN_DIST_OVERLAP")
@@ -861,7 +871,11 @@ class DistPipeline:
             yield ("alltoallv", (sp.ptr, sc, so, rp.ptr, rcnt, roff, 8))
         lap("exchange")
         n_gen = 0
-        gk, gv = self.part_bufs[0].get(8 * max(1, nr)), self.part_bufs[1].get(vb * max(1, nr))
+        if self.ordered:
+            gk, gv = self.part_bufs[0].get(8 * max(1, nr)), self.part_bufs[1].get(vb * max(1, nr))
+        else:  # (rows as a multiset: straight after the region rows; they fit, rows <= received k-mers)
+            gk, gv = (_View(ok_.ptr + 8 * (n_out + n_region), 8 * max(1, nr)),
+                      _View(ov_.ptr + vb * (n_out + n_region), vb * max(1, nr)))
         if nr:
             # a full-key sort, then run-length: these ranges are where keys
             # repeat far beyond a region's share, so equal-prefix segments are
@@ -884,7 +898,7 @@ class DistPipeline:
                                               byref(out)), "kman_rle_count")
             n_gen = int(out.value)
             lap("finish")
-        if n_gen:
+        if n_gen and self.ordered:
             # the region rows move to the (now free) round arenas, then the two
             # sorted, key-disjoint runs merge back into place
             N.check(ctx, L.kman_memcpy_d2d(ctx, c_void_p(A.ptr), c_void_p(ok_.ptr + 8 * n_out), 8 * n_region), "copy")
@@ -1077,7 +1091,7 @@ class DistPipeline:
 
 
 def local_groups(p: engine.Parsed, k: int, rc: bool, mode: str, canonical: bool = False,
-                 max_round_items: Optional[int] = None):
+                 max_round_items: Optional[int] = None, ordered: bool = True):
     """Count / uniq of one parsed input on one GPU through the key rounds of
     the multi-GPU path (shard histogram, exact extraction, per-bucket passes,
     LDS finish; a round whose regions overflow is redone by key range): the
@@ -1093,7 +1107,7 @@ def local_groups(p: engine.Parsed, k: int, rc: bool, mode: str, canonical: bool 
                       names=list(p.names), rec_seq=np.asarray(p.rec_seq, dtype=np.uint64))
     t0 = time.perf_counter()
     pipe = DistPipeline(p.dev, None, k, mode, 1, 0, None, canonical=canonical, rc=rc, shard=sh, local=True,
-                        max_round_items=max_round_items)
+                        max_round_items=max_round_items, ordered=ordered)
     try:
         t1 = time.perf_counter()
         pipe.step()
@@ -1115,11 +1129,11 @@ class LocalRounds:
     the key rounds over the resident codes, result() views the rows."""
 
     def __init__(self, p: engine.Parsed, k: int, rc: bool, mode: str, canonical: bool = False,
-                 max_round_items: Optional[int] = None):
+                 max_round_items: Optional[int] = None, ordered: bool = True):
         sh = S.ShardCodes(p.dev, S.ShardSpec(0, 0, 0, 0, 0), k, codes=p.codes, n_own=p.n_bases, n_eff=p.n_bases,
                           names=list(p.names), rec_seq=np.asarray(p.rec_seq, dtype=np.uint64))
         self.pipe = DistPipeline(p.dev, None, k, mode, 1, 0, None, canonical=canonical, rc=rc, shard=sh, local=True,
-                                 max_round_items=max_round_items)
+                                 max_round_items=max_round_items, ordered=ordered)
 
     def step(self) -> int:
         return self.pipe.step()

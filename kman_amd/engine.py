@@ -886,16 +886,18 @@ def read_input(path: str) -> bytes:
         return fh.read()
 
 
-def count_groups(p: Parsed, k: int, rc: bool = False, canonical: bool = False) -> CountResult:
+def count_groups(p: Parsed, k: int, rc: bool = False, canonical: bool = False, ordered: bool = True) -> CountResult:
     """(key, count) per distinct k-mer on the device: the region path, else
-    the prefix-split path (None only when there are no k-mers)."""
+    the prefix-split path (None only when there are no k-mers).
+    ordered=False: the rows may come in any order (a spectrum needs only
+    the multiset; the key rounds then skip merging a redone key range)."""
     r = groups(p, k, rc, "count", canonical)
     if r is not None:
         return r
     if p.n_bases:
         from . import dist
 
-        r = dist.local_groups(p, k, rc, "count", canonical)
+        r = dist.local_groups(p, k, rc, "count", canonical, ordered=ordered)
         if r is not None:
             return r
     km = extract_sorted(p, k, rc, want_pos=False, canonical=canonical)
@@ -916,7 +918,7 @@ def abundance_hist(text: bytes, k: int, canonical: bool = True, nbins: int = 100
     _check_k(k)
     p = parse(dev, text)
     try:
-        r = count_groups(p, k, False, canonical)
+        r = count_groups(p, k, False, canonical, ordered=False)
         d_h = dev.alloc(8 * nbins)
         try:
             if r is None:

@@ -196,6 +196,55 @@ def test_dist_overflow_redo_canonical_and_rc(G):
         _close(pipes)
 
 
+@pytest.mark.parametrize("G", [1, 3])
+def test_dist_unordered_redo_spectrum(G):
+    """ordered=False (the abundance spectrum, config 5): a redone key range is
+    appended after the region rows, not merged -- the rows are the oracle's
+    as a multiset and the all-reduced spectrum is exact."""
+    import inputs
+    from kman_amd import dist, engine
+
+    rep = b"TTGACCATGACCGATTACAGATTGGC"
+    body = inputs.SynthLayout(150_000, 6, record_len=40_000).read(0, 10**9)
+    text = body + b">sat\n" + b"\n".join([rep * 3] * 20_000) + b"\n"
+    outs, pipes, grp = _run(text, 21, "count", G, canonical=True, ordered=False)
+    try:
+        assert sum(p.partial_rounds for p in pipes) >= 1
+        wk, wc = _oracle(text, 21, "count", canonical=True)
+        for keys, counts in outs:
+            o = np.argsort(keys, kind="stable")
+            np.testing.assert_array_equal(keys[o], wk)
+            np.testing.assert_array_equal(counts[o], wc)
+        hs = grp.run(lambda p: p.hist_gen(1001))
+        want = np.bincount(np.minimum(wc.astype(np.int64), 1000), minlength=1001).astype(np.uint64)
+        want[0] = 0
+        for h in hs:
+            np.testing.assert_array_equal(h, want)
+    finally:
+        _close(pipes)
+    # one GPU through the key rounds (engine.abundance_hist's path for inputs
+    # kman_groups does not take), ordered and not
+    dev = engine.default_device()
+    p = engine.parse(dev, text)
+    try:
+        for ordered in (True, False):
+            r = dist.local_groups(p, 21, False, "count", True, max_round_items=200_000, ordered=ordered)
+            try:
+                keys = dev.download(r.ukeys, r.n, np.uint64)
+                counts = dev.download(r.counts, r.n, np.uint32 if r.count_bytes == 4 else np.uint64)
+            finally:
+                r.ukeys.free()
+                r.counts.free()
+            if ordered:
+                np.testing.assert_array_equal(keys, wk)
+            o = np.argsort(keys, kind="stable")
+            np.testing.assert_array_equal(keys[o], wk)
+            np.testing.assert_array_equal(counts[o].astype(np.uint64), wc.astype(np.uint64))
+            assert dist.LAST_LOCAL["partial_rounds"] >= 1
+    finally:
+        p.free()
+
+
 def test_dist_general_path_k27():
     """k = 27: count items still fit the region rounds; uniq (window index +
     key > 64 bits) and a forced path="general" take the general path (key

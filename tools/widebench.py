@@ -7,7 +7,8 @@ HBM (parse + count / uniq), results device-resident:
             count items; > 1 G k-mers go through the key rounds, dist.local_groups)
   rc1g      1 GB synthetic FASTA, k = 21, count -r (2 G k-mers: key rounds)
   grch38    GRCh38-shaped synthetic (inputs.grch38_like: N runs, soft-masking,
-            repeats, satellites), k = 21, canonical count + abundance spectrum
+            repeats, satellites), k = 21, canonical count + abundance spectrum,
+            then the spectrum alone (count rows as a multiset)
 
 Each line: k-mers/s, ms per step, the path taken and rounds.  Usage:
 widebench.py [config3|rc1g|grch38 ...] [--steps N] [--gb G]"""
@@ -27,7 +28,7 @@ import inputs  # noqa: E402
 from kman_amd import dist, engine, shard  # noqa: E402
 
 
-def run(name, dev, text_reader, k, mode, rc=False, canonical=False, steps=3, hist=False):
+def run(name, dev, text_reader, k, mode, rc=False, canonical=False, steps=3, hist=False, ordered=True):
     t0 = time.time()
     sp = shard.shard_specs(text_reader, 1, k)[0]
     ld = shard.ShardLoader(dev, text_reader, sp, k, chunk_bytes=1 << 30)
@@ -47,7 +48,7 @@ def run(name, dev, text_reader, k, mode, rc=False, canonical=False, steps=3, his
     in_groups = N.lib().kman_groups_plan(p.n_bases, k, fl, fm, byref(c_uint64(0))) == N.KMAN_OK
     # outside kman_groups: the key rounds with their buffers held across
     # steps (as bench.py holds ResidentPipeline's)
-    lr = None if in_groups else dist.LocalRounds(p, k, rc, mode, canonical)
+    lr = None if in_groups else dist.LocalRounds(p, k, rc, mode, canonical, ordered=ordered)
     for s in range(steps + 1):
         dev.sync()
         t = time.perf_counter()
@@ -55,7 +56,7 @@ def run(name, dev, text_reader, k, mode, rc=False, canonical=False, steps=3, his
             lr.step()
             r = lr.result()
         elif mode == "count":
-            r = engine.count_groups(p, k, rc, canonical)
+            r = engine.count_groups(p, k, rc, canonical, ordered=ordered)
         else:
             r = engine.join_groups(p, k, rc, mode)
         h = None
@@ -89,7 +90,7 @@ def run(name, dev, text_reader, k, mode, rc=False, canonical=False, steps=3, his
         lr.free()
     ms = 1e3 * sum(times) / len(times)
     out = {"line": name, "value": n_k / (ms / 1e3) if n_k else None, "unit": "k-mers/s", "ms_per_step": ms,
-           "kmers": n_k, "rows": n_out, "k": k, "mode": mode, "rc": rc, "canonical": canonical,
+           "kmers": n_k, "rows": n_out, "k": k, "mode": mode, "rc": rc, "canonical": canonical, "rows_in_key_order": ordered,
            "fasta_bytes": text_reader.size, "path": path,
            "note": "parse done once; a step = count/uniq of the resident codes to device-resident rows"}
     if h is not None:
@@ -121,6 +122,10 @@ def main():
             print("grch38-like generated in %.0f s" % (time.time() - t0), file=sys.stderr, flush=True)
             run("GRCh38-shaped 3.1 Gbp synthetic, k=21, canonical count + hist", dev, shard.BytesReader(text), 21,
                 "count", canonical=True, steps=a.steps, hist=True)
+            # config 5 asks for the spectrum only: the rows as a multiset (a
+            # redone key range appended, not merged into key order)
+            run("GRCh38-shaped 3.1 Gbp synthetic, k=21, canonical abundance spectrum (rows unordered)", dev,
+                shard.BytesReader(text), 21, "count", canonical=True, steps=a.steps, hist=True, ordered=False)
             del text
     dev.close()
 
