@@ -107,8 +107,17 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 // the codes arrive (kman_groups_extract): the epoch's ticket counter carries
 // on from one launch to the next, and a launch of n blocks takes the next n
 // tiles in stream order.
+// XG (a whole-stream launch): tickets per XCD partition -- chains
+// [p * NS / 8, (p + 1) * NS / 8) form partition p, counter[p] deals its tiles
+// in stream order, and a block takes tickets from its own XCD's partition
+// first (HW_REG_XCC_ID), then from the others once that one is dealt out.  So
+// a chain's consecutive tiles usually run on one XCD: the 128-byte line two of
+// them share at a digit-run boundary meets in that XCD's L2 instead of
+// leaving two partial lines, and the look-back's predecessor is a neighbour.
+// Placement changes only speed: a tile waits only on earlier tickets of its
+// own partition, and a block leaves only when every partition is dealt out.
 template <int EI, bool RC, bool ATOMIC, bool CANON = false, bool BR = false, bool EX = false, int NS = RS,
-          int XLB = LB, bool IL = false, int TPDX = 0>
+          int XLB = LB, bool IL = false, int TPDX = 0, bool XG = false>
 __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI == 8 ? 8 : 4)))) void rg_extract(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
                                                  uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
                                                  uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ cnt0,
@@ -130,7 +139,28 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     __shared__ uint32_t lds_tile;
     __shared__ uint32_t keep[EX ? RADIX / 32 : 1];
 
-    const uint32_t cid = (uint32_t)grab_tile(counter, &lds_tile);
+    static_assert(!XG || NS % 8 == 0, "XCD partitions of whole chains");
+    uint32_t cid;
+    if (XG) {
+        if (threadIdx.x == 0) {
+            constexpr uint32_t CPG = NS / 8;  // chains per partition
+            const uint32_t x = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // hwreg(HW_REG_XCC_ID, 0, 4)
+            uint32_t got = ~0u;
+            for (uint32_t a = 0; a < 8 && got == ~0u; a++) {
+                const uint32_t pp = (x + a) & 7u;
+                const uint32_t j = atomicAdd(counter + pp, 1u);
+                const uint64_t tt = (uint64_t)(j / CPG) * NS + pp * CPG + j % CPG;
+                if (tt < (IL ? (uint64_t)n_tiles : (uint64_t)NS * seg_tiles)) got = (uint32_t)tt;
+            }
+            lds_tile = got;
+        }
+        __syncthreads();
+        cid = lds_tile;
+        __syncthreads();
+        if (cid == ~0u) return;  // (block-uniform: every partition dealt out)
+    } else {
+        cid = (uint32_t)grab_tile(counter, &lds_tile);
+    }
     uint32_t sgi, jj;
     int64_t tile, first, stile;  // data tile; the chain's first status slot; this tile's status slot
     bool last;                   // the chain's last tile
@@ -1480,6 +1510,14 @@ int run_finish(kman_ctx *ctx, const FinishArgs &f, int mode, uint64_t *okeys, vo
 // the sort passes (LB = 8) cost rg_extract 4.6 GB of status reads per launch
 // (PMC: FETCH 2.27 GB raw, 8 GB of items out): 1 word per lane reads 2.6x
 // less at the same speed (3.69-3.73 vs 3.77-3.86 ms; KMAN_RG_XLB=2/4/8 for A/B)
+// rg_extract's tickets per XCD partition (XG): on by default; KMAN_RG_XG=0
+// takes one global ticket counter (A/B: 3.68 vs 3.75 ms, 10.35 vs 11.22 GB
+// per launch)
+static bool xcd_tickets() {
+    static const bool on = !(getenv("KMAN_RG_XG") && atoi(getenv("KMAN_RG_XG")) == 0);
+    return on;
+}
+
 template <int EI, bool RC, bool CANON, int NS, int XLB = 1>
 void launch_extract_ns(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                        uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp,
@@ -1499,6 +1537,14 @@ void launch_extract_ns(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes,
     // chain -- 3.59 vs 3.61 ms and 10 % less FETCH than contiguous chains
     // with two lanes per digit (KMAN_RG_IL=0, kept for A/B)
     static const bool contiguous = getenv("KMAN_RG_IL") && atoi(getenv("KMAN_RG_IL")) == 0;
+    static const bool xg = xcd_tickets();
+    if (!n_launch && !contiguous && xg && NS % 8 == 0) {  // tickets per XCD partition (one launch, whole stream)
+        hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS, XLB, true, 1, true>), dim3(p.n_tiles0),
+                           dim3(RT), 0, ctx->stream, codes, n_bases, (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0,
+                           c0, ctx->d_status, ctx->d_xcounters + 8 * (epoch & 63u), epoch, ctx->d_err, dbg, stp,
+                           nullptr);
+        return;
+    }
     if (n_launch || !contiguous) {
         hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS, XLB, true, 1>),
                            dim3(n_launch ? n_launch : p.n_tiles0), dim3(RT), 0, ctx->stream, codes, n_bases, (int)k,
@@ -2055,6 +2101,12 @@ template <int EI, bool RC, bool CANON>
 void launch_extract_ex(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                        uint64_t *out, uint32_t *cnt, const uint64_t *rtab, uint32_t epoch, uint32_t *counter) {
     const uint32_t grid = RS * p.seg_tiles;
+    if (xcd_tickets()) {
+        hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, true, RS, 1, false, 0, true>), dim3(grid), dim3(RT), 0,
+                           ctx->stream, codes, n_bases, (int)k, p.Q, out, (uint64_t)0, p.seg_tiles, p.n_tiles0, cnt,
+                           ctx->d_status, ctx->d_xcounters + 8 * (epoch & 63u), epoch, ctx->d_err, 0u, nullptr, rtab);
+        return;
+    }
     hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, true, RS, 1>), dim3(grid), dim3(RT), 0, ctx->stream, codes,
                        n_bases, (int)k, p.Q, out, (uint64_t)0, p.seg_tiles, p.n_tiles0, cnt, ctx->d_status, counter,
                        epoch, ctx->d_err, 0u, nullptr, rtab);

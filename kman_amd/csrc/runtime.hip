@@ -88,6 +88,7 @@ int kman_lookback_begin(kman_ctx *ctx, size_t words, uint32_t *epoch, uint32_t *
         // a fresh epoch range: every status word and tile counter back to zero
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_status, 0, ctx->status_words * sizeof(uint64_t), ctx->stream));
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_counters, 0, 64 * sizeof(uint32_t), ctx->stream));
+        HIP_TRY(ctx, hipMemsetAsync(ctx->d_xcounters, 0, 64 * 8 * sizeof(uint32_t), ctx->stream));
         ctx->epoch = 0;
     }
     ctx->epoch++;
@@ -245,6 +246,8 @@ int kman_create(int device, kman_ctx **out) {
     if ((e = hipMalloc(&ctx->d_counters, 64 * sizeof(uint32_t) + 256)) != hipSuccess) return bail(e, "hipMalloc");
     ctx->d_err = ctx->d_counters + 64;
     if ((e = hipMemset(ctx->d_counters, 0, 64 * sizeof(uint32_t) + 256)) != hipSuccess) return bail(e, "hipMemset");
+    if ((e = hipMalloc(&ctx->d_xcounters, 64 * 8 * sizeof(uint32_t))) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMemset(ctx->d_xcounters, 0, 64 * 8 * sizeof(uint32_t))) != hipSuccess) return bail(e, "hipMemset");
     if ((e = hipHostMalloc(&ctx->h_small, 4096, hipHostMallocDefault)) != hipSuccess) return bail(e, "hipHostMalloc");
     const char *force = getenv("KMAN_RANK");  // "ballot" forces the probe-free ranking
     ctx->lds_atomic_ordered = !(force && strcmp(force, "ballot") == 0) && probe_lds_order(ctx);
@@ -263,6 +266,7 @@ void kman_destroy(kman_ctx *ctx) {
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_aux) (void)hipFree(ctx->d_aux);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
+    if (ctx->d_xcounters) (void)hipFree(ctx->d_xcounters);
     if (ctx->h_small) (void)hipHostFree(ctx->h_small);
     if (ctx->copy_stream) {
         (void)hipStreamSynchronize(ctx->copy_stream);
