@@ -46,7 +46,8 @@ __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__
                                                      uint32_t *__restrict__ err, uint64_t *__restrict__ hist,
                                                      Plan plan, uint64_t key_lo, uint64_t key_hi, uint64_t cap,
                                                      const uint8_t *__restrict__ pmap, uint32_t pshift,
-                                                     uint32_t pval) {
+                                                     uint32_t pval, const uint32_t *__restrict__ pcoarse,
+                                                     uint32_t cshift, uint32_t cexact) {
     constexpr int TILE = ET * EI;
     constexpr int KPT = RC && !CANON ? 2 * EI : EI;  // keys per thread, max
     constexpr int MAXKEYS = ET * KPT;
@@ -61,6 +62,15 @@ __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__
     const uint64_t mask = k == 32 ? ~0ull : ((1ull << (2 * k)) - 1);
     if (hist) {
         for (int i = threadIdx.x; i < MAXPASS * 256; i += ET) (&lhist[0][0])[i] = 0;
+    }
+    // pmap (no hist then): the coarse bitmap of the map's marked prefixes
+    // (top cshift..2k key bits, map_coarse) held in the histogram's LDS, so
+    // most keys are rejected without reading the map in HBM; cexact: the
+    // bitmap is the map itself
+    const uint32_t *lbits = &lhist[0][0];
+    if (pmap) {
+        for (int i = threadIdx.x; i < MAXPASS * 256; i += ET) (&lhist[0][0])[i] = pcoarse[i];
+        __syncthreads();
     }
     for (;;) {
         const int64_t tile = grab_tile(counter, &lds_tile);
@@ -78,8 +88,16 @@ __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__
 #pragma unroll
             for (int j = 0; j < EI; j++) {
                 if ((valid >> j) & 1u) {
-                    vf |= (uint32_t)(pmap[kf[j] >> pshift] == pval) << j;
-                    if (RC && !CANON) vr |= (uint32_t)(pmap[kr[j] >> pshift] == pval) << j;
+                    const uint32_t cf = (uint32_t)(kf[j] >> cshift);
+                    bool hf = (lbits[cf >> 5] >> (cf & 31u)) & 1u;
+                    if (hf && !cexact) hf = pmap[kf[j] >> pshift] == pval;
+                    vf |= (uint32_t)hf << j;
+                    if (RC && !CANON) {
+                        const uint32_t cr = (uint32_t)(kr[j] >> cshift);
+                        bool hr = (lbits[cr >> 5] >> (cr & 31u)) & 1u;
+                        if (hr && !cexact) hr = pmap[kr[j] >> pshift] == pval;
+                        vr |= (uint32_t)hr << j;
+                    }
                 }
             }
         } else {
@@ -154,6 +172,28 @@ __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__
             if (c) atomicAdd((unsigned long long *)&hist[p * 256 + threadIdx.x], (unsigned long long)c);
         }
     }
+}
+
+// kman_extract_marked's coarse bitmap: bit c (c < 2^cb, the top cb key bits)
+// set when any map entry under prefix c holds val (map of mb key bits; for
+// mb <= cb the entry above c); one thread per c, packed by ballots, every
+// word written (bits past 2^cb zero)
+__global__ __launch_bounds__(256) void map_coarse(const uint8_t *__restrict__ map, uint32_t mb, uint32_t val,
+                                                  uint32_t cb, uint32_t *__restrict__ bits) {
+    const uint32_t c = blockIdx.x * 256 + threadIdx.x;  // (65536 threads: 2^16 >= 2^cb)
+    bool hit = false;
+    if (c < (1u << cb)) {
+        if (mb <= cb) {
+            hit = map[c >> (cb - mb)] == val;
+        } else {
+            const uint32_t s = mb - cb;
+            const uint8_t *e = map + ((uint64_t)c << s);
+            for (uint32_t i = 0; i < (1u << s) && !hit; i++) hit = e[i] == val;
+        }
+    }
+    const uint64_t m = __ballot(hit);
+    const int lane = threadIdx.x & 63;
+    if (lane < 2) bits[(c - lane) / 32 + lane] = (uint32_t)(m >> (32 * lane));
 }
 
 // valid-window count only (sizing)
@@ -266,7 +306,7 @@ __global__ __launch_bounds__(ET) void kmer_hist_kernel(const uint8_t *__restrict
 template <int EI, bool RC, bool CANON, typename P>
 int launch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k, uint64_t *keys, P *pos,
                    uint64_t *hist, const Plan &plan, uint64_t klo, uint64_t khi, uint64_t cap, const uint8_t *pmap,
-                   uint32_t pshift, uint32_t pval) {
+                   uint32_t pshift, uint32_t pval, uint32_t cshift, uint32_t cexact) {
     const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * EI);
     uint32_t epoch, *counter;
     KMAN_TRY(kman_lookback_begin(ctx, n_tiles, &epoch, &counter));
@@ -274,7 +314,8 @@ int launch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k,
     const int grid = kman_persistent_grid(ctx, (const void *)fn, ET, n_tiles);
     KTimer kt_(ctx, "extract");
     hipLaunchKernelGGL(fn, dim3(grid), dim3(ET), 0, ctx->stream, codes, n_bases, n_tiles, k, keys, pos,
-                       ctx->d_status, counter, epoch, ctx->d_err, hist, plan, klo, khi, cap, pmap, pshift, pval);
+                       ctx->d_status, counter, epoch, ctx->d_err, hist, plan, klo, khi, cap, pmap, pshift, pval,
+                       ctx->d_mapbits, cshift, cexact);
     HIP_TRY(ctx, hipGetLastError());
     return KMAN_OK;
 }
@@ -282,15 +323,15 @@ int launch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k,
 template <typename P>
 int dispatch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k, uint32_t flags, uint64_t *keys,
                      P *pos, uint64_t *hist, const Plan &plan, uint64_t klo, uint64_t khi, uint64_t cap,
-                     const uint8_t *pmap, uint32_t pshift, uint32_t pval) {
+                     const uint8_t *pmap, uint32_t pshift, uint32_t pval, uint32_t cshift, uint32_t cexact) {
     if (flags & KMAN_CANONICAL)
         return launch_extract<16, false, true, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap, pmap,
-                                                  pshift, pval);
+                                                  pshift, pval, cshift, cexact);
     if (flags & KMAN_RC)
         return launch_extract<8, true, false, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap, pmap,
-                                                 pshift, pval);
+                                                 pshift, pval, cshift, cexact);
     return launch_extract<16, false, false, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap, pmap,
-                                               pshift, pval);
+                                               pshift, pval, cshift, cexact);
 }
 
 }  // namespace
@@ -328,7 +369,7 @@ namespace {
 int extract_filtered(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
                      uint64_t key_lo, uint64_t key_hi, const uint8_t *pmap, uint32_t pshift, uint32_t pval,
                      uint64_t *d_keys, void *d_pos, uint32_t pos_bytes, uint64_t cap, uint64_t *d_hist,
-                     uint64_t *n_kmers) {
+                     uint64_t *n_kmers, uint32_t cshift = 0, uint32_t cexact = 0) {
     const bool ranged = key_lo != 0 || key_hi != ~0ull || pmap;
     if (!ctx || !n_kmers) return KMAN_EINVAL;
     if (k < 2 || k > 32) return kman_fail(ctx, KMAN_EINVAL, "k must be in [2, 32] on the GPU path, got %u", k);
@@ -367,13 +408,13 @@ int extract_filtered(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, ui
     }
     if (!want_pos) {
         KMAN_TRY(dispatch_extract<NoPos>(ctx, d_codes, n_bases, (int)k, flags, d_keys, nullptr, d_hist, plan, key_lo,
-                                         key_hi, cap, pmap, pshift, pval));
+                                         key_hi, cap, pmap, pshift, pval, cshift, cexact));
     } else if (pos_bytes == 4) {
         KMAN_TRY(dispatch_extract<uint32_t>(ctx, d_codes, n_bases, (int)k, flags, d_keys, (uint32_t *)d_pos, d_hist,
-                                            plan, key_lo, key_hi, cap, pmap, pshift, pval));
+                                            plan, key_lo, key_hi, cap, pmap, pshift, pval, cshift, cexact));
     } else {
         KMAN_TRY(dispatch_extract<uint64_t>(ctx, d_codes, n_bases, (int)k, flags, d_keys, (uint64_t *)d_pos, d_hist,
-                                            plan, key_lo, key_hi, cap, pmap, pshift, pval));
+                                            plan, key_lo, key_hi, cap, pmap, pshift, pval, cshift, cexact));
     }
     // the last tile's inclusive prefix is the number of k-mers written
     const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * ((flags & KMAN_RC) && !(flags & KMAN_CANONICAL) ? 8 : 16));
@@ -399,8 +440,15 @@ extern "C" int kman_extract_marked(kman_ctx *ctx, const uint8_t *d_codes, uint64
     if (!ctx || !n_kmers) return KMAN_EINVAL;
     if (!d_map || map_bits == 0 || map_bits > 2 * k || map_bits > 30)
         return kman_fail(ctx, KMAN_EINVAL, "kman_extract_marked: map of %u key bits (k = %u)", map_bits, k);
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (!ctx->d_mapbits) HIP_TRY(ctx, hipMalloc(&ctx->d_mapbits, MAXPASS * 256 * sizeof(uint32_t)));
+    // the coarse bitmap over the top CB key bits (exact when the map is no finer)
+    const uint32_t cb = 2 * k < 16 ? 2 * k : 16;
+    hipLaunchKernelGGL(map_coarse, dim3(256), dim3(256), 0, ctx->stream, d_map, map_bits, map_val, cb,
+                       ctx->d_mapbits);
+    HIP_TRY(ctx, hipGetLastError());
     return extract_filtered(ctx, d_codes, n_bases, k, flags, 0, ~0ull, d_map, 2 * k - map_bits, map_val, d_keys,
-                            d_pos, pos_bytes, cap, nullptr, n_kmers);
+                            d_pos, pos_bytes, cap, nullptr, n_kmers, 2 * k - cb, map_bits <= cb ? 1u : 0u);
 }
 
 // top-8-bit histogram of the stream's keys (the k-mer count is its sum): the

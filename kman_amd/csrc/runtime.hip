@@ -267,6 +267,7 @@ void kman_destroy(kman_ctx *ctx) {
     if (ctx->d_aux) (void)hipFree(ctx->d_aux);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->d_xcounters) (void)hipFree(ctx->d_xcounters);
+    if (ctx->d_mapbits) (void)hipFree(ctx->d_mapbits);
     if (ctx->h_small) (void)hipHostFree(ctx->h_small);
     if (ctx->copy_stream) {
         (void)hipStreamSynchronize(ctx->copy_stream);
