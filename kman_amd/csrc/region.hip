@@ -547,8 +547,8 @@ struct PassArgs {
 // BR: rank by one block-wide LDS atomic per item (no per-wave counters: the
 // order of equal digits inside a tile is then not stable, which the finish
 // does not need -- it sorts every remaining key bit and compares keys only).
-// NSG > 64 (the owned-chain pass 0's S <= NSG segments per bucket): each
-// item finds its segment in an LDS prefix table instead of the lanes' ballots.
+// NSG > 64 (pass 0 with 128 / 256 chains, or the owned-chain pass 0's S <=
+// NSG segments): each lane holds NSG / 64 of the segment prefixes.
 template <bool ATOMIC, int NT, int SI, bool PF, bool WC = false, bool BR = false, int NSG = 64>
 __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
                                                  uint32_t *__restrict__ err, uint32_t dbg,
@@ -569,7 +569,6 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
     __shared__ uint32_t lds_scan[NWAVE];
     __shared__ uint32_t s_items;
     __shared__ uint32_t lds_tile;
-    __shared__ uint32_t spre[NSG > 64 ? NSG + 1 : 1];  // NSG > 64: items before segment s
     const uint32_t shift = pa.shift, bits = pa.bits, nsg = pa.nsg, H = pa.H;
     const uint64_t C1 = pa.C1;
     const int lane = lane_id();
@@ -590,16 +589,25 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
         // segment s; segments >= nsg empty) and bases, in registers
         uint32_t spre_l = 0;
         uint64_t sbase_l = 0;
+        // NSG > 64: lane l holds the prefixes of segments l * SPL + j
+        constexpr int SPL = NSG > 64 ? NSG / 64 : 1;
+        uint32_t spre_q[SPL];
         if (NSG > 64) {
-            const uint32_t t = threadIdx.x;
-            const uint32_t c = t < nsg ? pa.seg_cnt[(uint64_t)b * nsg + t] : 0u;
-            uint32_t tot;
-            const uint32_t ex = block_exclusive_scan<NT>(c, SumU32(), 0u, lds_scan, &tot);
-            if (t < (uint32_t)NSG) spre[t] = ex;
-            if (t == 0) {
-                spre[NSG] = tot;
-                s_items = tot;
+            uint32_t acc = 0, cq[SPL];
+#pragma unroll
+            for (int j = 0; j < SPL; j++) {
+                const uint32_t sg = (uint32_t)lane * SPL + j;
+                cq[j] = sg < nsg ? pa.seg_cnt[(uint64_t)b * nsg + sg] : 0u;
+                acc += cq[j];
             }
+            const uint32_t inc = wave_inclusive_scan(acc, SumU32());
+            uint32_t run_ = inc - acc;
+#pragma unroll
+            for (int j = 0; j < SPL; j++) {
+                spre_q[j] = run_;
+                run_ += cq[j];
+            }
+            if (threadIdx.x == 63) s_items = inc;
         } else {
             const uint32_t sgl = (uint32_t)lane;
             const uint64_t gi = (uint64_t)b * nsg + sgl;
@@ -635,24 +643,39 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
 #pragma unroll
             for (int i = 0; i < (SI + 3) / 4; i++) sgp[i] = 0;
             if constexpr (NSG > 64) {
-                // the first row's segment by binary search (largest s with
-                // spre[s] <= li), then forward past the (rare) boundaries
-                const uint32_t lf = tt0 + (uint32_t)w * (SI * 64) + (uint32_t)lane;
-                uint32_t lo = 0, hi = NSG;
+                // as below with SPL prefixes per lane: the row start's segment
+                // = (segments whose prefix <= the row start) - 1 by ballots,
+                // its prefix by one readlane, then the (rare) boundaries
+                // inside the row -- no LDS, the loads issue back to back
+                auto pick = [&](uint32_t j) {  // spre_q[j], j wave-uniform
+                    uint32_t v = spre_q[0];
 #pragma unroll
-                for (int it = 0; (1 << it) < NSG; it++) {
-                    const uint32_t mid = (lo + hi) >> 1;
-                    if (spre[mid] <= lf) lo = mid;
-                    else hi = mid;
-                }
-                uint32_t sg = lo, po = spre[lo], nx = spre[lo + 1];
+                    for (int jj = 1; jj < SPL; jj++)
+                        if (j == (uint32_t)jj) v = spre_q[jj];
+                    return v;
+                };
 #pragma unroll
                 for (int i = 0; i < SI; i++) {
-                    const uint32_t li = lf + (uint32_t)i * 64;
-                    while (li >= nx && sg + 1 < (uint32_t)NSG) {
-                        sg++;
-                        po = nx;
-                        nx = spre[sg + 1];
+                    const uint32_t li0 = tt0 + (uint32_t)w * (SI * 64) + (uint32_t)i * 64;
+                    const uint32_t li = li0 + (uint32_t)lane;
+                    int cnt = 0;
+#pragma unroll
+                    for (int j = 0; j < SPL; j++) cnt += __popcll(__ballot(spre_q[j] <= li0));
+                    uint32_t sg = (uint32_t)(cnt - 1);
+                    uint32_t po = (uint32_t)__builtin_amdgcn_readlane((int)pick(sg % SPL), (int)(sg / SPL));
+#pragma unroll
+                    for (int j = 0; j < SPL; j++) {
+                        uint64_t inrow = __ballot(spre_q[j] > li0 && spre_q[j] <= li0 + 63);
+                        while (inrow) {  // (wave-uniform)
+                            const int l2 = __ffsll((unsigned long long)inrow) - 1;
+                            inrow &= inrow - 1;
+                            const uint32_t s2 = (uint32_t)l2 * SPL + j;
+                            const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)spre_q[j], l2);
+                            if (li >= p2 && s2 > sg) {  // (the largest segment starting at or before li)
+                                sg = s2;
+                                po = p2;
+                            }
+                        }
                     }
                     key[i] = ib + i * 64 < nn ? pa.in[((uint64_t)b * nsg + sg) * pa.stride + (li - po)] : 0;
                 }
@@ -1343,8 +1366,10 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
         const uint64_t win = (uint64_t)RT * p.ei;
         p.n_tiles0 = (uint32_t)ceil_div(n_bases, win);
         // RS = 64 look-back chains (KMAN_RG_NS=128 / 256: shorter chains, A/B
-        // only -- rg_extract 3.80-3.93 ms either way, and rg_pass finding its
-        // segments in an LDS table is slower: 3.71-3.82 vs 3.46-3.55 ms)
+        // only).  With the XCD-partitioned tickets and the segment prefixes
+        // held in registers (SPL per lane), one box, ms extract / pass: 64:
+        // 3.44 / 3.33, 128: 3.33 / 3.41, 256: 3.29 / 3.74-3.90 -- the step
+        // within 0.5 % at 128, so the default stays 64 (one prefix per lane)
         const char *e2 = getenv("KMAN_RG_NS");
         const uint32_t ns = e2 && (atoi(e2) == 128 || atoi(e2) == 256) ? (uint32_t)atoi(e2) : (uint32_t)RS;
         p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, ns);
@@ -1405,11 +1430,17 @@ void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32
 // 4 4.29, 5 3.78, 6 4.69; later boxes: 5 3.49-3.58 with per-digit store
 // parameters, 3.54 with 32-bit relative output indices (7: 3.56).
 void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
-    if (pa.nsg > 64) {  // the owned-chain pass 0's segments (<= 1024, no seg_base, no tag): shape 5
-        const void *fn = (const void *)rg_pass<true, 1024, 8, true, true, true, 1024>;
-        const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, 1024, (uint64_t)pa.nbk * pa.H);
-        hipLaunchKernelGGL((rg_pass<true, 1024, 8, true, true, true, 1024>), dim3(grid), dim3(1024), 0, ctx->stream,
-                           pa, counter, ctx->d_err, dbg, stp);
+    if (pa.nsg > 64) {  // 128 / 256 pass-0 chains, or the owned-chain pass 0's segments (<= 1024, no seg_base, no tag): shape 5
+        auto go = [&](auto nsg_c) {
+            constexpr int NSG = decltype(nsg_c)::value;
+            const void *fn = (const void *)rg_pass<true, 1024, 8, true, true, true, NSG>;
+            const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, 1024, (uint64_t)pa.nbk * pa.H);
+            hipLaunchKernelGGL((rg_pass<true, 1024, 8, true, true, true, NSG>), dim3(grid), dim3(1024), 0,
+                               ctx->stream, pa, counter, ctx->d_err, dbg, stp);
+        };
+        if (pa.nsg <= 128) go(std::integral_constant<int, 128>{});
+        else if (pa.nsg <= 256) go(std::integral_constant<int, 256>{});
+        else go(std::integral_constant<int, 1024>{});
         return;
     }
     const char *e = getenv("KMAN_RG_PASS");
