@@ -1033,6 +1033,8 @@ class DistPipeline:
     def text(self) -> bytes:
         """This rank's slice of the reference's output text (count rows, or
         uniq records with global headers), built on the device."""
+        if not self.ordered:
+            raise ValueError("ordered=False keeps the rows as a multiset (the spectrum): no output text")
         ok_, ov_, vb = self._out
         if self.mode == "count":
             r = engine.CountResult(ok_, ov_, vb, self.n_out, self.k)
