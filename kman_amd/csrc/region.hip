@@ -2404,9 +2404,21 @@ __global__ __launch_bounds__(256) void count_hist_kernel(const C *__restrict__ c
     extern __shared__ uint32_t lh[];
     for (uint32_t i = threadIdx.x; i < nbins; i += 256) lh[i] = 0;
     __syncthreads();
+    // counts of 1 and 2 (nearly every row of a genome's spectrum) in registers,
+    // one LDS atomic per wave: every lane adding to the same LDS word
+    // serialised the kernel (9.1 ms for 2.7 G rows, 1.2 TB/s)
+    uint32_t r1 = 0, r2 = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
         const uint64_t c = counts[i];
-        atomicAdd(&lh[c < nbins ? c : nbins - 1], 1u);
+        if (c == 1) r1++;
+        else if (c == 2) r2++;
+        else atomicAdd(&lh[c < nbins ? c : nbins - 1], 1u);
+    }
+    r1 = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_scan(r1, SumU32()), 63);
+    r2 = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_scan(r2, SumU32()), 63);
+    if ((threadIdx.x & 63) == 0) {
+        if (r1) atomicAdd(&lh[1], r1);  // (nbins >= 2)
+        if (r2) atomicAdd(&lh[2 < nbins ? 2 : nbins - 1], r2);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < nbins; i += 256)
