@@ -71,7 +71,8 @@ def cpu_baseline(k: int, mode: str, target_s: float = 10.0) -> dict:
     exe = os.path.join(ROOT, "oracle", "kman_oracle")
     if not os.path.isfile(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
-    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1))
+    # every core this process may run on (the box's CPU share; nproc shows the whole machine)
+    cores = max(1, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1)
     with tempfile.TemporaryDirectory() as d:
         def sample(nbases, seed):
             src = os.path.join(d, "s%d.fa" % seed)
@@ -92,13 +93,21 @@ def cpu_baseline(k: int, mode: str, target_s: float = 10.0) -> dict:
         n, s, _ = run([sample(2_000_000, 1)])
         nb = int(2_000_000 * max(1.0, min(32.0, target_s / max(s, 1e-3))))
         n1, s1, _ = run([sample(nb, 1)])
-        nbp = max(2_000_000, nb // 2)
+        # one process per core on independent samples; the total work is
+        # bounded (8 x the 1-core sample) so many cores do not stretch the run
+        nbp = max(1_000_000, min(nb // 2, 8 * nb // cores))
         srcs = [sample(nbp, 1 + i) for i in range(cores)]
         nP, _, wallP = run(srcs)
+        quota = None
+        try:  # the cgroup CPU quota, if any (the box's CPU share)
+            q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+            quota = None if q == "max" else float(q) / float(per)
+        except (OSError, ValueError):
+            pass
     return {"value": n1 / s1, "unit": "k-mers/s", "cores": 1, "kind": "port",
             "sample": "%d-base sample of the same generator (seed 1), %s k=%d, %d k-mers in %.2f s, 1 thread"
                       % (nb, mode, k, n1, s1),
-            "all_cores": {"value": nP / wallP, "cores": cores, "nproc": os.cpu_count(),
+            "all_cores": {"value": nP / wallP, "cores": cores, "nproc": os.cpu_count(), "cgroup_cpu_quota": quota,
                           "sample": "%d processes on independent %d-base samples (seeds 1..%d), %d k-mers in %.2f s "
                                     "wall" % (cores, nbp, cores, nP, wallP)}}
 
@@ -236,7 +245,10 @@ def run_single(args):
         "config": {"workload": "%.2f GB synthetic FASTA, k=%d, extract+radix-sort+%s single batch"
                                % (fasta_bytes / 1e9, args.k, args.mode),
                    "fasta_bytes_per_gpu": fasta_bytes, "kmers_per_step_per_gpu": pipe.n_kmers, "k": args.k,
-                   "mode": args.mode, "parallelism": "single", "path": pipe.path, "stages_ms_per_step": stages},
+                   "mode": args.mode, "parallelism": "single", "path": pipe.path, "stages_ms_per_step": stages,
+                   "value_scope": "FASTA bytes resident in HBM at the start of a step -> device-resident rows (the "
+                                  "harness contract); SURVEY 8(d)'s pinned-host -> device-resident region is the "
+                                  "pinned_host line, H2D included"},
         "roofline": dom, "sort_pass_roofline": sp, "cpu_baseline": None,
     }
     pipe.timing(False)
@@ -305,73 +317,47 @@ def run_single(args):
     dev.close()
 
 
-def _rendezvous(rank: int, world: int) -> bytes:
-    """The 128-byte RCCL id through a file keyed by the launcher's port (one
-    node: every rank sees the same /tmp)."""
-    from kman_amd import dist
-
-    if world == 1:
-        return dist.unique_id()
-    path = _uid_path()
-    if rank == 0:
-        uid = dist.unique_id()
-        with open(path + ".tmp", "wb") as fh:
-            fh.write(uid)
-        os.replace(path + ".tmp", path)
-        return uid
-    # (a file left by an earlier launch on the same port is older than this
-    # process: the ranks start together, rank 0 writes within seconds)
-    t0 = time.time()
-    while True:
-        try:
-            if os.path.getmtime(path) >= _START - 10:
-                break
-        except OSError:
-            pass
-        if time.time() - t0 > 120:
-            raise RuntimeError("no RCCL id from rank 0 at %s" % path)
-        time.sleep(0.05)
-    time.sleep(0.05)
-    with open(path, "rb") as fh:
-        return fh.read()
-
-
-_START = time.time()
-
-
-def _uid_path() -> str:
-    return os.path.join(tempfile.gettempdir(), "kman_rccl_id_%s_%s_%s" % (
-        os.environ.get("MASTER_PORT", "0"), os.environ.get("TORCHELASTIC_RUN_ID", ""), os.environ.get("WORLD_SIZE", "1")))
-
-
 def run_dist(args, world: int, rank: int, local: int):
     import numpy as np
     import inputs
-    from kman_amd import dist, engine, shard
+    from kman_amd import dist, engine, launch, shard
 
     dev = engine.Device(local)
     per = int(args.shard_gb * 1e9) if args.shard_gb else args.bases
     lay = inputs.SynthLayout(per * world, 1)
     rd = shard.SynthReader(lay)
-    uid = _rendezvous(rank, world)
+    uid = launch.rendezvous(rank, world, "bench")
     t0 = time.time()
     # the 1 GB-per-rank line keeps each rank's text in HBM and parses it in
     # every step (the single-GPU step's scope); config 4's 12.5 GB shards
     # stream through two 1 GiB staging buffers, parsed once at setup
     reparse = args.shard_gb is None
-    pipe = dist.DistPipeline(dev, rd, args.k, args.mode, world, rank, uid, chunk_bytes=1 << 30, reparse=reparse)
+    canon = args.canonical
+    if canon and args.mode != "count":
+        raise SystemExit("--canonical counts (config 5): use --mode count")
+    pipe = dist.DistPipeline(dev, rd, args.k, args.mode, world, rank, uid, chunk_bytes=1 << 30, reparse=reparse,
+                             canonical=canon, ordered=not canon)
+    if rank == 0:
+        launch.remove_id("bench")  # (every rank has joined the communicator)
     log("rank %d: shard %d..%d (%.2f GB) generated + parsed on the device, setup %.1f s"
         % (rank, pipe.spec.start, pipe.spec.own_end, (pipe.spec.own_end - pipe.spec.start) / 1e9, time.time() - t0))
     comm = pipe.comm
+
+    def one_step():
+        n = pipe.step()
+        if canon:  # config 5: the abundance spectrum of the global canonical counts, all-reduced
+            one_step.hist = comm.run(pipe.hist_gen(10001))
+        return n
+
     for _ in range(args.warmup):
-        pipe.step()
+        one_step()
     pipe.timing(True)
     comm.allreduce(np.zeros(1, np.uint64))  # barrier
     dev.sync()
     t0 = time.perf_counter()
     kmers = 0
     for _ in range(args.steps):
-        kmers += pipe.step()
+        kmers += one_step()
     dev.sync()
     elapsed = time.perf_counter() - t0
     el = comm.allgather(np.array([int(elapsed * 1e9)], np.uint64))
@@ -395,8 +381,13 @@ def run_dist(args, world: int, rank: int, local: int):
                     "byte-range sharded, each rank's bytes generated in its HBM; a step = %s shard histogram + key "
                     "rounds" % (world, per / 1e9, "parse of the resident text +" if reparse else "(parsed at setup)"),
             "config": {"workload": "%.2f GB synthetic FASTA in %d byte-range shards, k=%d, extract+radix-sort+%s, "
-                                   "key rounds + one RCCL all-to-all per round" % (lay.size / 1e9, world, args.k,
-                                                                                    args.mode),
+                                   "key rounds + one RCCL all-to-all per round%s"
+                                   % (lay.size / 1e9, world, args.k,
+                                      "canonical count + all-reduced abundance spectrum (config 5's pipeline)"
+                                      if canon else args.mode,
+                                      "" if not canon else "; the synthetic input stands in for GRCh38"),
+                       "canonical": canon,
+                       "spectrum_distinct": int(one_step.hist.sum()) if canon else None,
                        "fasta_bytes": lay.size, "kmers_per_step": total // max(args.steps, 1), "k": args.k,
                        "mode": args.mode, "parallelism": "dp%d: top-8-bit bucket parts + RCCL all-to-all" % world,
                        "path": pipe.path, "rounds": pipe.rounds, "fallback_rounds": pipe.fallback_rounds,
@@ -409,12 +400,7 @@ def run_dist(args, world: int, rank: int, local: int):
             "cpu_baseline": None,
         }
         emit(out)
-    comm.allreduce(np.zeros(1, np.uint64))  # every rank is done with the id file
-    if rank == 0 and world > 1:
-        try:
-            os.remove(_uid_path())
-        except OSError:
-            pass
+    comm.allreduce(np.zeros(1, np.uint64))  # every rank is done
     pipe.free()
     dev.close()
 
@@ -453,11 +439,14 @@ def main() -> None:
     ap.add_argument("--path", choices=["region", "split", "full"], default="region",
                     help="single-GPU engine path (region falls back to split outside its domain)")
     ap.add_argument("--dist", action="store_true", help="run the multi-GPU pipeline even at world size 1")
+    ap.add_argument("--canonical", action="store_true",
+                    help="multi-GPU path: canonical k-mers + the all-reduced abundance spectrum (config 5; "
+                         "with --mode count)")
     args = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1 or args.dist:
+    if world > 1 or args.dist or args.canonical:
         run_dist(args, world, rank, local)
     else:
         run_single(args)

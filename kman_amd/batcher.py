@@ -149,11 +149,15 @@ class FastaBatcher(BatcherThreading):
 
     def __init__(self, scan_mode: "FastaBatcher.MODE" = MODE.KMERS, reverse: bool = False, threads: int = 1,
                  size: int = BatcherThreading.DEFAULT_BATCH_SIZE, natype: NATYPES = BatcherThreading.DEFAULT_NATYPE,
-                 tmp: Optional[str] = None, device: Optional[engine.Device] = None):
+                 tmp: Optional[str] = None, device: Optional[engine.Device] = None,
+                 distributed: Optional[bool] = None):
         super().__init__(size, threads, natype, tmp if tmp is not None else tempfile.gettempdir())
         self.mode = scan_mode
         self.doReverseComplement = reverse
         self._device = device
+        # one process per GPU (kman_amd/launch.py): None = from the launcher's
+        # environment (WORLD_SIZE > 1, or KMAN_DIST=1)
+        self._distributed = distributed
         self.source = None
 
     @property
@@ -185,9 +189,20 @@ class FastaBatcher(BatcherThreading):
             raise AssertionError(f"k must be >= 1, got {k} instead.")
         if self.natype != NATYPES.DNA:
             raise NotImplementedError("the k-mer path is DNA-only, as the reference CLI")
+        from . import launch
         from .source import FastaSource
 
         dev = self._device or engine.default_device()
+        dist = launch.distributed() if self._distributed is None else self._distributed
+        if dist and k <= engine.MAX_K:
+            # this rank's byte range only; ONE batch of its windows, joined
+            # across the ranks by KJoiner.join (the batch cut does not change
+            # count / uniq output)
+            src = launch.ShardedSource(dev, fasta, k, self.doReverseComplement)
+            self.source = src
+            n = src.n_kmers
+            self.feed_collection([Batch.from_source(src, 0, n, max(1, n), self.tmp)], feedMode)
+            return self
         src = FastaSource(dev, engine.read_input(fasta), k, self.doReverseComplement)
         self.source = src
         for name in src.parsed.names:

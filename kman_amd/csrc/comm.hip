@@ -19,6 +19,12 @@ namespace {
 
 struct Comm {
     ncclComm_t comm = nullptr;
+    // a second communicator (ncclCommSplit of the first, same ranks) for the
+    // all-to-alls queued on the communication stream: the two streams never
+    // issue work on one communicator, so RCCL's per-communicator ordering
+    // cannot interleave the overlapped exchanges with the compute stream's
+    // all-reduces and all-gathers
+    ncclComm_t comm2 = nullptr;
     int rank = 0, nranks = 1;
 };
 
@@ -73,6 +79,12 @@ extern "C" int kman_comm_init(kman_ctx *ctx, const uint8_t *id128, int nranks, i
         delete c;
         return nccl_fail(ctx, r, "ncclCommInitRank");
     }
+    const ncclResult_t r2 = ncclCommSplit(c->comm, 0, rank, &c->comm2, nullptr);
+    if (r2 != ncclSuccess) {
+        ncclCommDestroy(c->comm);
+        delete c;
+        return nccl_fail(ctx, r2, "ncclCommSplit");
+    }
     ctx->comm = c;
     return KMAN_OK;
 }
@@ -82,6 +94,8 @@ extern "C" int kman_comm_destroy(kman_ctx *ctx) {
     Comm *c = comm_of(ctx);
     if (!c) return KMAN_OK;
     (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->comm_stream) (void)hipStreamSynchronize(ctx->comm_stream);
+    if (c->comm2) ncclCommDestroy(c->comm2);
     ncclCommDestroy(c->comm);
     delete c;
     ctx->comm = nullptr;
@@ -107,13 +121,14 @@ extern "C" int kman_allgather_u64(kman_ctx *ctx, const uint64_t *d_send, uint64_
 // All-to-all-v of elem_bytes elements: send_counts/offsets and
 // recv_counts/offsets are host arrays of nranks elements (in elements).
 namespace {
-int alltoallv_on(kman_ctx *ctx, hipStream_t st, const void *d_send, const uint64_t *send_counts,
+int alltoallv_on(kman_ctx *ctx, hipStream_t st, bool second, const void *d_send, const uint64_t *send_counts,
                  const uint64_t *send_offsets, void *d_recv, const uint64_t *recv_counts,
                  const uint64_t *recv_offsets, uint32_t elem_bytes) {
     if (!ctx || !send_counts || !send_offsets || !recv_counts || !recv_offsets) return KMAN_EINVAL;
     if (elem_bytes != 4 && elem_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "elem_bytes must be 4 or 8");
     Comm *c = comm_of(ctx);
     if (!c) return kman_fail(ctx, KMAN_EINVAL, "no communicator");
+    ncclComm_t cm = second ? c->comm2 : c->comm;
     const ncclDataType_t t = elem_bytes == 8 ? ncclUint64 : ncclUint32;
     // messages in chunks of <= 512 MiB: a single multi-GiB send/recv pair
     // was observed to move only part of its bytes (RCCL 2.27, 2.4 GB to self);
@@ -131,11 +146,11 @@ int alltoallv_on(kman_ctx *ctx, hipStream_t st, const void *d_send, const uint64
             const uint64_t o = r * CH;
             if (send_counts[p] > o) {
                 const uint64_t n = send_counts[p] - o < CH ? send_counts[p] - o : CH;
-                NCCL_TRY(ctx, ncclSend((const char *)d_send + (send_offsets[p] + o) * elem_bytes, n, t, p, c->comm, st));
+                NCCL_TRY(ctx, ncclSend((const char *)d_send + (send_offsets[p] + o) * elem_bytes, n, t, p, cm, st));
             }
             if (recv_counts[p] > o) {
                 const uint64_t n = recv_counts[p] - o < CH ? recv_counts[p] - o : CH;
-                NCCL_TRY(ctx, ncclRecv((char *)d_recv + (recv_offsets[p] + o) * elem_bytes, n, t, p, c->comm, st));
+                NCCL_TRY(ctx, ncclRecv((char *)d_recv + (recv_offsets[p] + o) * elem_bytes, n, t, p, cm, st));
             }
         }
         NCCL_TRY(ctx, ncclGroupEnd());
@@ -148,7 +163,7 @@ extern "C" int kman_alltoallv(kman_ctx *ctx, const void *d_send, const uint64_t 
                               const uint64_t *send_offsets, void *d_recv, const uint64_t *recv_counts,
                               const uint64_t *recv_offsets, uint32_t elem_bytes) {
     if (!ctx) return KMAN_EINVAL;
-    return alltoallv_on(ctx, ctx->stream, d_send, send_counts, send_offsets, d_recv, recv_counts, recv_offsets,
+    return alltoallv_on(ctx, ctx->stream, false, d_send, send_counts, send_offsets, d_recv, recv_counts, recv_offsets,
                         elem_bytes);
 }
 
@@ -167,7 +182,7 @@ extern "C" int kman_alltoallv_async(kman_ctx *ctx, const void *d_send, const uin
     if (!ctx->comm_ev[slot]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->comm_ev[slot], hipEventDisableTiming));
     HIP_TRY(ctx, hipEventRecord(ctx->comm_pre, ctx->stream));
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->comm_stream, ctx->comm_pre, 0));
-    KMAN_TRY(alltoallv_on(ctx, ctx->comm_stream, d_send, send_counts, send_offsets, d_recv, recv_counts, recv_offsets,
+    KMAN_TRY(alltoallv_on(ctx, ctx->comm_stream, true, d_send, send_counts, send_offsets, d_recv, recv_counts, recv_offsets,
                           elem_bytes));
     HIP_TRY(ctx, hipEventRecord(ctx->comm_ev[slot], ctx->comm_stream));
     return KMAN_OK;

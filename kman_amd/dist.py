@@ -443,7 +443,8 @@ class DistPipeline:
                  uid: Optional[bytes] = None, canonical: bool = False, rc: bool = False, path: str = "region",
                  max_round_items: Optional[int] = None, chunk_bytes: int = 256 << 20, reload: bool = False,
                  mem_frac: float = 0.85, shard: Optional[S.ShardCodes] = None, local: bool = False,
-                 reparse: bool = False, overlap: Optional[bool] = None, ordered: bool = True):
+                 reparse: bool = False, overlap: Optional[bool] = None, ordered: bool = True,
+                 exchange: bool = False):
         engine._check_k(k)
         if mode not in ("count", "uniq"):
             raise ValueError(mode)
@@ -453,10 +454,18 @@ class DistPipeline:
         self.canonical, self.rc = canonical, rc and not canonical
         self.path, self.max_round_items, self.reload, self.mem_frac = path, max_round_items, reload, mem_frac
         self.reparse, self.ordered = reparse, ordered
-        # overlapped rounds (round_pieces): default on for several ranks;
-        # KMAN_DIST_OVERLAP=0/1 overrides (A/B), tests force it on one rank
+        # overlapped rounds (round_pieces): opt-in (overlap=True or
+        # KMAN_DIST_OVERLAP=1) until a run on two or more GPUs has passed the
+        # dist region tests with it; their all-to-alls run on a second
+        # communicator (comm.hip), so the two streams never share one
         env = os.environ.get("KMAN_DIST_OVERLAP")
-        self.overlap = (env != "0") if env is not None else (overlap if overlap is not None else world > 1)
+        self.overlap = (env == "1") if env is not None else bool(overlap)
+        # exchange: run the round's all-to-all even on one rank (RCCL's
+        # send/recv to self), so the 8-GPU data path runs at world 1 (tests:
+        # exchange=True or KMAN_DIST_EXCHANGE=1); off, one rank extracts
+        # straight into its receive buffer
+        envx = os.environ.get("KMAN_DIST_EXCHANGE")
+        self.exchange = world > 1 or (envx == "1" if envx is not None else bool(exchange))
         self.pieces = 4
         self.overlapped_rounds = 0
         self.fmode = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
@@ -634,13 +643,14 @@ class DistPipeline:
                 dev.upload(self.d_rtab, rtab)
                 # the send buffer is arena A; one rank extracts straight into
                 # its receive buffer B (no exchange at all)
+                xch = self.exchange and not isinstance(self.comm, LocalComm)
                 N.check(ctx, L.kman_dshard_extract(ctx, c_void_p(sh.codes.ptr), sh.n_eff, self.n_bases_q, self.k,
                                                    self.flags, self.fmode, c_void_p(self.d_hist.ptr),
-                                                   c_void_p(self.d_rtab.ptr), c_void_p((A if G > 1 else B).ptr)),
+                                                   c_void_p(self.d_rtab.ptr), c_void_p((A if xch else B).ptr)),
                         "kman_dshard_extract")
                 lo, nb, counts, rcnt, roff = round_recv(C, cuts, R, me, r)
                 lap("extract")
-                if G > 1:
+                if xch:
                     yield ("alltoallv", (A.ptr, sc, so, B.ptr, rcnt, roff, 8))
                     lap("exchange")
                 got = c_uint64(0)
@@ -874,6 +884,11 @@ class DistPipeline:
         if self.ordered:
             gk, gv = self.part_bufs[0].get(8 * max(1, nr)), self.part_bufs[1].get(vb * max(1, nr))
         else:  # (rows as a multiset: straight after the region rows; they fit, rows <= received k-mers)
+            if (n_out + n_region + nr) * 8 > ok_.nbytes or (n_out + n_region + nr) * vb > ov_.nbytes:
+                # (the redone windows are a subset of the round's: the marked
+                # extraction and the shard extraction disagree if this fires)
+                raise RuntimeError("rank %d: %d region rows + %d redone k-mers past the output buffer (%d rows)"
+                                   % (me, n_out + n_region, nr, ok_.nbytes // 8))
             gk, gv = (_View(ok_.ptr + 8 * (n_out + n_region), 8 * max(1, nr)),
                       _View(ov_.ptr + vb * (n_out + n_region), vb * max(1, nr)))
         if nr:

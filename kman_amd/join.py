@@ -15,11 +15,15 @@ are joined as the whole device-resident stream without materialising them.
 
 VEC_COUNT / VEC_COUNT_MASKED (join.py:288-335): the reference's
 AbundanceVector.add_count first calls its abstract base (abundance.py:60,123),
-which raises NotImplementedError, so its join never gets past the first
-k-mer.  Here they do what the code around that call evidently means
-(abundance.py:103-168): one vector per (record, strand) indexed by window
-start, holding the k-mer's count (VEC_COUNT) or its occurrences in other
-records when it occurs in more than one (VEC_COUNT_MASKED), written as
+which raises NotImplementedError, so its join stops at the first add_count:
+VEC_COUNT at the first k-mer, VEC_COUNT_MASKED at the first k-mer seen in two
+records of different names (join.py:318-335); a join that never calls it
+writes the empty vector folder (abundance.py:151-172).  That is the default
+here too (the device answers whether add_count would be called).  With
+``KMAN_VEC_COUNT=1`` they instead do what the code around that call evidently
+means (abundance.py:103-168): one vector per (record, strand) indexed by
+window start, holding the k-mer's count (VEC_COUNT) or its occurrences in
+other records when it occurs in more than one (VEC_COUNT_MASKED), written as
 ``<out>/<ref>___<strand>.gz`` = "# k=<k>" + one count per line.  The counts
 come from one device sort + kman_vec_fill; tests/test_gpu_vectors.py checks
 them against a restatement of that code (parity unpinned: the reference
@@ -186,6 +190,17 @@ class KJoiner:
     def join(self, batches: List[Batch], outpath: str) -> None:
         """Join batches into ``outpath`` on the GPU (join.py:376-391)."""
         print("Joining...")
+        from .launch import ShardedSource
+
+        sharded = [b for b in batches if b is not None and isinstance(b.source, ShardedSource)]
+        if sharded:
+            # one rank of a multi-GPU run (kman_amd/launch.py): the key rounds
+            # across the ranks, every rank writing its slice of `outpath`
+            if self.mode.name.startswith("VEC_") or len(sharded) != len(batches):
+                raise NotImplementedError("a multi-GPU launch joins the FastaBatcher shard batches by UNIQUE / "
+                                          "SEQ_COUNT only")
+            sharded[0].source.join(self.mode == self.MODE.SEQ_COUNT, outpath)
+            return
         if self.mode.name.startswith("VEC_"):
             join_vectors(batches, self.mode == self.MODE.VEC_COUNT_MASKED, outpath)
             return
@@ -242,12 +257,22 @@ def join_bytes(batches: List[Batch], count: bool, sink=None):
     return engine._to(sink, format_sources(keys, pos, k, srcs, tagged))
 
 
+def vectors_enabled() -> bool:
+    """KMAN_VEC_COUNT=1: write abundance vectors (this engine's semantics);
+    otherwise VEC_* behave as the reference (NotImplementedError at its first
+    add_count)."""
+    return os.environ.get("KMAN_VEC_COUNT") == "1"
+
+
 def join_vectors(batches: List[Batch], masked: bool, outpath: str) -> None:
     """Abundance vectors of the joined batches (module docstring): the union
     sorted on the device (gather_sorted), each item's count (or masked count)
     written at its (source, window, strand) slot by kman_vec_fill, then one
     gzip file per (record, strand) that received a count, its vector running
-    to the last such window (AbundanceVector.add_ref grows it to pos + 1)."""
+    to the last such window (AbundanceVector.add_ref grows it to pos + 1).
+    Without KMAN_VEC_COUNT=1: NotImplementedError wherever the reference's
+    add_count would be called, else the empty folder."""
+    emulate = not vectors_enabled()
     import ctypes
     from ctypes import byref, c_size_t, c_void_p
 
@@ -265,6 +290,9 @@ def join_vectors(batches: List[Batch], masked: bool, outpath: str) -> None:
         return
     if os.path.isfile(dirpath):
         raise AssertionError
+    if emulate and not masked:
+        # (the first group's add_count raises, abundance.py:60 via :123)
+        raise NotImplementedError("AbundanceVector.add_count (the reference's VEC_COUNT)")
     if not all(isinstance(e[0], FastaSource) for e in entries):
         raise NotImplementedError("abundance vectors of reloaded batch files (-B)")
     km, srcs, tagged = gather_sorted(entries, want_pos=True)
@@ -281,11 +309,16 @@ def join_vectors(batches: List[Batch], masked: bool, outpath: str) -> None:
         names += list(p.names)
         rec_start.append(base[si] + 2 * rs)
         rec_end.append(base[si] + 2 * ends)
-    if len(set(names)) != len(names):
+    if emulate:
+        # masked counts by record NAME (the reference's ref): nonzero exactly
+        # where a group holds two refs, i.e. where add_count would be called
+        rec_id = np.unique(np.asarray(names, dtype=object), return_inverse=True)[1].astype(np.uint32)
+    elif len(set(names)) != len(names):
         raise AssertionError("abundance vectors need distinct record names (one vector per ref:strand)")
+    else:
+        rec_id = np.arange(len(names), dtype=np.uint32)
     rec_start = np.concatenate(rec_start).astype(np.uint64)
     rec_end = np.concatenate(rec_end).astype(np.uint64)
-    rec_id = np.arange(len(names), dtype=np.uint32)
     bufs = []
     try:
         vec = dev.alloc(4 * max(total, 1))
@@ -306,6 +339,12 @@ def join_vectors(batches: List[Batch], masked: bool, outpath: str) -> None:
         km.free()
         for b in bufs:
             b.free()
+    if emulate:
+        if v.any():
+            raise NotImplementedError("AbundanceVector.add_count (the reference's VEC_COUNT_MASKED)")
+        print('Writing output in "%s"' % dirpath)  # abundance.py:160: no vector was added
+        os.makedirs(dirpath, exist_ok=True)
+        return
     print('Writing output in "%s"' % dirpath)  # abundance.py:160
     os.makedirs(dirpath, exist_ok=True)
     for r, name in enumerate(names):

@@ -164,3 +164,30 @@ def test_sequence_kmerator_known_answers():
     ]
     assert [list(g) for g in s.kmerator_batched(s.text, 4, s.natype, 5, s.name, True)] == want
     assert [k.seq for k in Sequence.kmerator("ACGNACGT", 3, NATYPES.DNA)] == ["ACG", "ACG", "CGT"]
+
+
+@pytest.mark.parametrize("case", [c for c in _manifest()["cases"] if c["k"] <= 32 and c["cmd"] in ("count", "uniq")
+                                  and "-B" not in c["flags"]][::3], ids=lambda c: c["name"])
+def test_cli_multi_gpu_path_world1(case, golden_inputs, tmp_path, monkeypatch):
+    """The CLI's multi-GPU path (kman_amd/launch.py) without SimGroup: with
+    KMAN_DIST=1 at world size 1, FastaBatcher.do loads the byte-range shard,
+    KJoiner.join builds a real RCCL communicator (one rank), runs the key
+    rounds with every exchange through RCCL (exchange forced) and writes the
+    output through DistPipeline.emit_gen -- byte-identical to the reference's
+    golden output."""
+    monkeypatch.setenv("KMAN_DIST", "1")
+    monkeypatch.setenv("KMAN_DIST_EXCHANGE", "1")
+    out = str(tmp_path / "out.txt")
+    _cli([case["cmd"], golden_inputs[case["input"]], out, str(case["k"])] + case["flags"])
+    assert _sha(out) == case["sha256"]
+
+
+def test_cli_hist_multi_gpu_path_world1(golden_inputs, tmp_path, monkeypatch):
+    """`kmer hist` through the multi-GPU path at world size 1 equals the
+    single-GPU spectrum."""
+    out1, out2 = str(tmp_path / "h1.txt"), str(tmp_path / "h2.txt")
+    _cli(["hist", golden_inputs["messy1"], out1, "21"])
+    monkeypatch.setenv("KMAN_DIST", "1")
+    monkeypatch.setenv("KMAN_DIST_EXCHANGE", "1")
+    _cli(["hist", golden_inputs["messy1"], out2, "21"])
+    assert open(out1, "rb").read() == open(out2, "rb").read() and os.path.getsize(out1) > 0

@@ -95,3 +95,82 @@ def test_dist_pipeline_world1_equals_single(dev, mode, path, tmp_path, oracle_bi
     src.write_bytes(text)
     subprocess.run([oracle_bin, mode, str(src), str(tmp_path / "w.txt"), "13"], check=True)
     assert out.read_bytes() == (tmp_path / "w.txt").read_bytes()
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("mode", ["count", "uniq"])
+@pytest.mark.parametrize("input_", ["messy", "repeats"])
+def test_dist_region_rccl_exchange_world1(dev, mode, overlap, input_):
+    """The region path's data path of an N > 1 run, driven through RCCL at
+    world size 1: each round's packed items leave through kman_alltoallv (RCCL
+    send/recv to self, exchange=True) -- or, overlap=True, through the pieces'
+    kman_alltoallv_async on the communication stream (second communicator)
+    with kman_comm_wait before each piece's finish -- and the redo of
+    overflowing key ranges (input "repeats") exchanges through RCCL too.
+    Rows bit-exact against np_oracle."""
+    import sys, os
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import inputs
+    import np_oracle
+    from kman_amd import dist, shard
+
+    if input_ == "messy":
+        text = inputs.messy_records(11, n_records=30, max_len=30000)
+    else:  # a segment repeated far past a region's share: the partial redo
+        rng = np.random.default_rng(5)
+        seg = "".join(rng.choice(list("ACGT"), 300))
+        body = inputs.syn_numpy(300_000, 4).split(b"\n", 1)[1].replace(b"\n", b"")
+        text = b">r\n" + body + b"\n>s\n" + (seg * 3000).encode() + b"\n"
+    p = dist.DistPipeline(dev, shard.BytesReader(text), 21, mode, 1, 0, dist.unique_id(), overlap=overlap,
+                          exchange=True, max_round_items=None if overlap else 200_000)
+    try:
+        p.step()
+        assert p.path == "region"
+        if overlap:
+            assert p.overlapped_rounds >= 1, "the overlapped exchange did not run"
+        else:
+            assert p.rounds >= 1
+        if input_ == "repeats":
+            assert p.partial_rounds >= 1, "no region overflowed: the RCCL redo did not run"
+        keys, vals = p.results()
+    finally:
+        p.free()
+    recs = np_oracle.parse_fasta(text)
+    kk, pp = np_oracle.stream_kmers(recs, 21)
+    sk, sp = np_oracle.stable_sort(kk, pp)
+    if mode == "count":
+        wk, wc = np_oracle.rle_count(sk)
+        np.testing.assert_array_equal(keys, wk)
+        np.testing.assert_array_equal(vals, wc)
+    else:
+        wk, wv = np_oracle.rle_uniq(sk, sp)
+        np.testing.assert_array_equal(keys, wk)
+        np.testing.assert_array_equal(vals, wv)
+
+
+def test_dist_canonical_hist_rccl_world1(dev):
+    """Config 5's data path through RCCL at world 1: canonical keys, the
+    exchange forced through kman_alltoallv, rows as a multiset
+    (ordered=False), the spectrum all-reduced; equal to the bincount of the
+    oracle's canonical counts."""
+    import sys, os
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import inputs
+    import np_oracle
+    from kman_amd import dist, shard
+
+    text = inputs.messy_records(13, n_records=30, max_len=30000)
+    p = dist.DistPipeline(dev, shard.BytesReader(text), 21, "count", 1, 0, dist.unique_id(), canonical=True,
+                          exchange=True, ordered=False)
+    try:
+        p.step()
+        h = p.comm.run(p.hist_gen(1000))
+    finally:
+        p.free()
+    recs = np_oracle.parse_fasta(text)
+    canon, _ = np_oracle.stream_kmers(recs, 21, canonical=True)
+    _, c = np.unique(canon, return_counts=True)
+    want = np.bincount(np.minimum(c, 999), minlength=1000).astype(np.uint64)
+    np.testing.assert_array_equal(h, want)

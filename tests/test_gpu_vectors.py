@@ -80,8 +80,10 @@ def _texts():
 @pytest.mark.parametrize("masked", [False, True])
 @pytest.mark.parametrize("rc", [False, True])
 @pytest.mark.parametrize("k", [3, 9, 21])
-def test_vectors_match_restatement(tmp_path, masked, rc, k):
+def test_vectors_match_restatement(tmp_path, monkeypatch, masked, rc, k):
     import np_oracle
+
+    monkeypatch.setenv("KMAN_VEC_COUNT", "1")  # (this engine's vector writer; the default raises as the reference)
 
     from kman_amd.batcher import FastaBatcher
     from kman_amd.join import KJoiner
@@ -102,3 +104,31 @@ def test_vectors_match_restatement(tmp_path, masked, rc, k):
         for key, (head, v) in got.items():
             assert head == "# k=%d" % k
             np.testing.assert_array_equal(v, want[key])
+
+
+@pytest.mark.parametrize("masked", [False, True])
+@pytest.mark.parametrize("k", [3, 21])
+def test_vectors_default_raise_like_reference(tmp_path, monkeypatch, masked, k):
+    """Without KMAN_VEC_COUNT=1, VEC_* do what the reference does: the first
+    AbundanceVector.add_count raises NotImplementedError (abundance.py:60,
+    via :123) -- VEC_COUNT at any k-mer, VEC_COUNT_MASKED at a k-mer shared by
+    records of different names (join.py:318-335) -- and a join that never
+    calls it writes the empty vector folder (abundance.py:151-165)."""
+    from kman_amd.batcher import FastaBatcher
+    from kman_amd.join import KJoiner
+
+    monkeypatch.delenv("KMAN_VEC_COUNT", raising=False)
+    texts = _texts() + [b">same\nACGTACGTAC\n>same\nACGTACGTAC\n", b">solo\n" + b"ACGTTGCA" * 50 + b"\n"]
+    for ti, text in enumerate(texts):
+        fa = tmp_path / ("in%d.fa" % ti)
+        fa.write_bytes(text)
+        batches = FastaBatcher(size=1000).do(str(fa), k).collection
+        mode = KJoiner.MODE.VEC_COUNT_MASKED if masked else KJoiner.MODE.VEC_COUNT
+        out = tmp_path / ("vec%d_%d%d.out" % (ti, k, masked))
+        calls = any(len(v) for v in _expected(text, k, False, masked).values())
+        if calls:
+            with pytest.raises(NotImplementedError):
+                KJoiner(mode).join(batches, str(out))
+        else:
+            KJoiner(mode).join(batches, str(out))
+            assert os.path.isdir(str(out)[:-4]) and os.listdir(str(out)[:-4]) == []

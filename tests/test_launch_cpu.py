@@ -1,0 +1,122 @@
+"""kman_amd/launch.py on the CPU: the launcher environment, the file reader
+the ranks cut their byte ranges from, and the RCCL-id rendezvous (a fake id
+maker: no GPU, no RCCL) across real processes, including a stale id file
+left by an earlier launch."""
+
+from __future__ import annotations
+
+import gzip
+import multiprocessing as mp
+import os
+import time
+
+import pytest
+
+
+def test_world_env(monkeypatch):
+    from kman_amd import launch
+
+    for v in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "KMAN_DIST"):
+        monkeypatch.delenv(v, raising=False)
+    assert launch.world_env() == (1, 0, 0) and not launch.distributed() and launch.solo_rank()
+    monkeypatch.setenv("WORLD_SIZE", "4")
+    monkeypatch.setenv("RANK", "2")
+    monkeypatch.setenv("LOCAL_RANK", "2")
+    assert launch.world_env() == (4, 2, 2) and launch.distributed() and not launch.solo_rank()
+    monkeypatch.setenv("KMAN_DIST", "0")
+    assert not launch.distributed()
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("KMAN_DIST", "1")
+    assert launch.distributed()  # (forced at world size 1: the RCCL path with one rank)
+    monkeypatch.setenv("RANK", "5")
+    with pytest.raises(RuntimeError):
+        launch.world_env()
+
+
+@pytest.mark.parametrize("gz", [False, True])
+def test_file_reader_cuts_like_bytes(tmp_path, gz):
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+    import inputs
+    from kman_amd import launch, shard
+
+    text = inputs.messy_records(3, n_records=25, max_len=5000)
+    p = tmp_path / ("in.fa.gz" if gz else "in.fa")
+    if gz:
+        with gzip.open(p, "wb") as fh:
+            fh.write(text)
+    else:
+        p.write_bytes(text)
+    rd = launch.FileReader(str(p))
+    try:
+        assert rd.size == len(text) and rd.read(-5, 10) == text[:10] and rd.read(len(text) - 3, 10 ** 9) == text[-3:]
+        for G in (1, 3, 8):
+            assert shard.shard_specs(rd, G, 13) == shard.shard_specs(shard.BytesReader(text), G, 13)
+    finally:
+        rd.close()
+    e = tmp_path / "empty.fa"
+    e.write_bytes(b"")
+    rd = launch.FileReader(str(e))
+    assert rd.size == 0 and rd.read(0, 10) == b""
+    with pytest.raises(AssertionError):  # parsers.py:105-107, on every rank
+        shard.shard_specs(rd, 2, 5)
+    rd.close()
+
+
+def _rank(rank, world, d, q, delay):
+    from kman_amd import launch
+
+    time.sleep(delay)
+    uid = launch.rendezvous(rank, world, "t", make_uid=lambda: bytes([7]) * 100 + os.urandom(28), directory=d,
+                            timeout=30)
+    q.put((rank, uid))
+
+
+def test_rendezvous_processes_and_stale_file(tmp_path):
+    """Rank 0 writes the id; peers started before or after it read that id,
+    never the stale one an earlier (crashed) launch left under the same key."""
+    from kman_amd import launch
+
+    d = str(tmp_path)
+    stale = launch._id_path("t", d)
+    with open(stale, "wb") as fh:  # an id file from a launch that started long ago
+        import struct
+
+        fh.write(launch._MAGIC + struct.pack("<d", time.time() - 3600) + b"\0" * 8 + b"\x01" * 128)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world = 4
+    # peers start first (they must wait for rank 0's fresh id), rank 0 last
+    ps = [ctx.Process(target=_rank, args=(r, world, d, q, 0.0 if r else 1.0)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=60) for _ in range(world))
+    for p in ps:
+        p.join(timeout=30)
+    assert len(set(got.values())) == 1 and got[0][:100] == bytes([7]) * 100
+    launch.remove_id("t", d)
+    assert not os.path.exists(stale)
+
+
+def test_cli_leaves_solo_work_to_rank_zero(tmp_path, monkeypatch):
+    """Outside the multi-GPU domain (k > 32 here), ranks other than 0 leave
+    without touching the GPU or the output; k <= 1 still raises everywhere."""
+    from click.testing import CliRunner
+
+    from kman_amd.scripts.kmer import main
+
+    src = tmp_path / "in.fa"
+    src.write_bytes(b">a\nACGTACGTACGTACGTACGTACGTACGTACGTACGTACGTACGTACGT\n")
+    out = tmp_path / "o.txt"
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("RANK", "1")
+    monkeypatch.setenv("LOCAL_RANK", "1")
+    r = CliRunner().invoke(main, ["count", str(src), str(out), "40"])
+    assert r.exit_code == 0, r.output
+    assert not out.exists()
+    r = CliRunner().invoke(main, ["batch", str(src), str(tmp_path / "bd"), "5"])
+    assert r.exit_code == 0 and not (tmp_path / "bd").exists()
+    r = CliRunner().invoke(main, ["count", str(src), str(out), "1"])
+    assert isinstance(r.exception, AssertionError)
