@@ -363,6 +363,36 @@ int kman_gather(kman_ctx *ctx, const void *d_src, const uint64_t *d_idx, uint64_
 int kman_rle_wide(kman_ctx *ctx, int mode, const uint64_t *d_hi, const uint64_t *d_lo, const void *d_vals,
                   uint32_t val_bytes, uint64_t n, uint64_t *d_ohi, uint64_t *d_olo, void *d_ovals, uint64_t *n_out);
 
+/* Any k >= 2 (the reference has no k limit: Sequence.yield_kmers,
+ * seq.py:285-328; FastaBatcher.do asserts only k > 1, batcher.py:477-478):
+ * a k-mer as W = ceil(k / 32) words, MSB-first -- word 0 the first
+ * k - 32 (W - 1) bases, words 1 .. W-1 32 bases each -- so (w_0 .. w_{W-1})
+ * in lexicographic order is the reference's str order (Batch.sorted,
+ * batch.py:156-168).  Word-major planes: word j of item i at
+ * d_words[j * stride + i] (W = 2 is kman_extract_wide's (hi, lo)).
+ *   kman_extract_words  keys (+ pos, (global base << 1) | strand) of the valid
+ *                       windows in stream order (records, positions, + then
+ *                       - with KMAN_RC; one min(fwd, rc) key per window with
+ *                       KMAN_CANONICAL); d_words = d_pos = NULL only counts;
+ *                       KMAN_ECAP (with *n_out) when more than cap
+ *   kman_rle_words      count / uniq of sorted word keys (Crawler.do_batch +
+ *                       join_sequence_count / join_unique, join.py:95-130,
+ *                       244-285): KMAN_FINISH_COUNT -> d_ovals = group sizes;
+ *                       UNIQ -> the keys of groups of one with their d_vals
+ *   kman_batch_tags     d_tags[i] = (start + d_perm[i]) / per_batch: the batch
+ *                       of every item of a permutation of stream range
+ *                       [start, ..) (Batch.sorted per batch, batch.py:156-168)
+ * The sort is LSD over the planes: stable kman_sort passes with an index
+ * payload and kman_gather (kman_amd/engine.py sort_words). */
+int kman_extract_words(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, uint32_t k, uint32_t flags,
+                       uint64_t *d_words, uint64_t stride, void *d_pos, uint32_t pos_bytes, uint64_t cap,
+                       uint64_t *n_out);
+int kman_rle_words(kman_ctx *ctx, int mode, const uint64_t *d_words, uint32_t W, uint64_t stride, const void *d_vals,
+                   uint32_t val_bytes, uint64_t n, uint64_t *d_owords, uint64_t ostride, void *d_ovals,
+                   uint32_t oval_bytes, uint64_t *n_out);
+int kman_batch_tags(kman_ctx *ctx, const uint64_t *d_perm, uint64_t n, uint64_t start, uint64_t per_batch,
+                    uint64_t *d_tags);
+
 /* Run-length count of sorted keys (join.py:95-130 + 266-285):
  * d_ukeys[j], d_counts[j] (u32 if count_bytes == 4 else u64). */
 int kman_rle_count(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint64_t *d_ukeys,
@@ -488,6 +518,17 @@ int kman_format_uniq_mixed(const uint64_t *keys, const uint64_t *pos, uint64_t n
                            uint64_t n_records, char *out, size_t cap, size_t *used, int threads);
 int kman_format_count_wide(const uint64_t *hi, const uint64_t *lo, const void *counts, uint32_t count_bytes,
                            uint64_t n, uint32_t k, char *out, size_t cap, size_t *used, int threads);
+/* any k >= 2 over W word planes (kman_extract_words layout, row i's word j at
+ * words[j * stride + i]) */
+int kman_format_count_words(const uint64_t *words, uint64_t stride, const void *counts, uint32_t count_bytes,
+                            uint64_t n, uint32_t k, char *out, size_t cap, size_t *used, int threads);
+int kman_format_uniq_words(const uint64_t *words, uint64_t stride, const void *pos, uint32_t pos_bytes, uint64_t n,
+                           uint32_t k, const char *names, const uint64_t *name_off, const uint64_t *rec_seq,
+                           uint64_t n_records, char *out, size_t cap, size_t *used, int threads);
+int kman_format_uniq_mixed_words(const uint64_t *words, uint64_t stride, const uint64_t *pos, uint64_t n, uint32_t k,
+                                 const char *names, const uint64_t *name_off, const uint64_t *rec_seq,
+                                 const uint8_t *rec_kind, uint64_t n_records, char *out, size_t cap, size_t *used,
+                                 int threads);
 int kman_format_uniq_wide(const uint64_t *hi, const uint64_t *lo, const void *pos, uint32_t pos_bytes, uint64_t n,
                           uint32_t k, const char *names, const uint64_t *name_off, const uint64_t *rec_seq,
                           uint64_t n_records, char *out, size_t cap, size_t *used, int threads);
@@ -510,6 +551,14 @@ int kman_format_uniq_wide_dev(kman_ctx *ctx, const uint64_t *d_hi, const uint64_
                               uint32_t pos_bytes, uint64_t n, uint32_t k, const char *d_names,
                               const uint64_t *d_name_off, const uint64_t *d_rec_seq, uint64_t n_records, char *d_out,
                               size_t cap, size_t *used);
+
+/* any k >= 2: the device writers over W word planes */
+int kman_format_count_words_dev(kman_ctx *ctx, const uint64_t *d_words, uint64_t stride, const void *d_counts,
+                                uint32_t count_bytes, uint64_t n, uint32_t k, char *d_out, size_t cap, size_t *used);
+int kman_format_uniq_words_dev(kman_ctx *ctx, const uint64_t *d_words, uint64_t stride, const void *d_pos,
+                               uint32_t pos_bytes, uint64_t n, uint32_t k, const char *d_names,
+                               const uint64_t *d_name_off, const uint64_t *d_rec_seq, uint64_t n_records,
+                               char *d_out, size_t cap, size_t *used);
 
 #ifdef __cplusplus
 }

@@ -211,6 +211,35 @@ SIGNATURES = {
         c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64, c_void_p,
                 c_size_t, POINTER(c_size_t), c_int],
     ),
+    "kman_extract_words": (
+        c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_void_p, c_uint64, c_void_p, c_uint32, c_uint64,
+                POINTER(c_uint64)],
+    ),
+    "kman_rle_words": (
+        c_int, [c_void_p, c_int, c_void_p, c_uint32, c_uint64, c_void_p, c_uint32, c_uint64, c_void_p, c_uint64,
+                c_void_p, c_uint32, POINTER(c_uint64)],
+    ),
+    "kman_batch_tags": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_void_p]),
+    "kman_format_count_words": (
+        c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_size_t, POINTER(c_size_t),
+                c_int],
+    ),
+    "kman_format_uniq_words": (
+        c_int, [c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_uint64,
+                c_void_p, c_size_t, POINTER(c_size_t), c_int],
+    ),
+    "kman_format_uniq_mixed_words": (
+        c_int, [c_void_p, c_uint64, c_void_p, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p, c_uint64,
+                c_void_p, c_size_t, POINTER(c_size_t), c_int],
+    ),
+    "kman_format_count_words_dev": (
+        c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_size_t,
+                POINTER(c_size_t)],
+    ),
+    "kman_format_uniq_words_dev": (
+        c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_uint32, c_uint64, c_uint32, c_void_p, c_void_p, c_void_p,
+                c_uint64, c_void_p, c_size_t, POINTER(c_size_t)],
+    ),
     "kman_merge_runs": (c_int, [c_void_p, c_void_p, c_int, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kman_count_descents": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
     "kman_format_vector": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p, c_size_t, POINTER(c_size_t), c_int]),

@@ -141,13 +141,14 @@ class Batch:
         return sorted(self.record_gen(smart))
 
     def _kmers_from(self, keys, pos) -> Iterator[KMer]:
-        from .engine import decode_key
+        from .engine import decode_key, decode_words
         from .seq import SequenceCoords
 
         k = self._src.k
+        dec = (lambda x: decode_words(x, k)) if keys.ndim == 2 else (lambda x: decode_key(x, k))
         for key, p in zip(keys.tolist(), pos.tolist()):
             c = SequenceCoords.from_str(self._src.header(p))
-            yield KMer(c.ref, c.start, c.end, decode_key(key, k), strand=c.strand)
+            yield KMer(c.ref, c.start, c.end, dec(key), strand=c.strand)
 
     def _record_gen_from_handle(self, TH: IO, smart: bool = False) -> Iterator[Any]:
         if self.isFasta:

@@ -82,21 +82,37 @@ KMAN_DEV uint32_t put_key(const S &s, uint32_t at, const uint64_t *hi, uint64_t 
     return put_seq(s, at, key, 32);
 }
 
+// any k: W word planes (words.hip layout: word 0 the first k - 32 (W - 1)
+// bases, then 32 per word), row i's word j at words[j * stride + i]
+struct WordKeys {
+    const uint64_t *words = nullptr;
+    uint64_t stride = 0;
+    uint32_t W = 0;
+    template <typename S>
+    KMAN_DEV uint32_t put(const S &s, uint32_t at, uint64_t i, uint32_t k) const {
+        const uint32_t h = k - 32 * (W - 1);
+        for (uint32_t j = 0; j < W; j++) at = put_seq(s, at, words[j * stride + i], j ? 32u : h);
+        return at;
+    }
+};
+
 struct CountRows {
     const uint64_t *keys;
     const void *vals;
     uint32_t vb, k;
     const uint64_t *hi = nullptr;  // word-pair keys (k > 32)
+    WordKeys wk = {};              // or W word planes (keys unused)
     KMAN_DEV uint64_t val(uint64_t i) const {
         return vb == 4 ? ((const uint32_t *)vals)[i] : ((const uint64_t *)vals)[i];
     }
     struct Row {
-        uint64_t key, khi, c;
+        uint64_t key, khi, c, idx;
         uint32_t nd;
     };
     KMAN_DEV Row load(uint64_t i) const {
         Row r;
-        r.key = keys[i];
+        r.idx = i;
+        r.key = wk.words ? 0 : keys[i];
         r.khi = hi ? hi[i] : 0;
         r.c = val(i);
         r.nd = ndig(r.c);
@@ -105,7 +121,7 @@ struct CountRows {
     KMAN_DEV uint32_t len(const Row &r) const { return k + 2 + r.nd; }
     template <typename S>
     KMAN_DEV uint32_t write(const S &s, uint32_t at, const Row &r) const {
-        at = put_key(s, at, hi, r.khi, r.key, k);
+        at = wk.words ? wk.put(s, at, r.idx, k) : put_key(s, at, hi, r.khi, r.key, k);
         s.put(at++, '\t');
         at = put_dec(s, at, r.c, r.nd);
         s.put(at++, '\n');
@@ -121,14 +137,16 @@ struct UniqRows {
     const uint64_t *name_off, *rec_seq;
     uint64_t R;
     const uint64_t *hi = nullptr;  // word-pair keys (k > 32)
+    WordKeys wk = {};              // or W word planes (keys unused)
     struct Row {
-        uint64_t key, khi, st, noff;
+        uint64_t key, khi, st, noff, idx;
         uint32_t nlen, nd0, nd1;
         bool minus;
     };
     KMAN_DEV Row load(uint64_t i) const {
         Row r;
-        r.key = keys[i];
+        r.idx = i;
+        r.key = wk.words ? 0 : keys[i];
         r.khi = hi ? hi[i] : 0;
         const uint64_t v = vb == 4 ? ((const uint32_t *)vals)[i] : ((const uint64_t *)vals)[i];
         const uint64_t g = v >> 1;
@@ -162,7 +180,7 @@ struct UniqRows {
         s.put(at++, ':');
         s.put(at++, r.minus ? '-' : '+');
         s.put(at++, '\n');
-        at = put_key(s, at, hi, r.khi, r.key, k);
+        at = wk.words ? wk.put(s, at, r.idx, k) : put_key(s, at, hi, r.khi, r.key, k);
         s.put(at++, '\n');
         return at;
     }
@@ -308,4 +326,31 @@ extern "C" int kman_format_uniq_wide_dev(kman_ctx *ctx, const uint64_t *d_hi, co
                       UniqRows{d_lo, d_pos, pos_bytes, k, reinterpret_cast<const uint8_t *>(d_names), d_name_off,
                                d_rec_seq, n_records, d_hi},
                       n, d_out, cap, used);
+}
+
+// any k >= 2 as W = ceil(k / 32) word planes (words.hip)
+extern "C" int kman_format_count_words_dev(kman_ctx *ctx, const uint64_t *d_words, uint64_t stride,
+                                           const void *d_counts, uint32_t count_bytes, uint64_t n, uint32_t k,
+                                           char *d_out, size_t cap, size_t *used) {
+    if (!ctx || !used || (n && (!d_words || !d_counts))) return KMAN_EINVAL;
+    if (k < 2) return kman_fail(ctx, KMAN_EINVAL, "k must be >= 2, got %u", k);
+    if (count_bytes != 4 && count_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "count_bytes must be 4 or 8");
+    if (stride < n) return kman_fail(ctx, KMAN_EINVAL, "stride below n");
+    CountRows rows{nullptr, d_counts, count_bytes, k};
+    rows.wk = WordKeys{d_words, stride, (k + 31) / 32};
+    return run_format(ctx, rows, n, d_out, cap, used);
+}
+
+extern "C" int kman_format_uniq_words_dev(kman_ctx *ctx, const uint64_t *d_words, uint64_t stride, const void *d_pos,
+                                          uint32_t pos_bytes, uint64_t n, uint32_t k, const char *d_names,
+                                          const uint64_t *d_name_off, const uint64_t *d_rec_seq, uint64_t n_records,
+                                          char *d_out, size_t cap, size_t *used) {
+    if (!ctx || !used || (n && (!d_words || !d_pos || !d_name_off || !d_rec_seq || !n_records))) return KMAN_EINVAL;
+    if (k < 2) return kman_fail(ctx, KMAN_EINVAL, "k must be >= 2, got %u", k);
+    if (pos_bytes != 4 && pos_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "pos_bytes must be 4 or 8");
+    if (stride < n) return kman_fail(ctx, KMAN_EINVAL, "stride below n");
+    UniqRows rows{nullptr, d_pos, pos_bytes, k, reinterpret_cast<const uint8_t *>(d_names), d_name_off, d_rec_seq,
+                  n_records};
+    rows.wk = WordKeys{d_words, stride, (k + 31) / 32};
+    return run_format(ctx, rows, n, d_out, cap, used);
 }

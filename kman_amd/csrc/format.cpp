@@ -51,6 +51,18 @@ inline char *put_seq_wide(char *p, uint64_t hi, uint64_t lo, uint32_t k) {
     return put_seq(p, lo, 32);
 }
 
+// any k: W word planes (words.hip layout), row i's word j at w[j * stride + i]
+struct Words {
+    const uint64_t *w;
+    uint64_t stride;
+    uint32_t W;
+    char *put(char *p, uint64_t i, uint32_t k) const {
+        const uint32_t h = k - 32 * (W - 1);
+        for (uint32_t j = 0; j < W; j++) p = put_seq(p, w[j * stride + i], j ? 32u : h);
+        return p;
+    }
+};
+
 inline uint64_t get_val(const void *a, uint32_t bytes, uint64_t i) {
     return bytes == 4 ? ((const uint32_t *)a)[i] : ((const uint64_t *)a)[i];
 }
@@ -107,7 +119,7 @@ struct Names {
 
 int format_fasta_impl(const uint64_t *keys, const void *pos, uint32_t pos_bytes, uint64_t n, uint32_t k,
                       const Names &nm, char *out, size_t cap, size_t *used, int threads,
-                      const uint64_t *hi = nullptr) {
+                      const uint64_t *hi = nullptr, const Words *wd = nullptr) {
     auto size_of = [&](uint64_t i) -> size_t {
         const uint64_t v = get_val(pos, pos_bytes, i);
         const uint64_t p = v >> 1;
@@ -132,7 +144,7 @@ int format_fasta_impl(const uint64_t *keys, const void *pos, uint32_t pos_bytes,
         *p++ = ':';
         *p++ = (v & 1) ? '-' : '+';
         *p++ = '\n';
-        p = hi ? put_seq_wide(p, hi[i], keys[i], k) : put_seq(p, keys[i], k);
+        p = wd ? wd->put(p, i, k) : hi ? put_seq_wide(p, hi[i], keys[i], k) : put_seq(p, keys[i], k);
         *p++ = '\n';
         return p;
     };
@@ -184,12 +196,10 @@ extern "C" int kman_format_uniq(const uint64_t *keys, const void *pos, uint32_t 
 // rec_kind[r] = 0: a FASTA record (header name:start-end:strand), 1: a batch
 // file record whose title is the header as written (the k-mer's own
 // "ref:start-end:strand").
-extern "C" int kman_format_uniq_mixed(const uint64_t *keys, const uint64_t *pos, uint64_t n, uint32_t k,
-                                      const char *names, const uint64_t *name_off, const uint64_t *rec_seq,
-                                      const uint8_t *rec_kind, uint64_t n_records, char *out, size_t cap,
-                                      size_t *used, int threads) {
-    if (!used || (n && (!keys || !pos || !name_off || !rec_seq || !rec_kind || !n_records)) || k < 1 || k > 32)
-        return KMAN_EINVAL;
+namespace {
+int uniq_mixed_impl(const uint64_t *keys, const Words *wd, const uint64_t *pos, uint64_t n, uint32_t k,
+                    const char *names, const uint64_t *name_off, const uint64_t *rec_seq, const uint8_t *rec_kind,
+                    uint64_t n_records, char *out, size_t cap, size_t *used, int threads) {
     Names nm{names, name_off, rec_seq, n_records};
     auto size_of = [&](uint64_t i) -> size_t {
         const uint64_t g = pos[i] >> 1;
@@ -216,11 +226,64 @@ extern "C" int kman_format_uniq_mixed(const uint64_t *keys, const uint64_t *pos,
             *p++ = (v & 1) ? '-' : '+';
         }
         *p++ = '\n';
-        p = put_seq(p, keys[i], k);
+        p = wd ? wd->put(p, i, k) : put_seq(p, keys[i], k);
         *p++ = '\n';
         return p;
     };
     return run_sliced(n, out, cap, used, threads, size_of, write_at);
+}
+}  // namespace
+
+extern "C" int kman_format_uniq_mixed(const uint64_t *keys, const uint64_t *pos, uint64_t n, uint32_t k,
+                                      const char *names, const uint64_t *name_off, const uint64_t *rec_seq,
+                                      const uint8_t *rec_kind, uint64_t n_records, char *out, size_t cap,
+                                      size_t *used, int threads) {
+    if (!used || (n && (!keys || !pos || !name_off || !rec_seq || !rec_kind || !n_records)) || k < 1 || k > 32)
+        return KMAN_EINVAL;
+    return uniq_mixed_impl(keys, nullptr, pos, n, k, names, name_off, rec_seq, rec_kind, n_records, out, cap, used,
+                           threads);
+}
+
+// the same over W word planes (any k >= 2; words.hip layout)
+extern "C" int kman_format_uniq_mixed_words(const uint64_t *words, uint64_t stride, const uint64_t *pos, uint64_t n,
+                                            uint32_t k, const char *names, const uint64_t *name_off,
+                                            const uint64_t *rec_seq, const uint8_t *rec_kind, uint64_t n_records,
+                                            char *out, size_t cap, size_t *used, int threads) {
+    if (!used || (n && (!words || !pos || !name_off || !rec_seq || !rec_kind || !n_records)) || k < 2 || stride < n)
+        return KMAN_EINVAL;
+    const Words wd{words, stride, (k + 31) / 32};
+    return uniq_mixed_impl(nullptr, &wd, pos, n, k, names, name_off, rec_seq, rec_kind, n_records, out, cap, used,
+                           threads);
+}
+
+// any k >= 2 over W word planes: the count table and the uniq / batch FASTA
+extern "C" int kman_format_count_words(const uint64_t *words, uint64_t stride, const void *counts,
+                                       uint32_t count_bytes, uint64_t n, uint32_t k, char *out, size_t cap,
+                                       size_t *used, int threads) {
+    if (!used || (n && (!words || !counts)) || k < 2 || stride < n) return KMAN_EINVAL;
+    if (count_bytes != 4 && count_bytes != 8) return KMAN_EINVAL;
+    const Words wd{words, stride, (k + 31) / 32};
+    auto size_of = [&](uint64_t i) -> size_t { return k + 2 + ndigits(get_val(counts, count_bytes, i)); };
+    auto write_at = [&](uint64_t i, char *p) -> char * {
+        p = wd.put(p, i, k);
+        *p++ = '\t';
+        p = put_u64(p, get_val(counts, count_bytes, i));
+        *p++ = '\n';
+        return p;
+    };
+    return run_sliced(n, out, cap, used, threads, size_of, write_at);
+}
+
+extern "C" int kman_format_uniq_words(const uint64_t *words, uint64_t stride, const void *pos, uint32_t pos_bytes,
+                                      uint64_t n, uint32_t k, const char *names, const uint64_t *name_off,
+                                      const uint64_t *rec_seq, uint64_t n_records, char *out, size_t cap,
+                                      size_t *used, int threads) {
+    if (!used || (n && (!words || !pos || !name_off || !rec_seq || !n_records)) || k < 2 || stride < n)
+        return KMAN_EINVAL;
+    if (pos_bytes != 4 && pos_bytes != 8) return KMAN_EINVAL;
+    Names nm{names, name_off, rec_seq, n_records};
+    const Words wd{words, stride, (k + 31) / 32};
+    return format_fasta_impl(nullptr, pos, pos_bytes, n, k, nm, out, cap, used, threads, nullptr, &wd);
 }
 
 // k in 33..64: keys as (hi, lo) word pairs (kman_extract_wide)

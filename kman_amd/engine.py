@@ -32,7 +32,7 @@ import numpy as np
 from . import _native as N
 
 MAX_K = 32       # 2-bit keys in one u64 (the region / prefix-split paths)
-MAX_K_WIDE = 64  # (hi, lo) word-pair keys (kman_extract_wide + two sort passes)
+MAX_K_WIDE = 64  # k <= 64: kman_extract_wide rolls the two words of a key; beyond, kman_extract_words
 
 
 def host_threads() -> int:
@@ -266,6 +266,11 @@ def flags_for(rc: bool, want_pos: bool, canonical: bool = False) -> int:
 def count_kmers(p: Parsed, k: int, rc: bool, canonical: bool = False) -> int:
     _check_k(k, wide=True)
     out = c_uint64(0)
+    if k > MAX_K_WIDE:
+        N.check(p.dev.ctx, N.lib().kman_extract_words(p.dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
+                                                      flags_for(rc, False, canonical), None, 0, None, 0, 0,
+                                                      byref(out)), "kman_extract_words")
+        return int(out.value)
     if k > MAX_K:
         N.check(p.dev.ctx, N.lib().kman_extract_wide(p.dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
                                                      flags_for(rc, False, canonical), None, None, None, 0, 0,
@@ -277,13 +282,14 @@ def count_kmers(p: Parsed, k: int, rc: bool, canonical: bool = False) -> int:
 
 
 def _check_k(k: int, wide: bool = False) -> None:
-    """batcher.py:477-478 (k <= 1 raises AssertionError); k > 32 only where
-    the word-pair path runs (count / uniq), k > 64 not on the GPU."""
+    """batcher.py:477-478 (k <= 1 raises AssertionError); a path that packs a
+    k-mer in one 64-bit key (region / prefix-split / multi-GPU) takes
+    k <= 32, the word-key path (wide) every k."""
     if k <= 1:
         raise AssertionError("k must be >= 1, got %d instead." % k)
-    if k > (MAX_K_WIDE if wide else MAX_K):
-        raise NotImplementedError("k=%d: this MI355X path packs k-mers in %s (k <= %d)"
-                                  % (k, "two 64-bit words" if wide else "64-bit keys", MAX_K_WIDE if wide else MAX_K))
+    if not wide and k > MAX_K:
+        raise NotImplementedError("k=%d: this path packs k-mers in one 64-bit key (k <= %d); the word-key path "
+                                  "takes larger k" % (k, MAX_K))
 
 
 def extract(p: Parsed, k: int, rc: bool, want_pos: bool, canonical: bool = False) -> Kmers:
@@ -667,6 +673,21 @@ def _format(fn, *args) -> bytes:
     return buf.raw[: used.value]
 
 
+def format_fasta_words(rows: np.ndarray, pos: np.ndarray, k: int, p: Parsed) -> bytes:
+    """The batch-file FASTA (KMer.as_fasta, seq.py:489-495) of word-key rows
+    ((n, W) host array) with headers from the record table (host writer
+    kman_format_uniq_words)."""
+    planes = np.ascontiguousarray(np.asarray(rows, dtype=np.uint64).T)
+    n = planes.shape[1] if planes.ndim == 2 else 0
+    pos = np.ascontiguousarray(pos, dtype=np.uint64)
+    names = ctypes.create_string_buffer(p.names_blob, max(1, len(p.names_blob)))
+    off = np.ascontiguousarray(p.name_off, dtype=np.uint64)
+    rs = np.ascontiguousarray(p.rec_seq, dtype=np.uint64)
+    return _format(N.lib().kman_format_uniq_words, planes.ctypes.data_as(c_void_p), max(n, 1),
+                   pos.ctypes.data_as(c_void_p), 8, n, k, names, off.ctypes.data_as(c_void_p),
+                   rs.ctypes.data_as(c_void_p), max(p.n_records, 1))
+
+
 def format_count(ukeys: np.ndarray, counts: np.ndarray, k: int) -> bytes:
     """``"%s\\t%d\\n" % (seq, count)`` per group (join.py:283-284)."""
     ukeys = np.ascontiguousarray(ukeys, dtype=np.uint64)
@@ -890,7 +911,10 @@ def count_groups(p: Parsed, k: int, rc: bool = False, canonical: bool = False, o
     """(key, count) per distinct k-mer on the device: the region path, else
     the prefix-split path (None only when there are no k-mers).
     ordered=False: the rows may come in any order (a spectrum needs only
-    the multiset; the key rounds then skip merging a redone key range)."""
+    the multiset; the key rounds then skip merging a redone key range).
+    k > 32: a WordsResult (word keys, its counts in .vals)."""
+    if k > MAX_K:
+        return words_groups(p, k, rc, "count", canonical)
     r = groups(p, k, rc, "count", canonical)
     if r is not None:
         return r
@@ -915,7 +939,7 @@ def abundance_hist(text: bytes, k: int, canonical: bool = True, nbins: int = 100
     reference): h[c] = distinct (canonical) k-mers seen c times, h[-1] every
     count >= nbins - 1 (kman_count_hist over the count output)."""
     dev = dev or default_device()
-    _check_k(k)
+    _check_k(k, wide=True)
     p = parse(dev, text)
     try:
         r = count_groups(p, k, False, canonical, ordered=False)
@@ -924,12 +948,12 @@ def abundance_hist(text: bytes, k: int, canonical: bool = True, nbins: int = 100
             if r is None:
                 return np.zeros(nbins, np.uint64)
             try:
-                N.check(dev.ctx, N.lib().kman_count_hist(dev.ctx, c_void_p(r.counts.ptr), r.count_bytes, r.n,
+                cnt, cb = (r.vals, r.val_bytes) if isinstance(r, WordsResult) else (r.counts, r.count_bytes)
+                N.check(dev.ctx, N.lib().kman_count_hist(dev.ctx, c_void_p(cnt.ptr), cb, r.n,
                                                          c_void_p(d_h.ptr), nbins), "kman_count_hist")
                 return dev.download(d_h, nbins, np.uint64)
             finally:
-                r.ukeys.free()
-                r.counts.free()
+                free_result(r)
         finally:
             d_h.free()
     finally:
@@ -955,90 +979,199 @@ def _fits(p: Parsed, k: int, rc: bool, mode: str) -> bool:
     return need <= 0.85 * mem_info(p.dev)[0]
 
 
-@dataclass
-class WideResult:
-    """count / uniq rows of k > 32: keys as (hi, lo) word pairs."""
+def nwords(k: int) -> int:
+    """64-bit words per k-mer of the any-k path (words.hip): ceil(k / 32)."""
+    return (k + 31) // 32
 
-    hi: DeviceBuffer
-    lo: DeviceBuffer
+
+@dataclass
+class Words:
+    """k-mer keys of any k as W word planes (words.hip layout: word 0 the
+    first k - 32 (W - 1) bases, then 32 bases per word, all MSB-first; word j
+    of item i at words[j * stride + i]) + an optional u64 pos payload."""
+
+    words: DeviceBuffer
+    pos: Optional[DeviceBuffer]
+    n: int
+    k: int
+    stride: int
+
+    @property
+    def W(self) -> int:
+        return nwords(self.k)
+
+    def plane(self, j: int) -> int:
+        return self.words.ptr + 8 * j * self.stride
+
+    def free(self) -> None:
+        for b in (self.words, self.pos):
+            if b is not None:
+                b.free()
+
+
+@dataclass
+class WordsResult:
+    """count / uniq rows of k > 32: keys as W word planes (stride n)."""
+
+    words: DeviceBuffer
     vals: DeviceBuffer
     val_bytes: int
     n: int
     k: int
     mode: str
 
+    @property
+    def W(self) -> int:
+        return nwords(self.k)
 
-def wide_groups(p: Parsed, k: int, rc: bool, mode: str, canonical: bool = False) -> Optional[WideResult]:
-    """k in 33..64 (seq.py:285-328 has no k limit): kman_extract_wide (keys as
-    (hi, lo) + pos), two stable kman_sort passes -- by lo with an index
-    payload, then by the gathered hi -- (batch.py:156-168), kman_rle_wide
-    (join.py:95-130, 244-285).  None when the stream has no k-mers."""
+    def free(self) -> None:
+        self.words.free()
+        self.vals.free()
+
+
+def extract_words(p: Parsed, k: int, rc: bool, want_pos: bool, canonical: bool = False) -> Words:
+    """Keys (+ u64 pos) of the stream as word planes, in stream order
+    (Sequence.yield_kmers, seq.py:285-328): kman_extract_wide's rolled
+    LDS-staged kernel for k <= 64 (its (hi, lo) are planes 0 and 1),
+    kman_extract_words beyond."""
     _check_k(k, wide=True)
     dev, L = p.dev, N.lib()
-    uniq = mode == "uniq"
     n = count_kmers(p, k, rc, canonical)
+    W = nwords(k)
+    words = dev.alloc(8 * W * max(n, 1))
+    pos = dev.alloc(8 * max(n, 1)) if want_pos else None
+    w = Words(words, pos, n, k, max(n, 1))
     if n == 0:
-        return None
-    bufs = []
-
-    def alloc(nb):
-        b = dev.alloc(max(nb, 8))
-        bufs.append(b)
-        return b
-
+        return w
+    got = c_uint64(0)
     try:
-        hi, lo, pos = alloc(8 * n), alloc(8 * n), alloc(8 * n) if uniq else None
-        got = c_uint64(0)
-        N.check(dev.ctx, L.kman_extract_wide(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
-                                             flags_for(rc, uniq, canonical), c_void_p(hi.ptr), c_void_p(lo.ptr),
-                                             c_void_p(pos.ptr) if uniq else None, 8, n, byref(got)),
-                "kman_extract_wide")
-        assert int(got.value) == n
-        a, b, idx, idx2 = alloc(8 * n), alloc(8 * n), alloc(8 * n), alloc(8 * n)
+        if k <= MAX_K_WIDE:
+            N.check(dev.ctx, L.kman_extract_wide(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
+                                                 flags_for(rc, want_pos, canonical), c_void_p(w.plane(0)),
+                                                 c_void_p(w.plane(1)), c_void_p(pos.ptr) if pos else None, 8, n,
+                                                 byref(got)), "kman_extract_wide")
+        else:
+            N.check(dev.ctx, L.kman_extract_words(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k,
+                                                  flags_for(rc, want_pos, canonical), c_void_p(words.ptr), w.stride,
+                                                  c_void_p(pos.ptr) if pos else None, 8, n, byref(got)),
+                    "kman_extract_words")
+    except BaseException:
+        w.free()
+        raise
+    assert int(got.value) == n
+    return w
+
+
+def sort_words(w: Words, start: int = 0, per_batch: Optional[int] = None, dev: Optional[Device] = None) -> Words:
+    """A stably sorted copy of word keys (+ pos): LSD over the planes, last
+    word first, each a stable kman_sort of the gathered plane carrying the
+    permutation (ties keep stream order, as the reference's Timsort,
+    batch.py:156-168); per_batch: items in consecutive chunks of that many
+    from stream index `start` sorted chunk by chunk (one Batch each) -- a
+    final stable sort by the chunk tag (kman_batch_tags)."""
+    dev, L = dev or w.words.dev, N.lib()
+    n, W, k = w.n, w.W, w.k
+    out = Words(dev.alloc(8 * W * max(n, 1)), dev.alloc(8 * max(n, 1)) if w.pos is not None else None, n, k,
+                max(n, 1))
+    if n == 0:
+        return out
+    bufs = [dev.alloc(8 * n) for _ in range(4)]
+    try:
+        perm, key, alt_k, alt_p = bufs
+        N.check(dev.ctx, L.kman_iota_u64(dev.ctx, c_void_p(perm.ptr), n), "iota")
         res = c_int(0)
 
-        def stable_sort(keys, alt, vals, valt, bits):
-            N.check(dev.ctx, L.kman_sort(dev.ctx, c_void_p(keys.ptr), c_void_p(alt.ptr), c_void_p(vals.ptr),
-                                         c_void_p(valt.ptr), 8, n, bits, None, byref(res)), "kman_sort")
-            return (alt, valt, keys, vals) if res.value else (keys, vals, alt, valt)
+        def stable(keys_, bits):
+            nonlocal perm, alt_k, alt_p
+            N.check(dev.ctx, L.kman_sort(dev.ctx, c_void_p(keys_.ptr), c_void_p(alt_k.ptr), c_void_p(perm.ptr),
+                                         c_void_p(alt_p.ptr), 8, n, bits, None, byref(res)), "kman_sort")
+            if res.value:  # (the sorted copy is in the alternates)
+                perm, alt_p = alt_p, perm
+                return alt_k, keys_
+            return keys_, alt_k
 
-        # LSD over the 2k key bits: the low word first (index payload) ...
-        N.check(dev.ctx, L.kman_iota_u64(dev.ctx, c_void_p(idx.ptr), n), "iota")
-        lo_s, idx1, spare_k, spare_v = stable_sort(lo, a, idx, idx2, 64)
-        N.check(dev.ctx, L.kman_gather(dev.ctx, c_void_p(hi.ptr), c_void_p(idx1.ptr), n, c_void_p(spare_k.ptr), 8),
-                "gather")
-        # ... then the high word (stable: ties keep the low-word order)
-        perm = hi  # (hi is consumed: its gathered copy is in spare_k)
-        N.check(dev.ctx, L.kman_iota_u64(dev.ctx, c_void_p(perm.ptr), n), "iota")
-        hi_s, perm2, _, _ = stable_sort(spare_k, b, perm, spare_v, 2 * (k - 32))
-        lo_f = alloc(8 * n)
-        N.check(dev.ctx, L.kman_gather(dev.ctx, c_void_p(lo_s.ptr), c_void_p(perm2.ptr), n, c_void_p(lo_f.ptr), 8),
-                "gather")
-        vals = None
-        if uniq:
-            orig = alloc(8 * n)
-            N.check(dev.ctx, L.kman_gather(dev.ctx, c_void_p(idx1.ptr), c_void_p(perm2.ptr), n, c_void_p(orig.ptr), 8),
+        h = k - 32 * (W - 1)
+        for j in reversed(range(W)):
+            N.check(dev.ctx, L.kman_gather(dev.ctx, c_void_p(w.plane(j)), c_void_p(perm.ptr), n, c_void_p(key.ptr), 8),
                     "gather")
-            vals = alloc(8 * n)
-            N.check(dev.ctx, L.kman_gather(dev.ctx, c_void_p(pos.ptr), c_void_p(orig.ptr), n, c_void_p(vals.ptr), 8),
-                    "gather")
-        ohi, olo = dev.alloc(8 * n), dev.alloc(8 * n)
-        vb = 8 if uniq else (4 if n <= 0xFFFFFFFF else 8)
-        ov = dev.alloc(vb * n)
-        out = c_uint64(0)
-        try:
-            N.check(dev.ctx, L.kman_rle_wide(dev.ctx, N.KMAN_FINISH_UNIQ if uniq else N.KMAN_FINISH_COUNT,
-                                             c_void_p(hi_s.ptr), c_void_p(lo_f.ptr),
-                                             c_void_p(vals.ptr) if uniq else None, vb, n, c_void_p(ohi.ptr),
-                                             c_void_p(olo.ptr), c_void_p(ov.ptr), byref(out)), "kman_rle_wide")
-        except BaseException:
-            for x in (ohi, olo, ov):
-                x.free()
-            raise
-        return WideResult(ohi, olo, ov, vb, int(out.value), k, mode)
+            key, alt_k = stable(key, 64 if j else 2 * h)
+        if per_batch is not None:
+            last = (start + n - 1) // per_batch
+            N.check(dev.ctx, L.kman_batch_tags(dev.ctx, c_void_p(perm.ptr), n, start, per_batch, c_void_p(key.ptr)),
+                    "kman_batch_tags")
+            key, alt_k = stable(key, max(1, int(last).bit_length()))
+        for j in range(W):
+            N.check(dev.ctx, L.kman_gather(dev.ctx, c_void_p(w.plane(j)), c_void_p(perm.ptr), n,
+                                           c_void_p(out.plane(j)), 8), "gather")
+        if w.pos is not None:
+            N.check(dev.ctx, L.kman_gather(dev.ctx, c_void_p(w.pos.ptr), c_void_p(perm.ptr), n, c_void_p(out.pos.ptr),
+                                           8), "gather")
+    except BaseException:
+        out.free()
+        raise
     finally:
-        for x in bufs:
-            x.free()
+        for b in bufs:
+            b.free()
+    return out
+
+
+def rle_words(w: Words, mode: str) -> WordsResult:
+    """Run-length rows of sorted word keys (Crawler.do_batch + the count /
+    uniq writers, join.py:95-130, 244-285)."""
+    dev, L = w.words.dev, N.lib()
+    n, W = w.n, w.W
+    uniq = mode == "uniq"
+    vb = 8 if uniq else (4 if n <= 0xFFFFFFFF else 8)
+    ow = dev.alloc(8 * W * max(n, 1))
+    ov = dev.alloc(vb * max(n, 1))
+    out = c_uint64(0)
+    try:
+        N.check(dev.ctx, L.kman_rle_words(dev.ctx, N.KMAN_FINISH_UNIQ if uniq else N.KMAN_FINISH_COUNT,
+                                          c_void_p(w.words.ptr), W, w.stride, c_void_p(w.pos.ptr) if uniq else None,
+                                          8, n, c_void_p(ow.ptr), max(n, 1), c_void_p(ov.ptr), vb, byref(out)),
+                "kman_rle_words")
+    except BaseException:
+        ow.free()
+        ov.free()
+        raise
+    # (planes keep the input's stride n: row j's word q at ow[q * n + j])
+    return WordsResult(ow, ov, vb, int(out.value), w.k, mode)
+
+
+def words_groups(p: Parsed, k: int, rc: bool, mode: str, canonical: bool = False) -> Optional[WordsResult]:
+    """k > 32 (seq.py:285-328 has no k limit): the keys as word planes
+    (extract_words), an LSD sort over the planes (sort_words,
+    batch.py:156-168), kman_rle_words (join.py:95-130, 244-285).  None when
+    the stream has no k-mers."""
+    w = extract_words(p, k, rc, mode == "uniq", canonical)
+    try:
+        if w.n == 0:
+            return None
+        sw = sort_words(w)
+    finally:
+        w.free()
+    try:
+        return rle_words(sw, mode)
+    finally:
+        sw.free()
+
+
+wide_groups = words_groups  # (the word-pair name of round 2: k in 33..64 is W = 2)
+
+
+def download_words(dev: Device, words: DeviceBuffer, n: int, k: int, stride: Optional[int] = None) -> np.ndarray:
+    """Word planes to a host (n, W) uint64 array."""
+    W = nwords(k)
+    stride = n if stride is None else stride
+    flat = dev.download(words, W * stride, np.uint64) if n else np.zeros(0, np.uint64)
+    return np.ascontiguousarray(flat.reshape(W, stride)[:, :n].T) if n else np.zeros((0, W), np.uint64)
+
+
+def decode_words(row, k: int) -> str:
+    """The k-mer text of one (W,) word row."""
+    W = nwords(k)
+    h = k - 32 * (W - 1)
+    return "".join(decode_key(int(x), h if j == 0 else 32) for j, x in enumerate(row))
 
 
 def join_groups(p: Parsed, k: int, rc: bool, mode: str, max_keys: Optional[int] = None):
@@ -1049,7 +1182,7 @@ def join_groups(p: Parsed, k: int, rc: bool, mode: str, max_keys: Optional[int] 
     rle_*); k > 32: the word-pair path (wide_groups).  None when the stream
     has no k-mers."""
     if k > MAX_K:
-        return wide_groups(p, k, rc, mode)
+        return words_groups(p, k, rc, mode)
     r = groups(p, k, rc, mode) if max_keys is None else None
     if r is None and max_keys is None and p.n_bases:
         # outside kman_groups (too many k-mers for its regions, -r on large
@@ -1073,26 +1206,27 @@ def join_groups(p: Parsed, k: int, rc: bool, mode: str, max_keys: Optional[int] 
 def free_result(r) -> None:
     if r is None:
         return
-    if isinstance(r, WideResult):
-        bs = (r.hi, r.lo, r.vals)
+    if isinstance(r, WordsResult):
+        bs = (r.words, r.vals)
     else:
         bs = (r.ukeys, r.counts) if isinstance(r, CountResult) else (r.keys, r.pos)
     for b in bs:
         b.free()
 
 
-def _emit_wide(p: Parsed, r: WideResult, sink=None):
-    """Word-pair rows as the reference's text: built on the device
-    (kman_format_*_wide_dev), or by the host writers (kman_format_*_wide)
+def _emit_words(p: Parsed, r: WordsResult, sink=None):
+    """Word-key rows as the reference's text: built on the device
+    (kman_format_*_words_dev), or by the host writers (kman_format_*_words)
     with KMAN_HOST_FORMAT=1."""
     dev, L = p.dev, N.lib()
+    vb = r.val_bytes
+    # (row j's word q at words[q * n + j]: a slice of rows is the same planes offset by i0)
     if not host_format():
-        vb = r.val_bytes
         if r.mode == "count":
             def call(i0, m, d_out, cap, used):
-                return L.kman_format_count_wide_dev(dev.ctx, c_void_p(r.hi.ptr + 8 * i0), c_void_p(r.lo.ptr + 8 * i0),
-                                                    c_void_p(r.vals.ptr + vb * i0), vb, m, r.k, d_out, cap,
-                                                    byref(used))
+                return L.kman_format_count_words_dev(dev.ctx, c_void_p(r.words.ptr + 8 * i0), max(r.n, 1),
+                                                     c_void_p(r.vals.ptr + vb * i0), vb, m, r.k, d_out, cap,
+                                                     byref(used))
 
             return _format_dev(dev, r.n, r.k + 2 + 20, call, sink)
         nm = DeviceNames(p)
@@ -1100,26 +1234,28 @@ def _emit_wide(p: Parsed, r: WideResult, sink=None):
             D = len(str(p.n_bases + r.k))
 
             def call(i0, m, d_out, cap, used):
-                return L.kman_format_uniq_wide_dev(dev.ctx, c_void_p(r.hi.ptr + 8 * i0), c_void_p(r.lo.ptr + 8 * i0),
-                                                   c_void_p(r.vals.ptr + vb * i0), vb, m, r.k,
-                                                   c_void_p(nm.names.ptr), c_void_p(nm.off.ptr), c_void_p(nm.rec.ptr),
-                                                   nm.n_records, d_out, cap, byref(used))
+                return L.kman_format_uniq_words_dev(dev.ctx, c_void_p(r.words.ptr + 8 * i0), max(r.n, 1),
+                                                    c_void_p(r.vals.ptr + vb * i0), vb, m, r.k,
+                                                    c_void_p(nm.names.ptr), c_void_p(nm.off.ptr), c_void_p(nm.rec.ptr),
+                                                    nm.n_records, d_out, cap, byref(used))
 
             return _format_dev(dev, r.n, 1 + nm.max_name + 1 + D + 1 + D + 3 + r.k + 1, call, sink)
         finally:
             nm.free()
-    hi = dev.download(r.hi, r.n, np.uint64)
-    lo = dev.download(r.lo, r.n, np.uint64)
-    vals = dev.download(r.vals, r.n, np.uint32 if r.val_bytes == 4 else np.uint64)
+    words = dev.download(r.words, r.W * max(r.n, 1), np.uint64)
+    vals = dev.download(r.vals, r.n, np.uint32 if vb == 4 else np.uint64)
     if r.mode == "count":
-        return _to(sink, _format(L.kman_format_count_wide, hi.ctypes.data_as(c_void_p), lo.ctypes.data_as(c_void_p),
-                                 vals.ctypes.data_as(c_void_p), r.val_bytes, r.n, r.k))
+        return _to(sink, _format(L.kman_format_count_words, words.ctypes.data_as(c_void_p), max(r.n, 1),
+                                 vals.ctypes.data_as(c_void_p), vb, r.n, r.k))
     names = ctypes.create_string_buffer(p.names_blob, max(1, len(p.names_blob)))
     off = np.ascontiguousarray(p.name_off, dtype=np.uint64)
     rs = np.ascontiguousarray(p.rec_seq, dtype=np.uint64)
-    return _to(sink, _format(L.kman_format_uniq_wide, hi.ctypes.data_as(c_void_p), lo.ctypes.data_as(c_void_p),
-                             vals.ctypes.data_as(c_void_p), r.val_bytes, r.n, r.k, names, off.ctypes.data_as(c_void_p),
+    return _to(sink, _format(L.kman_format_uniq_words, words.ctypes.data_as(c_void_p), max(r.n, 1),
+                             vals.ctypes.data_as(c_void_p), vb, r.n, r.k, names, off.ctypes.data_as(c_void_p),
                              rs.ctypes.data_as(c_void_p), p.n_records))
+
+
+_emit_wide = _emit_words  # (round-2 name)
 
 
 def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = None,
@@ -1136,8 +1272,8 @@ def count_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = No
         if r is None:
             return b""
         try:
-            if isinstance(r, WideResult):
-                return _emit_wide(p, r)
+            if isinstance(r, WordsResult):
+                return _emit_words(p, r)
             return emit_count(dev, r)
         finally:
             free_result(r)
@@ -1158,8 +1294,8 @@ def uniq_text(text: bytes, k: int, rc: bool = False, dev: Optional[Device] = Non
         if r is None:
             return b""
         try:
-            if isinstance(r, WideResult):
-                return _emit_wide(p, r)
+            if isinstance(r, WordsResult):
+                return _emit_words(p, r)
             return emit_uniq(p, r)
         finally:
             free_result(r)

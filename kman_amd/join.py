@@ -97,16 +97,22 @@ class Crawler:
         from .source import gather_sorted
 
         km, srcs, tagged = gather_sorted(entries, want_pos=True)
+        k = srcs[0].k
         try:
             dev = srcs[0].dev
-            keys = dev.download(km.keys, km.n, np.uint64)
-            pos = dev.download(km.pos, km.n, np.uint32 if km.pos_bytes == 4 else np.uint64)
+            if isinstance(km, engine.Words):  # (k > 32: word rows)
+                keys = engine.download_words(dev, km.words, km.n, k, km.stride)
+                pos = dev.download(km.pos, km.n, np.uint64)
+                dec = lambda x: engine.decode_words(x, k)  # noqa: E731
+            else:
+                keys = dev.download(km.keys, km.n, np.uint64)
+                pos = dev.download(km.pos, km.n, np.uint32 if km.pos_bytes == 4 else np.uint64)
+                dec = lambda x: engine.decode_key(x, k)  # noqa: E731
         finally:
             km.free()
-        k = srcs[0].k
         for key, p in zip(keys.tolist(), pos.tolist()):
             src = srcs[p >> 56] if tagged else srcs[0]
-            yield (src.header(p & ((1 << 56) - 1)), engine.decode_key(key, k))
+            yield (src.header(p & ((1 << 56) - 1)), dec(key))
 
     def do_batch(self, batches: List[Batch]) -> Iterator[Tuple[List[str], str]]:
         crawler = self.do_records(batches)
@@ -196,7 +202,8 @@ class KJoiner:
         if sharded:
             # one rank of a multi-GPU run (kman_amd/launch.py): the key rounds
             # across the ranks, every rank writing its slice of `outpath`
-            if self.mode.name.startswith("VEC_") or len(sharded) != len(batches):
+            others = [b for b in batches if b is not None and b.current_size and b not in sharded]
+            if self.mode.name.startswith("VEC_") or others or len(sharded) != 1:
                 raise NotImplementedError("a multi-GPU launch joins the FastaBatcher shard batches by UNIQUE / "
                                           "SEQ_COUNT only")
             sharded[0].source.join(self.mode == self.MODE.SEQ_COUNT, outpath)
@@ -228,8 +235,8 @@ def join_bytes(batches: List[Batch], count: bool, sink=None):
         if r is None:
             return None if sink is not None else b""
         try:
-            if isinstance(r, engine.WideResult):
-                return engine._emit_wide(whole.parsed, r, sink)
+            if isinstance(r, engine.WordsResult):
+                return engine._emit_words(whole.parsed, r, sink)
             if count:
                 return engine.emit_count(whole.dev, r, sink)
             return engine.emit_uniq(whole.parsed, r, sink)
@@ -238,6 +245,19 @@ def join_bytes(batches: List[Batch], count: bool, sink=None):
     km, srcs, tagged = gather_sorted(entries, want_pos=not count)
     dev = srcs[0].dev
     k = srcs[0].k
+    if isinstance(km, engine.Words):  # word keys (k > 32): several sources, or reloaded batch files
+        try:
+            r = engine.rle_words(km, "count" if count else "uniq")
+        finally:
+            km.free()
+        try:
+            if count:
+                return engine._emit_words(_any_parsed(srcs), r, sink)
+            rows = engine.download_words(dev, r.words, r.n, k, max(r.n, 1))
+            pos = dev.download(r.vals, r.n, np.uint64)
+        finally:
+            r.free()
+        return engine._to(sink, format_sources(rows, pos, k, srcs, tagged))
     try:
         if count:
             r = engine.rle_count(km, dev)
@@ -262,6 +282,14 @@ def vectors_enabled() -> bool:
     otherwise VEC_* behave as the reference (NotImplementedError at its first
     add_count)."""
     return os.environ.get("KMAN_VEC_COUNT") == "1"
+
+
+def _any_parsed(srcs):
+    """A parsed source (only its device is used by the count writers)."""
+    for s in srcs:
+        if getattr(s, "parsed", None) is not None:
+            return s.parsed
+    raise AssertionError("no parsed source")
 
 
 def join_vectors(batches: List[Batch], masked: bool, outpath: str) -> None:
@@ -295,6 +323,8 @@ def join_vectors(batches: List[Batch], masked: bool, outpath: str) -> None:
         raise NotImplementedError("AbundanceVector.add_count (the reference's VEC_COUNT)")
     if not all(isinstance(e[0], FastaSource) for e in entries):
         raise NotImplementedError("abundance vectors of reloaded batch files (-B)")
+    if entries[0][0].k > engine.MAX_K:
+        raise NotImplementedError("abundance vectors of k > 32 (word keys)")
     km, srcs, tagged = gather_sorted(entries, want_pos=True)
     dev, k, L = srcs[0].dev, srcs[0].k, N.lib()
     base = np.concatenate([[0], np.cumsum([2 * s.parsed.n_bases for s in srcs])]).astype(np.uint64)
@@ -398,7 +428,8 @@ def format_sources(keys: np.ndarray, pos: np.ndarray, k: int, srcs, tagged: bool
     if tagged:
         src = (pos >> np.uint64(56)).astype(np.int64)
         pos = (pos & np.uint64((1 << 56) - 1)) + (np.asarray(base, dtype=np.uint64)[src] << np.uint64(1))
-    keys = np.ascontiguousarray(keys, dtype=np.uint64)
+    words = np.asarray(keys).ndim == 2  # (n, W) word rows, k > 32
+    keys = np.ascontiguousarray(np.asarray(keys, dtype=np.uint64).T if words else keys, dtype=np.uint64)
     pos = np.ascontiguousarray(pos, dtype=np.uint64)
     blob = b"".join(names)
     off = np.zeros(len(names) + 1, dtype=np.uint64)
@@ -408,14 +439,21 @@ def format_sources(keys: np.ndarray, pos: np.ndarray, k: int, srcs, tagged: bool
     kd = np.asarray(kind, dtype=np.uint8)
     nb = ctypes.create_string_buffer(blob, max(1, len(blob)))
     L = N.lib()
-    args = (keys.ctypes.data_as(c_void_p), pos.ctypes.data_as(c_void_p), len(keys), k, nb,
-            off.ctypes.data_as(c_void_p), rs.ctypes.data_as(c_void_p), kd.ctypes.data_as(c_void_p), len(names))
+    n = len(pos)
+    if words:
+        fn = L.kman_format_uniq_mixed_words
+        args = (keys.ctypes.data_as(c_void_p), max(n, 1), pos.ctypes.data_as(c_void_p), n, k, nb,
+                off.ctypes.data_as(c_void_p), rs.ctypes.data_as(c_void_p), kd.ctypes.data_as(c_void_p), len(names))
+    else:
+        fn = L.kman_format_uniq_mixed
+        args = (keys.ctypes.data_as(c_void_p), pos.ctypes.data_as(c_void_p), n, k, nb,
+                off.ctypes.data_as(c_void_p), rs.ctypes.data_as(c_void_p), kd.ctypes.data_as(c_void_p), len(names))
     used = c_size_t(0)
-    rc = L.kman_format_uniq_mixed(*args, None, 0, byref(used), engine.host_threads())
+    rc = fn(*args, None, 0, byref(used), engine.host_threads())
     if rc not in (N.KMAN_OK, N.KMAN_ECAP):
         raise RuntimeError("kman_format_uniq_mixed failed (%d)" % rc)
     buf = ctypes.create_string_buffer(max(1, used.value))
-    rc = L.kman_format_uniq_mixed(*args, buf, used.value, byref(used), engine.host_threads())
+    rc = fn(*args, buf, used.value, byref(used), engine.host_threads())
     if rc != N.KMAN_OK:
         raise RuntimeError("kman_format_uniq_mixed failed (%d)" % rc)
     return buf.raw[:used.value]

@@ -198,11 +198,14 @@ The INPUT file can be gzipped.
               help="Abundances from this one up share the last line (>=N).")
 def hist(input_path: str, output_path: str, k: int, forward: bool = False, max_count: int = 10000) -> None:
     input_file_exists(input_path)
-    if launch.distributed():
+    if k <= 1:
+        raise AssertionError("k must be >= 1, got %d instead." % k)
+    if launch.distributed() and k > engine.MAX_K and not launch.solo_rank():
+        launch.log_solo("kmer hist k=%d" % k)
+        return
+    if launch.distributed() and k <= engine.MAX_K:
         # every rank counts its shard's (canonical) k-mers, the spectrum is
         # all-reduced, rank 0 writes it
-        if k <= 1:
-            raise AssertionError("k must be >= 1, got %d instead." % k)
         src = launch.ShardedSource(engine.default_device(), input_path, k, False)
         try:
             h = src.hist(max_count + 1, canonical=not forward)

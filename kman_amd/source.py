@@ -34,12 +34,16 @@ class FastaSource:
         self._km = {}  # want_pos -> engine.Kmers (stream order)
 
     # ------------------------------------------------------------ extraction
-    def kmers(self, want_pos: bool) -> engine.Kmers:
-        """Keys (+ pos) in stream order; the cached arrays are never sorted in
-        place (sorts work on copies)."""
+    def kmers(self, want_pos: bool):
+        """Keys (+ pos) in stream order -- engine.Kmers (u64 keys, k <= 32)
+        or engine.Words (word planes, k > 32); the cached arrays are never
+        sorted in place (sorts work on copies)."""
         km = self._km.get(want_pos) or (self._km.get(True) if not want_pos else None)
         if km is None:
-            engine._check_k(self.k)  # (k > 32: whole-stream count / uniq only, see engine.wide_groups)
+            if self.k > engine.MAX_K:
+                km = engine.extract_words(self.parsed, self.k, self.rc, want_pos=True)
+                self._km[True] = km
+                return km
             km = engine.extract(self.parsed, self.k, self.rc, want_pos=want_pos)
             self._km[want_pos] = km
         return km
@@ -52,6 +56,8 @@ class FastaSource:
         return "%s:%d-%d:%s" % (name, st, st + self.k, "-" if int(pos) & 1 else "+")
 
     def format_fasta(self, keys: np.ndarray, pos: np.ndarray) -> bytes:
+        if keys.ndim == 2:  # word keys (k > 32): (n, W)
+            return engine.format_fasta_words(keys, pos, self.k, self.parsed)
         return engine.format_fasta(keys, pos, self.k, self.parsed)
 
     def free(self) -> None:
@@ -102,9 +108,12 @@ class BatchFileSource:
             j += 1
         return text[h + 1 : j].decode("utf-8", "surrogateescape").rstrip()
 
-    def kmers(self, want_pos: bool) -> engine.Kmers:
+    def kmers(self, want_pos: bool):
         if self._km is None:
-            self._km = engine.extract(self.parsed, self.k, False, want_pos=True)
+            if self.k > engine.MAX_K:
+                self._km = engine.extract_words(self.parsed, self.k, False, want_pos=True)
+            else:
+                self._km = engine.extract(self.parsed, self.k, False, want_pos=True)
         return self._km
 
     def header(self, pos: int) -> str:
@@ -135,6 +144,12 @@ def sorted_copy(src, start: int, end: int, want_pos: bool, per_batch: Optional[i
     km = src.kmers(want_pos)
     n = end - start
     L = N.lib()
+    if isinstance(km, engine.Words):
+        # word keys (k > 32): an LSD sort over the planes of the range (a
+        # view of the cached planes: same stride, offset by start)
+        view = engine.Words(_Ptr(km.words.ptr + 8 * start, dev), _Ptr(km.pos.ptr + 8 * start, dev)
+                            if (want_pos and km.pos is not None) else None, n, src.k, km.stride)
+        return engine.sort_words(view, start=start, per_batch=per_batch, dev=dev)
     out = engine.Kmers(dev.alloc(8 * max(n, 1)), dev.alloc(8 * max(n, 1)), None, None, 0, n, src.k,
                        dev.alloc(8 * 256 * 8))
     N.check(dev.ctx, L.kman_memcpy_d2d(dev.ctx, c_void_p(out.keys.ptr), c_void_p(km.keys.ptr + 8 * start), 8 * n),
@@ -172,8 +187,9 @@ def sorted_copy(src, start: int, end: int, want_pos: bool, per_batch: Optional[i
 class _Ptr:
     """A raw device pointer viewed like a DeviceBuffer (no ownership)."""
 
-    def __init__(self, ptr):
+    def __init__(self, ptr, dev=None):
         self.ptr = ptr
+        self.dev = dev
 
     def free(self):
         pass
@@ -199,7 +215,15 @@ def _sort(km: engine.Kmers, dev: engine.Device, key_bits: int, copy_back: bool =
 
 
 def download_sorted(src, start: int, end: int, want_pos: bool, per_batch: Optional[int] = None):
+    """Sorted keys (u64, or (n, W) word rows for k > 32) and pos on the host."""
     km = sorted_copy(src, start, end, want_pos, per_batch)
+    if isinstance(km, engine.Words):
+        try:
+            keys = engine.download_words(src.dev, km.words, km.n, src.k, km.stride)
+            pos = src.dev.download(km.pos, km.n, np.uint64) if want_pos else None
+        finally:
+            km.free()
+        return keys, pos
     try:
         mask = np.uint64((1 << (2 * src.k)) - 1) if src.k < 32 else np.uint64(0xFFFFFFFFFFFFFFFF)
         keys = src.dev.download(km.keys, km.n, np.uint64) & mask
@@ -236,6 +260,8 @@ def gather_sorted(entries, want_pos: bool):
     dev = srcs[0].dev
     L = N.lib()
     n = sum(e - s for _, s, e in entries)
+    if k > engine.MAX_K:
+        return _gather_sorted_words(entries, srcs, tagged, k, n, want_pos), srcs, tagged
     pb = 8 if tagged else (srcs[0].kmers(want_pos).pos_bytes if want_pos else 0)
     out = engine.Kmers(dev.alloc(8 * max(n, 1)), dev.alloc(8 * max(n, 1)), None, None, 0, n, k,
                        dev.alloc(8 * 256 * 8))
@@ -303,3 +329,36 @@ def _merge_sorted_runs(out: engine.Kmers, entries, dev: engine.Device) -> bool:
     out.pos, out.pos_alt = out.pos_alt, out.pos
     out.sorted = True
     return True
+
+
+def _gather_sorted_words(entries, srcs, tagged: bool, k: int, n: int, want_pos: bool) -> engine.Words:
+    """gather_sorted for word keys (k > 32): the ranges' planes concatenated
+    in batch order (pos tagged with the source index in bits 56-63 when
+    several sources are joined), then one stable LSD sort over the planes --
+    the heap merge's order (ties by batch, then in-batch order)."""
+    dev = srcs[0].dev
+    L = N.lib()
+    W = engine.nwords(k)
+    cat = engine.Words(dev.alloc(8 * W * max(n, 1)), dev.alloc(8 * max(n, 1)) if want_pos else None, n, k,
+                       max(n, 1))
+    try:
+        at = 0
+        for src, s, e in entries:
+            m = e - s
+            if m <= 0:
+                continue
+            km = src.kmers(True)
+            for j in range(W):
+                N.check(dev.ctx, L.kman_memcpy_d2d(dev.ctx, c_void_p(cat.plane(j) + 8 * at),
+                                                    c_void_p(km.plane(j) + 8 * s), 8 * m), "d2d")
+            if want_pos:
+                N.check(dev.ctx, L.kman_memcpy_d2d(dev.ctx, c_void_p(cat.pos.ptr + 8 * at),
+                                                    c_void_p(km.pos.ptr + 8 * s), 8 * m), "d2d")
+                if tagged:
+                    tag = next(i for i, x in enumerate(srcs) if x is src) << 56
+                    if tag:
+                        N.check(dev.ctx, L.kman_or_u64(dev.ctx, c_void_p(cat.pos.ptr + 8 * at), m, tag), "tag")
+            at += m
+        return engine.sort_words(cat, dev=dev)
+    finally:
+        cat.free()

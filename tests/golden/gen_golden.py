@@ -183,6 +183,11 @@ for inp in ("syn64k_a", "syn64k_b"):
         for cmd in ("count", "uniq"):
             for rc in (False, True):
                 CASES_SMALL.append((inp, cmd, k, ["-r"] if rc else []))
+# k > 32 (word-pair keys, k <= 64) and k > 64 (multi-word keys); round 3
+for inp, cmd, k, extra in (("messy1", "count", 65, []), ("messy1", "uniq", 65, []), ("messy1", "count", 80, []),
+                           ("messy1", "uniq", 80, []), ("messy2", "count", 33, ["-r"]), ("messy2", "uniq", 64, ["-r"]),
+                           ("messy2", "count", 100, ["-r"]), ("messy2", "uniq", 127, [])):
+    CASES_SMALL.append((inp, cmd, k, extra))
 # batch-size invariance and gzip input
 CASES_SMALL.append(("messy1", "count", 5, ["-b", "37"]))
 CASES_SMALL.append(("messy1", "uniq", 5, ["-b", "37", "-r"]))
@@ -193,6 +198,10 @@ BATCH_CASES = [
     ("edge", 4, ["-b", "25", "-r"]),
     ("messy1", 5, ["-b", "500"]),
     ("messy2", 21, ["-b", "1000", "-r"]),
+    # k > 32 batch files (round 3)
+    ("messy1", 33, ["-b", "500"]),
+    ("messy2", 40, ["-b", "1000", "-r"]),
+    ("messy1", 70, ["-b", "300"]),
 ]
 
 ERROR_CASES = [
@@ -207,6 +216,8 @@ ERROR_CASES = [
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true", help="skip the 1 MB config-1 runs")
+    ap.add_argument("--only-new", action="store_true",
+                    help="keep the committed manifest and run only the cases it does not hold yet")
     args = ap.parse_args()
     if not os.path.isdir(REFERENCE):
         sys.exit("reference not present: fixtures can only be generated in the build container")
@@ -221,6 +232,11 @@ def main() -> None:
     out_root = os.path.join(HERE, "ref_outputs")
     os.makedirs(out_root, exist_ok=True)
     manifest = {"cases": [], "batch_cases": [], "error_cases": [], "config1": []}
+    have = set()
+    if args.only_new:
+        with open(os.path.join(HERE, "manifest.json")) as fh:
+            manifest = json.load(fh)
+        have = {e["name"] for part in ("cases", "batch_cases", "error_cases", "config1") for e in manifest[part]}
 
     def case_name(inp, cmd, k, extra):
         tag = "".join(x.strip("-") for x in extra)
@@ -228,6 +244,8 @@ def main() -> None:
 
     for inp, cmd, k, extra in CASES_SMALL:
         name = case_name(inp, cmd, k, extra)
+        if name in have:
+            continue
         work = os.path.join(scratch, "w_" + name)
         os.makedirs(work)
         out = os.path.join(work, "out.txt")
@@ -242,6 +260,8 @@ def main() -> None:
 
     for inp, k, extra in BATCH_CASES:
         name = case_name(inp, "batch", k, extra)
+        if name in have:
+            continue
         work = os.path.join(scratch, "w_" + name)
         os.makedirs(work)
         outdir = os.path.join(work, "batches")
@@ -258,6 +278,8 @@ def main() -> None:
 
     for inp, cmd, k, extra in ERROR_CASES:
         name = case_name(inp, cmd, k, extra)
+        if name in have:
+            continue
         work = os.path.join(scratch, "w_" + name)
         os.makedirs(work)
         out = os.path.join(work, "out.txt")
@@ -267,7 +289,7 @@ def main() -> None:
         manifest["error_cases"].append(entry)
         print(name, res, flush=True)
 
-    if not args.quick:
+    if not args.quick and not args.only_new:
         for cmd, k in (("count", 4), ("count", 21), ("uniq", 21)):
             name = "syn1m__%s__k%d" % (cmd, k)
             work = os.path.join(scratch, "w_" + name)

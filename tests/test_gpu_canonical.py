@@ -33,7 +33,7 @@ def _ref_cases():
 
     with open(os.path.join(GOLDEN, "manifest.json")) as fh:
         cases = json.load(fh)["cases"]
-    return [c for c in cases if c["cmd"] == "count" and "-r" in c["flags"] and c["k"] % 2 == 1 and c["k"] <= 64
+    return [c for c in cases if c["cmd"] == "count" and "-r" in c["flags"] and c["k"] % 2 == 1
             and os.path.isfile(os.path.join(GOLDEN, "ref_outputs", c["name"] + ".txt"))]
 
 
@@ -48,7 +48,13 @@ def test_canonical_counts_pinned_by_reference_rc_counts(dev, golden_inputs, case
     p = engine.parse(dev, engine.read_input(golden_inputs[case["input"]]))
     try:
         r = engine.count_groups(p, case["k"], canonical=True)
-        got = b"" if r is None else engine.format_count(*engine.download_count(dev, r), case["k"])
+        if r is None:
+            got = b""
+        elif isinstance(r, engine.WordsResult):  # (k > 32: word keys)
+            got = bytes(engine._emit_words(p, r))
+            engine.free_result(r)
+        else:
+            got = engine.format_count(*engine.download_count(dev, r), case["k"])
     finally:
         p.free()
     assert got == want

@@ -32,7 +32,7 @@ def _sha(path):
         return hashlib.sha256(fh.read()).hexdigest()
 
 
-@pytest.mark.parametrize("case", [c for c in _manifest()["cases"] if c["k"] <= 64], ids=lambda c: c["name"])
+@pytest.mark.parametrize("case", [c for c in _manifest()["cases"] ], ids=lambda c: c["name"])
 def test_cli_matches_reference(case, golden_inputs, tmp_path):
     out = str(tmp_path / "out.txt")
     _cli([case["cmd"], golden_inputs[case["input"]], out, str(case["k"])] + case["flags"])

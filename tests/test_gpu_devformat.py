@@ -33,7 +33,7 @@ def _cases():
 
     with open(os.path.join(GOLDEN, "manifest.json")) as fh:
         cases = json.load(fh)["cases"]
-    return [c for c in cases if c["cmd"] in ("count", "uniq") and c["result"]["ok"] and 2 <= c["k"] <= 64]
+    return [c for c in cases if c["cmd"] in ("count", "uniq") and c["result"]["ok"] and 2 <= c["k"]]
 
 
 @pytest.mark.parametrize("case", _cases(), ids=lambda c: c["name"])

@@ -444,12 +444,13 @@ def test_full_size_properties(dev):
     p.free()
 
 
-@pytest.mark.parametrize("k", [33, 40, 57, 64])
+@pytest.mark.parametrize("k", [33, 40, 57, 64, 65, 96, 127, 200])
 @pytest.mark.parametrize("rc,canonical", [(False, False), (True, False), (False, True)])
 def test_wide_keys_match_oracle(dev, k, rc, canonical):
-    """k > 32 (word-pair keys): count and uniq rows bit-exact against
-    np_oracle over python-int keys (seq.py:285-328, batch.py:156-168,
-    join.py:95-130,244-285), including -r and canonical keys."""
+    """k > 32 (word keys: two rolled words up to k = 64, kman_extract_words
+    beyond): count and uniq rows bit-exact against a restatement over byte
+    strings (seq.py:285-328, batch.py:156-168, join.py:95-130,244-285),
+    including -r and canonical keys."""
     import inputs
     import np_oracle
     from kman_amd import engine
@@ -482,14 +483,13 @@ def test_wide_keys_match_oracle(dev, k, rc, canonical):
     p = engine.parse(dev, text)
     try:
         for mode in ("count", "uniq"):
-            r = engine.wide_groups(p, k, rc, mode, canonical)
+            r = engine.words_groups(p, k, rc, mode, canonical)
             try:
-                hi = dev.download(r.hi, r.n, np.uint64)
-                lo = dev.download(r.lo, r.n, np.uint64)
+                rows = engine.download_words(dev, r.words, r.n, k)
                 vals = dev.download(r.vals, r.n, np.uint32 if r.val_bytes == 4 else np.uint64)
             finally:
                 engine.free_result(r)
-            got = [np_oracle.decode(int(h), k - 32) + np_oracle.decode(int(l), 32) for h, l in zip(hi, lo)]
+            got = [engine.decode_words(row, k).encode() for row in rows]
             if mode == "count":
                 want_k, want_v = [], []
                 for j, x in enumerate(sk):
