@@ -116,6 +116,13 @@ int kman_memset(kman_ctx *ctx, void *dst, int value, size_t bytes);
 int kman_copy_h2d_async(kman_ctx *ctx, void *dst, const void *src, size_t bytes, int slot);
 int kman_copy_wait(kman_ctx *ctx, int slot);
 int kman_copy_sync(kman_ctx *ctx);
+/* Downloads that overlap the context's work (formatted output text):
+ * kman_copy_d2h_async queues a device -> host copy on the copy stream after
+ * the work already queued (dst: pinned host memory, kman_host_alloc), marked
+ * in d2h slot 0..3; kman_copy_d2h_wait blocks the calling host thread until
+ * that copy is done. */
+int kman_copy_d2h_async(kman_ctx *ctx, void *dst, const void *src, size_t bytes, int slot);
+int kman_copy_d2h_wait(kman_ctx *ctx, int slot);
 
 /* ------------------------------------------------------------------- timing
  * Optional per-kernel timing with HIP events recorded on the context's own

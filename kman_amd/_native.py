@@ -252,6 +252,8 @@ SIGNATURES = {
     "kman_synth_fasta": (c_int, [c_void_p, c_void_p, c_uint64, c_uint64, c_uint64, c_void_p, c_uint32, c_uint32]),
     "kman_copy_h2d_async": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int]),
     "kman_copy_wait": (c_int, [c_void_p, c_int]),
+    "kman_copy_d2h_async": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int]),
+    "kman_copy_d2h_wait": (c_int, [c_void_p, c_int]),
     "kman_copy_sync": (c_int, [c_void_p]),
     "kman_parse_fasta_at": (
         c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p],

@@ -54,6 +54,10 @@ struct kman_ctx {
     // H2D copies that overlap the work of `stream` (chunked FASTA uploads)
     hipStream_t copy_stream = nullptr;
     hipEvent_t copy_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    // D2H copies on the copy stream (formatted text leaving while the next
+    // slice is formatted): kman_copy_d2h_async / kman_copy_d2h_wait
+    hipEvent_t work_ev = nullptr;
+    hipEvent_t d2h_ev[4] = {nullptr, nullptr, nullptr, nullptr};
     // all-to-alls that overlap the work of `stream` (kman_alltoallv_async)
     hipStream_t comm_stream = nullptr;
     hipEvent_t comm_pre = nullptr;

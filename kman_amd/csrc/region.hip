@@ -1292,264 +1292,6 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
     }
 }
 
-// ---------------------------------------------------- finish, pipelined
-// Persistent blocks (the LDS residency: two per CU, three for 4-byte count
-// items) walk the regions in ticket order with the latencies of one region
-// hidden behind the work of the one before:
-//   * the NEXT region's ticket is taken (thread 0, held in a register) while
-//     this region's output is written, and published through LDS during this
-//     region's sort; its sub-region counts are read during the run-length pass;
-//   * its items are loaded into registers once this region's rows are staged
-//     in LDS (the sorted items in registers are dead by then), so they cross
-//     HBM while this region's look-back waits and its rows are written.
-// The one-block-per-region kernel above pays ticket -> counts -> items as a
-// serial prologue per region (and a persistent loop that grabs the next
-// ticket AFTER the writes waits for their acknowledgements first).
-// Forward progress: a block holds at most two tickets, its current region c
-// and the next one n > c; it publishes c before it starts n, and a region's
-// look-back waits only on smaller regions, so the smallest unpublished region
-// is always some block's current one and proceeds.
-template <int MODE, typename O, bool ATOMIC, typename T = uint64_t>
-__global__ __launch_bounds__(FT, sizeof(T) == 4 ? 6 : 4) void rg_finish_q(
-    const uint64_t *__restrict__ in, uint64_t C1, const uint32_t *__restrict__ cnt1, uint32_t Q, uint32_t rest,
-    uint32_t rc, uint64_t rbase, uint32_t tag_shift, uint32_t fsub, uint64_t *__restrict__ okeys,
-    O *__restrict__ ovals, uint64_t *__restrict__ status, uint32_t *__restrict__ counter, uint32_t epoch,
-    uint32_t *__restrict__ err, uint32_t nreg, uint8_t *__restrict__ freg) {
-    constexpr int NT = FT, NW_ = NT / 64, IPT = FIPT;
-    constexpr bool NARROW = sizeof(T) == 4;
-    static_assert(!NARROW || MODE == RG_COUNT, "narrow items: count mode");
-    __shared__ __attribute__((aligned(16))) T s[FCAP];
-    __shared__ uint32_t wh[NW_][FWORD];  // per-wave digit counters, u16 pairs
-    __shared__ uint32_t dstart[FRAD];
-    __shared__ uint32_t lds_scan[NW_];
-    __shared__ uint32_t s_next;
-    __shared__ uint64_t s_out;
-
-    const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
-    const uint64_t rmask = (1ull << rest) - 1;
-    // wave-striped positions; redefined opaquely in every loop trip so that
-    // the compiler does not hoist the 17 per-item addresses out of the loop
-    // and hold them in registers across it (which spills at 128 VGPRs)
-    uint32_t pw = (uint32_t)w * (IPT * 64) + (uint32_t)lane;
-    auto counts = [&](uint32_t rr, uint32_t &a0, uint32_t &a1) {
-        a0 = cnt1[(uint64_t)rr * fsub];
-        a1 = fsub > 1 ? cnt1[(uint64_t)rr * fsub + 1] : 0u;
-    };
-    // a region = fsub (1 or 2) sub-regions of capacity C1, concatenated
-    auto load = [&](uint32_t rr, uint32_t a0, uint32_t mm, T (&v)[IPT]) {
-        const uint64_t *src = in + (uint64_t)rr * fsub * C1;
-        const uint32_t skip = (uint32_t)C1 - a0;
-#pragma unroll
-        for (int i = 0; i < IPT; i++) {
-            const uint32_t p = pw + i * 64;
-            v[i] = p < mm ? (T)src[p < a0 ? p : p + skip] : (T)0;
-        }
-    };
-    auto fit = [&](uint32_t rr, uint32_t a0, uint32_t a1) -> uint32_t {
-        const uint32_t mm = a0 + a1;
-        if (freg && freg[rr]) return 0u;  // (block-uniform)
-        if (mm <= (uint32_t)FCAP) return mm;
-        if (t == 0) {
-            atomicOr(err, ERR_REGION);
-            if (freg) freg[rr] = 1;
-        }
-        return 0u;
-    };
-
-    if (t == 0) s_next = atomicAdd(counter, 1u);
-    __syncthreads();
-    uint32_t r = __builtin_amdgcn_readfirstlane(s_next);
-    if (r >= nreg) return;
-    __syncthreads();  // (every read of s_next before the sort rewrites it)
-    uint32_t m0, m1;
-    counts(r, m0, m1);
-    uint32_t m = fit(r, m0, m1);
-    T x[IPT];
-    load(r, m0, m, x);
-    uint32_t tk = 0;  // thread 0: the next region's ticket
-    if (t == 0) tk = atomicAdd(counter, 1u);
-    for (;;) {
-        asm volatile("" : "+v"(pw));
-        // ---- stable LSD passes of <= 9 bits over the rest bits (as rg_finish)
-        const uint32_t np = (rest + FBITS - 1) / FBITS;
-        uint32_t at = 0;
-        for (uint32_t p = 0; p < np; p++) {
-            const uint32_t bw = (rest - at + (np - p) - 1) / (np - p);
-            const uint32_t sh = Q + at, dm = (1u << bw) - 1;
-            at += bw;
-#pragma unroll
-            for (int q = 0; q < FWORD / 64; q++) wh[w][lane + 64 * q] = 0;
-            if (p == 0 && t == 0) s_next = tk;  // (read after the barriers below)
-            __builtin_amdgcn_wave_barrier();
-            uint32_t rk[IPT];
-#pragma unroll
-            for (int i = 0; i < IPT; i++) {
-                const bool valid = pw + i * 64 < m;
-                const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
-                const uint32_t hs = (d & 1u) * 16u;
-                if (ATOMIC) {
-                    rk[i] = valid ? (atomicAdd(&wh[w][d >> 1], 1u << hs) >> hs) & 0xffffu : 0u;
-                } else {
-                    uint64_t peers = __ballot(valid);
-                    for (uint32_t bb = 0; bb < bw; bb++) {
-                        const bool set = (d >> bb) & 1u;
-                        const uint64_t mm = __ballot(set);
-                        peers &= set ? mm : ~mm;
-                    }
-                    const uint32_t before = valid ? (wh[w][d >> 1] >> hs) & 0xffffu : 0u;
-                    rk[i] = before + (uint32_t)__popcll(peers & lanemask_lt());
-                    __builtin_amdgcn_wave_barrier();
-                    const int leader = __ffsll((unsigned long long)peers) - 1;
-                    if (valid && lane == leader) atomicAdd(&wh[w][d >> 1], (uint32_t)__popcll(peers) << hs);
-                    __builtin_amdgcn_wave_barrier();
-                }
-            }
-            __syncthreads();
-            uint32_t tlo = 0, thi = 0;
-            if (t < FWORD) {
-#pragma unroll
-                for (int ww = 0; ww < NW_; ww++) {
-                    const uint32_t c = wh[ww][t];
-                    wh[ww][t] = tlo | (thi << 16);
-                    tlo += c & 0xffffu;
-                    thi += c >> 16;
-                }
-            }
-            const uint32_t ls = block_exclusive_scan<NT>(tlo + thi, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
-            if (t < FWORD) {
-                dstart[2 * t] = ls;
-                dstart[2 * t + 1] = ls + tlo;
-            }
-            __syncthreads();
-#pragma unroll
-            for (int i = 0; i < IPT; i++) {
-                if (pw + i * 64 < m) {
-                    const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
-                    s[dstart[d] + ((wh[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rk[i]] = x[i];
-                }
-            }
-            __syncthreads();
-            if (p + 1 < np) {
-#pragma unroll
-                for (int i = 0; i < IPT; i++)
-                    if (pw + i * 64 < m) x[i] = s[pw + i * 64];
-            }
-        }
-        if (np == 0) {
-            if (t == 0) s_next = tk;
-#pragma unroll
-            for (int i = 0; i < IPT; i++)
-                if (pw + i * 64 < m) s[pw + i * 64] = x[i];
-            __syncthreads();
-        }
-        // the next region: its ticket (published above) and counts
-        const uint32_t rn = __builtin_amdgcn_readfirstlane(s_next);
-        uint32_t n0 = 0, n1 = 0;
-        if (rn < nreg) counts(rn, n0, n1);
-
-        // ---- run-length pass (thread t: sorted positions t*IPT ..)
-        uint32_t q0 = (uint32_t)t * IPT;
-        asm volatile("" : "+v"(q0));
-        uint32_t heads = 0, tails = 0;
-#define RKEY(v) (((v) >> Q) & rmask)
-        T kv[IPT];
-#pragma unroll
-        for (int j = 0; j < IPT; j++) kv[j] = q0 + j < m ? s[q0 + j] : 0;
-#pragma unroll
-        for (int j = 0; j < IPT; j++) {
-            const uint32_t q = q0 + j;
-            if (q < m) {
-                const uint64_t kq = RKEY(kv[j]);
-                const bool h = q == 0 || kq != RKEY(j ? kv[j - 1] : s[q - 1]);
-                const bool e = q + 1 == m || kq != RKEY(j + 1 < IPT ? kv[j + 1] : s[q + 1]);
-                heads |= (uint32_t)h << j;
-                tails |= (uint32_t)e << j;
-            }
-        }
-        uint32_t emit = 0, lh_before = 0;
-        if constexpr (MODE == RG_UNIQ) {
-            emit = heads & tails;
-        } else {
-            emit = tails;
-            const uint32_t lh = heads ? q0 + (31 - __clz(heads)) + 1 : 0u;
-            lh_before = block_exclusive_scan<NT>(
-                lh, [](uint32_t a, uint32_t b) { return a > b ? a : b; }, 0u, lds_scan, (uint32_t *)nullptr);
-        }
-        uint32_t total;
-        const uint32_t off = block_exclusive_scan<NT>((uint32_t)__popc(emit), SumU32(), 0u, lds_scan, &total);
-        // (the scan's barriers ordered every read of s above before the writes below)
-        // the emitted rows compacted in LDS as one word each: the item itself
-        // (UNIQ: key rest + pos) or key rest | group size << rest (COUNT).
-        // NARROW: the key rests, then (after they are written) the group sizes
-        auto stage = [&]() {
-            uint32_t o = off, cur = lh_before;  // head position + 1 of the open group
-#pragma unroll
-            for (int j = 0; j < IPT; j++) {
-                const uint32_t q = q0 + j;
-                if (MODE != RG_UNIQ && ((heads >> j) & 1u)) cur = q + 1;
-                if ((emit >> j) & 1u) {
-                    if constexpr (NARROW)
-                        s[o++] = kv[j];
-                    else
-                        s[o++] = MODE == RG_UNIQ ? kv[j] : (T)(RKEY(kv[j]) | ((uint64_t)(q + 2 - cur) << rest));
-                }
-            }
-        };
-        auto stage_sizes = [&]() {  // (NARROW; needs no item)
-            uint32_t o = off, cur = lh_before;
-#pragma unroll
-            for (int j = 0; j < IPT; j++) {
-                const uint32_t q = q0 + j;
-                if ((heads >> j) & 1u) cur = q + 1;
-                if ((emit >> j) & 1u) s[o++] = (T)(q + 2 - cur);
-            }
-        };
-        stage();
-        __syncthreads();
-        // the next region's items, now that x and kv are dead, and the ticket
-        // after it: both cross HBM while this region's rows go out
-        const uint32_t mn = rn < nreg ? fit(rn, n0, n1) : 0u;
-        if (rn < nreg) {
-            load(rn, n0, mn, x);
-            if (t == 0) tk = atomicAdd(counter, 1u);
-        }
-        if (w == 0) {
-            const uint64_t ob = wave_lookback<0>(status, r, total, epoch, err);
-            if (lane == 0) s_out = ob;
-        }
-        __syncthreads();
-        const uint64_t ob = s_out;
-        const uint64_t qmask = Q ? ((1ull << Q) - 1) : 0ull;
-        for (uint32_t q = t; q < total; q += NT) {
-            const uint64_t v = s[q];
-            okeys[ob + q] = ((uint64_t)(r + rbase) << rest) | RKEY(v);
-        }
-        if constexpr (NARROW) {
-            __syncthreads();  // (every key read before the sizes overwrite them)
-            stage_sizes();
-            __syncthreads();
-        }
-        for (uint32_t q = t; q < total; q += NT) {
-            const uint64_t v = s[q];
-            if constexpr (MODE == RG_UNIQ) {
-                const uint64_t idx = v & qmask;
-                const uint64_t pos = rc ? idx : (idx << 1);
-                ovals[ob + q] = (O)(tag_shift ? pos | (((v >> tag_shift) & 0x1ffull) << 56) : pos);
-            } else if constexpr (NARROW) {
-                ovals[ob + q] = (O)v;
-            } else {
-                ovals[ob + q] = (O)(v >> rest);
-            }
-        }
-#undef RKEY
-        if (rn >= nreg) break;  // (block-uniform)
-        __syncthreads();  // every read of s / s_out above before the next region writes them
-        r = rn;
-        m0 = n0;
-        m = mn;
-    }
-}
-
 struct RegionPlan {
     uint32_t K, Q, B2, rest;
     bool rc;
@@ -1776,12 +1518,11 @@ void launch_finish(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ov
     const bool pf = e && atoi(e) == 1;
     const bool db = e && atoi(e) == 2;
     const bool ps = e && atoi(e) == 3;  // (KMAN_RG_FIN=3: persistent blocks, A/B)
-    const bool fq = e && atoi(e) == 4;  // (KMAN_RG_FIN=4: rg_finish_q)
     // count rows whose key rest fits 32 bits: 4-byte items in LDS
     // (KMAN_RG_NARROW=0: the 8-byte items, for A/B)
     static const char *en = getenv("KMAN_RG_NARROW");
     if constexpr (MODE == RG_COUNT) {
-        if (!pf && !db && !fq && f.rest <= 32 && f.Q == 0 && f.tag_shift == 0 && !(en && atoi(en) == 0)) {
+        if (!pf && !db && f.rest <= 32 && f.Q == 0 && f.tag_shift == 0 && !(en && atoi(en) == 0)) {
             if (ctx->lds_atomic_ordered && ps)
                 launch_finish_as<MODE, O, true, false, false, uint32_t, true>(ctx, f, okeys, ovals, epoch, counter,
                                                                               dbg, stp);
@@ -1793,34 +1534,6 @@ void launch_finish(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ov
                                                                          stp);
             return;
         }
-    }
-    if (fq) {  // the pipelined persistent finish (rg_finish_q)
-        auto go = [&](auto atomic_c, auto narrow_c) {
-            constexpr bool A = decltype(atomic_c)::value;
-            using T = std::conditional_t<decltype(narrow_c)::value, uint32_t, uint64_t>;
-            const void *fn = (const void *)rg_finish_q<MODE, O, A, T>;
-            int cus = 256;
-            (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device);
-            // the LDS residency (the occupancy query may report fewer)
-            const uint64_t want = (uint64_t)cus * (sizeof(T) == 4 ? 3 : 2);
-            uint64_t grid = (uint64_t)kman_persistent_grid(ctx, fn, FT, f.nreg);
-            if (grid < want) grid = want < f.nreg ? want : f.nreg;
-            hipLaunchKernelGGL((rg_finish_q<MODE, O, A, T>), dim3((uint32_t)grid), dim3(FT), 0, ctx->stream, f.in,
-                               f.C1, f.cnt, f.Q, f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals,
-                               ctx->d_status, counter, epoch, ctx->d_err, f.nreg, f.freg);
-        };
-        const bool narrow = MODE == RG_COUNT && f.rest <= 32 && f.Q == 0 && f.tag_shift == 0 && !(en && atoi(en) == 0);
-        if constexpr (MODE == RG_COUNT) {
-            if (narrow) {
-                if (ctx->lds_atomic_ordered) go(std::true_type{}, std::true_type{});
-                else go(std::false_type{}, std::true_type{});
-                return;
-            }
-        }
-        (void)narrow;
-        if (ctx->lds_atomic_ordered) go(std::true_type{}, std::false_type{});
-        else go(std::false_type{}, std::false_type{});
-        return;
     }
     if (ctx->lds_atomic_ordered) {
         if (db) launch_finish_as<MODE, O, true, false, true>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);

@@ -273,6 +273,9 @@ void kman_destroy(kman_ctx *ctx) {
         (void)hipStreamSynchronize(ctx->copy_stream);
         (void)hipStreamDestroy(ctx->copy_stream);
     }
+    for (auto e : ctx->d2h_ev)
+        if (e) (void)hipEventDestroy(e);
+    if (ctx->work_ev) (void)hipEventDestroy(ctx->work_ev);
     for (auto e : ctx->copy_ev)
         if (e) (void)hipEventDestroy(e);
     if (ctx->comm_stream) {
@@ -358,6 +361,29 @@ int kman_copy_h2d_async(kman_ctx *ctx, void *dst, const void *src, size_t bytes,
 int kman_copy_wait(kman_ctx *ctx, int slot) {
     if (!ctx || slot < 0 || slot >= 4 || !ctx->copy_ev[slot]) return KMAN_EINVAL;
     HIP_TRY(ctx, hipStreamWaitEvent(ctx->stream, ctx->copy_ev[slot], 0));
+    return KMAN_OK;
+}
+
+// D2H on the copy stream after the work already queued on the work stream
+// (the text formatted into `src`), completion marked in d2h slot 0..3; the
+// work stream keeps going (the next slice is formatted meanwhile)
+int kman_copy_d2h_async(kman_ctx *ctx, void *dst, const void *src, size_t bytes, int slot) {
+    if (!ctx || slot < 0 || slot >= 4) return KMAN_EINVAL;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    if (!ctx->copy_stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&ctx->copy_stream, hipStreamNonBlocking));
+    if (!ctx->work_ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->work_ev, hipEventDisableTiming));
+    if (!ctx->d2h_ev[slot]) HIP_TRY(ctx, hipEventCreateWithFlags(&ctx->d2h_ev[slot], hipEventDisableTiming));
+    HIP_TRY(ctx, hipEventRecord(ctx->work_ev, ctx->stream));
+    HIP_TRY(ctx, hipStreamWaitEvent(ctx->copy_stream, ctx->work_ev, 0));
+    if (bytes) HIP_TRY(ctx, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->copy_stream));
+    HIP_TRY(ctx, hipEventRecord(ctx->d2h_ev[slot], ctx->copy_stream));
+    return KMAN_OK;
+}
+
+// the host waits for the D2H marked in `slot` (callable from any host thread)
+int kman_copy_d2h_wait(kman_ctx *ctx, int slot) {
+    if (!ctx || slot < 0 || slot >= 4 || !ctx->d2h_ev[slot]) return KMAN_EINVAL;
+    HIP_TRY(ctx, hipEventSynchronize(ctx->d2h_ev[slot]));
     return KMAN_OK;
 }
 

@@ -711,53 +711,106 @@ def format_fasta(keys: np.ndarray, pos: np.ndarray, k: int, p: Parsed) -> bytes:
 # device-side formatting: the text is built in HBM and only
 # the text crosses PCIe; slices of at most _FMT_CHUNK text bytes per launch
 _FMT_CHUNK = 1 << 31
+_FMT_SLICE = 256 << 20  # text bytes per pipelined slice (_format_dev)
+_FMT_THREADS = int(os.environ.get("KMAN_FMT_THREADS", "8"))  # host copy threads
 
 
 def _format_dev(dev: Device, n: int, row_bytes: int, call, sink=None):
     """Run a kman_format_*_dev call over row slices.  call(i0, rows, d_out,
     cap, used) formats rows [i0, i0 + rows); row_bytes bounds one row.
-    Returns the text (a bytearray filled straight from the device), or, with
-    a sink (a binary file), writes it there chunk by chunk through a pinned
-    staging buffer and returns None."""
+    Returns the text (a bytearray), or, with a sink (a binary file), writes
+    it there and returns None.
+
+    Pipelined over slices of <= _FMT_SLICE text bytes, two of everything:
+    slice i is formatted on the device while slice i - 1 crosses PCIe on the
+    copy stream into a pinned stage (kman_copy_d2h_async) and slice i - 2 is
+    copied out of its stage by a pool of host threads -- pwrite at its file
+    offset, or memmove into the result -- so the device, the copy engine and
+    the host copies run at once instead of one after another."""
     if n == 0:
         return None if sink is not None else bytearray()
-    rows = max(1, min(n, _FMT_CHUNK // max(1, row_bytes)))
+    import concurrent.futures as cf
+
+    L = N.lib()
+    rows = max(1, min(n, _FMT_SLICE // max(1, row_bytes)))
     cap = rows * row_bytes + 16
     used = c_size_t(0)
-    L = N.lib()
-    out, stage = None, None
+    out, fd, base = None, None, 0
     if sink is None:
         rc_ = call(0, n, None, 0, used)  # sizing pass over every row
         if rc_ not in (N.KMAN_OK, N.KMAN_ECAP):
             N.check(dev.ctx, rc_, "kman_format_*_dev")
         out = bytearray(int(used.value))
+        dst0 = ctypes.addressof((ctypes.c_char * max(1, len(out))).from_buffer(out)) if len(out) else 0
     else:
-        hp = c_void_p()
-        N.check(dev.ctx, L.kman_host_alloc(dev.ctx, byref(hp), cap), "kman_host_alloc")
-        stage = hp
-    buf = dev.alloc(cap)
+        try:
+            sink.flush()
+            fd, base = sink.fileno(), sink.tell()
+        except (AttributeError, OSError, ValueError):
+            fd = None  # (a sink without a file descriptor: written in order by this thread)
+    NB = 2
+    stages, dbufs = [], []
+    pool = cf.ThreadPoolExecutor(max_workers=_FMT_THREADS)
     try:
-        at = 0
-        for i0 in range(0, n, rows):
-            m = min(rows, n - i0)
-            N.check(dev.ctx, call(i0, m, c_void_p(buf.ptr), cap, used), "kman_format_*_dev")
-            u = int(used.value)
-            if not u:
-                continue
+        for _ in range(NB):
+            hp = c_void_p()
+            N.check(dev.ctx, L.kman_host_alloc(dev.ctx, byref(hp), cap), "kman_host_alloc")
+            stages.append(hp)
+            dbufs.append(dev.alloc(cap))
+        pending = [[] for _ in range(NB)]
+        piece = max(1 << 20, cap // _FMT_THREADS + 1)
+
+        def copy_piece(src, at, u):
             if out is not None:
-                dst = (ctypes.c_char * u).from_buffer(out, at)
-                N.check(dev.ctx, L.kman_memcpy_d2h(dev.ctx, dst, c_void_p(buf.ptr), u), "d2h")
+                ctypes.memmove(dst0 + at, src, u)
             else:
-                N.check(dev.ctx, L.kman_memcpy_d2h(dev.ctx, stage, c_void_p(buf.ptr), u), "d2h")
-                sink.write(memoryview((ctypes.c_char * u).from_address(stage.value)).cast("B"))
+                mv = memoryview((ctypes.c_char * u).from_address(src)).cast("B")
+                done = 0
+                while done < u:
+                    done += os.pwrite(fd, mv[done:], base + at + done)
+
+        def drain(b, at, u):
+            """slice in stage b (u bytes at text offset `at`) out to the host"""
+            N.check(dev.ctx, L.kman_copy_d2h_wait(dev.ctx, b), "kman_copy_d2h_wait")
+            if out is None and fd is None:
+                sink.write(memoryview((ctypes.c_char * u).from_address(stages[b].value)).cast("B"))
+                return
+            pending[b] = [pool.submit(copy_piece, stages[b].value + o, at + o, min(piece, u - o))
+                          for o in range(0, u, piece)]
+
+        at, last = 0, None
+        for i, i0 in enumerate(range(0, n, rows)):
+            b = i % NB
+            for f in pending[b]:  # slice i - 2 out of stage b (its D2H finished before)
+                f.result()
+            pending[b] = []
+            m = min(rows, n - i0)
+            N.check(dev.ctx, call(i0, m, c_void_p(dbufs[b].ptr), cap, used), "kman_format_*_dev")
+            u = int(used.value)
+            N.check(dev.ctx, L.kman_copy_d2h_async(dev.ctx, stages[b], c_void_p(dbufs[b].ptr), u, b),
+                    "kman_copy_d2h_async")
+            if last is not None:
+                drain(*last)
+            last = (b, at, u)
             at += u
+        if last is not None:
+            drain(*last)
+        for pb in pending:
+            for f in pb:
+                f.result()
     finally:
-        buf.free()
-        if stage is not None:
-            L.kman_host_free(dev.ctx, stage)
+        pool.shutdown(wait=True)
+        N.check(dev.ctx, L.kman_copy_sync(dev.ctx), "kman_copy_sync")
+        for x in dbufs:
+            x.free()
+        for hp in stages:
+            L.kman_host_free(dev.ctx, hp)
     if out is not None:
         assert at == len(out)
-    return out
+        return out
+    if fd is not None:
+        sink.seek(base + at)
+    return None
 
 
 def format_count_dev(dev: Device, r: CountResult, sink=None):
