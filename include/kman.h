@@ -70,6 +70,10 @@ extern "C" {
 #define KMAN_RC 1u          /* also emit reverse complements (kmer -r, seq.py:274-282) */
 #define KMAN_WANT_POS 2u    /* also emit the pos payload (uniq / batch modes) */
 #define KMAN_CANONICAL 4u   /* emit min(fwd, rc) instead (not in the reference) */
+#define KMAN_MIXED 8u       /* with KMAN_CANONICAL: the canonical key through a fixed bijection of the
+                             * 2k-bit keys (odd multiply, xorshift, odd multiply mod 2^2k), so the top
+                             * bits are uniform; the multiset of counts is unchanged -- for abundance
+                             * spectra (kman_groups, kman_dshard_*, kman_extract_marked / _range) */
 /* kman_extract: accumulate d_hist for the passes over bits [b, 2k) only
  * (the prefix passes of kman_split_bits); default b = 0, every bit */
 #define KMAN_HIST_LO(b) (((uint32_t)(b) & 0x7fu) << 8)
@@ -343,7 +347,7 @@ int kman_dround_failed(kman_ctx *ctx, uint64_t *ranges, uint64_t cap, uint64_t *
  * last bin collecting every count >= nbins - 1 (bin 0 stays 0).  With
  * KMAN_CANONICAL counts (kman_groups) this is the canonical k-mer spectrum;
  * for odd k those counts equal the `kmer count -r` rows with key <= rc(key)
- * (the reference's -r emits both strands, seq.py:274-282). */
+ * (the reference's -r emits both strands, seq.py:274-282).  d_counts 16-byte aligned. */
 int kman_count_hist(kman_ctx *ctx, const void *d_counts, uint32_t count_bytes, uint64_t n, uint64_t *d_hist,
                     uint32_t nbins);
 

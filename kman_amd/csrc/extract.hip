@@ -38,7 +38,7 @@ struct Plan {
 
 struct NoPos {};
 
-template <int EI, bool RC, bool CANON, typename P>
+template <int EI, bool RC, int CANON, typename P>
 __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__ codes, uint64_t n_bases,
                                                      uint64_t n_tiles, int k, uint64_t *__restrict__ keys,
                                                      P *__restrict__ pos, uint64_t *__restrict__ status,
@@ -303,7 +303,7 @@ __global__ __launch_bounds__(ET) void kmer_hist_kernel(const uint8_t *__restrict
     }
 }
 
-template <int EI, bool RC, bool CANON, typename P>
+template <int EI, bool RC, int CANON, typename P>
 int launch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k, uint64_t *keys, P *pos,
                    uint64_t *hist, const Plan &plan, uint64_t klo, uint64_t khi, uint64_t cap, const uint8_t *pmap,
                    uint32_t pshift, uint32_t pval, uint32_t cshift, uint32_t cexact) {
@@ -324,13 +324,16 @@ template <typename P>
 int dispatch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k, uint32_t flags, uint64_t *keys,
                      P *pos, uint64_t *hist, const Plan &plan, uint64_t klo, uint64_t khi, uint64_t cap,
                      const uint8_t *pmap, uint32_t pshift, uint32_t pval, uint32_t cshift, uint32_t cexact) {
+    if ((flags & KMAN_CANONICAL) && (flags & KMAN_MIXED))
+        return launch_extract<16, false, 2, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap, pmap,
+                                               pshift, pval, cshift, cexact);
     if (flags & KMAN_CANONICAL)
-        return launch_extract<16, false, true, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap, pmap,
-                                                  pshift, pval, cshift, cexact);
+        return launch_extract<16, false, 1, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap, pmap,
+                                               pshift, pval, cshift, cexact);
     if (flags & KMAN_RC)
-        return launch_extract<8, true, false, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap, pmap,
+        return launch_extract<8, true, 0, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap, pmap,
                                                  pshift, pval, cshift, cexact);
-    return launch_extract<16, false, false, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap, pmap,
+    return launch_extract<16, false, 0, P>(ctx, codes, n_bases, k, keys, pos, hist, plan, klo, khi, cap, pmap,
                                                pshift, pval, cshift, cexact);
 }
 

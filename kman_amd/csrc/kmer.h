@@ -67,7 +67,7 @@ KMAN_DEV void stage_codes(const uint8_t *__restrict__ codes, uint64_t n_bases, u
 
 // Roll the EI windows starting at s[base .. base+EI) (k from LDS bytes), one
 // base at a time (kept for A/B timing: make EXTRA=-DKMAN_ROLL_SEQ).
-template <int EI, bool CANON>
+template <int EI, int CANON>
 KMAN_DEV uint32_t roll_seq(const uint8_t *s, int base, int k, uint64_t mask, uint64_t p0, uint64_t n_bases,
                        uint64_t (&kf)[EI], uint64_t (&kr)[EI]) {
     uint64_t f = 0, r = 0;
@@ -91,6 +91,7 @@ KMAN_DEV uint32_t roll_seq(const uint8_t *s, int base, int k, uint64_t mask, uin
         const uint64_t fm = f & mask;
         if (CANON) {
             kf[j] = fm < r ? fm : r;
+            if (CANON == 2) kf[j] = mix_key(kf[j], k);
         } else {
             kf[j] = fm;
             kr[j] = r;
@@ -102,7 +103,7 @@ KMAN_DEV uint32_t roll_seq(const uint8_t *s, int base, int k, uint64_t mask, uin
 
 // The same windows bit-parallel (rollfast.h): aligned 32-bit LDS reads packed
 // four codes per multiply, each window a funnel shift of the packed stream.
-template <int EI, bool CANON>
+template <int EI, int CANON>
 KMAN_DEV uint32_t roll(const uint8_t *s, int base, int k, uint64_t mask, uint64_t p0, uint64_t n_bases,
                        uint64_t (&kf)[EI], uint64_t (&kr)[EI]) {
 #ifdef KMAN_ROLL_SEQ

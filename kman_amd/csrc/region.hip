@@ -87,6 +87,38 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
     return r;
 }
 
+// A block-wide LDS rank (+1 on counter ctr[d] per valid lane, unstable):
+// when >= 8 lanes of the wave hold the same digit as lane 0 (repeated keys,
+// a genome's repeats), those lanes take ONE atomic (64 same-address LDS
+// atomics serialise) and rank by their position among themselves.
+KMAN_DEV uint32_t rank_hot(uint32_t *ctr, uint32_t d, bool valid) {
+    // (one atomic instruction, no branch: the hot lanes other than the
+    // leader sit it out, the leader adds their count)
+    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+    const uint64_t same = __ballot(valid && d == d0);
+    const uint32_t ns = (uint32_t)__popcll(same);
+    const bool hot = ns >= 8u;  // (wave-uniform)
+    const int leader = __ffsll((unsigned long long)same) - 1;
+    const bool mine = hot && ((same >> lane_id()) & 1ull);
+    uint32_t old = 0;
+    if (valid && (!mine || lane_id() == leader)) old = atomicAdd(&ctr[d], mine ? ns : 1u);
+    if (!hot) return old;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)old, leader);
+    return mine ? lo + (uint32_t)__popcll(same & lanemask_lt()) : old;
+}
+
+// dbg bit RG_HOT (KMAN_RG_HOT=1): the hot-digit ranks above; else one atomic
+// per lane (a uniform branch on a kernel argument)
+constexpr uint32_t RG_HOT = 64;
+KMAN_DEV uint32_t rank_block(uint32_t *ctr, uint32_t d, bool valid, uint32_t dbg) {
+    if (dbg & RG_HOT) return rank_hot(ctr, d, valid);
+    return valid ? atomicAdd(&ctr[d], 1u) : 0u;
+}
+static uint32_t hot_bit() {
+    static const char *e = getenv("KMAN_RG_HOT");
+    return e && atoi(e) == 1 ? RG_HOT : 0u;
+}
+
 // ---------------------------------------------------------------- pass 0
 // A tile of RT*EI window starts: windows rolled from LDS-staged codes, the
 // valid ones compacted in stream order (tile-local window << 1 | strand
@@ -116,7 +148,7 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 // leaving two partial lines, and the look-back's predecessor is a neighbour.
 // Placement changes only speed: a tile waits only on earlier tickets of its
 // own partition, and a block leaves only when every partition is dealt out.
-template <int EI, bool RC, bool ATOMIC, bool CANON = false, bool BR = false, bool EX = false, int NS = RS,
+template <int EI, bool RC, bool ATOMIC, int CANON = 0, bool BR = false, bool EX = false, int NS = RS,
           int XLB = LB, bool IL = false, int TPDX = 0, bool XG = false>
 __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI == 8 ? 8 : 4)))) void rg_extract(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
                                                  uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
@@ -245,7 +277,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
 #define KEPT(d) (!EX || ((keep[(d) >> 5] >> ((d) & 31)) & 1u))
     if (BR) {
 #pragma unroll
-        for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&thist[XDIGIT(key[i])], 1u) : 0u;
+        for (int i = 0; i < SI; i++) rank[i] = rank_block(thist, XDIGIT(key[i]), ib + i * 64 < tcnt, dbg);
         __syncthreads();
         // (EX: a digit not kept this round has no chain: nothing published)
         if (threadIdx.x < RADIX && KEPT(threadIdx.x))
@@ -357,7 +389,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
 // combining).  The next tile's codes load into registers behind this tile's
 // rank and stores.  Rank by one block-wide LDS atomic per item (unstable
 // inside a tile, as rg_extract<BR>).
-template <int NT, int EI, bool RC, bool CANON = false, int WL = 16>
+template <int NT, int EI, bool RC, int CANON = 0, int WL = 16>
 __global__ __launch_bounds__(NT, NT == 256 ? 4 : 1024 / NT) void rg_xown(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
                                                    uint32_t Q, uint64_t *__restrict__ out, uint64_t C0, uint32_t S,
                                                    uint32_t seg_tiles, uint32_t n_tiles,
@@ -737,8 +769,7 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
 #define PDIGIT(x) ((uint32_t)((x) >> shift) & dmask)
             if (BR) {
 #pragma unroll
-                for (int i = 0; i < SI; i++)
-                    rank[i] = ib + i * 64 < n ? atomicAdd(&thist[PDIGIT(key[i])], 1u) : 0u;
+                for (int i = 0; i < SI; i++) rank[i] = rank_block(thist, PDIGIT(key[i]), ib + i * 64 < n, dbg);
                 __syncthreads();
                 const uint32_t ls = block_exclusive_scan<NT>(threadIdx.x < R1 ? thist[threadIdx.x] : 0u, SumU32(), 0u,
                                                              lds_scan, (uint32_t *)nullptr);
@@ -1098,7 +1129,31 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
             const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
             const uint32_t hs = (d & 1u) * 16u;
             if (ATOMIC) {
-                rk[i] = valid ? (atomicAdd(&wh[w][d >> 1], 1u << hs) >> hs) & 0xffffu : 0u;
+                // a hot digit (repeated keys: a genome's repeats fill whole
+                // waves with one key) takes ONE atomic for all its lanes --
+                // 64 same-address LDS atomics serialise; the other lanes rank
+                // as usual (their atomics return in lane order).  One atomic
+                // instruction either way: the leader adds the hot lanes' count
+                // (NARROW: not at all -- the ballot masks cost the VGPR
+                // budget of three blocks per CU: 72 -> 80 + 2.5 KB of spills)
+                if constexpr (NARROW) {
+                    rk[i] = valid ? (atomicAdd(&wh[w][d >> 1], 1u << hs) >> hs) & 0xffffu : 0u;
+                } else {
+                    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+                    const uint64_t same = __ballot(valid && d == d0);
+                    const uint32_t ns = (uint32_t)__popcll(same);
+                    const bool hot = ns >= 8u;  // (wave-uniform)
+                    const int leader = __ffsll((unsigned long long)same) - 1;
+                    const bool mine = hot && ((same >> lane) & 1ull);
+                    uint32_t old = 0;
+                    if (valid && (!mine || lane == leader)) old = atomicAdd(&wh[w][d >> 1], (mine ? ns : 1u) << hs);
+                    old = (old >> hs) & 0xffffu;
+                    if (hot) {
+                        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)old, leader);
+                        if (mine) old = lo + (uint32_t)__popcll(same & lanemask_lt());
+                    }
+                    rk[i] = old;
+                }
             } else {
                 uint64_t peers = __ballot(valid);
                 for (uint32_t bb = 0; bb < bw; bb++) {
@@ -1297,6 +1352,7 @@ struct RegionPlan {
     bool rc;
     uint64_t W;          // windows (x2 with rc): bound on the k-mers
     bool canon;          // canonical keys (KMAN_CANONICAL)
+    bool mix;            // canonical keys through mix_key (KMAN_MIXED: spectra)
     uint64_t C0, C1;     // region capacities (items)
     uint32_t H;          // pass-1 chains (sub-regions) per bucket
     uint64_t C1h;        // pass-1 sub-region capacity
@@ -1320,6 +1376,7 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     RegionPlan p{};
     // canonical: one key per window, min(forward, reverse complement)
     p.canon = flags & KMAN_CANONICAL;
+    p.mix = p.canon && (flags & KMAN_MIXED);
     p.rc = (flags & KMAN_RC) && !p.canon;
     p.K = 2 * k;
     p.W = n_bases * (p.rc ? 2 : 1);
@@ -1404,6 +1461,7 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
 
 template <int NT, int SI, bool PF, bool WC = false, bool BR = false>
 void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
+    dbg |= hot_bit();
     if constexpr (BR) {  // no ordered LDS atomics needed
         const void *fn = (const void *)rg_pass<true, NT, SI, PF, WC, BR>;
         const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, NT, (uint64_t)pa.nbk * pa.H);
@@ -1522,16 +1580,12 @@ void launch_finish(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ov
     // (KMAN_RG_NARROW=0: the 8-byte items, for A/B)
     static const char *en = getenv("KMAN_RG_NARROW");
     if constexpr (MODE == RG_COUNT) {
-        if (!pf && !db && f.rest <= 32 && f.Q == 0 && f.tag_shift == 0 && !(en && atoi(en) == 0)) {
-            if (ctx->lds_atomic_ordered && ps)
-                launch_finish_as<MODE, O, true, false, false, uint32_t, true>(ctx, f, okeys, ovals, epoch, counter,
-                                                                              dbg, stp);
-            else if (ctx->lds_atomic_ordered)
-                launch_finish_as<MODE, O, true, false, false, uint32_t>(ctx, f, okeys, ovals, epoch, counter, dbg,
-                                                                        stp);
-            else
-                launch_finish_as<MODE, O, false, false, false, uint32_t>(ctx, f, okeys, ovals, epoch, counter, dbg,
-                                                                         stp);
+        // (atomic ranks only: the ballot ranks overflow the 80 VGPRs of three
+        // blocks per CU -- 2.5 KB of spills per lane, and results that were
+        // not the sort's: such code is not built)
+        if (!pf && !db && !ps && ctx->lds_atomic_ordered && f.rest <= 32 && f.Q == 0 && f.tag_shift == 0 &&
+            !(en && atoi(en) == 0)) {
+            launch_finish_as<MODE, O, true, false, false, uint32_t>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
             return;
         }
     }
@@ -1576,10 +1630,11 @@ static bool xcd_tickets() {
     return on;
 }
 
-template <int EI, bool RC, bool CANON, int NS, int XLB = 1>
+template <int EI, bool RC, int CANON, int NS, int XLB = 1>
 void launch_extract_ns(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                        uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp,
                        uint32_t n_launch) {
+    dbg |= hot_bit();
     if (NS == RS && XLB == 1) {
         static const char *e = getenv("KMAN_RG_XLB");
         const int x = e ? atoi(e) : 1;
@@ -1615,7 +1670,7 @@ void launch_extract_ns(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes,
                        counter, epoch, ctx->d_err, dbg, stp);
 }
 
-template <int EI, bool RC, bool CANON = false>
+template <int EI, bool RC, int CANON = 0>
 void launch_extract(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                     uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp,
                     uint32_t n_launch) {
@@ -1640,7 +1695,7 @@ void launch_extract(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, ui
                            ctx->d_err, dbg, stp);
 }
 
-template <int EI, bool RC, bool CANON = false>
+template <int EI, bool RC, int CANON = 0>
 void launch_xown(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                  uint64_t *r0, uint32_t *c0, uint32_t *counter, uint64_t *stp) {
     if (p.xnt == 256) {  // four blocks per CU, write combining in 64-byte lines
@@ -1667,13 +1722,15 @@ void launch_extract_any(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes
                         uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp,
                         uint32_t n_launch = 0) {
     if (p.own) {
-        if (p.canon) launch_xown<8, false, true>(ctx, p, codes, n_bases, k, r0, c0, counter, stp);
+        if (p.canon) launch_xown<8, false, 1>(ctx, p, codes, n_bases, k, r0, c0, counter, stp);
         else if (p.rc) launch_xown<4, true>(ctx, p, codes, n_bases, k, r0, c0, counter, stp);
         else launch_xown<8, false>(ctx, p, codes, n_bases, k, r0, c0, counter, stp);
         return;
     }
-    if (p.canon && p.ei == 12) launch_extract<12, false, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
-    else if (p.canon) launch_extract<16, false, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
+    if (p.canon && p.mix && p.ei == 12) launch_extract<12, false, 2>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
+    else if (p.canon && p.mix) launch_extract<16, false, 2>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
+    else if (p.canon && p.ei == 12) launch_extract<12, false, 1>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
+    else if (p.canon) launch_extract<16, false, 1>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
     else if (p.rc && p.ei == 6) launch_extract<6, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
     else if (p.rc) launch_extract<8, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
     else if (p.ei == 12) launch_extract<12, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
@@ -1995,7 +2052,7 @@ constexpr uint32_t HIST_BLOCKS_PER_SEG = 32;
 
 // exact (bucket, segment) counts of rg_extract's items: block (j, s) rolls
 // the tiles j, j + J, ... of segment s
-template <int EI, bool RC, bool CANON>
+template <int EI, bool RC, int CANON>
 __global__ __launch_bounds__(RT) void rg_hist(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
                                              uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ hist) {
     constexpr int NT = RT, NWAVE = NT / 64, WIN = NT * EI;
@@ -2042,6 +2099,7 @@ int make_shard_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t f
     if (mode == KMAN_FINISH_UNIQ && k > 25) return KMAN_EFALLBACK;  // (the tile-local window index above the key)
     RegionPlan p{};
     p.canon = flags & KMAN_CANONICAL;
+    p.mix = p.canon && (flags & KMAN_MIXED);
     p.rc = (flags & KMAN_RC) && !p.canon;
     p.K = 2 * k;
     if (p.K < B1 + 9 + 1) return KMAN_EFALLBACK;  // (the rounds' passes need 8 + 9 key bits and one more)
@@ -2147,7 +2205,7 @@ int read_err(kman_ctx *ctx, uint32_t *e) {
     return KMAN_OK;
 }
 
-template <int EI, bool RC, bool CANON>
+template <int EI, bool RC, int CANON>
 void launch_hist(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                  uint32_t *hist) {
     const uint32_t gx = p.seg_tiles < HIST_BLOCKS_PER_SEG ? p.seg_tiles : HIST_BLOCKS_PER_SEG;
@@ -2155,19 +2213,19 @@ void launch_hist(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint6
                        p.seg_tiles, p.n_tiles0, hist);
 }
 
-template <int EI, bool RC, bool CANON>
+template <int EI, bool RC, int CANON>
 void launch_extract_ex(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                        uint64_t *out, uint32_t *cnt, const uint64_t *rtab, uint32_t epoch, uint32_t *counter) {
     const uint32_t grid = RS * p.seg_tiles;
     if (xcd_tickets()) {
         hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, true, RS, 1, false, 0, true>), dim3(grid), dim3(RT), 0,
                            ctx->stream, codes, n_bases, (int)k, p.Q, out, (uint64_t)0, p.seg_tiles, p.n_tiles0, cnt,
-                           ctx->d_status, ctx->d_xcounters + 8 * (epoch & 63u), epoch, ctx->d_err, 0u, nullptr, rtab);
+                           ctx->d_status, ctx->d_xcounters + 8 * (epoch & 63u), epoch, ctx->d_err, hot_bit(), nullptr, rtab);
         return;
     }
     hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, true, RS, 1>), dim3(grid), dim3(RT), 0, ctx->stream, codes,
                        n_bases, (int)k, p.Q, out, (uint64_t)0, p.seg_tiles, p.n_tiles0, cnt, ctx->d_status, counter,
-                       epoch, ctx->d_err, 0u, nullptr, rtab);
+                       epoch, ctx->d_err, hot_bit(), nullptr, rtab);
 }
 
 }  // namespace
@@ -2189,9 +2247,10 @@ extern "C" int kman_dshard_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t 
     if (n_bases) {
         if (!d_codes) return kman_fail(ctx, KMAN_EINVAL, "null codes");
         KTimer kt_(ctx, "shard_hist");
-        if (p.canon) launch_hist<12, false, true>(ctx, p, d_codes, n_bases, k, d_hist);
-        else if (p.rc) launch_hist<6, true, false>(ctx, p, d_codes, n_bases, k, d_hist);
-        else launch_hist<12, false, false>(ctx, p, d_codes, n_bases, k, d_hist);
+        if (p.canon && p.mix) launch_hist<12, false, 2>(ctx, p, d_codes, n_bases, k, d_hist);
+        else if (p.canon) launch_hist<12, false, 1>(ctx, p, d_codes, n_bases, k, d_hist);
+        else if (p.rc) launch_hist<6, true, 0>(ctx, p, d_codes, n_bases, k, d_hist);
+        else launch_hist<12, false, 0>(ctx, p, d_codes, n_bases, k, d_hist);
         HIP_TRY(ctx, hipGetLastError());
     }
     HIP_TRY(ctx, hipMemcpyAsync(hist, d_hist, (size_t)RADIX * RS * 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -2215,9 +2274,10 @@ extern "C" int kman_dshard_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64
     {
         KTimer kt_(ctx, "region_extract");
         uint32_t *cnt = const_cast<uint32_t *>(d_hist);  // read-only in EX mode
-        if (p.canon) launch_extract_ex<12, false, true>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
-        else if (p.rc) launch_extract_ex<6, true, false>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
-        else launch_extract_ex<12, false, false>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
+        if (p.canon && p.mix) launch_extract_ex<12, false, 2>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
+        else if (p.canon) launch_extract_ex<12, false, 1>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
+        else if (p.rc) launch_extract_ex<6, true, 0>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
+        else launch_extract_ex<12, false, 0>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
         HIP_TRY(ctx, hipGetLastError());
     }
     uint32_t e;
@@ -2406,14 +2466,37 @@ __global__ __launch_bounds__(256) void count_hist_kernel(const C *__restrict__ c
     __syncthreads();
     // counts of 1 and 2 (nearly every row of a genome's spectrum) in registers,
     // one LDS atomic per wave: every lane adding to the same LDS word
-    // serialised the kernel (9.1 ms for 2.7 G rows, 1.2 TB/s)
+    // serialised the kernel (9.1 ms for 2.7 G rows, 1.2 TB/s).  16-byte loads,
+    // four in flight per thread (one scalar load per trip ran at 1.6 TB/s)
     uint32_t r1 = 0, r2 = 0;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
-        const uint64_t c = counts[i];
+    auto add = [&](uint64_t c) {
         if (c == 1) r1++;
         else if (c == 2) r2++;
         else atomicAdd(&lh[c < nbins ? c : nbins - 1], 1u);
+    };
+    constexpr uint32_t PV = 16 / sizeof(C);  // counts per 16-byte vector
+    const uint64_t nv = n / PV;
+    const uint4 *v = reinterpret_cast<const uint4 *>(counts);
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + 3 * stride < nv; i += 4 * stride) {
+        uint4 a[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) a[u] = v[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const C *c = reinterpret_cast<const C *>(&a[u]);
+#pragma unroll
+            for (uint32_t e = 0; e < PV; e++) add((uint64_t)c[e]);
+        }
     }
+    for (; i < nv; i += stride) {
+        const uint4 a = v[i];
+        const C *c = reinterpret_cast<const C *>(&a);
+#pragma unroll
+        for (uint32_t e = 0; e < PV; e++) add((uint64_t)c[e]);
+    }
+    for (uint64_t j = nv * PV + (uint64_t)blockIdx.x * 256 + threadIdx.x; j < n; j += stride) add((uint64_t)counts[j]);
     r1 = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_scan(r1, SumU32()), 63);
     r2 = (uint32_t)__builtin_amdgcn_readlane((int)wave_inclusive_scan(r2, SumU32()), 63);
     if ((threadIdx.x & 63) == 0) {
@@ -2432,6 +2515,7 @@ extern "C" int kman_count_hist(kman_ctx *ctx, const void *d_counts, uint32_t cou
     if (count_bytes != 4 && count_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "count_bytes must be 4 or 8");
     if (nbins < 2 || nbins > 16384) return kman_fail(ctx, KMAN_EINVAL, "nbins must be in [2, 16384]");
     if (!d_hist || (n && !d_counts)) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    if ((uintptr_t)d_counts & 15) return kman_fail(ctx, KMAN_EINVAL, "counts must be 16-byte aligned");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     HIP_TRY(ctx, hipMemsetAsync(d_hist, 0, (size_t)nbins * 8, ctx->stream));
     if (n) {

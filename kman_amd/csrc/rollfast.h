@@ -8,7 +8,8 @@
 // window j covers codes [base + j, base + j + k); it is valid when none of its
 // k codes is not-ACGT, no code after its first starts a record, and its start
 // p0 + j < n_bases.  kf = forward key (first base most significant), kr =
-// reverse complement; CANON: kf = min(forward, reverse complement).
+// reverse complement; CANON: kf = min(forward, reverse complement) (CANON == 2:
+// through mix_key).
 //
 // Host-compilable (tests/test_rollfast.py checks it against a per-base roll).
 #pragma once
@@ -30,7 +31,20 @@ KMAN_RF_HD uint32_t rf_bit4(uint32_t x, int bit) {
     return ((((x >> bit) & 0x01010101u) * 0x00204081u) >> 21) & 0xfu;
 }
 
-template <int EI, bool CANON>
+// A bijection of the 2k-bit keys (odd multiply, xorshift, odd multiply, all
+// mod 2^2k): canonical keys mixed by it keep their multiset of counts, so an
+// abundance spectrum is unchanged, while the top key bits -- the buckets of
+// the region passes -- become uniform (min(fwd, rc) alone puts about twice
+// the average into the low buckets).  CANON == 2 selects it.
+KMAN_RF_HD uint64_t mix_key(uint64_t x, int k) {
+    const int kb = 2 * k;
+    const uint64_t m = kb >= 64 ? ~0ull : ((1ull << kb) - 1);
+    x = (x * 0x9E3779B97F4A7C15ull) & m;
+    x ^= x >> (kb / 2);
+    return (x * 0xBF58476D1CE4E5B9ull) & m;
+}
+
+template <int EI, int CANON>
 KMAN_RF_HD uint32_t roll_fast(const uint8_t *s, int base, int k, uint64_t mask, uint64_t p0, uint64_t n_bases,
                               uint64_t (&kf)[EI], uint64_t (&kr)[EI]) {
     // words covering (base & 3) + k - 1 + EI codes for any k <= 32
@@ -70,6 +84,7 @@ KMAN_RF_HD uint32_t roll_fast(const uint8_t *s, int base, int k, uint64_t mask, 
         const uint64_t rc = (u & mask) ^ mask;
         if (CANON) {
             kf[j] = fwd < rc ? fwd : rc;
+            if (CANON == 2) kf[j] = mix_key(kf[j], k);
         } else {
             kf[j] = fwd;
             kr[j] = rc;

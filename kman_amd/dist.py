@@ -156,22 +156,37 @@ def gather_ranges(cnt: np.ndarray, allr: np.ndarray, G: int) -> List[np.ndarray]
 def redo_map(ranges: List[np.ndarray], key_bits: int, max_bits: int = 24) -> Tuple[int, np.ndarray]:
     """(pbits, map): map[p] = q + 1 when the keys with top pbits bits p lie in
     one of destination q's left-out ranges (0 elsewhere); pbits is the
-    coarsest prefix length at which every range is whole."""
+    coarsest prefix length at which every range is whole.  Vectorised: a
+    skewed genome leaves out thousands of ranges per round."""
     K = key_bits
+    lo = np.concatenate([np.asarray(r, np.uint64).reshape(-1, 2)[:, 0] for r in ranges] + [np.zeros(0, np.uint64)])
+    hi = np.concatenate([np.asarray(r, np.uint64).reshape(-1, 2)[:, 1] for r in ranges] + [np.zeros(0, np.uint64)])
+    dst = np.concatenate([np.full(len(np.asarray(r).reshape(-1, 2)), q + 1, np.int64) for q, r in enumerate(ranges)]
+                         + [np.zeros(0, np.int64)])
     pbits = 1
-    for rq in ranges:
-        for lo, hi in rq:
-            lo, end = int(lo), int(hi) + 1
-            a = (lo & -lo).bit_length() - 1 if lo else K
-            b = (end & -end).bit_length() - 1 if end < (1 << K) else K
-            pbits = max(pbits, K - min(a, b))
+    if len(lo):
+        def tz(x, full):
+            # trailing zero bits (full when x == 0): exact via the lowest set bit's power of two
+            low = x & (~x + np.uint64(1))
+            t = np.zeros(len(x), np.int64)
+            nz = low != 0
+            t[nz] = np.round(np.log2(low[nz].astype(np.float64))).astype(np.int64)
+            t[~nz] = full
+            return t
+
+        top = np.uint64((1 << K) - 1) if K < 64 else np.uint64(0xFFFFFFFFFFFFFFFF)
+        end = hi + np.uint64(1)  # (wraps to 0 for the last key: a whole-space end)
+        a = tz(lo, K)
+        b = np.where(hi >= top, K, tz(end, K))
+        pbits = max(1, int((K - np.minimum(a, b)).max()))
     if pbits > max_bits:
         raise NotImplementedError("left-out key ranges finer than %d key bits" % max_bits)
-    sh = K - pbits
-    pmap = np.zeros(1 << pbits, np.uint8)
-    for q, rq in enumerate(ranges):
-        for lo, hi in rq:
-            pmap[int(lo) >> sh:(int(hi) >> sh) + 1] = q + 1
+    sh = np.uint64(K - pbits)
+    marks = np.zeros((1 << pbits) + 1, np.int64)
+    if len(lo):
+        np.add.at(marks, (lo >> sh).astype(np.int64), dst)
+        np.add.at(marks, (hi >> sh).astype(np.int64) + 1, -dst)
+    pmap = np.cumsum(marks[:-1]).astype(np.uint8)  # (the ranges are disjoint)
     return pbits, pmap
 
 
@@ -469,7 +484,10 @@ class DistPipeline:
         self.pieces = 4
         self.overlapped_rounds = 0
         self.fmode = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
-        self.flags = engine.flags_for(self.rc, mode == "uniq", canonical)
+        # rows wanted as a multiset only (the spectrum): canonical keys are
+        # mixed (KMAN_MIXED) so the key rounds see uniform buckets
+        self.mixed = canonical and not ordered
+        self.flags = engine.flags_for(self.rc, mode == "uniq", canonical, self.mixed)
         self.reader = reader
         if shard is None:
             self.spec = S.shard_specs(reader, world, k)[rank]
@@ -813,7 +831,7 @@ class DistPipeline:
         pbits, pmap = redo_map(ranges, 2 * k)
         d_map = self.part_bufs[2].get(len(pmap))
         dev.upload(d_map, pmap)
-        flags = engine.flags_for(self.rc, uniq, self.canonical)
+        flags = engine.flags_for(self.rc, uniq, self.canonical, self.mixed)
 
         def marked(q, keys_ptr, pos_ptr, cap):
             got = c_uint64(0)
@@ -967,7 +985,7 @@ class DistPipeline:
         shift = max(0, 2 * k - 8)
         sc = np.zeros(G, np.uint64)
         at = 0
-        flags = engine.flags_for(self.rc, uniq, self.canonical)
+        flags = engine.flags_for(self.rc, uniq, self.canonical, self.mixed)
         for q in range(G):
             lo, hi = part_of(cuts, R, q, r)
             want = int(np.asarray(C, np.uint64)[me, lo:hi].sum())
@@ -1116,7 +1134,7 @@ def local_groups(p: engine.Parsed, k: int, rc: bool, mode: str, canonical: bool 
     k-mers than its region capacities, `-r` on large inputs, skewed keys.
     None when the rounds do not take the input either (uniq with k > 25 or
     more pos bits than an item holds)."""
-    flags = engine.flags_for(rc and not canonical, mode == "uniq", canonical)
+    flags = engine.flags_for(rc and not canonical, mode == "uniq", canonical, canonical and not ordered)
     fm = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
     if k > engine.MAX_K or N.lib().kman_dshard_plan(p.n_bases, p.n_bases, k, flags, fm) != N.KMAN_OK:
         return None

@@ -259,8 +259,11 @@ class Kmers:
                 b.free()
 
 
-def flags_for(rc: bool, want_pos: bool, canonical: bool = False) -> int:
-    return (N.KMAN_RC if rc else 0) | (N.KMAN_WANT_POS if want_pos else 0) | (N.KMAN_CANONICAL if canonical else 0)
+def flags_for(rc: bool, want_pos: bool, canonical: bool = False, mixed: bool = False) -> int:
+    """kman_extract flags; mixed (with canonical): the keys through the
+    bijection of KMAN_MIXED -- spectra only, the keys are not printed."""
+    return ((N.KMAN_RC if rc else 0) | (N.KMAN_WANT_POS if want_pos else 0) | (N.KMAN_CANONICAL if canonical else 0)
+            | (N.KMAN_MIXED if canonical and mixed else 0))
 
 
 def count_kmers(p: Parsed, k: int, rc: bool, canonical: bool = False) -> int:
@@ -440,14 +443,14 @@ def rle_uniq(km: Kmers, dev: Device) -> UniqResult:
     return UniqResult(okeys, opos, km.pos_bytes, int(out.value), km.k)
 
 
-def groups(p: Parsed, k: int, rc: bool, mode: str, canonical: bool = False):
+def groups(p: Parsed, k: int, rc: bool, mode: str, canonical: bool = False, mixed: bool = False):
     """kman_groups: count / uniq of the whole stream straight from the codes
     (region.hip).  Returns a CountResult / UniqResult, or None when the input
     is outside the region path (kman_groups_plan / a region overflow said
     KMAN_EFALLBACK): the caller then runs extract_sorted + rle_*."""
     L, dev = N.lib(), p.dev
     m = N.KMAN_FINISH_UNIQ if mode == "uniq" else N.KMAN_FINISH_COUNT
-    flags = flags_for(rc, mode == "uniq", canonical)
+    flags = flags_for(rc, mode == "uniq", canonical, mixed)
     wb = c_uint64(0)
     rc_ = L.kman_groups_plan(p.n_bases, k, flags, m, byref(wb))
     if rc_ == N.KMAN_EFALLBACK:
@@ -968,7 +971,10 @@ def count_groups(p: Parsed, k: int, rc: bool = False, canonical: bool = False, o
     k > 32: a WordsResult (word keys, its counts in .vals)."""
     if k > MAX_K:
         return words_groups(p, k, rc, "count", canonical)
-    r = groups(p, k, rc, "count", canonical)
+    # a spectrum (ordered=False) of canonical keys counts mixed keys
+    # (KMAN_MIXED): the same counts, uniform buckets for the region passes
+    mixed = canonical and not ordered
+    r = groups(p, k, rc, "count", canonical, mixed)
     if r is not None:
         return r
     if p.n_bases:

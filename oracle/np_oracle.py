@@ -146,3 +146,16 @@ def rle_uniq(sorted_keys: np.ndarray, vals: np.ndarray):
 
 def decode(key: int, k: int) -> bytes:
     return bytes(b"ACGT"[(int(key) >> (2 * (k - 1 - j))) & 3] for j in range(k))
+
+
+def mix_keys(x, k: int):
+    """KMAN_MIXED's bijection of the 2k-bit keys (kman_amd/csrc/rollfast.h
+    mix_key: odd multiply, xorshift by k, odd multiply, mod 2^2k) -- the
+    engine's own key transform for abundance spectra, not the reference's."""
+    x = np.asarray(x, dtype=np.uint64)
+    kb = 2 * k
+    m = np.uint64((1 << kb) - 1) if kb < 64 else np.uint64(0xFFFFFFFFFFFFFFFF)
+    with np.errstate(over="ignore"):
+        x = (x * np.uint64(0x9E3779B97F4A7C15)) & m
+        x = x ^ (x >> np.uint64(kb // 2))
+        return (x * np.uint64(0xBF58476D1CE4E5B9)) & m

@@ -18,6 +18,9 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
+    # `kmer count` declares -m twice, exactly as the reference CLI does
+    # (arguments.py:104-115 and 134-149); click warns at every parse
+    config.addinivalue_line("filterwarnings", "ignore:The parameter -m is used more than once")
 
 
 @pytest.fixture(scope="session")

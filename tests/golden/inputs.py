@@ -182,6 +182,75 @@ def grch38_like(seed: int, n_bases: int = 1_000_000, n_records: int = 5, width: 
     return b"".join(out)
 
 
+def grch38_skewed(seed: int, n_bases: int = 1_000_000, n_records: int = 5, width: int = 60) -> bytes:
+    """A GRCh38-shaped synthetic FASTA with a genome's repeat skew (BASELINE
+    config 5 stand-in; GRCh38 itself is not in this container): besides
+    grch38_like's records, soft-masking and N blocks,
+      * an Alu-like family: one 300-bp consensus, a copy every ~3.1 kb (about
+        a million copies over 3.1 Gbp, ~10 % of the sequence), each ~10 %
+        diverged (independent substitutions), on either strand;
+      * per record a tandem satellite array of min(L / 40, 3 Mbp): a 171-bp
+        monomer, ~2 % diverged copy to copy (the alpha-satellite arrays of
+        the centromeres);
+      * long poly-A / poly-T runs (1-20 kb) and poly-N gaps (10 kb - 1 Mb).
+    Vectorised (numpy), ~10 s per Gbp."""
+    rng = np.random.default_rng(seed)
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    alu = rng.integers(0, 4, size=300, dtype=np.uint8)
+    mono = rng.integers(0, 4, size=171, dtype=np.uint8)
+    out = []
+    per = n_bases // n_records
+    for r in range(n_records):
+        L = per if r + 1 < n_records else n_bases - per * (n_records - 1)
+        seq = rng.integers(0, 4, size=L, dtype=np.uint8)
+        # Alu-like copies, 10 % diverged, half reverse-complemented
+        n_alu = L // 3100
+        if n_alu and L > 300:
+            for c0 in range(0, n_alu, 1 << 16):
+                m = min(1 << 16, n_alu - c0)
+                cp = np.broadcast_to(alu, (m, 300)).copy()
+                mut = rng.random((m, 300)) < 0.10
+                cp[mut] = rng.integers(0, 4, size=int(mut.sum()), dtype=np.uint8)
+                flip = rng.random(m) < 0.5
+                cp[flip] = 3 - cp[flip, ::-1]
+                at = rng.integers(0, L - 300, size=m)
+                idx = at[:, None] + np.arange(300)[None, :]
+                seq[idx.reshape(-1)] = cp.reshape(-1)
+        # a tandem satellite array, ~2 % diverged monomers
+        n_sat = min(L // 40, 3_000_000) // 171
+        if n_sat:
+            arr = np.broadcast_to(mono, (n_sat, 171)).copy()
+            mut = rng.random((n_sat, 171)) < 0.02
+            arr[mut] = rng.integers(0, 4, size=int(mut.sum()), dtype=np.uint8)
+            at = int(rng.integers(0, max(1, L - n_sat * 171)))
+            seq[at:at + n_sat * 171] = arr.reshape(-1)[:L - at]
+        # poly-A / poly-T runs
+        for _ in range(max(1, L // 2_000_000)):
+            a = int(rng.integers(0, L))
+            seq[a:a + int(rng.integers(1_000, 20_000))] = 0 if rng.random() < 0.5 else 3
+        chars = acgt[seq].copy()
+        # soft-masking in runs
+        for _ in range(L // 50_000):
+            a = int(rng.integers(0, L))
+            chars[a:a + int(rng.integers(500, 15_000))] += 32
+        # N: the record ends (telomeres) and gaps of 10 kb - 1 Mb
+        nN = min(L // 20, 10_000)
+        chars[:nN] = ord("N")
+        chars[L - nN:] = ord("N")
+        for _ in range(max(1, L // 20_000_000)):
+            a = int(rng.integers(0, L))
+            chars[a:a + int(rng.integers(10_000, min(1_000_000, max(10_001, L // 10))))] = ord("N")
+        out.append(b">chr%d AC:CM0006%02d.2 gi:5688%02d LN:%d rl:Chromosome M5:x AS:GRCh38\n" % (r + 1, r, r, L))
+        full = L // width
+        grid = np.empty((full, width + 1), dtype=np.uint8)
+        grid[:, :width] = chars[:full * width].reshape(full, width)
+        grid[:, width] = ord("\n")
+        out.append(grid.tobytes())
+        if L > full * width:
+            out.append(bytes(chars[full * width:]) + b"\n")
+    return b"".join(out)
+
+
 def messy_records(seed: int, n_records: int = 24, max_len: int = 3000) -> bytes:
     """Multi-record FASTA exercising the parser/extractor edge cases of §8c/§A:
     descriptions after the name, a tab inside the title, lowercase runs, N and

@@ -289,3 +289,39 @@ def test_round_pieces_partition_each_part(G, S):
                 sizes = [tot[x:y].sum() for x, y in zip(b, b[1:])]
                 # no piece above its share plus one bucket
                 assert max(sizes) <= tot[lo:hi].sum() / S + tot[lo:hi].max()
+
+
+def _redo_map_loops(ranges, K):
+    """redo_map restated range by range (the vectorised version must agree)."""
+    pbits = 1
+    for rq in ranges:
+        for lo, hi in rq:
+            lo, end = int(lo), int(hi) + 1
+            a = (lo & -lo).bit_length() - 1 if lo else K
+            b = (end & -end).bit_length() - 1 if end < (1 << K) else K
+            pbits = max(pbits, K - min(a, b))
+    sh = K - pbits
+    pmap = np.zeros(1 << pbits, np.uint8)
+    for q, rq in enumerate(ranges):
+        for lo, hi in rq:
+            pmap[int(lo) >> sh:(int(hi) >> sh) + 1] = q + 1
+    return pbits, pmap
+
+
+@pytest.mark.parametrize("K", [16, 30, 42, 64])
+def test_redo_map_matches_range_loops(K):
+    from kman_amd import dist
+
+    rng = np.random.default_rng(K)
+    for _ in range(40):
+        G = int(rng.integers(1, 6))
+        pb = int(rng.integers(1, min(K, 20) + 1))
+        cuts = np.sort(rng.choice(1 << pb, size=min(1 << pb, 2 * int(rng.integers(0, 60))), replace=False))
+        ranges = [[] for _ in range(G)]
+        for i in range(0, len(cuts) - 1, 2):
+            a, b = int(cuts[i]), int(cuts[i + 1])
+            ranges[int(rng.integers(0, G))].append([a << (K - pb), ((b + 1) << (K - pb)) - 1])
+        ranges = [np.array(r, np.uint64).reshape(-1, 2) for r in ranges]
+        got, want = dist.redo_map(ranges, K), _redo_map_loops(ranges, K)
+        assert got[0] == want[0]
+        np.testing.assert_array_equal(got[1], want[1])

@@ -133,3 +133,28 @@ def test_hist_cli(tmp_path):
     want = "".join("%d\t%d\n" % (c, h[c]) for c in np.nonzero(h)[0])
     assert out.read_text() == want
     del root
+
+
+@pytest.mark.parametrize("k", [15, 21, 31])
+def test_mixed_canonical_spectrum_keys(dev, k):
+    """ordered=False (a spectrum) counts canonical keys through KMAN_MIXED's
+    bijection: the rows are exactly {mix(x): occ(x)} over the oracle's
+    canonical keys -- the same counts, so the same spectrum -- including the
+    repeat-heavy input whose regions overflow and are redone."""
+    import np_oracle
+    from kman_amd import engine
+
+    for text in _texts():
+        keys, _ = np_oracle.stream_kmers(np_oracle.parse_fasta(text), k, canonical=True)
+        wk, wc = np.unique(np_oracle.mix_keys(keys, k), return_counts=True)
+        p = engine.parse(dev, text)
+        try:
+            r = engine.count_groups(p, k, canonical=True, ordered=False)
+            gk, gc = engine.download_count(dev, r)
+            r.ukeys.free()
+            r.counts.free()
+        finally:
+            p.free()
+        o = np.argsort(gk, kind="stable")
+        np.testing.assert_array_equal(gk[o], wk)
+        np.testing.assert_array_equal(np.asarray(gc)[o].astype(np.int64), wc)
