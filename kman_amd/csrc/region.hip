@@ -87,38 +87,6 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
     return r;
 }
 
-// A block-wide LDS rank (+1 on counter ctr[d] per valid lane, unstable):
-// when >= 8 lanes of the wave hold the same digit as lane 0 (repeated keys,
-// a genome's repeats), those lanes take ONE atomic (64 same-address LDS
-// atomics serialise) and rank by their position among themselves.
-KMAN_DEV uint32_t rank_hot(uint32_t *ctr, uint32_t d, bool valid) {
-    // (one atomic instruction, no branch: the hot lanes other than the
-    // leader sit it out, the leader adds their count)
-    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-    const uint64_t same = __ballot(valid && d == d0);
-    const uint32_t ns = (uint32_t)__popcll(same);
-    const bool hot = ns >= 8u;  // (wave-uniform)
-    const int leader = __ffsll((unsigned long long)same) - 1;
-    const bool mine = hot && ((same >> lane_id()) & 1ull);
-    uint32_t old = 0;
-    if (valid && (!mine || lane_id() == leader)) old = atomicAdd(&ctr[d], mine ? ns : 1u);
-    if (!hot) return old;
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)old, leader);
-    return mine ? lo + (uint32_t)__popcll(same & lanemask_lt()) : old;
-}
-
-// dbg bit RG_HOT (KMAN_RG_HOT=1): the hot-digit ranks above; else one atomic
-// per lane (a uniform branch on a kernel argument)
-constexpr uint32_t RG_HOT = 64;
-KMAN_DEV uint32_t rank_block(uint32_t *ctr, uint32_t d, bool valid, uint32_t dbg) {
-    if (dbg & RG_HOT) return rank_hot(ctr, d, valid);
-    return valid ? atomicAdd(&ctr[d], 1u) : 0u;
-}
-static uint32_t hot_bit() {
-    static const char *e = getenv("KMAN_RG_HOT");
-    return e && atoi(e) == 1 ? RG_HOT : 0u;
-}
-
 // ---------------------------------------------------------------- pass 0
 // A tile of RT*EI window starts: windows rolled from LDS-staged codes, the
 // valid ones compacted in stream order (tile-local window << 1 | strand
@@ -277,7 +245,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
 #define KEPT(d) (!EX || ((keep[(d) >> 5] >> ((d) & 31)) & 1u))
     if (BR) {
 #pragma unroll
-        for (int i = 0; i < SI; i++) rank[i] = rank_block(thist, XDIGIT(key[i]), ib + i * 64 < tcnt, dbg);
+        for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&thist[XDIGIT(key[i])], 1u) : 0u;
         __syncthreads();
         // (EX: a digit not kept this round has no chain: nothing published)
         if (threadIdx.x < RADIX && KEPT(threadIdx.x))
@@ -769,7 +737,8 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
 #define PDIGIT(x) ((uint32_t)((x) >> shift) & dmask)
             if (BR) {
 #pragma unroll
-                for (int i = 0; i < SI; i++) rank[i] = rank_block(thist, PDIGIT(key[i]), ib + i * 64 < n, dbg);
+                for (int i = 0; i < SI; i++)
+                    rank[i] = ib + i * 64 < n ? atomicAdd(&thist[PDIGIT(key[i])], 1u) : 0u;
                 __syncthreads();
                 const uint32_t ls = block_exclusive_scan<NT>(threadIdx.x < R1 ? thist[threadIdx.x] : 0u, SumU32(), 0u,
                                                              lds_scan, (uint32_t *)nullptr);
@@ -1113,6 +1082,9 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
     // wave return in lane order (probed: ATOMIC), else ballot match-any.
     // (dbg & 1: timing ablation only, no sort passes)
     RSTAMP(r, 1);
+#ifdef KMAN_RG_STAMPS
+    if (stp && t == 0) stp[(uint64_t)r * 8 + 7] = m;  // (the region's items, beside its phase stamps)
+#endif
     const uint32_t np = (dbg & 1) ? 0u : (rest + FBITS - 1) / FBITS;
     uint32_t at = 0;
     for (uint32_t p = 0; p < np; p++) {
@@ -1129,31 +1101,7 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
             const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
             const uint32_t hs = (d & 1u) * 16u;
             if (ATOMIC) {
-                // a hot digit (repeated keys: a genome's repeats fill whole
-                // waves with one key) takes ONE atomic for all its lanes --
-                // 64 same-address LDS atomics serialise; the other lanes rank
-                // as usual (their atomics return in lane order).  One atomic
-                // instruction either way: the leader adds the hot lanes' count
-                // (NARROW: not at all -- the ballot masks cost the VGPR
-                // budget of three blocks per CU: 72 -> 80 + 2.5 KB of spills)
-                if constexpr (NARROW) {
-                    rk[i] = valid ? (atomicAdd(&wh[w][d >> 1], 1u << hs) >> hs) & 0xffffu : 0u;
-                } else {
-                    const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
-                    const uint64_t same = __ballot(valid && d == d0);
-                    const uint32_t ns = (uint32_t)__popcll(same);
-                    const bool hot = ns >= 8u;  // (wave-uniform)
-                    const int leader = __ffsll((unsigned long long)same) - 1;
-                    const bool mine = hot && ((same >> lane) & 1ull);
-                    uint32_t old = 0;
-                    if (valid && (!mine || lane == leader)) old = atomicAdd(&wh[w][d >> 1], (mine ? ns : 1u) << hs);
-                    old = (old >> hs) & 0xffffu;
-                    if (hot) {
-                        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)old, leader);
-                        if (mine) old = lo + (uint32_t)__popcll(same & lanemask_lt());
-                    }
-                    rk[i] = old;
-                }
+                rk[i] = valid ? (atomicAdd(&wh[w][d >> 1], 1u << hs) >> hs) & 0xffffu : 0u;
             } else {
                 uint64_t peers = __ballot(valid);
                 for (uint32_t bb = 0; bb < bw; bb++) {
@@ -1461,7 +1409,6 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
 
 template <int NT, int SI, bool PF, bool WC = false, bool BR = false>
 void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
-    dbg |= hot_bit();
     if constexpr (BR) {  // no ordered LDS atomics needed
         const void *fn = (const void *)rg_pass<true, NT, SI, PF, WC, BR>;
         const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, NT, (uint64_t)pa.nbk * pa.H);
@@ -1634,7 +1581,6 @@ template <int EI, bool RC, int CANON, int NS, int XLB = 1>
 void launch_extract_ns(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                        uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp,
                        uint32_t n_launch) {
-    dbg |= hot_bit();
     if (NS == RS && XLB == 1) {
         static const char *e = getenv("KMAN_RG_XLB");
         const int x = e ? atoi(e) : 1;
@@ -1739,6 +1685,47 @@ void launch_extract_any(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes
 }
 
 // mean phase durations (us) per kernel from the stamp rows; frees the buffers
+// the round finish's regions (KMAN_RG_STAMPS diagnostic build): mean phases,
+// the spread of per-region times and of the look-back wait, by region size
+int report_finish_stamps(kman_ctx *ctx, uint64_t *st, uint64_t nreg) {
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<uint64_t> h(nreg * 8);
+    HIP_TRY(ctx, hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(ctx, hipFree(st));
+    std::vector<double> tot, wait;
+    double ph[7] = {0}, sz_t[4] = {0};
+    uint64_t n = 0, sz_n[4] = {0}, t0 = ~0ull, t1 = 0;
+    for (uint64_t r = 0; r < nreg; r++) {
+        const uint64_t *x = &h[r * 8];
+        if (!x[0] || !x[5]) continue;
+        t0 = x[0] < t0 ? x[0] : t0;
+        t1 = x[5] > t1 ? x[5] : t1;
+        for (int i = 1; i < 6; i++) ph[i] += (double)(x[i] - x[i - 1]) / 100.0;
+        tot.push_back((double)(x[5] - x[0]) / 100.0);
+        wait.push_back((double)(x[4] - x[3]) / 100.0);
+        const int b = x[7] < 2048 ? 0 : x[7] < 4096 ? 1 : x[7] < 6144 ? 2 : 3;
+        sz_t[b] += tot.back();
+        sz_n[b]++;
+        n++;
+    }
+    if (!n) return KMAN_OK;
+    auto pct = [](std::vector<double> v, double q) {
+        std::sort(v.begin(), v.end());
+        return v[(size_t)(q * (double)(v.size() - 1))];
+    };
+    fprintf(stderr, "stamps round finish: regions %llu span %.1f us  mean us/region %.2f  phases:",
+            (unsigned long long)n, (double)(t1 - t0) / 100.0, pct(tot, 0.5));
+    for (int i = 1; i < 6; i++) fprintf(stderr, " %d:%.2f", i, ph[i] / (double)n);
+    fprintf(stderr, "\n  total p50 %.2f p90 %.2f p99 %.2f max %.2f | look-back wait p50 %.2f p90 %.2f p99 %.2f max %.2f\n",
+            pct(tot, 0.5), pct(tot, 0.9), pct(tot, 0.99), pct(tot, 1.0), pct(wait, 0.5), pct(wait, 0.9),
+            pct(wait, 0.99), pct(wait, 1.0));
+    fprintf(stderr, "  mean us by items <2K %.2f (%llu) <4K %.2f (%llu) <6K %.2f (%llu) >=6K %.2f (%llu)\n",
+            sz_n[0] ? sz_t[0] / sz_n[0] : 0.0, (unsigned long long)sz_n[0], sz_n[1] ? sz_t[1] / sz_n[1] : 0.0,
+            (unsigned long long)sz_n[1], sz_n[2] ? sz_t[2] / sz_n[2] : 0.0, (unsigned long long)sz_n[2],
+            sz_n[3] ? sz_t[3] / sz_n[3] : 0.0, (unsigned long long)sz_n[3]);
+    return KMAN_OK;
+}
+
 int report_stamps(kman_ctx *ctx, uint64_t **st, const uint64_t *rows) {
     static const char *names[3] = {"rg_extract", "rg_pass", "rg_finish"};
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
@@ -2220,12 +2207,12 @@ void launch_extract_ex(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes,
     if (xcd_tickets()) {
         hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, true, RS, 1, false, 0, true>), dim3(grid), dim3(RT), 0,
                            ctx->stream, codes, n_bases, (int)k, p.Q, out, (uint64_t)0, p.seg_tiles, p.n_tiles0, cnt,
-                           ctx->d_status, ctx->d_xcounters + 8 * (epoch & 63u), epoch, ctx->d_err, hot_bit(), nullptr, rtab);
+                           ctx->d_status, ctx->d_xcounters + 8 * (epoch & 63u), epoch, ctx->d_err, 0u, nullptr, rtab);
         return;
     }
     hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, true, RS, 1>), dim3(grid), dim3(RT), 0, ctx->stream, codes,
                        n_bases, (int)k, p.Q, out, (uint64_t)0, p.seg_tiles, p.n_tiles0, cnt, ctx->d_status, counter,
-                       epoch, ctx->d_err, hot_bit(), nullptr, rtab);
+                       epoch, ctx->d_err, 0u, nullptr, rtab);
 }
 
 }  // namespace
@@ -2369,12 +2356,21 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         HIP_TRY(ctx, hipGetLastError());
     }
     KMAN_TRY(rg_check(ctx, "pass 1", c1, d.nsub));
+    const char *dbg_env = getenv("KMAN_RG_DBG");  // finish timing ablations only (bits 1, 2)
+    const uint32_t fdbg = dbg_env ? (uint32_t)atoi(dbg_env) & 3u : 0u;
+    uint64_t *fst = nullptr;
+#ifdef KMAN_RG_STAMPS
+    if (getenv("KMAN_RG_STAMPS")) {
+        HIP_TRY(ctx, hipMalloc((void **)&fst, d.nreg * 64));
+        HIP_TRY(ctx, hipMemsetAsync(fst, 0, d.nreg * 64, ctx->stream));
+    }
+#endif
     if (d.g == 0) {
         // one source, two chains: the finish reads the pass-1 sub-regions
         FinishArgs f{r1, d.C1s, c1, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << 9, 0u, (uint32_t)d.nreg};
         f.fsub = d.H;
         f.freg = freg;
-        KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, 0, nullptr));
+        KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, fdbg, fst));
     } else {
     // (c2 may lie in the receive buffer: cleared only once pass 1 has read it)
     HIP_TRY(ctx, hipMemsetAsync(c2, 0, d.nreg * 4, ctx->stream));
@@ -2412,9 +2408,10 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         FinishArgs f{r2, d.C1, c2, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << (9 + d.g),
                      mode == KMAN_FINISH_UNIQ ? d.Q + d.rest + d.g : 0u, (uint32_t)d.nreg};
         f.freg = freg;
-        KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, 0, nullptr));
+        KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, fdbg, fst));
     }
     }
+    if (fst) KMAN_TRY(report_finish_stamps(ctx, fst, d.nreg));
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small + 4, ctx->d_status + (d.nreg - 1), 8, hipMemcpyDeviceToHost, ctx->stream));
     uint32_t e;
     KMAN_TRY(read_err(ctx, &e));  // synchronises

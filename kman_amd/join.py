@@ -350,9 +350,9 @@ def join_vectors(batches: List[Batch], masked: bool, outpath: str) -> None:
     rec_start = np.concatenate(rec_start).astype(np.uint64)
     rec_end = np.concatenate(rec_end).astype(np.uint64)
     bufs = []
+    vec = None
     try:
         vec = dev.alloc(4 * max(total, 1))
-        bufs.append(vec)
         dev.memset(vec, 0, 4 * max(total, 1))
         d_base, d_rs, d_id = dev.alloc(8 * len(base)), dev.alloc(8 * max(1, len(rec_start))), dev.alloc(
             4 * max(1, len(rec_id)))
@@ -364,41 +364,72 @@ def join_vectors(batches: List[Batch], masked: bool, outpath: str) -> None:
                                          1 if masked else 0, c_void_p(d_base.ptr), 1 if tagged else 0,
                                          c_void_p(d_rs.ptr), c_void_p(d_id.ptr), len(rec_start), c_void_p(vec.ptr)),
                 "kman_vec_fill")
-        v = dev.download(vec, total, np.uint32)
-    finally:
         km.free()
+        km = None
         for b in bufs:
             b.free()
-    if emulate:
-        if v.any():
-            raise NotImplementedError("AbundanceVector.add_count (the reference's VEC_COUNT_MASKED)")
-        print('Writing output in "%s"' % dirpath)  # abundance.py:160: no vector was added
+        bufs = []
+        # the slots stay in HBM (8 B per base): the host takes bounded slices
+        if emulate:
+            for lo in range(0, total, _VEC_SLICE):
+                if dev.download(vec, min(_VEC_SLICE, total - lo), np.uint32, 4 * lo).any():
+                    raise NotImplementedError("AbundanceVector.add_count (the reference's VEC_COUNT_MASKED)")
+            print('Writing output in "%s"' % dirpath)  # abundance.py:160: no vector was added
+            os.makedirs(dirpath, exist_ok=True)
+            return
+        print('Writing output in "%s"' % dirpath)  # abundance.py:160
         os.makedirs(dirpath, exist_ok=True)
-        return
-    print('Writing output in "%s"' % dirpath)  # abundance.py:160
-    os.makedirs(dirpath, exist_ok=True)
-    for r, name in enumerate(names):
-        for strand in (0, 1):
-            sl = v[int(rec_start[r]) + strand:int(rec_end[r]):2]
-            nz = np.flatnonzero(sl)
-            if not len(nz):
-                continue  # no add_count for this ref:strand: no vector, no file
-            n = int(nz[-1]) + 1
-            arr = np.ascontiguousarray(sl[:n])
-            used = c_size_t(0)
-            rc = L.kman_format_vector(arr.ctypes.data_as(c_void_p), n, 1, None, 0, byref(used), engine.host_threads())
-            if rc not in (N.KMAN_OK, N.KMAN_ECAP):
-                raise RuntimeError("kman_format_vector failed (%d)" % rc)
-            buf = ctypes.create_string_buffer(max(1, used.value))
-            rc = L.kman_format_vector(arr.ctypes.data_as(c_void_p), n, 1, buf, used.value, byref(used),
-                                      engine.host_threads())
-            if rc != N.KMAN_OK:
-                raise RuntimeError("kman_format_vector failed (%d)" % rc)
-            ref = name.decode("utf-8", "surrogateescape")
-            with gzip.open(os.path.join(dirpath, "%s___%s.gz" % (ref, "+-"[strand])), "wb") as OH:
-                OH.write(b"# k=%d\n" % k)
-                OH.write(buf.raw[:used.value])
+        for r, name in enumerate(names):
+            for strand in (0, 1):
+                n = _vector_len(dev, vec, int(rec_start[r]) + strand, int(rec_end[r]))
+                if not n:
+                    continue  # no add_count for this ref:strand: no vector, no file
+                arr = np.empty(n, np.uint32)
+                for lo in range(0, n, _VEC_SLICE // 2):
+                    m = min(_VEC_SLICE // 2, n - lo)
+                    arr[lo:lo + m] = dev.download(vec, 2 * m - 1, np.uint32,
+                                                  4 * (int(rec_start[r]) + strand + 2 * lo))[::2]
+                used = c_size_t(0)
+                rc = L.kman_format_vector(arr.ctypes.data_as(c_void_p), n, 1, None, 0, byref(used),
+                                          engine.host_threads())
+                if rc not in (N.KMAN_OK, N.KMAN_ECAP):
+                    raise RuntimeError("kman_format_vector failed (%d)" % rc)
+                buf = ctypes.create_string_buffer(max(1, used.value))
+                rc = L.kman_format_vector(arr.ctypes.data_as(c_void_p), n, 1, buf, used.value, byref(used),
+                                          engine.host_threads())
+                if rc != N.KMAN_OK:
+                    raise RuntimeError("kman_format_vector failed (%d)" % rc)
+                ref = name.decode("utf-8", "surrogateescape")
+                with gzip.open(os.path.join(dirpath, "%s___%s.gz" % (ref, "+-"[strand])), "wb") as OH:
+                    OH.write(b"# k=%d\n" % k)
+                    OH.write(buf.raw[:used.value])
+    finally:
+        if km is not None:
+            km.free()
+        for b in bufs:
+            b.free()
+        if vec is not None:
+            vec.free()
 
+
+_VEC_SLICE = 1 << 26  # u32 slots per host slice (256 MiB)
+
+
+def _vector_len(dev, vec, first: int, end: int) -> int:
+    """Length of one (record, strand) vector: its last nonzero slot + 1
+    (slots first, first + 2, .. < end), found from the back in bounded
+    slices; 0 when the record's strand received no count."""
+    n_slots = (end - first + 1) // 2
+    hi = n_slots
+    while hi > 0:
+        lo = max(0, hi - _VEC_SLICE // 2)
+        m = hi - lo
+        sl = dev.download(vec, 2 * m - 1, np.uint32, 4 * (first + 2 * lo))[::2]
+        nz = np.flatnonzero(sl)
+        if len(nz):
+            return lo + int(nz[-1]) + 1
+        hi = lo
+    return 0
 
 def format_sources(keys: np.ndarray, pos: np.ndarray, k: int, srcs, tagged: bool) -> bytes:
     """uniq rows whose pos point into one or several sources (FastaSource /
