@@ -2215,6 +2215,70 @@ void launch_extract_ex(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes,
                        epoch, ctx->d_err, 0u, nullptr, rtab);
 }
 
+// Pass 1b's width g, refitted from the pass-1 counts.  The plan takes g from
+// the largest bucket, and a genome's repeats inflate every bucket that holds
+// one (a satellite k-mer with 10^5 copies): g = 4 instead of 2 on the
+// GRCh38-shaped input, 2 M finish regions of 1.4 K items where per-region
+// costs dominate (16.6 us per region at 1.4 K items, 20 us at 3.8 K).  Here g
+// covers all but the largest 0.5 % of the (b, d) sub-buckets (the ones a
+// repeat fills, which overflow at any g and are redone by key range), never
+// above the plan's.  Pass 1 flagged overflowing sub-buckets per (b, d);
+// they are spread over their 2^g regions here.
+int refit_g(kman_ctx *ctx, RoundPlan &d, const uint32_t *c1, uint8_t *freg, uint32_t G) {
+    const uint64_t nbd = (uint64_t)d.nb * 512, gh = (uint64_t)G * d.H;
+    std::vector<uint32_t> hc(d.nsub);
+    std::vector<uint8_t> hf(nbd);
+    HIP_TRY(ctx, hipMemcpyAsync(hc.data(), c1, d.nsub * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(hf.data(), freg, nbd, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    uint32_t gmin = 1;
+    if (const char *e = getenv("KMAN_DROUND_MIN_G")) gmin = std::max<uint32_t>(gmin, std::min(9, atoi(e)));
+    std::vector<uint8_t> need(nbd);
+    std::vector<uint64_t> size(nbd);
+    for (uint64_t j = 0; j < nbd; j++) {
+        uint64_t t = 0;
+        for (uint64_t q = 0; q < gh; q++) t += hc[j * gh + q];
+        size[j] = t;
+        uint32_t g = gmin;
+        while (g < 9 && (t >> g) > 6144) g++;
+        need[j] = (uint8_t)g;
+    }
+    std::vector<uint64_t> ss(size);
+    const uint64_t qi = (uint64_t)(0.995 * (double)(nbd - 1));
+    std::nth_element(ss.begin(), ss.begin() + qi, ss.end());
+    std::vector<uint8_t> ns(need);
+    std::nth_element(ns.begin(), ns.begin() + qi, ns.end());
+    uint32_t g = std::max<uint32_t>(gmin, ns[qi]);
+    if (g < d.g) {
+        const uint64_t nreg = nbd << g;
+        const uint64_t e2 = ss[qi] >> g;
+        uint64_t C1 = std::min<uint64_t>(ceil_div(e2 + e2 / 2 + 512, 64) * 64, (uint64_t)FCAP);
+        C1 = std::max<uint64_t>(C1, d.C1);  // (never tighter than planned)
+        C1 = std::min<uint64_t>(C1, (uint64_t)FCAP);
+        const uint64_t off_c2 = nreg * C1 * 8;
+        if (off_c2 + ceil_div(nreg * 4 + 64, 64) * 64 <= d.b_bytes) {
+            d.g = g;
+            d.rest = d.K - B1 - 9 - g;
+            d.nreg = nreg;
+            d.C1 = C1;
+            d.off_c2 = off_c2;
+        }
+    }
+    // pass 1's (b, d) flags -> the regions they feed
+    bool any = false;
+    for (uint64_t j = 0; j < nbd; j++) any |= hf[j] != 0;
+    if (any) {
+        std::vector<uint8_t> fr(d.nreg, 0);
+        for (uint64_t j = 0; j < nbd; j++)
+            if (hf[j]) memset(&fr[j << d.g], 1, (size_t)1 << d.g);
+        HIP_TRY(ctx, hipMemcpyAsync(freg, fr.data(), d.nreg, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (fr leaves scope)
+    } else {
+        HIP_TRY(ctx, hipMemsetAsync(freg, 0, nbd, ctx->stream));
+    }
+    return KMAN_OK;
+}
+
 }  // namespace
 
 extern "C" int kman_dshard_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t flags, int mode) {
@@ -2349,13 +2413,17 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         pa.out = r1;
         pa.C1 = d.C1s;
         pa.cnt1 = c1;
-        pa.fail = freg;  // sub-region (b, d, src, h) -> regions ((b, d) << g) + *
+        pa.fail = freg;  // sub-region (b, d, src, h) -> flag (b, d) (spread over its 2^g regions below)
         pa.fail_div = G * d.H;
-        pa.fail_shift = d.g;
+        pa.fail_shift = 0;
         launch_pass(ctx, pa, counter, 0, nullptr);
         HIP_TRY(ctx, hipGetLastError());
     }
     KMAN_TRY(rg_check(ctx, "pass 1", c1, d.nsub));
+    if (d.g > 0) {
+        KMAN_TRY(refit_g(ctx, d, c1, freg, G));
+        c2 = (uint32_t *)(wb + d.off_c2);
+    }
     const char *dbg_env = getenv("KMAN_RG_DBG");  // finish timing ablations only (bits 1, 2)
     const uint32_t fdbg = dbg_env ? (uint32_t)atoi(dbg_env) & 3u : 0u;
     uint64_t *fst = nullptr;
