@@ -119,7 +119,13 @@ __global__ __launch_bounds__(ET) void extract_kernel(const uint8_t *__restrict__
             st_store(&status[tile], st_make(ST_INCL, epoch, tb + total));
         }
 #else
-        if (threadIdx.x < 64) {
+        if (pmap) {
+            // marked windows (a redo that sorts them next): places by one
+            // atomic per tile that has any, no look-back chain through the
+            // tiles that have none (`status` is the u64 cursor here)
+            if (threadIdx.x == 0)
+                lds_base = total ? (uint64_t)atomicAdd((unsigned long long *)status, (unsigned long long)total) : 0ull;
+        } else if (threadIdx.x < 64) {
             const uint64_t b = wave_lookback<0>(status, tile, total, epoch, err);
             if (threadIdx.x == 0) lds_base = b;
         }
@@ -310,12 +316,19 @@ int launch_extract(kman_ctx *ctx, const uint8_t *codes, uint64_t n_bases, int k,
     const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * EI);
     uint32_t epoch, *counter;
     KMAN_TRY(kman_lookback_begin(ctx, n_tiles, &epoch, &counter));
+    uint64_t *status = ctx->d_status;
+    if (pmap) {  // (the marked windows' cursor: extract_filtered reads it back)
+        void *scr;
+        KMAN_TRY(kman_scratch(ctx, 256, &scr));
+        HIP_TRY(ctx, hipMemsetAsync(scr, 0, 8, ctx->stream));
+        status = (uint64_t *)scr;
+    }
     auto fn = extract_kernel<EI, RC, CANON, P>;
     const int grid = kman_persistent_grid(ctx, (const void *)fn, ET, n_tiles);
     KTimer kt_(ctx, "extract");
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(ET), 0, ctx->stream, codes, n_bases, n_tiles, k, keys, pos,
-                       ctx->d_status, counter, epoch, ctx->d_err, hist, plan, klo, khi, cap, pmap, pshift, pval,
-                       ctx->d_mapbits, cshift, cexact);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(ET), 0, ctx->stream, codes, n_bases, n_tiles, k, keys, pos, status,
+                       counter, epoch, ctx->d_err, hist, plan, klo, khi, cap, pmap, pshift, pval, ctx->d_mapbits,
+                       cshift, cexact);
     HIP_TRY(ctx, hipGetLastError());
     return KMAN_OK;
 }
@@ -419,9 +432,19 @@ int extract_filtered(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bases, ui
         KMAN_TRY(dispatch_extract<uint64_t>(ctx, d_codes, n_bases, (int)k, flags, d_keys, (uint64_t *)d_pos, d_hist,
                                             plan, key_lo, key_hi, cap, pmap, pshift, pval, cshift, cexact));
     }
-    // the last tile's inclusive prefix is the number of k-mers written
-    const uint64_t n_tiles = ceil_div(n_bases, (uint64_t)ET * ((flags & KMAN_RC) && !(flags & KMAN_CANONICAL) ? 8 : 16));
-    KMAN_TRY(kman_lookback_total(ctx, n_tiles, n_kmers));
+    // the last tile's inclusive prefix is the number of k-mers written (a
+    // marked extraction: its cursor)
+    if (pmap) {
+        void *scr;
+        KMAN_TRY(kman_scratch(ctx, 256, &scr));
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small, scr, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        *n_kmers = ctx->h_small[0];
+    } else {
+        const uint64_t n_tiles =
+            ceil_div(n_bases, (uint64_t)ET * ((flags & KMAN_RC) && !(flags & KMAN_CANONICAL) ? 8 : 16));
+        KMAN_TRY(kman_lookback_total(ctx, n_tiles, n_kmers));
+    }
     if (*n_kmers > cap)
         return kman_fail(ctx, KMAN_ECAP, "key range holds %llu keys > capacity %llu", (unsigned long long)*n_kmers,
                          (unsigned long long)cap);
