@@ -1450,11 +1450,13 @@ void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t 
     }
     const char *e = getenv("KMAN_RG_PASS");
     const int shape = e ? atoi(e) : 5;
-    if (pa.bits <= 4 && shape >= 3) {
-        // a few digits (the multi-GPU pass 1b: 1-3 bits): block-wide or
-        // per-wave LDS atomics would all hit the same few counters, so rank
-        // by ballots (rg_pass<false>: per-wave counters, one update per
-        // distinct digit of a row)
+    // a few digits (pass 1b: 1-4 bits) rank by the same block-wide LDS
+    // atomics: config 4's shard 290.6 -> 277.4 ms per step, the skewed
+    // spectrum line's passes 3 ms faster, than ballots (rg_pass<false>:
+    // per-wave counters, one update per distinct digit of a row), which
+    // KMAN_RG_1B=0 keeps for A/B
+    static const char *e1b = getenv("KMAN_RG_1B");
+    if (pa.bits <= 4 && shape >= 3 && e1b && atoi(e1b) == 0) {
         // (KMAN_RG_SMALL=0: 512-thread blocks without write combining, for
         // A/B timing; pass 1b at world 1, ms: 8.7 vs 7.2 for the default)
         const char *e2 = getenv("KMAN_RG_SMALL");
