@@ -116,8 +116,15 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 // leaving two partial lines, and the look-back's predecessor is a neighbour.
 // Placement changes only speed: a tile waits only on earlier tickets of its
 // own partition, and a block leaves only when every partition is dealt out.
+// AT (with BR, not EX): no look-back -- a tile takes its place in region
+// (b, s) by one atomic add per digit on the region's cursor (cnt0[b * NS +
+// s], zeroed before the launch; it ends as the region's count).  A region's
+// items are then in no particular order, which nothing downstream needs: pass
+// 1 ranks unstably and the finish sorts every remaining key bit (uniq items
+// carry their window index, so equal keys are dropped or counted whatever
+// their order).  No tile waits on another tile.
 template <int EI, bool RC, bool ATOMIC, int CANON = 0, bool BR = false, bool EX = false, int NS = RS,
-          int XLB = LB, bool IL = false, int TPDX = 0, bool XG = false>
+          int XLB = LB, bool IL = false, int TPDX = 0, bool XG = false, bool AT = false>
 __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI == 8 ? 8 : 4)))) void rg_extract(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
                                                  uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
                                                  uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ cnt0,
@@ -140,6 +147,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     __shared__ uint32_t keep[EX ? RADIX / 32 : 1];
 
     static_assert(!XG || NS % 8 == 0, "XCD partitions of whole chains");
+    static_assert(!AT || (BR && !EX), "atomic cursors: block-wide ranks, padded regions");
     uint32_t cid;
     if (XG) {
         if (threadIdx.x == 0) {
@@ -239,6 +247,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
     uint64_t key[SI];
     uint32_t rank[SI];
+    uint32_t at_base = 0;  // (AT: this tile's first slot in region (d, sgi), thread d)
 #pragma unroll
     for (int i = 0; i < SI; i++) key[i] = ib + i * 64 < tcnt ? skeys[ib + i * 64] : 0;
 #define XDIGIT(x) ((uint32_t)(((x) & keymask) >> shift))
@@ -247,9 +256,17 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
 #pragma unroll
         for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&thist[XDIGIT(key[i])], 1u) : 0u;
         __syncthreads();
-        // (EX: a digit not kept this round has no chain: nothing published)
-        if (threadIdx.x < RADIX && KEPT(threadIdx.x))
+        if (AT) {
+            // the tile's place in each region, claimed now: the atomics'
+            // round trip overlaps the digit scan and the LDS scatter below
+            if (threadIdx.x < RADIX) {
+                const uint32_t c = thist[threadIdx.x];
+                at_base = c ? atomicAdd(cnt0 + threadIdx.x * NS + sgi, c) : 0u;
+            }
+        } else if (threadIdx.x < RADIX && KEPT(threadIdx.x)) {
+            // (EX: a digit not kept this round has no chain: nothing published)
             digit_publish(status + threadIdx.x, stile, first, thist[threadIdx.x], epoch);
+        }
     } else if (ATOMIC) {
 #pragma unroll
         for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&whist[w][XDIGIT(key[i])], 1u) : 0u;
@@ -294,7 +311,13 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
             skeys[lstart[d] + (BR ? 0u : whist[w][d]) + rank[i]] = key[i];
         }
     }
-    {
+    if (AT) {
+        if (threadIdx.x < RADIX) {
+            const uint32_t d = threadIdx.x;
+            gexcl[d] = at_base;
+            if ((uint64_t)at_base + thist[d] > C0) atomicOr(err, ERR_REGION);
+        }
+    } else {
         // TPD lanes per digit walk its chain (TPDX: an A/B override)
         constexpr uint32_t TPD = TPDX ? TPDX : (NT / RADIX >= 4 ? 4 : (NT / RADIX >= 2 ? 2 : 1));
         if (threadIdx.x < RADIX * TPD && KEPT(threadIdx.x / TPD)) {
@@ -598,6 +621,8 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
             for (int j = 0; j < SPL; j++) {
                 const uint32_t sg = (uint32_t)lane * SPL + j;
                 cq[j] = sg < nsg ? pa.seg_cnt[(uint64_t)b * nsg + sg] : 0u;
+                // (pass 0's atomic cursors run past a capacity that overflowed)
+                cq[j] = cq[j] < pa.stride ? cq[j] : (uint32_t)pa.stride;
                 acc += cq[j];
             }
             const uint32_t inc = wave_inclusive_scan(acc, SumU32());
@@ -611,7 +636,8 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
         } else {
             const uint32_t sgl = (uint32_t)lane;
             const uint64_t gi = (uint64_t)b * nsg + sgl;
-            const uint32_t c = sgl < nsg ? pa.seg_cnt[gi] : 0u;
+            uint32_t c = sgl < nsg ? pa.seg_cnt[gi] : 0u;
+            if (!pa.seg_base && c > pa.stride) c = (uint32_t)pa.stride;  // (an overflowed atomic cursor)
             const uint32_t inc = wave_inclusive_scan(c, SumU32());
             spre_l = inc - c;
             sbase_l = sgl < nsg ? (pa.seg_base ? pa.seg_base[gi] : gi * pa.stride) : 0ull;
@@ -1599,6 +1625,22 @@ void launch_extract_ns(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes,
     // with two lanes per digit (KMAN_RG_IL=0, kept for A/B)
     static const bool contiguous = getenv("KMAN_RG_IL") && atoi(getenv("KMAN_RG_IL")) == 0;
     static const bool xg = xcd_tickets();
+    // atomic region cursors instead of the look-back (KMAN_RG_AT=0: the
+    // look-back chains, A/B)
+    static const bool at = !(getenv("KMAN_RG_AT") && atoi(getenv("KMAN_RG_AT")) == 0);
+    if (at && !contiguous && XLB == 1) {
+        if (!n_launch && xg && NS % 8 == 0)
+            hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS, 1, true, 1, true, true>),
+                               dim3(p.n_tiles0), dim3(RT), 0, ctx->stream, codes, n_bases, (int)k, p.Q, r0, p.C0,
+                               p.seg_tiles, p.n_tiles0, c0, ctx->d_status, ctx->d_xcounters + 8 * (epoch & 63u), epoch,
+                               ctx->d_err, dbg, stp, nullptr);
+        else
+            hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS, 1, true, 1, false, true>),
+                               dim3(n_launch ? n_launch : p.n_tiles0), dim3(RT), 0, ctx->stream, codes, n_bases,
+                               (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch,
+                               ctx->d_err, dbg, stp, nullptr);
+        return;
+    }
     if (!n_launch && !contiguous && xg && NS % 8 == 0) {  // tickets per XCD partition (one launch, whole stream)
         hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS, XLB, true, 1, true>), dim3(p.n_tiles0),
                            dim3(RT), 0, ctx->stream, codes, n_bases, (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0,
