@@ -228,34 +228,38 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
             }
         }
     }
-    uint32_t tcnt;
-    const uint32_t off = block_exclusive_scan<NT>((uint32_t)(__popc(vf) + __popc(vr)), SumU32(), 0u, lds_scan, &tcnt);
-    {
-        uint32_t o = off;
-#pragma unroll
-        for (int j = 0; j < EI; j++) {
-            // the tile-local (window << 1 | strand) above the key bits: only
-            // uniq items carry it (Q > 0, k <= 25); count items are the key
-            const uint64_t tag = Q ? (uint64_t)((w0 + j) << 1) << kb : 0ull;
-            if ((vf >> j) & 1u) skeys[o++] = kf[j] | tag;
-            if (RC && ((vr >> j) & 1u)) skeys[o++] = kr[j] | tag | (Q ? 1ull << kb : 0ull);
-        }
-    }
-    __syncthreads();
-    RSTAMP(tile, 2);
-
+    uint32_t tcnt = 0;
     const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
     uint64_t key[SI];
     uint32_t rank[SI];
+    uint32_t vmask = 0;    // (BR: item i of this thread is valid)
     uint32_t at_base = 0;  // (AT: this tile's first slot in region (d, sgi), thread d)
-#pragma unroll
-    for (int i = 0; i < SI; i++) key[i] = ib + i * 64 < tcnt ? skeys[ib + i * 64] : 0;
 #define XDIGIT(x) ((uint32_t)(((x) & keymask) >> shift))
 #define KEPT(d) (!EX || ((keep[(d) >> 5] >> ((d) & 31)) & 1u))
-    if (BR) {
+    // the tile-local (window << 1 | strand) rides above the key bits: only
+    // uniq items carry it (Q > 0, k <= 25); count items are the key
+    auto tagged = [&](int j, bool strand) -> uint64_t {
+        return Q ? (uint64_t)(((w0 + j) << 1) | (uint32_t)strand) << kb : 0ull;
+    };
+    if constexpr (BR) {
+        // ranked straight from the roll's registers (item i = window i, or
+        // 2j / 2j + 1 = window j's two strands with RC): the block-wide rank is
+        // unstable anyway, so no compaction pass through LDS is needed
 #pragma unroll
-        for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&thist[XDIGIT(key[i])], 1u) : 0u;
-        __syncthreads();
+        for (int j = 0; j < EI; j++) {
+            if (RC) {
+                key[2 * j] = kf[j] | tagged(j, false);
+                key[2 * j + 1] = kr[j] | tagged(j, true);
+                vmask |= (((vf >> j) & 1u) << (2 * j)) | (((vr >> j) & 1u) << (2 * j + 1));
+            } else {
+                key[j] = kf[j] | tagged(j, false);
+            }
+        }
+        if (!RC) vmask = vf;
+#pragma unroll
+        for (int i = 0; i < SI; i++) rank[i] = (vmask >> i) & 1u ? atomicAdd(&thist[XDIGIT(key[i])], 1u) : 0u;
+        __syncthreads();  // (also: every roll read of the staged codes before the scatter below)
+        RSTAMP(tile, 2);
         if (AT) {
             // the tile's place in each region, claimed now: the atomics'
             // round trip overlaps the digit scan and the LDS scatter below
@@ -267,27 +271,43 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
             // (EX: a digit not kept this round has no chain: nothing published)
             digit_publish(status + threadIdx.x, stile, first, thist[threadIdx.x], epoch);
         }
-    } else if (ATOMIC) {
-#pragma unroll
-        for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&whist[w][XDIGIT(key[i])], 1u) : 0u;
-        __syncthreads();
-        if (threadIdx.x < RADIX) {
-            uint32_t c = 0;
-#pragma unroll
-            for (int ww = 0; ww < NWAVE; ww++) c += whist[ww][threadIdx.x];
-            thist[threadIdx.x] = c;
-            digit_publish(status + threadIdx.x, stile, first, c, epoch);
-        }
     } else {
+        const uint32_t off =
+            block_exclusive_scan<NT>((uint32_t)(__popc(vf) + __popc(vr)), SumU32(), 0u, lds_scan, &tcnt);
+        {
+            uint32_t o = off;
 #pragma unroll
-        for (int i = 0; i < SI; i++)
-            if (ib + i * 64 < tcnt) atomicAdd(&thist[XDIGIT(key[i])], 1u);
+            for (int j = 0; j < EI; j++) {
+                if ((vf >> j) & 1u) skeys[o++] = kf[j] | tagged(j, false);
+                if (RC && ((vr >> j) & 1u)) skeys[o++] = kr[j] | tagged(j, true);
+            }
+        }
         __syncthreads();
-        if (threadIdx.x < RADIX) digit_publish(status + threadIdx.x, stile, first, thist[threadIdx.x], epoch);
+        RSTAMP(tile, 2);
 #pragma unroll
-        for (int i = 0; i < SI; i++) rank[i] = ballot_rank(whist[w], XDIGIT(key[i]), ib + i * 64 < tcnt, B1);
+        for (int i = 0; i < SI; i++) key[i] = ib + i * 64 < tcnt ? skeys[ib + i * 64] : 0;
+        if (ATOMIC) {
+#pragma unroll
+            for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&whist[w][XDIGIT(key[i])], 1u) : 0u;
+            __syncthreads();
+            if (threadIdx.x < RADIX) {
+                uint32_t c = 0;
+#pragma unroll
+                for (int ww = 0; ww < NWAVE; ww++) c += whist[ww][threadIdx.x];
+                thist[threadIdx.x] = c;
+                digit_publish(status + threadIdx.x, stile, first, c, epoch);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < SI; i++)
+                if (ib + i * 64 < tcnt) atomicAdd(&thist[XDIGIT(key[i])], 1u);
+            __syncthreads();
+            if (threadIdx.x < RADIX) digit_publish(status + threadIdx.x, stile, first, thist[threadIdx.x], epoch);
+#pragma unroll
+            for (int i = 0; i < SI; i++) rank[i] = ballot_rank(whist[w], XDIGIT(key[i]), ib + i * 64 < tcnt, B1);
+        }
+        __syncthreads();
     }
-    __syncthreads();
     RSTAMP(tile, 3);
     const uint32_t d0 = threadIdx.x;
     uint32_t tot = 0;
@@ -301,12 +321,14 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
             tot += c;
         }
     }
-    const uint32_t ls = block_exclusive_scan<NT>(tot, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
+    uint32_t btot;
+    const uint32_t ls = block_exclusive_scan<NT>(tot, SumU32(), 0u, lds_scan, &btot);
+    if (BR) tcnt = btot;
     if (d0 < RADIX) lstart[d0] = ls;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < SI; i++) {
-        if (ib + i * 64 < tcnt) {
+        if (BR ? ((vmask >> i) & 1u) : ib + i * 64 < tcnt) {
             const uint32_t d = XDIGIT(key[i]);
             skeys[lstart[d] + (BR ? 0u : whist[w][d]) + rank[i]] = key[i];
         }
@@ -1001,7 +1023,6 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
     static_assert(!NARROW || (MODE == RG_COUNT && !DB && !PF), "narrow items: count mode, one region per block");
     __shared__ __attribute__((aligned(16))) T sb[DB ? 2 : 1][SCAP];
     __shared__ uint32_t wh[NW_][FWORD];  // per-wave digit counters, u16 pairs
-    __shared__ uint32_t dstart[FRAD];
     __shared__ uint32_t lds_scan[NW_];
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_out;
@@ -1107,6 +1128,9 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
     // to a word (a wave ranks <= 64 * FIPT items), same-word LDS atomics of one
     // wave return in lane order (probed: ATOMIC), else ballot match-any.
     // (dbg & 1: timing ablation only, no sort passes)
+#ifdef KMAN_RG_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);  // (diagnostic build: phase 1 = the wait for the region's items)
+#endif
     RSTAMP(r, 1);
 #ifdef KMAN_RG_STAMPS
     if (stp && t == 0) stp[(uint64_t)r * 8 + 7] = m;  // (the region's items, beside its phase stamps)
@@ -1144,29 +1168,35 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
             }
         }
         __syncthreads();
-        // thread t < FWORD: digits 2t, 2t+1 -> per-wave exclusive offsets (in
-        // place) and their totals; block scan of the totals -> digit starts
-        uint32_t tlo = 0, thi = 0;
+        // thread t < FWORD: digits 2t, 2t+1 -> their totals, block scan of the
+        // totals -> digit starts, then each wave's first slot per digit
+        // (digit start + the earlier waves' counts, < 2^16) in place of its
+        // counters, so the scatter reads one word per item
+        uint32_t tlo = 0, thi = 0, cw[NW_];
         if (t < FWORD) {
 #pragma unroll
             for (int ww = 0; ww < NW_; ww++) {
-                const uint32_t c = wh[ww][t];
-                wh[ww][t] = tlo | (thi << 16);
-                tlo += c & 0xffffu;
-                thi += c >> 16;
+                cw[ww] = wh[ww][t];
+                tlo += cw[ww] & 0xffffu;
+                thi += cw[ww] >> 16;
             }
         }
         const uint32_t ls = block_exclusive_scan<NT>(tlo + thi, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
         if (t < FWORD) {
-            dstart[2 * t] = ls;
-            dstart[2 * t + 1] = ls + tlo;
+            uint32_t plo = ls, phi = ls + tlo;
+#pragma unroll
+            for (int ww = 0; ww < NW_; ww++) {
+                wh[ww][t] = plo | (phi << 16);
+                plo += cw[ww] & 0xffffu;
+                phi += cw[ww] >> 16;
+            }
         }
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < IPT; i++) {
             if (pw + i * 64 < m) {
                 const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
-                s[dstart[d] + ((wh[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rk[i]] = x[i];
+                s[((wh[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rk[i]] = x[i];
             }
         }
         __syncthreads();
