@@ -28,6 +28,7 @@ struct kman_ctx {
     uint32_t *d_counters = nullptr; // one dynamic-tile counter per epoch (64)
     uint32_t *d_mapbits = nullptr;   // kman_extract_marked's coarse bitmap (2048 words)
     uint32_t *d_xcounters = nullptr; // eight per epoch: one tile counter per XCD partition (rg_extract XG)
+    uint32_t *d_cursors = nullptr;   // 256 x 64 region cursors of the shard extraction (rg_extract EX + AT)
     uint32_t *d_err = nullptr;      // device-side error word (spin timeouts)
     uint32_t epoch = 63;            // last epoch handed out; wraps 63 -> 1 with a reset
     // small pinned host area for results

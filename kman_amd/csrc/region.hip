@@ -36,6 +36,7 @@
 #include "kmer.h"
 #include "onesweep.h"
 
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 
@@ -116,9 +117,10 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 // leaving two partial lines, and the look-back's predecessor is a neighbour.
 // Placement changes only speed: a tile waits only on earlier tickets of its
 // own partition, and a block leaves only when every partition is dealt out.
-// AT (with BR, not EX): no look-back -- a tile takes its place in region
-// (b, s) by one atomic add per digit on the region's cursor (cnt0[b * NS +
-// s], zeroed before the launch; it ends as the region's count).  A region's
+// AT (with BR): no look-back -- a tile takes its place in region (b, s) by
+// one atomic add per digit on the region's cursor (cnt0[b * NS + s], zeroed
+// before the launch; it ends as the region's count; EX: the cursors are
+// `status` as u32, zeroed before the launch, and cnt0 keeps the exact sizes).  A region's
 // items are then in no particular order, which nothing downstream needs: pass
 // 1 ranks unstably and the finish sorts every remaining key bit (uniq items
 // carry their window index, so equal keys are dropped or counted whatever
@@ -147,7 +149,8 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     __shared__ uint32_t keep[EX ? RADIX / 32 : 1];
 
     static_assert(!XG || NS % 8 == 0, "XCD partitions of whole chains");
-    static_assert(!AT || (BR && !EX), "atomic cursors: block-wide ranks, padded regions");
+    static_assert(!AT || BR, "atomic cursors: block-wide ranks");
+    uint32_t *const cursor = EX ? reinterpret_cast<uint32_t *>(status) : cnt0;  // (AT)
     uint32_t cid;
     if (XG) {
         if (threadIdx.x == 0) {
@@ -265,7 +268,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
             // round trip overlaps the digit scan and the LDS scatter below
             if (threadIdx.x < RADIX) {
                 const uint32_t c = thist[threadIdx.x];
-                at_base = c ? atomicAdd(cnt0 + threadIdx.x * NS + sgi, c) : 0u;
+                at_base = c ? atomicAdd(cursor + threadIdx.x * NS + sgi, c) : 0u;
             }
         } else if (threadIdx.x < RADIX && KEPT(threadIdx.x)) {
             // (EX: a digit not kept this round has no chain: nothing published)
@@ -336,8 +339,16 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     if (AT) {
         if (threadIdx.x < RADIX) {
             const uint32_t d = threadIdx.x;
-            gexcl[d] = at_base;
-            if ((uint64_t)at_base + thist[d] > C0) atomicOr(err, ERR_REGION);
+            const uint64_t incl = (uint64_t)at_base + thist[d];
+            if (EX) {  // (digits not kept this round have no items)
+                const uint64_t rb = rtab[(uint64_t)d * RS + sgi];
+                const bool over = thist[d] && incl > cnt0[d * RS + sgi];
+                if (over && rb != ~0ull) atomicOr(err, ERR_REGION);  // (the input changed under the plan)
+                gexcl[d] = rb == ~0ull || over ? ~0ull : rb + at_base;
+            } else {
+                gexcl[d] = at_base;
+                if (incl > C0) atomicOr(err, ERR_REGION);
+            }
         }
     } else {
         // TPD lanes per digit walk its chain (TPDX: an A/B override)
@@ -594,7 +605,11 @@ struct PassArgs {
 // does not need -- it sorts every remaining key bit and compares keys only).
 // NSG > 64 (pass 0 with 128 / 256 chains, or the owned-chain pass 0's S <=
 // NSG segments): each lane holds NSG / 64 of the segment prefixes.
-template <bool ATOMIC, int NT, int SI, bool PF, bool WC = false, bool BR = false, int NSG = 64>
+// EPF (KMAN_RG_PASS=8, A/B only): the next tile's loads issued as soon as this
+// tile's keys are in LDS, before its stores, so that waiting for them does not
+// wait for the stores' write acknowledgements too (vmcnt completes in issue
+// order) -- measured slower: 3.80 vs 3.43 ms
+template <bool ATOMIC, int NT, int SI, bool PF, bool WC = false, bool BR = false, int NSG = 64, bool EPF = false>
 __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
                                                  uint32_t *__restrict__ err, uint32_t dbg,
                                                  uint64_t *__restrict__ stp) {
@@ -869,6 +884,7 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
             }  // !BR
             __syncthreads();
             RSTAMP(r, 1);
+            if (EPF && r + 1 < rb) load_tile(r + 1);
             if (WC) {
                 // a digit whose partial line completes in this tile: its
                 // pending items go out first, 16 lanes per digit (one line
@@ -915,7 +931,7 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                 // the next tile's loads behind the stores (issued before the
                 // store phase instead, they overlap it and the pass slows
                 // down: 6.2 vs 4.9 ms)
-                if (PF && r + 1 < rb) load_tile(r + 1);
+                if (PF && !EPF && r + 1 < rb) load_tile(r + 1);
             } else if (!PF) {
                 // one store per LDS read: the compiler reuses one register
                 // pair and waits for each store before the next read, which
@@ -1463,12 +1479,12 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     return KMAN_OK;
 }
 
-template <int NT, int SI, bool PF, bool WC = false, bool BR = false>
+template <int NT, int SI, bool PF, bool WC = false, bool BR = false, bool EPF = false>
 void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
     if constexpr (BR) {  // no ordered LDS atomics needed
-        const void *fn = (const void *)rg_pass<true, NT, SI, PF, WC, BR>;
+        const void *fn = (const void *)rg_pass<true, NT, SI, PF, WC, BR, 64, EPF>;
         const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, NT, (uint64_t)pa.nbk * pa.H);
-        hipLaunchKernelGGL((rg_pass<true, NT, SI, PF, WC, BR>), dim3(grid), dim3(NT), 0, ctx->stream, pa, counter,
+        hipLaunchKernelGGL((rg_pass<true, NT, SI, PF, WC, BR, 64, EPF>), dim3(grid), dim3(NT), 0, ctx->stream, pa, counter,
                            ctx->d_err, dbg, stp);
     } else {
     const void *fn = ctx->lds_atomic_ordered ? (const void *)rg_pass<true, NT, SI, PF, WC>
@@ -1530,6 +1546,7 @@ void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t 
         return;
     }
     if (shape == 5) launch_pass_as<1024, 8, true, true, true>(ctx, pa, counter, dbg, stp);
+    else if (shape == 8) launch_pass_as<1024, 8, true, true, true, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 7) launch_pass_as<1024, 10, true, true, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 6) launch_pass_as<RT, RSI, false, false, true>(ctx, pa, counter, dbg, stp);
     else if (shape == 4) launch_pass_as<1024, 8, true, true>(ctx, pa, counter, dbg, stp);
@@ -2187,6 +2204,18 @@ struct RoundPlan {
     uint64_t off_c1, off_tab, off_fail, a_bytes, off_c2, b_bytes;
 };
 
+// Capacity of a region that expects e items: a fixed 1.5 x e (KMAN_DROUND_PAD=0,
+// A/B) or e + max(e / 8, 8 sd of a Poisson fill) -- the round path's arenas
+// are most of a rank's HBM, and at config 4's size (12.5 G k-mers per rank)
+// the 1.5 x slack cost one key round (a re-read and re-roll of the whole
+// shard).  A region that overflows anyway (a repeat) is redone by key range.
+uint64_t round_cap(uint64_t e, uint64_t extra) {
+    static const bool old = getenv("KMAN_DROUND_PAD") && atoi(getenv("KMAN_DROUND_PAD")) == 0;
+    if (old) return ceil_div(e + e / 2 + extra, 64) * 64;
+    const uint64_t sd8 = (uint64_t)(8.0 * sqrt((double)e)) + 1;
+    return ceil_div(e + (e / 8 > sd8 ? e / 8 : sd8) + extra, 64) * 64;
+}
+
 // counts[src * nb + j] = items of bucket b_lo + j from rank src
 int make_rplan(uint32_t k, uint32_t flags, int mode, uint32_t world, uint64_t n_bases_q, uint32_t nb,
                const uint64_t *counts, RoundPlan *rp) {
@@ -2216,8 +2245,22 @@ int make_rplan(uint32_t k, uint32_t flags, int mode, uint32_t world, uint64_t n_
     // pass 1: H block-owned chains per (bucket, source), enough chains to
     // fill the CUs (a round of few buckets on few ranks has few chains);
     // pass 1b concatenates the G * H sub-regions of a (b, d): at most 64
-    d.H = 2;
-    while ((uint64_t)nb * world * d.H < 256 && world * d.H * 2 <= 64) d.H *= 2;
+    // H: the fewest chains with the shortest makespan on the 256 CUs (one
+    // 1024-thread pass block each): ceil(nb G H / 256) / H bucket-chunks per
+    // CU -- 85 buckets take H = 3 (255 chains), not 4 (340: a second wave of
+    // 84 chains on 84 CUs, pass 1 19.7 vs 10.1 ms per config-4 round)
+    {
+        const uint64_t ch1 = (uint64_t)nb * world;
+        d.H = 2;
+        double best = 1e30;
+        for (uint32_t h = 2; h <= 16 && world * h <= 64; h++) {
+            const double ms = (double)ceil_div(ch1 * h, 256) / h;
+            if (ms < best * 0.95) {  // (more chains only for a clear gain)
+                best = ms;
+                d.H = h;
+            }
+        }
+    }
     // pass 1b bits g: until a final region expects <= 6144 items (the LDS
     // finish holds FCAP = 8704).  g = 0 (no pass 1b, the finish reads the
     // pass-1 sub-regions) when one rank's 9-bit regions already fit: with one
@@ -2236,10 +2279,10 @@ int make_rplan(uint32_t k, uint32_t flags, int mode, uint32_t world, uint64_t n_
     d.g = g;
     d.rest = d.K - B1 - 9 - g;
     const uint64_t e1 = maxsb / (512ull * d.H);
-    d.C1s = ceil_div(e1 + e1 / 2 + 256, 64) * 64;
+    d.C1s = round_cap(e1, 256);
     if ((uint64_t)512 * world * d.H * d.C1s >= (1ull << 31)) return KMAN_EFALLBACK;  // (32-bit WC offsets)
     const uint64_t e2 = (maxb >> 9) >> g;
-    const uint64_t c2 = ceil_div(e2 + e2 / 2 + 512, 64) * 64;
+    const uint64_t c2 = round_cap(e2, 512);
     d.C1 = c2 < (uint64_t)FCAP ? c2 : (uint64_t)FCAP;
     d.nsub = (uint64_t)nb * 512 * world * d.H;
     d.nreg = (uint64_t)nb * 512 << g;
@@ -2278,6 +2321,16 @@ template <int EI, bool RC, int CANON>
 void launch_extract_ex(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                        uint64_t *out, uint32_t *cnt, const uint64_t *rtab, uint32_t epoch, uint32_t *counter) {
     const uint32_t grid = RS * p.seg_tiles;
+    // atomic region cursors instead of the look-back chains (KMAN_RG_AT=0: A/B)
+    static const bool at = !(getenv("KMAN_RG_AT") && atoi(getenv("KMAN_RG_AT")) == 0);
+    if (at && xcd_tickets()) {
+        (void)hipMemsetAsync(ctx->d_cursors, 0, (size_t)RADIX * RS * 4, ctx->stream);  // (errors: the caller's hipGetLastError)
+        hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, true, RS, 1, false, 0, true, true>), dim3(grid),
+                           dim3(RT), 0, ctx->stream, codes, n_bases, (int)k, p.Q, out, (uint64_t)0, p.seg_tiles,
+                           p.n_tiles0, cnt, (uint64_t *)ctx->d_cursors, ctx->d_xcounters + 8 * (epoch & 63u), epoch,
+                           ctx->d_err, 0u, nullptr, rtab);
+        return;
+    }
     if (xcd_tickets()) {
         hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, true, RS, 1, false, 0, true>), dim3(grid), dim3(RT), 0,
                            ctx->stream, codes, n_bases, (int)k, p.Q, out, (uint64_t)0, p.seg_tiles, p.n_tiles0, cnt,
@@ -2326,7 +2379,7 @@ int refit_g(kman_ctx *ctx, RoundPlan &d, const uint32_t *c1, uint8_t *freg, uint
     if (g < d.g) {
         const uint64_t nreg = nbd << g;
         const uint64_t e2 = ss[qi] >> g;
-        uint64_t C1 = std::min<uint64_t>(ceil_div(e2 + e2 / 2 + 512, 64) * 64, (uint64_t)FCAP);
+        uint64_t C1 = std::min<uint64_t>(round_cap(e2, 512), (uint64_t)FCAP);
         C1 = std::max<uint64_t>(C1, d.C1);  // (never tighter than planned)
         C1 = std::min<uint64_t>(C1, (uint64_t)FCAP);
         const uint64_t off_c2 = nreg * C1 * 8;

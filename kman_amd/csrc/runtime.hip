@@ -248,6 +248,7 @@ int kman_create(int device, kman_ctx **out) {
     if ((e = hipMemset(ctx->d_counters, 0, 64 * sizeof(uint32_t) + 256)) != hipSuccess) return bail(e, "hipMemset");
     if ((e = hipMalloc(&ctx->d_xcounters, 64 * 8 * sizeof(uint32_t))) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMemset(ctx->d_xcounters, 0, 64 * 8 * sizeof(uint32_t))) != hipSuccess) return bail(e, "hipMemset");
+    if ((e = hipMalloc(&ctx->d_cursors, 256 * 64 * sizeof(uint32_t))) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipHostMalloc(&ctx->h_small, 4096, hipHostMallocDefault)) != hipSuccess) return bail(e, "hipHostMalloc");
     const char *force = getenv("KMAN_RANK");  // "ballot" forces the probe-free ranking
     ctx->lds_atomic_ordered = !(force && strcmp(force, "ballot") == 0) && probe_lds_order(ctx);
@@ -267,6 +268,7 @@ void kman_destroy(kman_ctx *ctx) {
     if (ctx->d_aux) (void)hipFree(ctx->d_aux);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->d_xcounters) (void)hipFree(ctx->d_xcounters);
+    if (ctx->d_cursors) (void)hipFree(ctx->d_cursors);
     if (ctx->d_mapbits) (void)hipFree(ctx->d_mapbits);
     if (ctx->h_small) (void)hipHostFree(ctx->h_small);
     if (ctx->copy_stream) {
