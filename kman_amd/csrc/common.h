@@ -243,6 +243,29 @@ KMAN_DEV T block_exclusive_scan(T v, Op op, T identity, T *lds, T *total) {
     return res;
 }
 
+// The same scan with ONE barrier: each wave's total to lds[w], a barrier,
+// then every thread folds the earlier waves' totals itself (NW broadcast LDS
+// reads).  The caller must order this scan's reads of `lds` before the next
+// write of it (a barrier between two scans on one lds array).
+template <int NT, typename T, typename Op>
+KMAN_DEV T block_exclusive_scan1(T v, Op op, T identity, T *lds, T *total) {
+    constexpr int NW = NT / 64;
+    const int lane = lane_id();
+    const int w = threadIdx.x >> 6;
+    const T inc = wave_inclusive_scan(v, op, identity);
+    if (lane == 63) lds[w] = inc;
+    __syncthreads();
+    T pre = identity, all = identity;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        const T x = lds[i];
+        if (i < w) pre = op(pre, x);
+        all = op(all, x);
+    }
+    if (total) *total = all;
+    return op(pre, wave_shr1(inc, identity));
+}
+
 struct SumU64 {
     KMAN_DEV uint64_t operator()(uint64_t a, uint64_t b) const { return a + b; }
 };

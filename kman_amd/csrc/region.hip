@@ -325,7 +325,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
         }
     }
     uint32_t btot;
-    const uint32_t ls = block_exclusive_scan<NT>(tot, SumU32(), 0u, lds_scan, &btot);
+    const uint32_t ls = block_exclusive_scan1<NT>(tot, SumU32(), 0u, lds_scan, &btot);
     if (BR) tcnt = btot;
     if (d0 < RADIX) lstart[d0] = ls;
     __syncthreads();
@@ -803,8 +803,8 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                 for (int i = 0; i < SI; i++)
                     rank[i] = ib + i * 64 < n ? atomicAdd(&thist[PDIGIT(key[i])], 1u) : 0u;
                 __syncthreads();
-                const uint32_t ls = block_exclusive_scan<NT>(threadIdx.x < R1 ? thist[threadIdx.x] : 0u, SumU32(), 0u,
-                                                             lds_scan, (uint32_t *)nullptr);
+                const uint32_t ls = block_exclusive_scan1<NT>(threadIdx.x < R1 ? thist[threadIdx.x] : 0u, SumU32(),
+                                                              0u, lds_scan, (uint32_t *)nullptr);
                 if (threadIdx.x < R1) lstart[threadIdx.x] = ls;
                 __syncthreads();
 #pragma unroll
@@ -1039,7 +1039,7 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
     static_assert(!NARROW || (MODE == RG_COUNT && !DB && !PF), "narrow items: count mode, one region per block");
     __shared__ __attribute__((aligned(16))) T sb[DB ? 2 : 1][SCAP];
     __shared__ uint32_t wh[NW_][FWORD];  // per-wave digit counters, u16 pairs
-    __shared__ uint32_t lds_scan[NW_];
+    __shared__ uint32_t lds_scan[NW_], lds_scan2[NW_];
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_out;
     uint32_t cur = 0;
@@ -1061,7 +1061,10 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
 #pragma unroll
         for (int i = 0; i < IPT; i++) {
             const uint32_t p = pw + i * 64;
-            v[i] = p < mm ? (T)src[p < a0 ? p : p + skip] : (T)0;
+            // (dbg & 8: timing ablation only -- synthetic items, no HBM reads)
+            v[i] = p < mm ? ((dbg & 8) ? (T)((uint64_t)(rr * 8704u + p) * 0x9E3779B97F4A7C15ull)
+                                       : (T)src[p < a0 ? p : p + skip])
+                          : (T)0;
         }
     };
     // DB: region rr's items into an LDS buffer in 16-byte chunks, one per
@@ -1197,7 +1200,7 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
                 thi += cw[ww] >> 16;
             }
         }
-        const uint32_t ls = block_exclusive_scan<NT>(tlo + thi, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
+        const uint32_t ls = block_exclusive_scan1<NT>(tlo + thi, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
         if (t < FWORD) {
             uint32_t plo = ls, phi = ls + tlo;
 #pragma unroll
@@ -1263,16 +1266,20 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
     } else {
         emit = tails;
         const uint32_t lh = heads ? q0 + (31 - __clz(heads)) + 1 : 0u;
-        lh_before = block_exclusive_scan<NT>(
-            lh, [](uint32_t a, uint32_t b) { return a > b ? a : b; }, 0u, lds_scan, (uint32_t *)nullptr);
+        lh_before = block_exclusive_scan1<NT>(
+            lh, [](uint32_t a, uint32_t b) { return a > b ? a : b; }, 0u, lds_scan2, (uint32_t *)nullptr);
     }
     const uint32_t ne = (uint32_t)__popc(emit);
     uint32_t total;
-    const uint32_t off = block_exclusive_scan<NT>(ne, SumU32(), 0u, lds_scan, &total);
+    // (its barrier orders every read of s above before the staging writes below)
+    const uint32_t off = block_exclusive_scan1<NT>(ne, SumU32(), 0u, lds_scan, &total);
     // (the scan's barriers ordered every read of s above before the writes below)
     RSTAMP(r, 3);
     if (w == 0) {
-        const uint64_t ob = wave_lookback<0>(status, r, total, epoch, err);
+        // (dbg & 4: timing ablation only -- regions placed by one atomic
+        // cursor in completion order, no look-back: rows unsorted across regions)
+        const uint64_t ob = (dbg & 4) ? (lane == 0 ? atomicAdd((unsigned long long *)(status + nreg), (unsigned long long)total) : 0ull)
+                                      : wave_lookback<0>(status, r, total, epoch, err);
         if (lane == 0) s_out = ob;
     }
     // the emitted rows compacted in LDS as one word each: the item itself
@@ -1626,7 +1633,8 @@ void launch_finish(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ov
 int run_finish(kman_ctx *ctx, const FinishArgs &f, int mode, uint64_t *okeys, void *ovals, uint32_t oval_bytes,
                uint32_t dbg, uint64_t *stp) {
     uint32_t epoch, *counter;
-    KMAN_TRY(kman_lookback_begin(ctx, f.nreg, &epoch, &counter));
+    KMAN_TRY(kman_lookback_begin(ctx, f.nreg + 1, &epoch, &counter));
+    if (dbg & 4) HIP_TRY(ctx, hipMemsetAsync(ctx->d_status + f.nreg, 0, 8, ctx->stream));  // (the ablation's cursor)
     KTimer kt_(ctx, "region_finish");
     if (mode == KMAN_FINISH_UNIQ) {
         if (oval_bytes == 4) launch_finish<RG_UNIQ, uint32_t>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
@@ -1944,7 +1952,11 @@ int groups_tail(kman_ctx *ctx, const GroupsCall &g, int mode, uint64_t *d_okeys,
         if (e == ERR_REGION) return KMAN_EFALLBACK;  // a region overflowed: outputs invalid
         return kman_fail(ctx, KMAN_ETIMEOUT, "device look-back wait exceeded its bound (code %u)", e);
     }
-    const uint64_t wd = h[4];
+    uint64_t wd = h[4];
+    if (dbg & 4) {  // (the unordered-output timing ablation: the total is its cursor)
+        HIP_TRY(ctx, hipMemcpy(&wd, ctx->d_status + g.nreg, 8, hipMemcpyDeviceToHost));
+        wd = ((uint64_t)ST_INCL << 62) | ((uint64_t)ctx->epoch << 56) | wd;
+    }
     if (((wd >> 56) & 63u) != ctx->epoch || (wd >> 62) != ST_INCL)
         return kman_fail(ctx, KMAN_EHIP, "region output total not published");
     uint64_t nk = 0;

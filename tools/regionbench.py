@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """Stage timings of the region path (kman_groups) with timing ablations
 (KMAN_RG_DBG, region.hip): 1 = finish without its LDS sort passes, 2 = finish
-without output writes, 16 = rg_pass without look-back, 256 = rg_extract
+without output writes, 4 = finish without look-back (regions placed in
+completion order), 8 = finish on synthetic items (no HBM reads), 16 = rg_pass
+without look-back, 256 = rg_extract
 without look-back.  Results of ablated
 runs are wrong by construction; only their timings are read."""
 import os
