@@ -1438,13 +1438,14 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
         p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, s);
         p.S = (uint32_t)ceil_div(p.n_tiles0, p.seg_tiles);
     } else {
-        // windows per thread: 12 (6 with -r: two items per window) makes
-        // 6144-item tiles, 53 KiB of LDS, three blocks per CU: 3.92 ms vs 4.77
-        // with the 16-window tiles (two blocks per CU) and 4.63 with 8
-        // (four blocks, but twice the tiles and look-back steps).
-        // KMAN_RG_EI=16 / 8 select those for A/B timing.
+        // windows per thread: 16 (8 with -r: two items per window) makes
+        // 8192-item tiles, 69 KiB of LDS, two blocks per CU.  With the
+        // look-back chains, 12 (6144-item tiles, three blocks per CU) was
+        // faster (3.92 vs 4.77 ms); with the atomic region cursors a tile waits
+        // on nothing and the longer digit runs win: 3.27 vs 3.35 ms (8, four
+        // blocks per CU: 3.83).  KMAN_RG_EI=12 / 8 select those for A/B.
         const char *e = getenv("KMAN_RG_EI");
-        const int ei = e ? atoi(e) : 12;
+        const int ei = e ? atoi(e) : 16;
         if (p.rc) p.ei = ei == 16 ? 8u : 6u;  // two windows per item slot
         else p.ei = ei == 16 ? 16u : (ei == 8 && !p.canon ? 8u : 12u);
         const uint64_t win = (uint64_t)RT * p.ei;
@@ -2197,7 +2198,15 @@ int make_shard_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t f
     const uint64_t Wq = n_bases_q * (p.rc ? 2 : 1);
     p.Q = mode == KMAN_FINISH_UNIQ ? (bitlen(Wq - 1) ? bitlen(Wq - 1) : 1u) : 0u;
     if (p.K - B1 + p.Q > 64) return KMAN_EFALLBACK;
-    p.ei = p.rc ? 6u : 12u;
+    {
+        // the shard extraction's tiles (rg_hist counts in the same geometry):
+        // 12 windows per thread (6 with -r); KMAN_RG_XEI=16: 16 / 8 (A/B:
+        // config-4 shard extraction 80.0 vs 76.0 ms -- a round keeps 1/R of
+        // the windows, so the tiles' digit runs stay short either way)
+        const char *e = getenv("KMAN_RG_XEI");
+        const bool wide = e && atoi(e) == 16;
+        p.ei = p.rc ? (wide ? 8u : 6u) : (wide ? 16u : 12u);
+    }
     const uint64_t win = (uint64_t)RT * p.ei;
     p.n_tiles0 = (uint32_t)ceil_div(n_bases ? n_bases : 1, win);
     p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, RS);
@@ -2437,7 +2446,12 @@ extern "C" int kman_dshard_hist(kman_ctx *ctx, const uint8_t *d_codes, uint64_t 
     if (n_bases) {
         if (!d_codes) return kman_fail(ctx, KMAN_EINVAL, "null codes");
         KTimer kt_(ctx, "shard_hist");
-        if (p.canon && p.mix) launch_hist<12, false, 2>(ctx, p, d_codes, n_bases, k, d_hist);
+        if (p.ei == 16 || p.ei == 8) {
+            if (p.canon && p.mix) launch_hist<16, false, 2>(ctx, p, d_codes, n_bases, k, d_hist);
+            else if (p.canon) launch_hist<16, false, 1>(ctx, p, d_codes, n_bases, k, d_hist);
+            else if (p.rc) launch_hist<8, true, 0>(ctx, p, d_codes, n_bases, k, d_hist);
+            else launch_hist<16, false, 0>(ctx, p, d_codes, n_bases, k, d_hist);
+        } else if (p.canon && p.mix) launch_hist<12, false, 2>(ctx, p, d_codes, n_bases, k, d_hist);
         else if (p.canon) launch_hist<12, false, 1>(ctx, p, d_codes, n_bases, k, d_hist);
         else if (p.rc) launch_hist<6, true, 0>(ctx, p, d_codes, n_bases, k, d_hist);
         else launch_hist<12, false, 0>(ctx, p, d_codes, n_bases, k, d_hist);
@@ -2464,7 +2478,12 @@ extern "C" int kman_dshard_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64
     {
         KTimer kt_(ctx, "region_extract");
         uint32_t *cnt = const_cast<uint32_t *>(d_hist);  // read-only in EX mode
-        if (p.canon && p.mix) launch_extract_ex<12, false, 2>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
+        if (p.ei == 16 || p.ei == 8) {
+            if (p.canon && p.mix) launch_extract_ex<16, false, 2>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
+            else if (p.canon) launch_extract_ex<16, false, 1>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
+            else if (p.rc) launch_extract_ex<8, true, 0>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
+            else launch_extract_ex<16, false, 0>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
+        } else if (p.canon && p.mix) launch_extract_ex<12, false, 2>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
         else if (p.canon) launch_extract_ex<12, false, 1>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
         else if (p.rc) launch_extract_ex<6, true, 0>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
         else launch_extract_ex<12, false, 0>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
