@@ -207,10 +207,12 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     if (!BR)
         for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&whist[0][0])[i] = 0;
     if (threadIdx.x < RADIX) thist[threadIdx.x] = 0;
-    if (EX && threadIdx.x < RADIX / 32) {
-        uint32_t m = 0;
-        for (int b = 0; b < 32; b++) m |= (uint32_t)(rtab[(uint64_t)(threadIdx.x * 32 + b) * RS + sgi] != ~0ull) << b;
-        keep[threadIdx.x] = m;
+    if (EX && threadIdx.x < RADIX) {  // (one table load per thread, a ballot per wave)
+        const uint64_t bal = __ballot(rtab[(uint64_t)threadIdx.x * RS + sgi] != ~0ull);
+        if ((threadIdx.x & 63) == 0) {
+            keep[threadIdx.x / 32] = (uint32_t)bal;
+            keep[threadIdx.x / 32 + 1] = (uint32_t)(bal >> 32);
+        }
     }
     __syncthreads();
     RSTAMP(tile, 1);
