@@ -219,6 +219,12 @@ KMAN_DEV T wave_shr1(T v, T fill) {
     return dpp_move<0x138, 0xf>(v, fill);
 }
 
+// the next lane's value (lane 63: fill), DPP wave_shl:1
+template <typename T>
+KMAN_DEV T wave_shl1(T v, T fill) {
+    return dpp_move<0x130, 0xf>(v, fill);
+}
+
 // Exclusive block scan for NT threads (NT multiple of 64, <= 1024).
 // lds must hold NT/64 elements.  Returns the exclusive prefix; *total (if not
 // null) receives the block aggregate in every thread.
@@ -309,6 +315,51 @@ KMAN_DEV uint64_t wave_lookback(uint64_t *status, int64_t tile, uint64_t agg, ui
         }
         uint64_t v = (j >= 0 && (need >> lane) & 1ull) ? (w & ST_VMASK) : 0ull;
         // wave reduce
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) {
+            uint64_t o = shfl_any(v, lane ^ d);
+            v = OP == 0 ? v + o : (v > o ? v : o);
+        }
+        excl = OP == 0 ? excl + v : (excl > v ? excl : v);
+        if (first_incl < 64 || end - 64 <= 0) break;
+        end -= 64;
+    }
+    const uint64_t inc = OP == 0 ? excl + agg : (excl > agg ? excl : agg);
+    if (lane == 0) st_store(&status[tile], st_make(ST_INCL, epoch, inc));
+    return excl;
+}
+
+// wave_lookback for a tile that published its aggregate earlier itself
+// (publish_agg): no second AGG store; tile 0 already stored its INCL
+template <int OP>
+KMAN_DEV void publish_agg(uint64_t *status, int64_t tile, uint64_t agg, uint32_t epoch) {
+    st_store(&status[tile], st_make(tile == 0 ? ST_INCL : ST_AGG, epoch, agg));
+}
+template <int OP>
+KMAN_DEV uint64_t wave_lookback_published(uint64_t *status, int64_t tile, uint64_t agg, uint32_t epoch,
+                                          uint32_t *err) {
+    const int lane = lane_id();
+    if (tile == 0) return 0;
+    uint64_t excl = 0;
+    int64_t end = tile;
+    uint32_t spins = 0;
+    for (;;) {
+        const int64_t j = end - 1 - lane;
+        uint64_t w = 0, f = ST_INCL;
+        if (j >= 0) {
+            w = st_load(&status[j]);
+            f = st_flag(w, epoch);
+        }
+        const uint64_t notready = __ballot(f == 0);
+        const uint64_t incl = __ballot(f == ST_INCL && j >= 0);
+        const int first_incl = incl ? __ffsll((unsigned long long)incl) - 1 : 64;
+        const uint64_t need = first_incl == 64 ? ~0ull : (~0ull >> (63 - first_incl));
+        if (notready & need) {
+            if (spin_give_up(spins, err, 1u)) break;
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint64_t v = (j >= 0 && (need >> lane) & 1ull) ? (w & ST_VMASK) : 0ull;
 #pragma unroll
         for (int d = 32; d >= 1; d >>= 1) {
             uint64_t o = shfl_any(v, lane ^ d);

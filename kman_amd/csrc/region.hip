@@ -1157,6 +1157,18 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
     if (stp && t == 0) stp[(uint64_t)r * 8 + 7] = m;  // (the region's items, beside its phase stamps)
 #endif
     const uint32_t np = (dbg & 1) ? 0u : (rest + FBITS - 1) / FBITS;
+    // EARLY (uniq, single-GPU items): the region's row count is found after
+    // the second-to-last pass, when equal keys already share a run of equal
+    // low bits (a run of one item almost always), and published then, so the
+    // look-back after the last pass finds its predecessors' counts in place
+    // instead of waiting for the slowest region in flight (1.0 of 5.8 ms,
+    // the dbg & 4 ablation).  A singleton's mark rides in item bit 63 (above
+    // the key rest and the pos: the top bit of the pass-1 digit, constant in
+    // a region and never read here, so it is overwritten) through the last
+    // pass.  KMAN_RG_EARLY=0: A/B.
+    constexpr uint64_t MARK = 1ull << 63;
+    const bool early = MODE == RG_UNIQ && !tag_shift && np >= 2 && !(dbg & 16);
+    uint32_t etot = 0;
     uint32_t at = 0;
     for (uint32_t p = 0; p < np; p++) {
         const uint32_t bw = (rest - at + (np - p) - 1) / (np - p);
@@ -1226,6 +1238,78 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
             for (int i = 0; i < IPT; i++)
                 if (pw + i * 64 < m) x[i] = s[pw + i * 64];
         }
+        if (early && p + 2 == np) {
+            // The items are sorted by their low `at` rest bits, and x holds
+            // them wave-striped (item (i, lane) at position pw + i * 64), so a
+            // neighbour in position is a neighbouring lane (DPP) or the next /
+            // previous row's edge lane (readlane); only the wave's two edges
+            // come from LDS.  A key is a singleton iff no item of its run of
+            // equal low bits has its whole rest: runs of one or two decide
+            // from the neighbours, the rare runs of three or more scan LDS.
+            const uint64_t lm = ((1ull << at) - 1) << Q, km = rmask << Q;
+            const uint32_t wb = (uint32_t)w * (IPT * 64), we = wb + IPT * 64;
+            auto rl64 = [](uint64_t v, int l) -> uint64_t {
+                return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+            };
+            auto eq = [](uint64_t a, uint64_t b, uint64_t mask) { return !((a ^ b) & mask); };
+            // the wave's edges: positions wb - 2, wb - 1 and we, we + 1
+            const uint64_t eL = wb >= 1 && wb - 1 < m ? (uint64_t)s[wb - 1] : 0;
+            const uint64_t eLL = wb >= 2 && wb - 2 < m ? (uint64_t)s[wb - 2] : 0;
+            const uint64_t eR = we < m ? (uint64_t)s[we] : 0;
+            const uint64_t eRR = we + 1 < m ? (uint64_t)s[we + 1] : 0;
+            // LE / FE bit i: item (i, lane) has the low bits / the whole rest
+            // of its left neighbour (position - 1)
+            uint32_t LE = 0, FE = 0, V = 0;
+#pragma unroll
+            for (int i = 0; i < IPT; i++) {
+                const uint32_t pos = pw + i * 64;
+                const uint64_t v = x[i];
+                const uint64_t left = wave_shr1(v, i ? rl64(x[i - 1], 63) : eL);
+                const bool ok = pos < m && pos > 0;
+                const bool le = ok && eq(left, v, lm);
+                LE |= (uint32_t)le << i;
+                FE |= (uint32_t)(le && eq(left, v, km)) << i;
+                V |= (uint32_t)(pos < m) << i;
+            }
+            // the same of position + 1 (RE, RF), of position - 1 (LL) and of
+            // position + 2 (RR): lane shifts, rows carried through lanes 0 / 63
+            const uint64_t vlast = rl64(x[IPT - 1], 63);
+            const bool eRle = we < m && eq(eR, vlast, lm), eRfe = eRle && eq(eR, vlast, km);
+            const bool eRRle = we + 1 < m && eq(eRR, eR, lm);
+            const bool eLle = wb >= 2 && wb - 1 < m && eq(eL, eLL, lm);
+            const uint32_t top = 1u << (IPT - 1);
+            const uint32_t RE = wave_shl1(LE, ((uint32_t)__builtin_amdgcn_readlane((int)LE, 0) >> 1) | (eRle ? top : 0u));
+            const uint32_t RF = wave_shl1(FE, ((uint32_t)__builtin_amdgcn_readlane((int)FE, 0) >> 1) | (eRfe ? top : 0u));
+            const uint32_t LL = wave_shr1(LE, ((uint32_t)__builtin_amdgcn_readlane((int)LE, 63) << 1) | (eLle ? 1u : 0u));
+            const uint32_t RR = wave_shl1(RE, ((uint32_t)__builtin_amdgcn_readlane((int)RE, 0) >> 1) | (eRRle ? top : 0u));
+            const uint32_t lng = ((LE & RE) | (LE & LL) | (RE & RR)) & V;  // in a run of three or more
+            uint32_t S = V & ~FE & ~RF & ~lng;
+            for (uint32_t sl = lng; sl;) {  // (rare: the exact scan over the run in LDS)
+                const int i = __ffs(sl) - 1;
+                sl &= sl - 1;
+                const uint32_t q = pw + (uint32_t)i * 64;
+                const uint64_t v = s[q];
+                bool single = true;
+                for (uint32_t a2 = q; single && a2 > 0;) {
+                    const uint64_t u = s[--a2];
+                    if (!eq(u, v, lm)) break;
+                    if (eq(u, v, km)) single = false;
+                }
+                for (uint32_t a2 = q + 1; single && a2 < m; a2++) {
+                    const uint64_t u = s[a2];
+                    if (!eq(u, v, lm)) break;
+                    if (eq(u, v, km)) single = false;
+                }
+                S |= (uint32_t)single << i;
+            }
+            // (bit 63 is the top bit of the region's pass-1 digit before it
+            // becomes the mark: set or cleared on every item)
+#pragma unroll
+            for (int i = 0; i < IPT; i++) x[i] = (x[i] & ~(T)MARK) | (((S >> i) & 1u) ? (T)MARK : (T)0);
+            (void)block_exclusive_scan1<NT>((uint32_t)__popc(S), SumU32(), 0u, lds_scan2, &etot);
+            if (t == 0) publish_agg<0>(status, r, etot, epoch);
+        }
     }
     if (np == 0) {
 #pragma unroll
@@ -1254,6 +1338,12 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
 #pragma unroll
     for (int j = 0; j < IPT; j++) {
         const uint32_t q = q0 + j;
+        if (early) {  // (the marks of the early count: heads & tails below)
+            const bool e = q < m && ((uint64_t)kv[j] & MARK);
+            heads |= (uint32_t)e << j;
+            tails |= (uint32_t)e << j;
+            continue;
+        }
         if (q < m) {
             const uint64_t kq = RKEY(kv[j]);
             const bool h = q == 0 || kq != RKEY(j ? kv[j - 1] : s[q - 1]);
@@ -1275,13 +1365,15 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
     uint32_t total;
     // (its barrier orders every read of s above before the staging writes below)
     const uint32_t off = block_exclusive_scan1<NT>(ne, SumU32(), 0u, lds_scan, &total);
+    if (early && t == 0 && total != etot) atomicOr(err, 1u << 9);  // (tripwire: the early count was not the rows')
     // (the scan's barriers ordered every read of s above before the writes below)
     RSTAMP(r, 3);
     if (w == 0) {
         // (dbg & 4: timing ablation only -- regions placed by one atomic
         // cursor in completion order, no look-back: rows unsorted across regions)
         const uint64_t ob = (dbg & 4) ? (lane == 0 ? atomicAdd((unsigned long long *)(status + nreg), (unsigned long long)total) : 0ull)
-                                      : wave_lookback<0>(status, r, total, epoch, err);
+                            : early ? wave_lookback_published<0>(status, r, total, epoch, err)
+                                    : wave_lookback<0>(status, r, total, epoch, err);
         if (lane == 0) s_out = ob;
     }
     // the emitted rows compacted in LDS as one word each: the item itself
@@ -1604,6 +1696,8 @@ void launch_finish_as(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void 
 template <int MODE, typename O>
 void launch_finish(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ovals, uint32_t epoch,
                    uint32_t *counter, uint32_t dbg, uint64_t *stp) {
+    static const bool no_early = getenv("KMAN_RG_EARLY") && atoi(getenv("KMAN_RG_EARLY")) == 0;
+    if (no_early) dbg |= 16;  // (the uniq finish's early row count off: A/B)
     static const char *e = getenv("KMAN_RG_FIN");
     const bool pf = e && atoi(e) == 1;
     const bool db = e && atoi(e) == 2;
