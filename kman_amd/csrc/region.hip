@@ -1167,7 +1167,9 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
     // a region and never read here, so it is overwritten) through the last
     // pass.  KMAN_RG_EARLY=0: A/B.
     constexpr uint64_t MARK = 1ull << 63;
-    const bool early = MODE == RG_UNIQ && !tag_shift && np >= 2 && !(dbg & 16);
+    // (the round path's items carry the source rank in the 9 bits at
+    // tag_shift, read as 8 bits below: bit 63 is free there as well)
+    const bool early = MODE == RG_UNIQ && (!tag_shift || tag_shift + 8 <= 63) && np >= 2 && !(dbg & 16);
     uint32_t etot = 0;
     uint32_t at = 0;
     for (uint32_t p = 0; p < np; p++) {
@@ -1416,7 +1418,8 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
                 const uint64_t pos = rc ? idx : (idx << 1);
                 // N > 1: the source rank (tagged into the item by the pass after
                 // the exchange) in bits 56-63, as DistPipeline's payloads
-                ovals[ob + q] = (O)(tag_shift ? pos | (((v >> tag_shift) & 0x1ffull) << 56) : pos);
+                // (ranks < 256: 8 tag bits, so bit 63 -- the early count's mark -- is not read)
+                ovals[ob + q] = (O)(tag_shift ? pos | (((v >> tag_shift) & 0xffull) << 56) : pos);
             } else if constexpr (NARROW) {
                 ovals[ob + q] = (O)v;
             } else {
