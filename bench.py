@@ -27,7 +27,9 @@ Reported beside it:
     core on the host's cores (count stated).
 
 N > 1 (``python -m torch.distributed.run --nproc-per-node N bench.py --gpus
-N``, or ``--dist`` at N = 1): ONE global synthetic FASTA of N x 1 GB (seed 1,
+N``; or plain ``python bench.py --gpus N``, which starts the N rank processes
+itself -- see ``spawn_ranks``; or ``--dist`` at N = 1): ONE global synthetic
+FASTA of N x 1 GB (seed 1,
 kman_synth_fasta / inputs.SynthLayout), byte-range sharded (each rank
 generates its own bytes + halo on its GPU); per step every rank runs the
 shard histogram, the key rounds (extraction into the send buffer, one RCCL
@@ -61,6 +63,24 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def cgroup_cpu_quota(path: str = "/sys/fs/cgroup/cpu.max"):
+    """The cgroup v2 CPU quota in CPUs (quota / period), None when unlimited
+    or absent."""
+    try:
+        with open(path) as fh:
+            q, per = fh.read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
+def effective_cores(affinity: int, quota) -> int:
+    """CPUs the process can actually keep busy: min(affinity, cgroup quota)."""
+    if quota is None:
+        return max(1, affinity)
+    return max(1, min(affinity, int(quota + 0.5)))
+
+
 def cpu_baseline(k: int, mode: str, target_s: float = 10.0) -> dict:
     """oracle/kman_oracle (C restatement of the reference algorithm) on a
     sample of the same synthetic workload scaled to ~target_s seconds: one
@@ -71,8 +91,11 @@ def cpu_baseline(k: int, mode: str, target_s: float = 10.0) -> dict:
     exe = os.path.join(ROOT, "oracle", "kman_oracle")
     if not os.path.isfile(exe):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
-    # every core this process may run on (the box's CPU share; nproc shows the whole machine)
-    cores = max(1, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1)
+    # the CPUs this process may run on (nproc shows the whole machine); the
+    # effective count is capped by the cgroup CPU quota (the box's share)
+    affinity = max(1, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count() or 1)
+    quota = cgroup_cpu_quota()
+    cores = effective_cores(affinity, quota)
     with tempfile.TemporaryDirectory() as d:
         def sample(nbases, seed):
             src = os.path.join(d, "s%d.fa" % seed)
@@ -98,16 +121,11 @@ def cpu_baseline(k: int, mode: str, target_s: float = 10.0) -> dict:
         nbp = max(1_000_000, min(nb // 2, 8 * nb // cores))
         srcs = [sample(nbp, 1 + i) for i in range(cores)]
         nP, _, wallP = run(srcs)
-        quota = None
-        try:  # the cgroup CPU quota, if any (the box's CPU share)
-            q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-            quota = None if q == "max" else float(q) / float(per)
-        except (OSError, ValueError):
-            pass
     return {"value": n1 / s1, "unit": "k-mers/s", "cores": 1, "kind": "port",
             "sample": "%d-base sample of the same generator (seed 1), %s k=%d, %d k-mers in %.2f s, 1 thread"
                       % (nb, mode, k, n1, s1),
-            "all_cores": {"value": nP / wallP, "cores": cores, "nproc": os.cpu_count(), "cgroup_cpu_quota": quota,
+            "all_cores": {"value": nP / wallP, "cores": cores, "affinity_cpus": affinity, "nproc": os.cpu_count(),
+                          "cgroup_cpu_quota": quota,
                           "sample": "%d processes on independent %d-base samples (seeds 1..%d), %d k-mers in %.2f s "
                                     "wall" % (cores, nbp, cores, nP, wallP)}}
 
@@ -399,10 +417,8 @@ def run_dist(args, world: int, rank: int, local: int):
         c, ms = pipe.timed(tag)
         if c:
             stages[tag] = round(ms / args.steps, 3)
-    n_pass, pass_ms = pipe.timed("region_pass")
     if rank == 0:
-        avg = pass_ms / max(n_pass, 1) / 1e3
-        ach = 16.0 * pipe.n_recv / max(n_pass // args.steps, 1) / avg / 1e9 if n_pass else None
+        dom, sp = dist_roofline(pipe, args.steps, args.mode, args.k, per, world, canon)
         out = {
             "metric": METRIC, "value": total / elapsed, "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -410,29 +426,103 @@ def run_dist(args, world: int, rank: int, local: int):
             "data": "synthetic: ONE global FASTA (kman_synth_fasta seed 1, uniform ACGT, 80 col) of %d x %.2f GB, "
                     "byte-range sharded, each rank's bytes generated in its HBM; a step = %s shard histogram + key "
                     "rounds" % (world, per / 1e9, "parse of the resident text +" if reparse else "(parsed at setup)"),
-            "config": {"workload": "%.2f GB synthetic FASTA in %d byte-range shards, k=%d, extract+radix-sort+%s, "
-                                   "key rounds + one RCCL all-to-all per round%s"
-                                   % (lay.size / 1e9, world, args.k,
+            "config": {"workload": "%.2f GB synthetic FASTA in %d byte-range shards of %.2f GB per rank, k=%d, "
+                                   "extract+radix-sort+%s, key rounds + one RCCL all-to-all per round%s"
+                                   % (lay.size / 1e9, world, per / 1e9, args.k,
                                       "canonical count + all-reduced abundance spectrum (config 5's pipeline)"
                                       if canon else args.mode,
                                       "" if not canon else "; the synthetic input stands in for GRCh38"),
                        "canonical": canon,
                        "spectrum_distinct": int(one_step.hist.sum()) if canon else None,
-                       "fasta_bytes": lay.size, "kmers_per_step": total // max(args.steps, 1), "k": args.k,
+                       "fasta_bytes": lay.size, "fasta_bytes_per_rank": per,
+                       "kmers_per_step": total // max(args.steps, 1), "k": args.k,
                        "mode": args.mode, "parallelism": "dp%d: top-8-bit bucket parts + RCCL all-to-all" % world,
                        "path": pipe.path, "rounds": pipe.rounds, "fallback_rounds": pipe.fallback_rounds,
                        "partial_rounds": pipe.partial_rounds,
                        "memory_plan": getattr(pipe, "plan_info", None),
                        "stages_ms_per_step_rank0": stages},
-            "roofline": {"kernel": "rg_pass (pass 1 after the exchange, rank 0)", "bound": "hbm", "achieved": ach,
-                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS if ach else None,
-                         "traffic": None, "avg_launch_ms": avg * 1e3},
-            "cpu_baseline": None,
+            "roofline": dom, "sort_pass_roofline": sp, "cpu_baseline": None,
         }
-        emit(out)
     comm.allreduce(np.zeros(1, np.uint64))  # every rank is done
     pipe.free()
     dev.close()
+    if rank == 0:
+        # the C port on the host's cores, after every rank has left the GPU
+        # work (the other ranks exit; the GPUs are idle while it runs)
+        if not args.no_cpu_baseline:
+            try:
+                out["cpu_baseline"] = cpu_baseline(args.k, args.mode)
+            except Exception as e:  # reported, never fatal to the GPU number
+                out["cpu_baseline"] = {"error": repr(e)}
+        emit(out)
+
+
+def dist_pmc_traffic(kernel: str, mode: str, k: int, per_rank: int, canonical: bool, alg_bytes: float):
+    """HBM bytes per launch of `kernel` on the multi-GPU path, from the
+    committed world-1 PMC summary of the same per-rank workload
+    (profiles/pmc_dist_current.json: HBM bytes and algorithmic bytes per
+    launch there): that run's measured/algorithmic ratio times this launch's
+    algorithmic bytes (at world 1: the measured bytes themselves).  None if
+    no summary of this workload is committed."""
+    p = os.path.join(ROOT, "profiles", "pmc_dist_current.json")
+    if not os.path.isfile(p):
+        return None
+    with open(p) as fh:
+        d = json.load(fh)
+    m = d.get("_meta", {})
+    if (m.get("mode"), m.get("k"), m.get("bases_per_rank"), bool(m.get("canonical"))) != (mode, k, per_rank,
+                                                                                         canonical):
+        return None
+    e = d.get(kernel)
+    if not e or not e.get("alg_bytes_per_launch"):
+        return None
+    return e["hbm_bytes_per_launch"] / e["alg_bytes_per_launch"] * alg_bytes
+
+
+def dist_stage_bytes(pipe, steps: int, mode: str) -> dict:
+    """Algorithmic HBM bytes per step of each region-path stage on this rank
+    (DESIGN.md §5, multi-GPU rows): shard_hist 1 code read per base;
+    rg_extract R code reads per base (every round re-rolls the shard) + 8 B
+    per item sent; rg_pass and pass 1b 8 + 8 B per received item; rg_finish
+    8 B per received item + 8 B key and the value (u32 count | u64 pos) per
+    row."""
+    sh = pipe.shard
+    R = max(1, int(pipe.rounds or 1))
+    vb = pipe._out[2] if getattr(pipe, "_out", None) else (4 if mode == "count" else 8)
+    nb = float(sh.n_eff)
+    return {"shard_hist": ("rg_hist", nb),
+            "region_extract": ("rg_extract", R * nb + 8.0 * pipe.n_local),
+            "region_pass": ("rg_pass", 16.0 * pipe.n_recv),
+            "region_pass1b": ("rg_pass", 16.0 * pipe.n_recv),
+            "region_finish": ("rg_finish", 8.0 * pipe.n_recv + (8.0 + vb) * pipe.n_out)}
+
+
+def dist_roofline(pipe, steps: int, mode: str, k: int, per_rank: int, world: int, canonical: bool):
+    """(dominant-stage roofline, digit-pass roofline) of rank 0's step: the
+    stage with the most kernel time, its algorithmic bytes per launch over
+    its HIP-event average launch time."""
+    per = dist_stage_bytes(pipe, steps, mode)
+
+    def line(tag):
+        kern, alg_step = per[tag]
+        c, ms = pipe.timed(tag)
+        if not c:
+            return None
+        launches = max(1, c // steps)
+        alg = alg_step / launches
+        avg = ms / c / 1e3
+        a = alg / avg / 1e9
+        tr = dist_pmc_traffic(tag, mode, k, per_rank, canonical, alg)
+        return {"kernel": "%s (%s, rank 0 of %d)" % (kern, tag, world), "bound": "hbm", "achieved": a,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": a / HBM_PEAK_GBS, "traffic": tr,
+                "algorithmic_bytes_per_launch": alg, "avg_launch_ms": avg * 1e3, "launches_per_step": launches,
+                "traffic_basis": None if tr is None else
+                "profiles/pmc_dist_current.json: world-1 PMC bytes per algorithmic byte x this launch's "
+                "algorithmic bytes"}
+
+    timed = {t: pipe.timed(t)[1] for t in per}
+    dom = max(timed, key=lambda t: timed[t])
+    return line(dom), line("region_pass")
 
 
 _RESULT_FD = None  # stdout as the driver sees it (main() points fd 1 at stderr)
@@ -473,13 +563,131 @@ def main() -> None:
                     help="multi-GPU path: canonical k-mers + the all-reduced abundance spectrum (config 5; "
                          "with --mode count)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.dist or args.canonical):
+        # no launcher: start the ranks here (this process never touches the GPU)
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but the launcher started %d ranks (WORLD_SIZE)" % (args.gpus, world))
     if world > 1 or args.dist or args.canonical:
         run_dist(args, world, rank, local)
     else:
         run_single(args)
+
+
+_COUNT_GPUS = r"""
+import ctypes, sys
+for name in ("libamdhip64.so", "/opt/rocm/lib/libamdhip64.so"):
+    try:
+        hip = ctypes.CDLL(name)
+        break
+    except OSError:
+        hip = None
+n = ctypes.c_int(0)
+print(n.value if hip is not None and hip.hipGetDeviceCount(ctypes.byref(n)) == 0 else 0)
+"""
+
+
+def visible_gpus(timeout: float = 180.0) -> int:
+    """GPUs visible to a rank, counted in a short-lived child process: the
+    spawning process itself never initialises the GPU."""
+    try:
+        r = subprocess.run([sys.executable, "-c", _COUNT_GPUS], capture_output=True, text=True, timeout=timeout)
+        return int(r.stdout.strip().splitlines()[-1]) if r.returncode == 0 and r.stdout.strip() else 0
+    except (subprocess.TimeoutExpired, ValueError, IndexError):
+        return 0
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def rank_env(base: dict, world: int, rank: int, port: int, run_id: str) -> dict:
+    """The launcher environment of rank `rank` (what torch.distributed.run
+    sets: one process per GPU, LOCAL_RANK = the GPU)."""
+    e = dict(base)
+    e.update({"WORLD_SIZE": str(world), "RANK": str(rank), "LOCAL_RANK": str(rank), "LOCAL_WORLD_SIZE": str(world),
+              "GROUP_RANK": "0", "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "KMAN_RUN_ID": run_id})
+    return e
+
+
+def spawn_ranks(n: int, argv, cmd=None, gpus=None, poll_s: float = 0.2, grace_s: float = 10.0) -> int:
+    """Run the N-rank benchmark without an external launcher: N child
+    processes of this script (or `cmd`), each with WORLD_SIZE / RANK /
+    LOCAL_RANK / MASTER_* set, started before this process makes any GPU
+    call (it never makes one; it does not re-exec itself).  Rank 0's stdout
+    (the JSON line) is passed to this process's result stream; the others'
+    stdout goes to stderr.  Returns the exit status: non-zero, with a
+    message, if fewer than N GPUs are visible or any rank fails (the other
+    ranks are then terminated, by PID)."""
+    import secrets
+    import signal
+    import threading
+
+    have = visible_gpus() if gpus is None else gpus
+    if have < n:
+        log("bench.py: --gpus %d needs %d visible GPUs, %d visible; no result" % (n, n, have))
+        return 2
+    cmd = list(cmd) if cmd is not None else [sys.executable, os.path.abspath(__file__)]
+    port, run_id = free_port(), secrets.token_hex(8)
+    procs = []
+    chunks = []
+
+    def pump(fh):  # rank 0's stdout, read as it comes (no pipe back-pressure)
+        for line in iter(fh.readline, b""):
+            chunks.append(line)
+        fh.close()
+
+    reader = None
+    try:
+        for r in range(n):
+            p = subprocess.Popen(cmd + list(argv), env=rank_env(os.environ, n, r, port, run_id),
+                                 stdout=subprocess.PIPE if r == 0 else 2, stdin=subprocess.DEVNULL)
+            procs.append(p)
+            if r == 0:
+                reader = threading.Thread(target=pump, args=(p.stdout,), daemon=True)
+                reader.start()
+        failed = None
+        while failed is None:
+            codes = [p.poll() for p in procs]
+            bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+            if bad:
+                failed = bad[0]
+                break
+            if all(c == 0 for c in codes):
+                break
+            time.sleep(poll_s)
+    finally:
+        live = [p for p in procs if p.poll() is None]
+        for p in live:
+            p.send_signal(signal.SIGTERM)
+        t_end = time.time() + grace_s
+        for p in live:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.time()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if reader is not None:
+        reader.join(timeout=grace_s)
+    if failed is not None:
+        log("bench.py: rank %d of %d exited with status %d; no result" % (failed[0], n, failed[1]))
+        return failed[1] if failed[1] > 0 else 1
+    text = b"".join(chunks).decode(errors="replace")
+    lines = [ln for ln in text.splitlines() if ln.strip().startswith("{")]
+    if not lines:
+        log("bench.py: rank 0 printed no result line")
+        return 1
+    emit(json.loads(lines[-1]))
+    return 0
 
 
 if __name__ == "__main__":

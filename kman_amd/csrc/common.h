@@ -121,10 +121,14 @@ constexpr uint64_t ST_VMASK = (1ull << 56) - 1;
 constexpr uint32_t SPIN_LIMIT = 1u << 20; // ~1 s of polling; a hit is an engine bug
 
 // true when this waiter must give up: its own bound is spent, or another wave
-// already flagged an error (so one fault does not cascade into serial timeouts)
+// already flagged a fault (so one fault does not cascade into serial
+// timeouts).  Bit 8 (region.hip's ERR_REGION, a region that would overflow)
+// is not a fault: the round path keeps every other region's rows, so their
+// look-backs must still complete.
 KMAN_DEV bool spin_give_up(uint32_t &spins, uint32_t *err, uint32_t code) {
     ++spins;
-    if ((spins & 255u) == 0 && __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return true;
+    if ((spins & 255u) == 0 && (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & ~(1u << 8)) != 0)
+        return true;
     if (spins > SPIN_LIMIT) {
         atomicOr(err, code);
         return true;

@@ -47,13 +47,13 @@ constexpr int RS = 64;            // position segments of pass 0 (one wave of co
 constexpr int RSI = 16;           // items per thread, pass 1
 constexpr uint64_t T1 = (uint64_t)RT * RSI;  // pass-1 tile
 constexpr int FT = 512;           // finish threads (two blocks per CU)
-constexpr int FW = FT / 64;
 constexpr int FIPT = 17;          // finish items per thread
 constexpr int FCAP = FT * FIPT;   // 8704 items = 68 KiB: largest region
 constexpr int FBITS = 9;          // finish LSD digit (26 bits: 3 passes)
 constexpr int FRAD = 1 << FBITS;
 constexpr int FWORD = FRAD / 2;   // per-wave counters: two u16 per word
 constexpr uint32_t ERR_REGION = 1u << 8;  // a region would overflow (not an engine fault)
+constexpr uint32_t ERR_EARLY = 1u << 9;   // the uniq finish's early row count was not its rows'
 constexpr uint32_t B1 = 8;        // pass-0 digit = top 8 key bits
 
 // phase stamps (s_memrealtime, 100 MHz) per tile, thread 0, into `stp`: only
@@ -89,58 +89,53 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 }
 
 // ---------------------------------------------------------------- pass 0
-// A tile of RT*EI window starts: windows rolled from LDS-staged codes, the
-// valid ones compacted in stream order (tile-local window << 1 | strand
-// packed above the 2k key bits), ranked by the top 8 key bits, digit counts
-// published early, grouped look-back per digit along the segment's chain,
-// LDS-staged coalesced scatter into region (b, s).
-// BR: rank by one block-wide LDS atomic per item (unstable inside a tile;
-// nothing downstream needs the order of a region's items).
-// EX (the multi-GPU shard path, kman_dshard_extract): no padded regions --
-// region (b, s) is written at rtab[b * RS + s] (exact sizes from rg_hist, in
-// cnt0, which is then read-only); buckets with rtab == ~0 are not kept this
-// round, and their windows are dropped before the rank (keep bitmap).
-// NS: position segments (look-back chains); RS for the shard path (EX), more
-// for kman_groups (shorter chains, pass 1 finds segments in an LDS table)
-// IL (kman_groups): interleaved chains -- tile t is step t / NS of chain
-// t % NS (status words chain-major), so any prefix of the stream spreads over
-// every chain and pass 0 can run in consecutive launches over tile ranges as
-// the codes arrive (kman_groups_extract): the epoch's ticket counter carries
-// on from one launch to the next, and a launch of n blocks takes the next n
-// tiles in stream order.
-// XG (a whole-stream launch): tickets per XCD partition -- chains
-// [p * NS / 8, (p + 1) * NS / 8) form partition p, counter[p] deals its tiles
+// A tile of RT*EI window starts: windows rolled from LDS-staged codes and
+// ranked straight from the roll's registers by one block-wide LDS atomic per
+// item on the top 8 key bits (item i = window i, or 2j / 2j + 1 = window j's
+// two strands with RC; tile-local (window << 1 | strand) packed above the 2k
+// key bits), LDS-staged coalesced scatter into region (b, s).
+// A tile takes its place in region (b, s) by one atomic add per digit on the
+// region's cursor (cursor[b * RS + s], zeroed before the launch; it ends as the
+// region's count), issued right after the rank so its round trip overlaps the
+// digit scan and the LDS scatter.  A region's items are then in no particular
+// order, which nothing downstream needs: pass 1 ranks unstably and the finish
+// sorts every remaining key bit (uniq items carry their window index, so
+// equal keys are dropped or counted whatever their order).  No tile waits on
+// another tile.
+// Segment s of a tile:
+//   kman_groups (IL = !EX): interleaved chains -- tile t is in segment t % RS,
+//     so any prefix of the stream spreads over every segment and pass 0 can
+//     run in consecutive launches over tile ranges as the codes arrive
+//     (kman_groups_extract: the epoch's ticket counter carries on from one
+//     launch to the next, and a launch of n blocks takes the next n tiles);
+//   EX (the multi-GPU shard path, kman_dshard_extract): contiguous runs of
+//     seg_tiles tiles, rg_hist's geometry; no padded regions -- region (b, s)
+//     is written at rtab[b * RS + s] (exact sizes from rg_hist in cnt0, which
+//     is read-only); buckets with rtab == ~0 are not kept this round, and
+//     their windows are dropped before the rank (keep bitmap).
+// XG (a whole-stream launch): tickets per XCD partition -- segments
+// [p * RS / 8, (p + 1) * RS / 8) form partition p, counter[p] deals its tiles
 // in stream order, and a block takes tickets from its own XCD's partition
 // first (HW_REG_XCC_ID), then from the others once that one is dealt out.  So
-// a chain's consecutive tiles usually run on one XCD: the 128-byte line two of
-// them share at a digit-run boundary meets in that XCD's L2 instead of
-// leaving two partial lines, and the look-back's predecessor is a neighbour.
-// Placement changes only speed: a tile waits only on earlier tickets of its
-// own partition, and a block leaves only when every partition is dealt out.
-// AT (with BR): no look-back -- a tile takes its place in region (b, s) by
-// one atomic add per digit on the region's cursor (cnt0[b * NS + s], zeroed
-// before the launch; it ends as the region's count; EX: the cursors are
-// `status` as u32, zeroed before the launch, and cnt0 keeps the exact sizes).  A region's
-// items are then in no particular order, which nothing downstream needs: pass
-// 1 ranks unstably and the finish sorts every remaining key bit (uniq items
-// carry their window index, so equal keys are dropped or counted whatever
-// their order).  No tile waits on another tile.
-template <int EI, bool RC, bool ATOMIC, int CANON = 0, bool BR = false, bool EX = false, int NS = RS,
-          int XLB = LB, bool IL = false, int TPDX = 0, bool XG = false, bool AT = false>
-__global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI == 8 ? 8 : 4)))) void rg_extract(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
-                                                 uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
-                                                 uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ cnt0,
-                                                 uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
-                                                 uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg,
-                                                 uint64_t *__restrict__ stp, const uint64_t *__restrict__ rtab = nullptr) {
+// the tiles that claim consecutive slots of a region usually run on one XCD:
+// the 128-byte line two of them share meets in that XCD's L2 instead of
+// leaving two partial lines.  Placement changes only speed; a block leaves
+// only when every partition is dealt out.
+template <int EI, bool RC, int CANON, bool EX, bool XG>
+__global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI == 8 ? 8 : 4)))) void rg_extract(
+    const uint8_t *__restrict__ codes, uint64_t n_bases, int k, uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
+    uint32_t seg_tiles, uint32_t n_tiles, const uint32_t *__restrict__ cnt0, uint32_t *__restrict__ cursor,
+    uint32_t *__restrict__ counter, uint32_t *__restrict__ err, uint64_t *__restrict__ stp,
+    const uint64_t *__restrict__ rtab) {
     constexpr int NT = RT;
     constexpr int NWAVE = NT / 64;
     constexpr int WIN = NT * EI;
     constexpr int TILE = WIN * (RC ? 2 : 1);
     constexpr int SI = TILE / NT;
+    constexpr bool IL = !EX;
     static_assert(WIN + 64 <= TILE * 8, "codes fit in the key staging area");
+    static_assert(RS % 8 == 0, "XCD partitions of whole segments");
     __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
-    __shared__ uint32_t whist[BR ? 1 : NWAVE][RADIX];
     __shared__ uint32_t thist[RADIX];
     __shared__ uint32_t lstart[RADIX];
     __shared__ uint64_t gexcl[RADIX];
@@ -148,20 +143,17 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     __shared__ uint32_t lds_tile;
     __shared__ uint32_t keep[EX ? RADIX / 32 : 1];
 
-    static_assert(!XG || NS % 8 == 0, "XCD partitions of whole chains");
-    static_assert(!AT || BR, "atomic cursors: block-wide ranks");
-    uint32_t *const cursor = EX ? reinterpret_cast<uint32_t *>(status) : cnt0;  // (AT)
     uint32_t cid;
     if (XG) {
         if (threadIdx.x == 0) {
-            constexpr uint32_t CPG = NS / 8;  // chains per partition
+            constexpr uint32_t CPG = RS / 8;  // segments per partition
             const uint32_t x = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // hwreg(HW_REG_XCC_ID, 0, 4)
             uint32_t got = ~0u;
             for (uint32_t a = 0; a < 8 && got == ~0u; a++) {
                 const uint32_t pp = (x + a) & 7u;
                 const uint32_t j = atomicAdd(counter + pp, 1u);
-                const uint64_t tt = (uint64_t)(j / CPG) * NS + pp * CPG + j % CPG;
-                if (tt < (IL ? (uint64_t)n_tiles : (uint64_t)NS * seg_tiles)) got = (uint32_t)tt;
+                const uint64_t tt = (uint64_t)(j / CPG) * RS + pp * CPG + j % CPG;
+                if (tt < (IL ? (uint64_t)n_tiles : (uint64_t)RS * seg_tiles)) got = (uint32_t)tt;
             }
             lds_tile = got;
         }
@@ -172,31 +164,21 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     } else {
         cid = (uint32_t)grab_tile(counter, &lds_tile);
     }
-    uint32_t sgi, jj;
-    int64_t tile, first, stile;  // data tile; the chain's first status slot; this tile's status slot
-    bool last;                   // the chain's last tile
+    uint32_t sgi;
+    int64_t tile;
     if (IL) {
         tile = cid;
         if (tile >= (int64_t)n_tiles) return;  // (block-uniform)
-        sgi = (uint32_t)(tile % NS);
-        jj = (uint32_t)(tile / NS);
-        first = (int64_t)sgi * seg_tiles;
-        stile = first + jj;
-        last = tile + NS >= (int64_t)n_tiles;
+        sgi = (uint32_t)(tile % RS);
     } else {
-        sgi = cid % NS;
-        jj = cid / NS;
+        sgi = cid % RS;
+        const uint32_t jj = cid / RS;
         const uint32_t t0 = sgi * seg_tiles;
         const uint32_t t1 = t0 + seg_tiles < n_tiles ? t0 + seg_tiles : n_tiles;
         if (t0 + jj >= t1) return;  // (block-uniform) past a segment's end
         tile = (int64_t)t0 + jj;
-        first = t0;
-        stile = tile;
-        last = tile == (int64_t)t1 - 1;
     }
     RSTAMP(tile, 0);
-    const int lane = lane_id();
-    const int w = threadIdx.x >> 6;
     const uint32_t kb = 2u * (uint32_t)k;
     const uint32_t shift = kb - B1;
     const uint64_t keymask = kb >= 64 ? ~0ull : ((1ull << kb) - 1);
@@ -204,8 +186,6 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     const uint64_t wb = (uint64_t)tile * WIN;
     uint8_t *scodes = reinterpret_cast<uint8_t *>(skeys);
     stage_codes<NT, EI>(codes, n_bases, wb, scodes);
-    if (!BR)
-        for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&whist[0][0])[i] = 0;
     if (threadIdx.x < RADIX) thist[threadIdx.x] = 0;
     if (EX && threadIdx.x < RADIX) {  // (one table load per thread, a ballot per wave)
         const uint64_t bal = __ballot(rtab[(uint64_t)threadIdx.x * RS + sgi] != ~0ull);
@@ -233,147 +213,60 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
             }
         }
     }
-    uint32_t tcnt = 0;
-    const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
     uint64_t key[SI];
     uint32_t rank[SI];
-    uint32_t vmask = 0;    // (BR: item i of this thread is valid)
-    uint32_t at_base = 0;  // (AT: this tile's first slot in region (d, sgi), thread d)
+    uint32_t vmask = 0;    // item i of this thread is valid
+    uint32_t at_base = 0;  // this tile's first slot in region (d, sgi), thread d
 #define XDIGIT(x) ((uint32_t)(((x) & keymask) >> shift))
-#define KEPT(d) (!EX || ((keep[(d) >> 5] >> ((d) & 31)) & 1u))
     // the tile-local (window << 1 | strand) rides above the key bits: only
     // uniq items carry it (Q > 0, k <= 25); count items are the key
     auto tagged = [&](int j, bool strand) -> uint64_t {
         return Q ? (uint64_t)(((w0 + j) << 1) | (uint32_t)strand) << kb : 0ull;
     };
-    if constexpr (BR) {
-        // ranked straight from the roll's registers (item i = window i, or
-        // 2j / 2j + 1 = window j's two strands with RC): the block-wide rank is
-        // unstable anyway, so no compaction pass through LDS is needed
 #pragma unroll
-        for (int j = 0; j < EI; j++) {
-            if (RC) {
-                key[2 * j] = kf[j] | tagged(j, false);
-                key[2 * j + 1] = kr[j] | tagged(j, true);
-                vmask |= (((vf >> j) & 1u) << (2 * j)) | (((vr >> j) & 1u) << (2 * j + 1));
-            } else {
-                key[j] = kf[j] | tagged(j, false);
-            }
-        }
-        if (!RC) vmask = vf;
-#pragma unroll
-        for (int i = 0; i < SI; i++) rank[i] = (vmask >> i) & 1u ? atomicAdd(&thist[XDIGIT(key[i])], 1u) : 0u;
-        __syncthreads();  // (also: every roll read of the staged codes before the scatter below)
-        RSTAMP(tile, 2);
-        if (AT) {
-            // the tile's place in each region, claimed now: the atomics'
-            // round trip overlaps the digit scan and the LDS scatter below
-            if (threadIdx.x < RADIX) {
-                const uint32_t c = thist[threadIdx.x];
-                at_base = c ? atomicAdd(cursor + threadIdx.x * NS + sgi, c) : 0u;
-            }
-        } else if (threadIdx.x < RADIX && KEPT(threadIdx.x)) {
-            // (EX: a digit not kept this round has no chain: nothing published)
-            digit_publish(status + threadIdx.x, stile, first, thist[threadIdx.x], epoch);
-        }
-    } else {
-        const uint32_t off =
-            block_exclusive_scan<NT>((uint32_t)(__popc(vf) + __popc(vr)), SumU32(), 0u, lds_scan, &tcnt);
-        {
-            uint32_t o = off;
-#pragma unroll
-            for (int j = 0; j < EI; j++) {
-                if ((vf >> j) & 1u) skeys[o++] = kf[j] | tagged(j, false);
-                if (RC && ((vr >> j) & 1u)) skeys[o++] = kr[j] | tagged(j, true);
-            }
-        }
-        __syncthreads();
-        RSTAMP(tile, 2);
-#pragma unroll
-        for (int i = 0; i < SI; i++) key[i] = ib + i * 64 < tcnt ? skeys[ib + i * 64] : 0;
-        if (ATOMIC) {
-#pragma unroll
-            for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&whist[w][XDIGIT(key[i])], 1u) : 0u;
-            __syncthreads();
-            if (threadIdx.x < RADIX) {
-                uint32_t c = 0;
-#pragma unroll
-                for (int ww = 0; ww < NWAVE; ww++) c += whist[ww][threadIdx.x];
-                thist[threadIdx.x] = c;
-                digit_publish(status + threadIdx.x, stile, first, c, epoch);
-            }
+    for (int j = 0; j < EI; j++) {
+        if (RC) {
+            key[2 * j] = kf[j] | tagged(j, false);
+            key[2 * j + 1] = kr[j] | tagged(j, true);
+            vmask |= (((vf >> j) & 1u) << (2 * j)) | (((vr >> j) & 1u) << (2 * j + 1));
         } else {
-#pragma unroll
-            for (int i = 0; i < SI; i++)
-                if (ib + i * 64 < tcnt) atomicAdd(&thist[XDIGIT(key[i])], 1u);
-            __syncthreads();
-            if (threadIdx.x < RADIX) digit_publish(status + threadIdx.x, stile, first, thist[threadIdx.x], epoch);
-#pragma unroll
-            for (int i = 0; i < SI; i++) rank[i] = ballot_rank(whist[w], XDIGIT(key[i]), ib + i * 64 < tcnt, B1);
+            key[j] = kf[j] | tagged(j, false);
         }
-        __syncthreads();
+    }
+    if (!RC) vmask = vf;
+#pragma unroll
+    for (int i = 0; i < SI; i++) rank[i] = (vmask >> i) & 1u ? atomicAdd(&thist[XDIGIT(key[i])], 1u) : 0u;
+    __syncthreads();  // (also: every roll read of the staged codes before the scatter below)
+    RSTAMP(tile, 2);
+    if (threadIdx.x < RADIX) {  // the tile's place in each region, claimed now
+        const uint32_t c = thist[threadIdx.x];
+        at_base = c ? atomicAdd(cursor + threadIdx.x * RS + sgi, c) : 0u;
     }
     RSTAMP(tile, 3);
     const uint32_t d0 = threadIdx.x;
-    uint32_t tot = 0;
-    if (BR) {
-        if (d0 < RADIX) tot = thist[d0];
-    } else if (d0 < RADIX) {
-#pragma unroll
-        for (int ww = 0; ww < NWAVE; ww++) {
-            const uint32_t c = whist[ww][d0];
-            whist[ww][d0] = tot;
-            tot += c;
-        }
-    }
-    uint32_t btot;
-    const uint32_t ls = block_exclusive_scan1<NT>(tot, SumU32(), 0u, lds_scan, &btot);
-    if (BR) tcnt = btot;
+    const uint32_t tot = d0 < RADIX ? thist[d0] : 0u;
+    uint32_t tcnt;
+    const uint32_t ls = block_exclusive_scan1<NT>(tot, SumU32(), 0u, lds_scan, &tcnt);
     if (d0 < RADIX) lstart[d0] = ls;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < SI; i++) {
-        if (BR ? ((vmask >> i) & 1u) : ib + i * 64 < tcnt) {
+        if ((vmask >> i) & 1u) {
             const uint32_t d = XDIGIT(key[i]);
-            skeys[lstart[d] + (BR ? 0u : whist[w][d]) + rank[i]] = key[i];
+            skeys[lstart[d] + rank[i]] = key[i];
         }
     }
-    if (AT) {
-        if (threadIdx.x < RADIX) {
-            const uint32_t d = threadIdx.x;
-            const uint64_t incl = (uint64_t)at_base + thist[d];
-            if (EX) {  // (digits not kept this round have no items)
-                const uint64_t rb = rtab[(uint64_t)d * RS + sgi];
-                const bool over = thist[d] && incl > cnt0[d * RS + sgi];
-                if (over && rb != ~0ull) atomicOr(err, ERR_REGION);  // (the input changed under the plan)
-                gexcl[d] = rb == ~0ull || over ? ~0ull : rb + at_base;
-            } else {
-                gexcl[d] = at_base;
-                if (incl > C0) atomicOr(err, ERR_REGION);
-            }
-        }
-    } else {
-        // TPD lanes per digit walk its chain (TPDX: an A/B override)
-        constexpr uint32_t TPD = TPDX ? TPDX : (NT / RADIX >= 4 ? 4 : (NT / RADIX >= 2 ? 2 : 1));
-        if (threadIdx.x < RADIX * TPD && KEPT(threadIdx.x / TPD)) {
-            const uint32_t d = threadIdx.x / TPD;
-            const uint64_t excl =
-                (dbg & 1) ? 0ull  // timing ablation only: no look-back (wrong offsets)
-                          : group_lookback<TPD, XLB>(status + d, stile, first, thist[d], epoch, err);
-            if (threadIdx.x % TPD == 0) {
-                const uint64_t incl = excl + thist[d];
-                if (EX) {  // (only kept digits get here)
-                    // exact region: base from the table, size from rg_hist
-                    const uint64_t rb = rtab[(uint64_t)d * RS + sgi];
-                    const bool over = incl > cnt0[d * RS + sgi];
-                    if (over && rb != ~0ull) atomicOr(err, ERR_REGION);  // (the input changed under the plan)
-                    gexcl[d] = rb == ~0ull || over ? ~0ull : rb + excl;
-                } else {
-                    gexcl[d] = excl;
-                    if (incl > C0) atomicOr(err, ERR_REGION);
-                    if (last) cnt0[d * NS + sgi] = (uint32_t)(incl < C0 ? incl : C0);
-                }
-            }
+    if (threadIdx.x < RADIX) {
+        const uint32_t d = threadIdx.x;
+        const uint64_t incl = (uint64_t)at_base + thist[d];
+        if (EX) {  // (digits not kept this round have no items)
+            const uint64_t rb = rtab[(uint64_t)d * RS + sgi];
+            const bool over = thist[d] && incl > cnt0[d * RS + sgi];
+            if (over && rb != ~0ull) atomicOr(err, ERR_REGION);  // (the input changed under the plan)
+            gexcl[d] = rb == ~0ull || over ? ~0ull : rb + at_base;
+        } else {
+            gexcl[d] = at_base;
+            if (incl > C0) atomicOr(err, ERR_REGION);
         }
     }
     __syncthreads();
@@ -396,7 +289,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
             if (EX) {
                 if (gexcl[d] != ~0ull) out[at] = v;
             } else if (at < C0) {
-                out[((uint64_t)d * NS + sgi) * C0 + at] = v;
+                out[((uint64_t)d * RS + sgi) * C0 + at] = v;
             }
         }
     }
@@ -404,178 +297,17 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
 #undef XDIGIT
 }
 
-// ------------------------------------------------- pass 0, owned chains
-// The same extraction with block-owned position chains: chain c (one of S)
-// is a contiguous run of seg_tiles tiles that one 1024-thread block walks in
-// order, carrying each digit's running count in LDS, into region (d, c) of
-// capacity C0 (digit d's region is d * S * C0 items after digit 0's).  No
-// tile waits on another block (no status words, no look-back), and each
-// digit's last partial 128-byte line stays in LDS until a later tile of the
-// chain completes it, so only whole lines leave the CU (rg_pass's write
-// combining).  The next tile's codes load into registers behind this tile's
-// rank and stores.  Rank by one block-wide LDS atomic per item (unstable
-// inside a tile, as rg_extract<BR>).
-template <int NT, int EI, bool RC, int CANON = 0, int WL = 16>
-__global__ __launch_bounds__(NT, NT == 256 ? 4 : 1024 / NT) void rg_xown(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
-                                                   uint32_t Q, uint64_t *__restrict__ out, uint64_t C0, uint32_t S,
-                                                   uint32_t seg_tiles, uint32_t n_tiles,
-                                                   uint32_t *__restrict__ cnt0, uint32_t *__restrict__ counter,
-                                                   uint32_t *__restrict__ err, uint64_t *__restrict__ stp) {
-    constexpr int NWAVE = NT / 64;
-    constexpr int WIN = NT * EI;
-    constexpr int TILE = WIN * (RC ? 2 : 1);
-    constexpr int SI = TILE / NT;
-    static_assert(WIN + 64 <= TILE * 8 && NT >= RADIX, "codes fit in the key staging area; a thread per digit");
-    __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
-    __shared__ uint64_t wcb[RADIX][WL];  // the pending items of digit d at wcb[d][pos % WL]
-    __shared__ uint64_t qpar[RADIX];     // (q bound of the whole-line items << 32) | rel. index of tile item 0
-    __shared__ uint32_t thist[RADIX];
-    __shared__ uint32_t lstart[RADIX];
-    __shared__ uint32_t run[RADIX];
-    __shared__ uint32_t lds_scan[NWAVE];
-    __shared__ uint32_t lds_tile;
-    const int lane = lane_id();
-    const int w = threadIdx.x >> 6;
-    const uint32_t kb = 2u * (uint32_t)k;
-    const uint32_t shift = kb - B1;
-    const uint64_t keymask = kb >= 64 ? ~0ull : ((1ull << kb) - 1);
-    const uint64_t restmask = (1ull << shift) - 1;
-    const uint32_t dstride = S * (uint32_t)C0;  // (the host keeps RADIX * S * C0 < 2^32)
-    uint8_t *scodes = reinterpret_cast<uint8_t *>(skeys);
-    const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
-    for (;;) {
-        const uint32_t c = (uint32_t)grab_tile(counter, &lds_tile);
-        if (c >= S) break;
-        const uint32_t ta = c * seg_tiles;
-        const uint32_t tb = ta + seg_tiles < n_tiles ? ta + seg_tiles : n_tiles;
-        uint64_t *const obase0 = out + (uint64_t)c * C0;
-        if (threadIdx.x < RADIX) run[threadIdx.x] = 0;
-        CodeVecs<NT, EI> cv;
-        if (ta < tb) load_codes<NT, EI>(codes, n_bases, (uint64_t)ta * WIN, cv);
-        for (uint32_t t = ta; t < tb; t++) {
-            const uint64_t wb = (uint64_t)t * WIN;
-            RSTAMP(t, 0);
-            if (threadIdx.x < RADIX) thist[threadIdx.x] = 0;
-            store_codes<NT, EI>(cv, codes, n_bases, wb, scodes);
-            __syncthreads();
-            RSTAMP(t, 1);
-            uint64_t kf[EI], kr[EI];
-            const uint32_t w0 = threadIdx.x * EI;
-            const uint32_t valid = roll<EI, CANON>(scodes, w0, k, keymask, wb + w0, n_bases, kf, kr);
-            // the next tile's codes, behind this tile's work
-            RSTAMP(t, 2);
-            if (t + 1 < tb) load_codes<NT, EI>(codes, n_bases, wb + WIN, cv);
-            uint32_t tcnt;
-            const uint32_t off = block_exclusive_scan<NT>((uint32_t)(__popc(valid) * (RC ? 2 : 1)), SumU32(), 0u,
-                                                          lds_scan, &tcnt);
-            {
-                uint32_t o = off;
-#pragma unroll
-                for (int j = 0; j < EI; j++) {
-                    // the tile-local (window << 1 | strand) above the key bits
-                    // (uniq items only: Q > 0, k <= 25)
-                    const uint64_t tag = Q ? (uint64_t)((w0 + j) << 1) << kb : 0ull;
-                    if ((valid >> j) & 1u) {
-                        skeys[o++] = kf[j] | tag;
-                        if (RC) skeys[o++] = kr[j] | tag | (Q ? 1ull << kb : 0ull);
-                    }
-                }
-            }
-            __syncthreads();
-            RSTAMP(t, 3);
-#define XDIGIT(x) ((uint32_t)(((x) & keymask) >> shift))
-            uint64_t key[SI];
-            uint32_t rank[SI];
-#pragma unroll
-            for (int i = 0; i < SI; i++) key[i] = ib + i * 64 < tcnt ? skeys[ib + i * 64] : 0;
-#pragma unroll
-            for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < tcnt ? atomicAdd(&thist[XDIGIT(key[i])], 1u) : 0u;
-            __syncthreads();
-            const uint32_t ls = block_exclusive_scan<NT>(threadIdx.x < RADIX ? thist[threadIdx.x] : 0u, SumU32(), 0u,
-                                                         lds_scan, (uint32_t *)nullptr);
-            if (threadIdx.x < RADIX) lstart[threadIdx.x] = ls;
-            __syncthreads();
-            RSTAMP(t, 4);
-#pragma unroll
-            for (int i = 0; i < SI; i++)
-                if (ib + i * 64 < tcnt) skeys[lstart[XDIGIT(key[i])] + rank[i]] = key[i];
-            __syncthreads();
-            RSTAMP(t, 5);
-            // a digit whose partial line completes in this tile: its pending
-            // items go out first, 16 lanes per digit
-#pragma unroll
-            for (uint32_t d = threadIdx.x / WL; d < (uint32_t)RADIX; d += NT / WL) {
-                const uint32_t j = threadIdx.x & (WL - 1u), rn = run[d], p = rn & (WL - 1u);
-                if (j < p && ((rn + thist[d]) / WL) > (rn / WL) && rn - p + j < C0)
-                    obase0[d * dstride + rn - p + j] = wcb[d][j];
-            }
-            if (threadIdx.x < RADIX) {
-                // tile item q of digit d goes to position q + off in its
-                // region; whole lines end at fe; positions >= C0 are dropped
-                // (the overflow flag turns the call into KMAN_EFALLBACK)
-                const uint32_t d = threadIdx.x, rn = run[d], off2 = rn - lstart[d];
-                const int32_t fe = (int32_t)((rn + thist[d]) & ~(WL - 1u));
-                const int32_t qlim = (fe < (int32_t)C0 ? fe : (int32_t)C0) - (int32_t)off2;
-                qpar[d] = ((uint64_t)(uint32_t)qlim << 32) | (d * dstride + off2);
-            }
-            __syncthreads();
-            RSTAMP(t, 6);
-#pragma unroll
-            for (int rr = 0; rr < SI; rr++) {
-                const uint32_t q = threadIdx.x + rr * NT;
-                if (q < tcnt) {
-                    const uint64_t kk = skeys[q];
-                    const uint32_t d = XDIGIT(kk);
-                    uint64_t v = kk & restmask;
-                    if (Q) {
-                        const uint64_t f = kk >> kb;  // tile-local (window << 1 | strand)
-                        const uint64_t win = wb + (f >> 1);
-                        v = (v << Q) | (RC ? ((win << 1) | (f & 1u)) : win);
-                    }
-                    const uint64_t qp = qpar[d];
-                    const uint32_t rel = (uint32_t)qp + q;
-                    if ((int32_t)q < (int32_t)(qp >> 32)) obase0[rel] = v;
-                    else wcb[d][rel & (WL - 1u)] = v;
-                }
-            }
-#undef XDIGIT
-            __syncthreads();  // every read of run[] and skeys above before their updates
-            RSTAMP(t, 7);
-            if (threadIdx.x < RADIX) run[threadIdx.x] += thist[threadIdx.x];
-        }
-        __syncthreads();
-        // the chain's last partial lines and its final region counts
-#pragma unroll
-        for (uint32_t d = threadIdx.x / WL; d < (uint32_t)RADIX; d += NT / WL) {
-            const uint32_t j = threadIdx.x & (WL - 1u), rn = run[d], p = rn & (WL - 1u);
-            if (j < p && rn - p + j < C0) obase0[d * dstride + rn - p + j] = wcb[d][j];
-        }
-        if (threadIdx.x < RADIX) {
-            const uint32_t d = threadIdx.x;
-            if (run[d] > C0) atomicOr(err, ERR_REGION);
-            cnt0[d * S + c] = run[d] < C0 ? run[d] : (uint32_t)C0;
-        }
-        __syncthreads();  // (run and wcb are the next chain's)
-    }
-}
-
 // ---------------------------------------------------------------- pass 1
-// One tile of bucket b's items (cid round robin over the buckets; the RS
-// regions (b, *) read as one concatenated sequence, so each bucket is its own
-// look-back chain with no partial tiles but its last).  Digit = item bits
-// [shift, shift + bits), bits <= 9; output region (b << bits | d) of capacity
-// C1.  Per-wave digit counters are u16 pairs (a wave ranks <= 1024 items), so
-// radix 512 keeps the block at 78 KiB of LDS: two blocks per CU.  The
-// bucket's last tile writes the final region counts.
-constexpr int R1 = 512;  // pass-1 radix bound
 // The input of a digit pass: nbk buckets, each the concatenation of nsg <= 64
 // segments (bucket bk, segment s: seg_cnt[bk * nsg + s] items at seg_base[..],
-// or at (bk * nsg + s) * stride when seg_base is null).  Each bucket is its own
-// look-back chain; its tiles are handed out round robin over the buckets.
-// Output region of digit d: ((bk / gsub) << bits | d) * gsub + bk % gsub (gsub
-// > 1 keeps the sub-buckets' outputs apart, as sub-regions of one region).
-// With tag, bits [tag_shift, tag_shift + tag_bits) of each item are replaced
-// by its segment index as it is loaded (the source rank on N > 1).
+// or at (bk * nsg + s) * stride when seg_base is null).  Digit = item bits
+// [shift, shift + bits), bits <= 9.  Output region of digit d: ((bk / gsub)
+// << bits | d) * gsub + bk % gsub (gsub > 1 keeps the sub-buckets' outputs
+// apart, as sub-regions of one region), split into H sub-regions (one per
+// chain of the bucket) of capacity C1.  With tag, bits [tag_shift, tag_shift +
+// tag_bits) of each item are replaced by its segment index / tag_div as it is
+// loaded (the source rank on N > 1).
+constexpr int R1 = 512;  // pass-1 radix bound
 struct PassArgs {
     const uint64_t *in;
     const uint64_t *seg_base;
@@ -596,35 +328,34 @@ struct PassArgs {
     uint32_t fail_div, fail_shift;
 };
 
-// NT threads x SI items per tile: (512, 16) runs two blocks per CU, (1024, 8)
-// one block per CU (half the blocks, so half the open output lines per L2)
-// with the next tile's loads issued behind this tile's stores (PF).
-// WC: write combining -- each digit's last partial 128-byte line (< 16 items)
-// stays in LDS until a later tile completes it, so only whole lines leave the
-// CU, each written within one tile's store phase (64 KiB of LDS: NT = 1024).
-// BR: rank by one block-wide LDS atomic per item (no per-wave counters: the
-// order of equal digits inside a tile is then not stable, which the finish
-// does not need -- it sorts every remaining key bit and compares keys only).
-// NSG > 64 (pass 0 with 128 / 256 chains, or the owned-chain pass 0's S <=
-// NSG segments): each lane holds NSG / 64 of the segment prefixes.
-// EPF (KMAN_RG_PASS=8, A/B only): the next tile's loads issued as soon as this
-// tile's keys are in LDS, before its stores, so that waiting for them does not
-// wait for the stores' write acknowledgements too (vmcnt completes in issue
-// order) -- measured slower: 3.80 vs 3.43 ms
-template <bool ATOMIC, int NT, int SI, bool PF, bool WC = false, bool BR = false, int NSG = 64, bool EPF = false>
-__global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
-                                                 uint32_t *__restrict__ err, uint32_t dbg,
-                                                 uint64_t *__restrict__ stp) {
-    constexpr int TILE = NT * SI, NWAVE = NT / 64;
-    static_assert(NT >= R1 && 64 * SI <= 65535 && (NSG <= 64 || NSG <= NT), "a thread per digit / segment; u16 wave counters");
+// Persistent 1024-thread blocks (one per CU; 141 KiB of LDS), block-owned
+// chains: a block takes a whole chain (bucket b, part h: the h-th of H runs of
+// the bucket's PT-item tiles) and walks its tiles in order, carrying each
+// digit's running count in LDS, so no tile ever waits on another block (no
+// look-back, no status words).  Per tile:
+//   * loads: logical item -> (segment, offset) by ballots over the lanes'
+//     segment prefixes (the 64 items of a wave row are consecutive, so their
+//     segment is the row start's, past the rare boundaries inside the row):
+//     no LDS and no dependent chain, so the loads issue back to back; the
+//     next tile's loads are issued behind this tile's stores;
+//   * rank by one block-wide LDS atomic per item (the order of equal digits
+//     inside a tile is then not stable, which the finish does not need -- it
+//     sorts every remaining key bit and compares keys only), LDS scatter;
+//   * write combining: each digit's last partial 128-byte line (< 16 items)
+//     stays in LDS until a later tile completes it, so only whole lines leave
+//     the CU, each written within one tile's store phase (64 KiB of LDS).
+constexpr int PT_NT = 1024, PT_SI = 8, PT = PT_NT * PT_SI;
+__global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
+                                                   uint32_t *__restrict__ err, uint64_t *__restrict__ stp) {
+    constexpr int NT = PT_NT, SI = PT_SI, TILE = PT, NWAVE = NT / 64;
+    static_assert(NT >= R1 && NT / 16 <= R1, "a thread per digit");
     __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
-    __shared__ uint64_t wcb[WC ? R1 : 1][16];  // WC: the pending items of digit d at wcb[d][pos % 16]
-    // WC, per digit for the store loop: qpar[d] = (q bound of the whole-line
+    __shared__ uint64_t wcb[R1][16];  // the pending items of digit d at wcb[d][pos % 16]
+    // per digit for the store loop: qpar[d] = (q bound of the whole-line
     // items << 32) | the output index of tile item 0 relative to the chain's
     // first sub-region (digit d's sub-region is d * gsub * H after it, and
     // C1 is a multiple of 16, so the low 4 bits are the line slot)
-    __shared__ uint64_t qpar[WC ? R1 : 1];
-    __shared__ uint32_t whist[BR ? 1 : NWAVE][R1 / 2];
+    __shared__ uint64_t qpar[R1];
     __shared__ uint32_t thist[R1];
     __shared__ uint32_t lstart[R1];
     __shared__ uint32_t run[R1];  // the chain's running count per digit
@@ -637,12 +368,7 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
     const int w = threadIdx.x >> 6;
     const uint32_t radix = 1u << bits, dmask = radix - 1;
     const uint32_t nchain = pa.nbk * H;
-    (void)dbg;
 
-    // block-owned chains: a block takes a whole chain (bucket b, part h: the
-    // h-th of H runs of the bucket's tiles) and walks its tiles in order,
-    // carrying each digit's running count in LDS, so no tile ever waits on
-    // another block (no look-back, no status words)
     for (;;) {
         const uint32_t ch = (uint32_t)grab_tile(counter, &lds_tile);
         if (ch >= nchain) break;
@@ -651,28 +377,7 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
         // segment s; segments >= nsg empty) and bases, in registers
         uint32_t spre_l = 0;
         uint64_t sbase_l = 0;
-        // NSG > 64: lane l holds the prefixes of segments l * SPL + j
-        constexpr int SPL = NSG > 64 ? NSG / 64 : 1;
-        uint32_t spre_q[SPL];
-        if (NSG > 64) {
-            uint32_t acc = 0, cq[SPL];
-#pragma unroll
-            for (int j = 0; j < SPL; j++) {
-                const uint32_t sg = (uint32_t)lane * SPL + j;
-                cq[j] = sg < nsg ? pa.seg_cnt[(uint64_t)b * nsg + sg] : 0u;
-                // (pass 0's atomic cursors run past a capacity that overflowed)
-                cq[j] = cq[j] < pa.stride ? cq[j] : (uint32_t)pa.stride;
-                acc += cq[j];
-            }
-            const uint32_t inc = wave_inclusive_scan(acc, SumU32());
-            uint32_t run_ = inc - acc;
-#pragma unroll
-            for (int j = 0; j < SPL; j++) {
-                spre_q[j] = run_;
-                run_ += cq[j];
-            }
-            if (threadIdx.x == 63) s_items = inc;
-        } else {
+        {
             const uint32_t sgl = (uint32_t)lane;
             const uint64_t gi = (uint64_t)b * nsg + sgl;
             uint32_t c = sgl < nsg ? pa.seg_cnt[gi] : 0u;
@@ -691,61 +396,17 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
         // output sub-region of digit d
         const uint64_t reg0 = (uint64_t)(b / pa.gsub) << bits, rsub = b % pa.gsub;
 #define SUBREG(d) (((reg0 | (d)) * pa.gsub + rsub) * H + h)
-        // WC: digit d's sub-region is d * dstride items after digit 0's
+        // digit d's sub-region is d * dstride items after digit 0's
         uint64_t *const obase0 = pa.out + SUBREG(0u) * C1;
         const uint32_t dstride = pa.gsub * H * (uint32_t)C1;
         const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
         uint64_t key[SI];
         uint32_t sgp[(SI + 3) / 4];  // the items' segments, 8 bits each (for the tag)
-        // the keys of tile rt into key[] (logical item -> (segment, offset)
-        // with ballots over the lanes' prefixes: the 64 items of a wave row
-        // are consecutive, so their segment is the row start's, past the
-        // (rare) boundaries inside the row; no LDS and no dependent chain, so
-        // all the loads issue back to back)
         auto load_tile = [&](uint32_t rt) {
             const uint32_t tt0 = rt * TILE;
             const uint32_t nn = items - tt0 < (uint32_t)TILE ? items - tt0 : (uint32_t)TILE;
 #pragma unroll
             for (int i = 0; i < (SI + 3) / 4; i++) sgp[i] = 0;
-            if constexpr (NSG > 64) {
-                // as below with SPL prefixes per lane: the row start's segment
-                // = (segments whose prefix <= the row start) - 1 by ballots,
-                // its prefix by one readlane, then the (rare) boundaries
-                // inside the row -- no LDS, the loads issue back to back
-                auto pick = [&](uint32_t j) {  // spre_q[j], j wave-uniform
-                    uint32_t v = spre_q[0];
-#pragma unroll
-                    for (int jj = 1; jj < SPL; jj++)
-                        if (j == (uint32_t)jj) v = spre_q[jj];
-                    return v;
-                };
-#pragma unroll
-                for (int i = 0; i < SI; i++) {
-                    const uint32_t li0 = tt0 + (uint32_t)w * (SI * 64) + (uint32_t)i * 64;
-                    const uint32_t li = li0 + (uint32_t)lane;
-                    int cnt = 0;
-#pragma unroll
-                    for (int j = 0; j < SPL; j++) cnt += __popcll(__ballot(spre_q[j] <= li0));
-                    uint32_t sg = (uint32_t)(cnt - 1);
-                    uint32_t po = (uint32_t)__builtin_amdgcn_readlane((int)pick(sg % SPL), (int)(sg / SPL));
-#pragma unroll
-                    for (int j = 0; j < SPL; j++) {
-                        uint64_t inrow = __ballot(spre_q[j] > li0 && spre_q[j] <= li0 + 63);
-                        while (inrow) {  // (wave-uniform)
-                            const int l2 = __ffsll((unsigned long long)inrow) - 1;
-                            inrow &= inrow - 1;
-                            const uint32_t s2 = (uint32_t)l2 * SPL + j;
-                            const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)spre_q[j], l2);
-                            if (li >= p2 && s2 > sg) {  // (the largest segment starting at or before li)
-                                sg = s2;
-                                po = p2;
-                            }
-                        }
-                    }
-                    key[i] = ib + i * 64 < nn ? pa.in[((uint64_t)b * nsg + sg) * pa.stride + (li - po)] : 0;
-                }
-                return;
-            }
 #pragma unroll
             for (int i = 0; i < SI; i++) {
                 const uint32_t li0 = tt0 + (uint32_t)w * (SI * 64) + (uint32_t)i * 64;
@@ -770,26 +431,17 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                     }
                 }
                 sgp[i >> 2] |= sg << (8 * (i & 3));
-#ifdef RG_PASS_ABL
-                if (dbg & 32) {  // timing ablation: no loads (uniform synthetic keys)
-                    key[i] = ib + i * 64 < nn ? (uint64_t)(li + 1) * 0x9E3779B97F4A7C15ull : 0;
-                    continue;
-                }
-#endif
                 key[i] = ib + i * 64 < nn ? pa.in[bs + (li - po)] : 0;
             }
         };
-        if (PF && ra < rb) load_tile(ra);
+        if (ra < rb) load_tile(ra);
         for (uint32_t r = ra; r < rb; r++) {
-            if (!BR)
-                for (int i = threadIdx.x; i < NWAVE * R1 / 2; i += NT) (&whist[0][0])[i] = 0;
-            if ((BR || !ATOMIC) && threadIdx.x < R1) thist[threadIdx.x] = 0;
+            if (threadIdx.x < R1) thist[threadIdx.x] = 0;
             __syncthreads();
             const uint32_t t0 = r * TILE;
             const uint32_t n = items - t0 < (uint32_t)TILE ? items - t0 : (uint32_t)TILE;
             RSTAMP(r, 0);
             uint32_t rank[SI];
-            if (!PF) load_tile(r);
             if (pa.tag) {
                 // (a separate loop, so the loads above are not serialised on it)
                 const uint64_t tm = ((1ull << pa.tag_bits) - 1) << pa.tag_shift;
@@ -800,182 +452,54 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
                 }
             }
 #define PDIGIT(x) ((uint32_t)((x) >> shift) & dmask)
-            if (BR) {
 #pragma unroll
-                for (int i = 0; i < SI; i++)
-                    rank[i] = ib + i * 64 < n ? atomicAdd(&thist[PDIGIT(key[i])], 1u) : 0u;
-                __syncthreads();
-                const uint32_t ls = block_exclusive_scan1<NT>(threadIdx.x < R1 ? thist[threadIdx.x] : 0u, SumU32(),
-                                                              0u, lds_scan, (uint32_t *)nullptr);
-                if (threadIdx.x < R1) lstart[threadIdx.x] = ls;
-                __syncthreads();
-#pragma unroll
-                for (int i = 0; i < SI; i++)
-                    if (ib + i * 64 < n) skeys[lstart[PDIGIT(key[i])] + rank[i]] = key[i];
-            } else {
-            if (ATOMIC) {
-#pragma unroll
-                for (int i = 0; i < SI; i++) {
-                    const uint32_t d = PDIGIT(key[i]), hs = (d & 1u) * 16u;
-                    rank[i] = ib + i * 64 < n ? (atomicAdd(&whist[w][d >> 1], 1u << hs) >> hs) & 0xffffu : 0u;
-                }
-                __syncthreads();
-                if (threadIdx.x < R1) {
-                    const uint32_t d = threadIdx.x, hs = (d & 1u) * 16u;
-                    uint32_t c = 0;
-#pragma unroll
-                    for (int ww = 0; ww < NWAVE; ww++) c += (whist[ww][d >> 1] >> hs) & 0xffffu;
-                    thist[d] = c;
-                }
-            } else {
-                // ballot match ranks: no atomics on a few hot addresses (the
-                // small-radix passes of the multi-GPU path use this)
-#pragma unroll
-                for (int i = 0; i < SI; i++) {
-                    const bool valid = ib + i * 64 < n;
-                    const uint32_t d = PDIGIT(key[i]), hs = (d & 1u) * 16u;
-                    uint64_t peers = __ballot(valid);
-                    for (uint32_t bb = 0; bb < bits; bb++) {
-                        const bool set = (d >> bb) & 1u;
-                        const uint64_t mm = __ballot(set);
-                        peers &= set ? mm : ~mm;
-                    }
-                    const uint32_t before = valid ? (whist[w][d >> 1] >> hs) & 0xffffu : 0u;
-                    rank[i] = before + (uint32_t)__popcll(peers & lanemask_lt());
-                    __builtin_amdgcn_wave_barrier();
-                    const int leader = __ffsll((unsigned long long)peers) - 1;
-                    if (valid && lane == leader) atomicAdd(&whist[w][d >> 1], (uint32_t)__popcll(peers) << hs);
-                    __builtin_amdgcn_wave_barrier();
-                }
-                __syncthreads();
-                if (threadIdx.x < R1) {
-                    const uint32_t d = threadIdx.x, hs = (d & 1u) * 16u;
-                    uint32_t c = 0;
-#pragma unroll
-                    for (int ww = 0; ww < NWAVE; ww++) c += (whist[ww][d >> 1] >> hs) & 0xffffu;
-                    thist[d] = c;
-                }
-            }
+            for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < n ? atomicAdd(&thist[PDIGIT(key[i])], 1u) : 0u;
             __syncthreads();
-            // digit pairs (2t, 2t+1), t < R1/2: per-wave exclusive offsets in
-            // place, then the block scan of the digit totals
-            const uint32_t t = threadIdx.x;
-            uint32_t tlo = 0, thi = 0;
-            if (t < R1 / 2) {
-#pragma unroll
-                for (int ww = 0; ww < NWAVE; ww++) {
-                    const uint32_t c = whist[ww][t];
-                    whist[ww][t] = tlo | (thi << 16);
-                    tlo += c & 0xffffu;
-                    thi += c >> 16;
-                }
-            }
-            const uint32_t ls = block_exclusive_scan<NT>(tlo + thi, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
-            if (t < R1 / 2) {
-                lstart[2 * t] = ls;
-                lstart[2 * t + 1] = ls + tlo;
-            }
+            const uint32_t ls = block_exclusive_scan1<NT>(threadIdx.x < R1 ? thist[threadIdx.x] : 0u, SumU32(), 0u,
+                                                          lds_scan, (uint32_t *)nullptr);
+            if (threadIdx.x < R1) lstart[threadIdx.x] = ls;
             __syncthreads();
 #pragma unroll
-            for (int i = 0; i < SI; i++) {
-                if (ib + i * 64 < n) {
-                    const uint32_t d = PDIGIT(key[i]);
-                    skeys[lstart[d] + ((whist[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rank[i]] = key[i];
-                }
-            }
-            }  // !BR
+            for (int i = 0; i < SI; i++)
+                if (ib + i * 64 < n) skeys[lstart[PDIGIT(key[i])] + rank[i]] = key[i];
             __syncthreads();
             RSTAMP(r, 1);
-            if (EPF && r + 1 < rb) load_tile(r + 1);
-            if (WC) {
-                // a digit whose partial line completes in this tile: its
-                // pending items go out first, 16 lanes per digit (one line
-                // per quarter wave, so a store covers 4 lines)
+            // a digit whose partial line completes in this tile: its pending
+            // items go out first, 16 lanes per digit (one line per quarter
+            // wave, so a store covers 4 lines)
 #pragma unroll
-                for (uint32_t d = threadIdx.x >> 4; d < (uint32_t)R1; d += NT / 16) {
-                    const uint32_t j = threadIdx.x & 15u, rn = run[d], p = rn & 15u;
-#ifdef RG_PASS_ABL
-                    if (dbg & 4) continue;  // timing ablation: no stores
-#endif
-                    if (j < p && ((rn + thist[d]) >> 4) > (rn >> 4) && rn - p + j < C1)
-                        obase0[d * dstride + rn - p + j] = wcb[d][j];
-                }
-                if (threadIdx.x < R1) {
-                    // item q of digit d goes to position at = q + off; whole
-                    // lines end at fe; positions >= C1 are dropped (an
-                    // overflowing region raises ERR_REGION and the whole
-                    // call falls back, so where its items go is moot)
-                    const uint32_t d = threadIdx.x, rn = run[d], off = rn - lstart[d];
-                    const int32_t fe = (int32_t)((rn + thist[d]) & ~15u);
-                    const int32_t qlim = (fe < (int32_t)C1 ? fe : (int32_t)C1) - (int32_t)off;
-                    qpar[d] = ((uint64_t)(uint32_t)qlim << 32) | (d * dstride + off);
-                }
-                __syncthreads();  // those wcb reads before the leftovers below
-                // items of whole lines to HBM, the new partial line to LDS
-#pragma unroll
-                for (int rr = 0; rr < SI; rr++) {
-                    const uint32_t q = threadIdx.x + rr * NT;
-                    if (q < n) {
-                        const uint64_t kk = skeys[q];
-                        const uint32_t d = PDIGIT(kk);
-                        const uint64_t qp = qpar[d];
-                        const uint32_t rel = (uint32_t)qp + q;
-                        if ((int32_t)q < (int32_t)(qp >> 32)) {
-#ifdef RG_PASS_ABL
-                            if (dbg & 4) continue;  // timing ablation: no stores
-#endif
-                            obase0[rel] = kk;
-                        } else {
-                            wcb[d][rel & 15u] = kk;
-                        }
-                    }
-                }
-                // the next tile's loads behind the stores (issued before the
-                // store phase instead, they overlap it and the pass slows
-                // down: 6.2 vs 4.9 ms)
-                if (PF && !EPF && r + 1 < rb) load_tile(r + 1);
-            } else if (!PF) {
-                // one store per LDS read: the compiler reuses one register
-                // pair and waits for each store before the next read, which
-                // keeps one store in flight per wave -- measured faster than
-                // 16 back to back (5.7 vs 5.9 ms) with two blocks per CU
-#pragma unroll
-                for (int rr = 0; rr < SI; rr++) {
-                    const uint32_t q = threadIdx.x + rr * NT;
-                    if (q < n) {
-                        const uint64_t kk = skeys[q];
-                        const uint32_t d = PDIGIT(kk);
-                        const uint64_t at = (uint64_t)run[d] + (q - lstart[d]);
-#ifdef RG_PASS_ABL
-                        // timing ablations: no stores (4); stores streamed to
-                        // the chain's own contiguous area, not scattered (8)
-                        if (dbg & 4) continue;
-                        if (dbg & 8) {
-                            pa.out[(uint64_t)ch * radix * C1 + (uint64_t)(r - ra) * TILE + q] = kk;
-                            continue;
-                        }
-#endif
-                        if (at < C1) pa.out[SUBREG(d) * C1 + at] = kk;
-                    }
-                }
-            } else {
-                // every LDS read and address first, the stores back to back,
-                // then the next tile's loads behind them
-                uint64_t wat[SI];
-#pragma unroll
-                for (int rr = 0; rr < SI; rr++) {
-                    const uint32_t q = threadIdx.x + rr * NT;
-                    const uint64_t kk = skeys[q < n ? q : 0];
-                    const uint32_t d = PDIGIT(kk);
-                    const uint64_t at = (uint64_t)run[d] + (q - lstart[d]);
-                    key[rr] = kk;
-                    wat[rr] = q < n && at < C1 ? SUBREG(d) * C1 + at : ~0ull;
-                }
-#pragma unroll
-                for (int rr = 0; rr < SI; rr++)
-                    if (wat[rr] != ~0ull) pa.out[wat[rr]] = key[rr];
-                if (r + 1 < rb) load_tile(r + 1);
+            for (uint32_t d = threadIdx.x >> 4; d < (uint32_t)R1; d += NT / 16) {
+                const uint32_t j = threadIdx.x & 15u, rn = run[d], p = rn & 15u;
+                if (j < p && ((rn + thist[d]) >> 4) > (rn >> 4) && rn - p + j < C1)
+                    obase0[d * dstride + rn - p + j] = wcb[d][j];
             }
+            if (threadIdx.x < R1) {
+                // item q of digit d goes to position at = q + off; whole lines
+                // end at fe; positions >= C1 are dropped (an overflowing
+                // region raises ERR_REGION, so where its items go is moot)
+                const uint32_t d = threadIdx.x, rn = run[d], off = rn - lstart[d];
+                const int32_t fe = (int32_t)((rn + thist[d]) & ~15u);
+                const int32_t qlim = (fe < (int32_t)C1 ? fe : (int32_t)C1) - (int32_t)off;
+                qpar[d] = ((uint64_t)(uint32_t)qlim << 32) | (d * dstride + off);
+            }
+            __syncthreads();  // those wcb reads before the leftovers below
+            // items of whole lines to HBM, the new partial line to LDS
+#pragma unroll
+            for (int rr = 0; rr < SI; rr++) {
+                const uint32_t q = threadIdx.x + rr * NT;
+                if (q < n) {
+                    const uint64_t kk = skeys[q];
+                    const uint32_t d = PDIGIT(kk);
+                    const uint64_t qp = qpar[d];
+                    const uint32_t rel = (uint32_t)qp + q;
+                    if ((int32_t)q < (int32_t)(qp >> 32)) obase0[rel] = kk;
+                    else wcb[d][rel & 15u] = kk;
+                }
+            }
+            // the next tile's loads behind the stores (issued before the
+            // store phase instead, they overlap it and the pass slows down:
+            // 6.2 vs 4.9 ms; issued right after the LDS scatter: 3.80 vs 3.43)
+            if (r + 1 < rb) load_tile(r + 1);
             __syncthreads();  // every read of run[] above before its update
             if (threadIdx.x < R1) run[threadIdx.x] += thist[threadIdx.x];
             RSTAMP(r, 2);
@@ -983,12 +507,11 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
         }
         // the chain's sub-region counts (every digit, also of empty chains)
         __syncthreads();
-        if (WC) {  // the last partial lines, 16 lanes per digit
+        // the last partial lines, 16 lanes per digit
 #pragma unroll
-            for (uint32_t d = threadIdx.x >> 4; d < (uint32_t)R1; d += NT / 16) {
-                const uint32_t j = threadIdx.x & 15u, rn = run[d], p = rn & 15u;
-                if (j < p && rn - p + j < C1) pa.out[SUBREG(d) * C1 + rn - p + j] = wcb[d][j];
-            }
+        for (uint32_t d = threadIdx.x >> 4; d < (uint32_t)R1; d += NT / 16) {
+            const uint32_t j = threadIdx.x & 15u, rn = run[d], p = rn & 15u;
+            if (j < p && rn - p + j < C1) pa.out[SUBREG(d) * C1 + rn - p + j] = wcb[d][j];
         }
         if (threadIdx.x < R1) {
             const uint32_t d = threadIdx.x;
@@ -1008,168 +531,94 @@ __global__ __launch_bounds__(NT, 4) void rg_pass(PassArgs pa, uint32_t *__restri
 
 // ---------------------------------------------------------------- finish
 // One block per region r (regions in key order = grab order): LSD sort of the
-// item bits [Q, Q + rest) in LDS (7-bit digits, per-wave counters, stable),
+// item bits [Q, Q + rest) in LDS (<= 9-bit digits, per-wave counters, stable),
 // run-length pass, output compacted through one look-back over the regions.
 // COUNT: okeys[j], ovals[j] = group size; UNIQ: keys of groups of one and
 // their pos ((window << 1) | strand).
+// T = uint32_t (count mode, rest <= 32 bits, no tag): items held as their key
+// rest in 4 bytes, half the LDS (three blocks per CU); rows staged in two
+// rounds (keys, then counts).
+// CHK (uniq): the early row count (below) is checked against the rows the
+// sorted keys give -- per thread, the singleton marks against heads & tails
+// computed from the keys -- and a disagreement raises ERR_EARLY; CHK = 2 also
+// flips one mark of region `hook` (a test of the check itself).
 enum { RG_COUNT = 1, RG_UNIQ = 2 };
 
-// DB: persistent 1024-thread blocks (one per CU) with two LDS region
-// buffers: while region r is sorted in one, region r + 1 streams into the
-// other by direct global -> LDS loads (global_load_lds_dwordx4: no registers
-// held, unlike PF), so the region loads hide behind the LDS work.
-// T = uint32_t (count mode, rest <= 32 bits, no tag): items held as their
-// key rest in 4 bytes, half the LDS (three blocks per CU); rows staged in two
-// rounds (keys, then counts)
-// PS: persistent blocks without prefetch (a block takes the next region once
-// it has written this one: no block launch per region).  A/B only
-// (KMAN_RG_FIN=3): 7.4 vs 5.8 ms uniq, 9.0 vs 5.6 count -- whatever a block
-// launch costs, the loop costs more
-template <int MODE, typename O, bool ATOMIC, bool PF = false, bool DB = false, typename T = uint64_t, bool PS = false>
-__global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) void rg_finish(const uint64_t *__restrict__ in, uint64_t C1,
-                                                const uint32_t *__restrict__ cnt1, uint32_t Q, uint32_t rest,
-                                                uint32_t rc, uint64_t rbase, uint32_t tag_shift, uint32_t fsub,
-                                                uint64_t *__restrict__ okeys, O *__restrict__ ovals,
-                                                uint64_t *__restrict__ status, uint32_t *__restrict__ counter,
-                                                uint32_t epoch, uint32_t *__restrict__ err, uint32_t dbg,
-                                                uint64_t *__restrict__ stp, uint32_t nreg,
-                                                uint8_t *__restrict__ freg) {
-    constexpr int NT = DB ? 1024 : FT, NW_ = NT / 64;
-    constexpr int IPT = DB ? (FCAP + 1023) / 1024 : FIPT;  // items per thread (DB: 9 x 1024 >= FCAP)
-    constexpr int SCAP = DB ? FCAP + 2 : FCAP;  // (DB: + the alignment holes of two odd sub-regions)
+template <int MODE, typename O, bool ATOMIC, typename T = uint64_t, int CHK = 0>
+__global__ __launch_bounds__(FT, (sizeof(T) == 4 ? 6 : 4)) void rg_finish(
+    const uint64_t *__restrict__ in, uint64_t C1, const uint32_t *__restrict__ cnt1, uint32_t Q, uint32_t rest,
+    uint32_t rc, uint64_t rbase, uint32_t tag_shift, uint32_t fsub, uint64_t *__restrict__ okeys,
+    O *__restrict__ ovals, uint64_t *__restrict__ status, uint32_t *__restrict__ counter, uint32_t epoch,
+    uint32_t *__restrict__ err, uint32_t hook, uint64_t *__restrict__ stp, uint32_t nreg,
+    uint8_t *__restrict__ freg) {
+    constexpr int NT = FT, NW_ = NT / 64;
+    constexpr int IPT = FIPT;  // items per thread
     constexpr bool NARROW = sizeof(T) == 4;
-    static_assert(!NARROW || (MODE == RG_COUNT && !DB && !PF), "narrow items: count mode, one region per block");
-    __shared__ __attribute__((aligned(16))) T sb[DB ? 2 : 1][SCAP];
+    static_assert(!NARROW || MODE == RG_COUNT, "narrow items: count mode");
+    static_assert(CHK == 0 || MODE == RG_UNIQ, "the early count is uniq's");
+    __shared__ __attribute__((aligned(16))) T s[FCAP];
     __shared__ uint32_t wh[NW_][FWORD];  // per-wave digit counters, u16 pairs
     __shared__ uint32_t lds_scan[NW_], lds_scan2[NW_];
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_out;
-    uint32_t cur = 0;
-    T *s = sb[0];
 
     const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
     const uint64_t rmask = (1ull << rest) - 1;
     const uint32_t pw = (uint32_t)w * (IPT * 64) + (uint32_t)lane;  // wave-striped positions
-    // a region r = fsub (1 or 2) sub-regions of capacity C1, concatenated:
-    // position p < m0 at in[r * fsub * C1 + p], p >= m0 at .. + C1 - m0 + p
-    auto counts = [&](uint32_t rr, uint32_t &a0, uint32_t &a1) {
-        a0 = cnt1[(uint64_t)rr * fsub];
-        a1 = fsub > 1 ? cnt1[(uint64_t)rr * fsub + 1] : 0u;
-    };
-    auto load = [&](uint32_t rr, uint32_t a0, uint32_t mm, T (&v)[IPT]) {
-        // (a uniform base and one 32-bit offset per item: few address VGPRs)
-        const uint64_t *src = in + (uint64_t)rr * fsub * C1;
-        const uint32_t skip = (uint32_t)C1 - a0;
-#pragma unroll
-        for (int i = 0; i < IPT; i++) {
-            const uint32_t p = pw + i * 64;
-            // (dbg & 8: timing ablation only -- synthetic items, no HBM reads)
-            v[i] = p < mm ? ((dbg & 8) ? (T)((uint64_t)(rr * 8704u + p) * 0x9E3779B97F4A7C15ull)
-                                       : (T)src[p < a0 ? p : p + skip])
-                          : (T)0;
-        }
-    };
-    // DB: region rr's items into an LDS buffer in 16-byte chunks, one per
-    // lane (a wave's 64 chunks land contiguously at the M0 base): sub-region
-    // 1 starts at the even slot after sub-region 0 (a hole when a0 is odd;
-    // reading one item past an odd count stays inside the capacity C1)
-    auto dma = [&](uint32_t rr, uint32_t a0, uint32_t a1, T *dst_) {
-        uint64_t *dst = reinterpret_cast<uint64_t *>(dst_);  // (DB: T is the u64 item)
-        const uint64_t *src0 = in + (uint64_t)rr * fsub * C1, *src1 = src0 + C1;
-        const uint32_t c0 = (a0 + 1) >> 1, ctot = c0 + ((a1 + 1) >> 1);
-        for (uint32_t cb = (uint32_t)w * 64; cb < ctot; cb += NT) {  // (wave-uniform)
-            const uint32_t c = cb + (uint32_t)lane;
-            if (c < ctot) {
-                const uint64_t *g = c < c0 ? src0 + 2 * c : src1 + 2 * (c - c0);
-                __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void *)(dst + 2 * cb), 16, 0, 0);
-            }
-        }
-    };
-    auto from_lds = [&](uint32_t a0, uint32_t mm, T (&v)[IPT]) {
-        const uint32_t hole = a0 & 1u;
-#pragma unroll
-        for (int i = 0; i < IPT; i++) {
-            const uint32_t p = pw + i * 64;
-            v[i] = p < mm ? s[p + (p >= a0 ? hole : 0u)] : 0;
-        }
-    };
-    // freg (the round path): a region flagged by a pass (a sub-region
-    // overflowed) or here (more than the LDS holds) emits nothing
-    auto fit = [&](uint32_t rr, uint32_t a0, uint32_t a1) -> uint32_t {
-        const uint32_t mm = a0 + a1;
-        if (freg && freg[rr]) return 0u;  // (block-uniform)
-        if (mm <= (uint32_t)FCAP) return mm;
-        if (t == 0) {
-            atomicOr(err, ERR_REGION);  // (block-uniform) more than the LDS holds
-            if (freg) freg[rr] = 1;
-        }
-        return 0u;
-    };
-    // PF (persistent blocks): a block walks regions in grab order; while it
-    // sorts region r the items of the next region rn are in flight to its
-    // registers and the counts of the one after (rnn) to its SGPRs, so HBM
-    // is read during the LDS work (the barriers wait on LDS only).  Regions
-    // are published in key order by the look-back; a block's smallest
-    // unpublished region is always its current one, so the walk cannot stall.
     if (t == 0) s_tile = atomicAdd(counter, 1u);
     __syncthreads();
-    uint32_t r = __builtin_amdgcn_readfirstlane(s_tile);
+    const uint32_t r = __builtin_amdgcn_readfirstlane(s_tile);
     if (r >= nreg) return;
-    uint32_t m0, m1, rn = nreg, n0 = 0, n1 = 0;
-    counts(r, m0, m1);
-    uint32_t m = fit(r, m0, m1);
-    T x[IPT];
-    if (DB) {
-        if (m) dma(r, m0, m1, sb[0]);
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-        from_lds(m0, m, x);
-        if (t == 0) s_tile = atomicAdd(counter, 1u);
-        __syncthreads();
-        rn = __builtin_amdgcn_readfirstlane(s_tile);
-        if (rn < nreg) {
-            counts(rn, n0, n1);
-            if (fit(rn, n0, n1)) dma(rn, n0, n1, sb[1]);
-        }
-    } else {
-        load(r, m0, m, x);
-    }
-    if (PF) {
-        __syncthreads();  // (every read of s_tile above before it is reused)
-        if (t == 0) s_tile = atomicAdd(counter, 1u);
-        __syncthreads();
-        rn = __builtin_amdgcn_readfirstlane(s_tile);
-        if (rn < nreg) counts(rn, n0, n1);
-    }
-    for (;;) {
     RSTAMP(r, 0);
-    uint32_t rnn = nreg, nn0 = 0, nn1 = 0;
+    // a region r = fsub (1 or 2 ...) sub-regions of capacity C1, concatenated:
+    // position p < m0 at in[r * fsub * C1 + p], p >= m0 at .. + C1 - m0 + p
+    const uint32_t m0 = cnt1[(uint64_t)r * fsub];
+    const uint32_t m1 = fsub > 1 ? cnt1[(uint64_t)r * fsub + 1] : 0u;
+    // freg (the round path): a region flagged by a pass (a sub-region
+    // overflowed) or here (more than the LDS holds) emits nothing
+    uint32_t m = m0 + m1;
+    if (freg && freg[r]) {
+        m = 0;  // (block-uniform)
+    } else if (m > (uint32_t)FCAP) {
+        if (t == 0) {
+            atomicOr(err, ERR_REGION);  // (block-uniform) more than the LDS holds
+            if (freg) freg[r] = 1;
+        }
+        m = 0;
+    }
+    T x[IPT];
+    {
+        // (a uniform base and one 32-bit offset per item: few address VGPRs)
+        const uint64_t *src = in + (uint64_t)r * fsub * C1;
+        const uint32_t skip = (uint32_t)C1 - m0;
+#pragma unroll
+        for (int i = 0; i < IPT; i++) {
+            const uint32_t p = pw + i * 64;
+            x[i] = p < m ? (T)src[p < m0 ? p : p + skip] : (T)0;
+        }
+    }
+#ifdef KMAN_RG_STAMPS
+    __builtin_amdgcn_s_waitcnt(0);  // (diagnostic build: phase 1 = the wait for the region's items)
+    if (stp && t == 0) stp[(uint64_t)r * 8 + 7] = m;  // (the region's items, beside its phase stamps)
+#endif
+    RSTAMP(r, 1);
 
     // stable LSD passes of <= 9 bits.  Ranks: per-wave u16 counters packed two
     // to a word (a wave ranks <= 64 * FIPT items), same-word LDS atomics of one
     // wave return in lane order (probed: ATOMIC), else ballot match-any.
-    // (dbg & 1: timing ablation only, no sort passes)
-#ifdef KMAN_RG_STAMPS
-    __builtin_amdgcn_s_waitcnt(0);  // (diagnostic build: phase 1 = the wait for the region's items)
-#endif
-    RSTAMP(r, 1);
-#ifdef KMAN_RG_STAMPS
-    if (stp && t == 0) stp[(uint64_t)r * 8 + 7] = m;  // (the region's items, beside its phase stamps)
-#endif
-    const uint32_t np = (dbg & 1) ? 0u : (rest + FBITS - 1) / FBITS;
-    // EARLY (uniq, single-GPU items): the region's row count is found after
-    // the second-to-last pass, when equal keys already share a run of equal
-    // low bits (a run of one item almost always), and published then, so the
-    // look-back after the last pass finds its predecessors' counts in place
-    // instead of waiting for the slowest region in flight (1.0 of 5.8 ms,
-    // the dbg & 4 ablation).  A singleton's mark rides in item bit 63 (above
-    // the key rest and the pos: the top bit of the pass-1 digit, constant in
-    // a region and never read here, so it is overwritten) through the last
-    // pass.  KMAN_RG_EARLY=0: A/B.
+    const uint32_t np = (rest + FBITS - 1) / FBITS;
+    // EARLY (uniq): the region's row count is found after the second-to-last
+    // pass, when equal keys already share a run of equal low bits (a run of
+    // one item almost always), and published then, so the look-back after the
+    // last pass finds its predecessors' counts in place instead of waiting
+    // for the slowest region in flight (1.0 of 5.8 ms).  A singleton's mark
+    // rides in item bit 63 (above the key rest and the pos: the top bit of the
+    // pass-1 digit, constant in a region and never read here, so it is
+    // overwritten) through the last pass.
     constexpr uint64_t MARK = 1ull << 63;
     // (the round path's items carry the source rank in the 9 bits at
     // tag_shift, read as 8 bits below: bit 63 is free there as well)
-    const bool early = MODE == RG_UNIQ && (!tag_shift || tag_shift + 8 <= 63) && np >= 2 && !(dbg & 16);
+    const bool early = MODE == RG_UNIQ && (!tag_shift || tag_shift + 8 <= 63) && np >= 2;
     uint32_t etot = 0;
     uint32_t at = 0;
     for (uint32_t p = 0; p < np; p++) {
@@ -1305,6 +754,7 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
                 }
                 S |= (uint32_t)single << i;
             }
+            if (CHK == 2 && r == hook && t == 0) S ^= 1u;  // (the check's own test: one wrong mark)
             // (bit 63 is the top bit of the region's pass-1 digit before it
             // becomes the mark: set or cleared on every item)
 #pragma unroll
@@ -1319,15 +769,6 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
             if (pw + i * 64 < m) s[pw + i * 64] = x[i];
         __syncthreads();
     }
-    if (PF) {
-        // the next region's items are loaded now (x is dead: the sorted
-        // region is in LDS), arriving while this one is grouped and written
-        if (t == 0) s_tile = atomicAdd(counter, 1u);
-        if (rn < nreg) load(rn, n0, n0 + n1 <= (uint32_t)FCAP && !(freg && freg[rn]) ? n0 + n1 : 0u, x);
-        __syncthreads();
-        rnn = __builtin_amdgcn_readfirstlane(s_tile);
-        if (rnn < nreg) counts(rnn, nn0, nn1);
-    }
 
     RSTAMP(r, 2);
     // ---- run-length pass (thread t: sorted positions t*FIPT ..)
@@ -1337,21 +778,39 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
     T kv[IPT];
 #pragma unroll
     for (int j = 0; j < IPT; j++) kv[j] = q0 + j < m ? s[q0 + j] : 0;
+    if (early) {
+        // the early count's marks are the rows (heads & tails below)
+        uint32_t marks = 0;
 #pragma unroll
-    for (int j = 0; j < IPT; j++) {
-        const uint32_t q = q0 + j;
-        if (early) {  // (the marks of the early count: heads & tails below)
-            const bool e = q < m && ((uint64_t)kv[j] & MARK);
-            heads |= (uint32_t)e << j;
-            tails |= (uint32_t)e << j;
-            continue;
+        for (int j = 0; j < IPT; j++) marks |= (uint32_t)(q0 + j < m && ((uint64_t)kv[j] & MARK)) << j;
+        heads = tails = marks;
+        if (CHK) {
+            // the rows the sorted keys give: a singleton differs from both
+            // neighbours in its whole rest
+            uint32_t single = 0;
+            const uint64_t kl = q0 > 0 && q0 - 1 < m ? RKEY((uint64_t)s[q0 - 1]) : ~0ull;
+            const uint64_t kr = q0 + IPT < m ? RKEY((uint64_t)s[q0 + IPT]) : ~0ull;
+#pragma unroll
+            for (int j = 0; j < IPT; j++) {
+                const uint32_t q = q0 + j;
+                const uint64_t kq = RKEY((uint64_t)kv[j]);
+                const bool h = q == 0 || kq != (j ? RKEY((uint64_t)kv[j - 1]) : kl);
+                const bool e = q + 1 == m || kq != (j + 1 < IPT ? RKEY((uint64_t)kv[j + 1]) : kr);
+                single |= (uint32_t)(q < m && h && e) << j;
+            }
+            if (single != marks) atomicOr(err, ERR_EARLY);
         }
-        if (q < m) {
-            const uint64_t kq = RKEY(kv[j]);
-            const bool h = q == 0 || kq != RKEY(j ? kv[j - 1] : s[q - 1]);
-            const bool e = q + 1 == m || kq != RKEY(j + 1 < IPT ? kv[j + 1] : s[q + 1]);
-            heads |= (uint32_t)h << j;
-            tails |= (uint32_t)e << j;
+    } else {
+#pragma unroll
+        for (int j = 0; j < IPT; j++) {
+            const uint32_t q = q0 + j;
+            if (q < m) {
+                const uint64_t kq = RKEY(kv[j]);
+                const bool h = q == 0 || kq != RKEY(j ? kv[j - 1] : s[q - 1]);
+                const bool e = q + 1 == m || kq != RKEY(j + 1 < IPT ? kv[j + 1] : s[q + 1]);
+                heads |= (uint32_t)h << j;
+                tails |= (uint32_t)e << j;
+            }
         }
     }
     uint32_t emit = 0, lh_before = 0;
@@ -1367,15 +826,11 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
     uint32_t total;
     // (its barrier orders every read of s above before the staging writes below)
     const uint32_t off = block_exclusive_scan1<NT>(ne, SumU32(), 0u, lds_scan, &total);
-    if (early && t == 0 && total != etot) atomicOr(err, 1u << 9);  // (tripwire: the early count was not the rows')
-    // (the scan's barriers ordered every read of s above before the writes below)
+    if (early && t == 0 && total != etot) atomicOr(err, ERR_EARLY);  // (the published count is not the rows')
     RSTAMP(r, 3);
     if (w == 0) {
-        // (dbg & 4: timing ablation only -- regions placed by one atomic
-        // cursor in completion order, no look-back: rows unsorted across regions)
-        const uint64_t ob = (dbg & 4) ? (lane == 0 ? atomicAdd((unsigned long long *)(status + nreg), (unsigned long long)total) : 0ull)
-                            : early ? wave_lookback_published<0>(status, r, total, epoch, err)
-                                    : wave_lookback<0>(status, r, total, epoch, err);
+        const uint64_t ob = early ? wave_lookback_published<0>(status, r, total, epoch, err)
+                                  : wave_lookback<0>(status, r, total, epoch, err);
         if (lane == 0) s_out = ob;
     }
     // the emitted rows compacted in LDS as one word each: the item itself
@@ -1400,75 +855,33 @@ __global__ __launch_bounds__(DB ? 1024 : FT, DB ? 1 : (sizeof(T) == 4 ? 6 : 4)) 
     __syncthreads();
     RSTAMP(r, 4);
     const uint64_t ob = s_out;
-    if (!(dbg & 2)) {  // (dbg & 2: timing ablation only, no output writes)
-        const uint64_t qmask = Q ? ((1ull << Q) - 1) : 0ull;
-        for (uint32_t q = t; q < total; q += NT) {
-            const uint64_t v = s[q];
-            okeys[ob + q] = ((uint64_t)(r + rbase) << rest) | RKEY(v);
-        }
-        if constexpr (NARROW) {
-            __syncthreads();  // (every key read before the sizes overwrite them)
-            stage(true);
-            __syncthreads();
-        }
-        for (uint32_t q = t; q < total; q += NT) {
-            const uint64_t v = s[q];
-            if constexpr (MODE == RG_UNIQ) {
-                const uint64_t idx = v & qmask;
-                const uint64_t pos = rc ? idx : (idx << 1);
-                // N > 1: the source rank (tagged into the item by the pass after
-                // the exchange) in bits 56-63, as DistPipeline's payloads
-                // (ranks < 256: 8 tag bits, so bit 63 -- the early count's mark -- is not read)
-                ovals[ob + q] = (O)(tag_shift ? pos | (((v >> tag_shift) & 0xffull) << 56) : pos);
-            } else if constexpr (NARROW) {
-                ovals[ob + q] = (O)v;
-            } else {
-                ovals[ob + q] = (O)(v >> rest);
-            }
+    const uint64_t qmask = Q ? ((1ull << Q) - 1) : 0ull;
+    for (uint32_t q = t; q < total; q += NT) {
+        const uint64_t v = s[q];
+        okeys[ob + q] = ((uint64_t)(r + rbase) << rest) | RKEY(v);
+    }
+    if constexpr (NARROW) {
+        __syncthreads();  // (every key read before the sizes overwrite them)
+        stage(true);
+        __syncthreads();
+    }
+    for (uint32_t q = t; q < total; q += NT) {
+        const uint64_t v = s[q];
+        if constexpr (MODE == RG_UNIQ) {
+            const uint64_t idx = v & qmask;
+            const uint64_t pos = rc ? idx : (idx << 1);
+            // N > 1: the source rank (tagged into the item by the pass after
+            // the exchange) in bits 56-63, as DistPipeline's payloads
+            // (ranks < 256: 8 tag bits, so bit 63 -- the early count's mark -- is not read)
+            ovals[ob + q] = (O)(tag_shift ? pos | (((v >> tag_shift) & 0xffull) << 56) : pos);
+        } else if constexpr (NARROW) {
+            ovals[ob + q] = (O)v;
+        } else {
+            ovals[ob + q] = (O)(v >> rest);
         }
     }
 #undef RKEY
     RSTAMP(r, 5);
-    if (PS) {
-        __syncthreads();  // (every read of s / s_out / s_tile above before the next region writes them)
-        if (t == 0) s_tile = atomicAdd(counter, 1u);
-        __syncthreads();
-        r = __builtin_amdgcn_readfirstlane(s_tile);
-        if (r >= nreg) break;  // (block-uniform)
-        counts(r, m0, m1);
-        m = fit(r, m0, m1);
-        load(r, m0, m, x);
-        continue;
-    }
-    if (!(PF || DB) || rn >= nreg) break;
-    __syncthreads();  // (every read of s / s_out / s_tile above before the next region writes them)
-    if (DB) {
-        // region rn has landed in the other buffer (vmcnt: every load and
-        // store of this wave; the barrier: every wave's chunks)
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-        cur ^= 1u;
-        s = sb[cur];
-        r = rn;
-        m0 = n0;
-        m = fit(r, n0, n1);
-        from_lds(m0, m, x);
-        if (t == 0) s_tile = atomicAdd(counter, 1u);
-        __syncthreads();
-        rn = __builtin_amdgcn_readfirstlane(s_tile);
-        if (rn < nreg) {
-            counts(rn, n0, n1);
-            if (fit(rn, n0, n1)) dma(rn, n0, n1, sb[cur ^ 1u]);
-        }
-        continue;
-    }
-    r = rn;
-    m0 = n0;
-    m = fit(r, n0, n1);
-    rn = rnn;
-    n0 = nn0;
-    n1 = nn1;
-    }
 }
 
 struct RegionPlan {
@@ -1482,9 +895,6 @@ struct RegionPlan {
     uint64_t C1h;        // pass-1 sub-region capacity
     uint32_t n_tiles0, seg_tiles, maxt1;
     uint32_t ei;         // windows per thread of pass 0
-    bool own;            // pass 0 = rg_xown (S block-owned chains), else rg_extract (RS look-back segments)
-    uint32_t xnt;        // rg_xown block size
-    uint32_t S;          // pass-0 segments (chains)
     uint64_t off_r1, off_c0, off_c1, off_lim, bytes;
 };
 
@@ -1493,7 +903,7 @@ uint32_t bitlen(uint64_t x) { return x ? 64u - (uint32_t)__builtin_clzll(x) : 0u
 int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan *pl) {
     if (mode != KMAN_FINISH_COUNT && mode != KMAN_FINISH_UNIQ) return KMAN_EINVAL;
     if (k < 2 || k > 32) return KMAN_EINVAL;
-    if (getenv("KMAN_NO_REGION")) return KMAN_EFALLBACK;
+    if (getenv("KMAN_NO_REGION")) return KMAN_EFALLBACK;  // (tests: the general path)
     // uniq: k <= 25 (the tile-local window index rides above the key bits in
     // pass 0); count items carry no index: k <= 32
     if ((mode == KMAN_FINISH_UNIQ && k > 25) || n_bases == 0) return KMAN_EFALLBACK;
@@ -1514,151 +924,40 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     if (p.K < B1 + b2 + 1) return KMAN_EFALLBACK;
     p.B2 = b2;
     p.rest = p.K - B1 - b2;
-    {
-        // KMAN_RG_OWN=1: pass 0 by block-owned chains (rg_xown; A/B only --
-        // exact HBM traffic, 9.15 GB vs 14.3 for the config-2 step, but 4.9 ms
-        // at 256 threads (5.4 at 512 or 1024) vs 3.7 for rg_extract)
-        const char *e = getenv("KMAN_RG_OWN");
-        p.own = e && atoi(e) != 0;
-    }
-    if (p.own) {
-        // 1024 threads x 8 windows (4 with -r); up to 256 chains (one per
-        // CU), each at least 4 tiles long
-        const char *e = getenv("KMAN_RG_XNT");  // 512 / 1024: two / one block per CU (A/B timing)
-        p.xnt = e && atoi(e) == 1024 ? 1024u : (e && atoi(e) == 512 ? 512u : 256u);
-        p.ei = p.rc ? 4u : 8u;
-        const uint64_t win = (uint64_t)p.xnt * p.ei;
-        p.n_tiles0 = (uint32_t)ceil_div(n_bases, win);
-        const uint64_t smax = 256ull * (1024 / p.xnt);  // the resident blocks
-        uint64_t s = ceil_div(p.n_tiles0, 4);
-        s = s < 1 ? 1 : (s > smax ? smax : s);
-        p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, s);
-        p.S = (uint32_t)ceil_div(p.n_tiles0, p.seg_tiles);
-    } else {
-        // windows per thread: 16 (8 with -r: two items per window) makes
-        // 8192-item tiles, 69 KiB of LDS, two blocks per CU.  With the
-        // look-back chains, 12 (6144-item tiles, three blocks per CU) was
-        // faster (3.92 vs 4.77 ms); with the atomic region cursors a tile waits
-        // on nothing and the longer digit runs win: 3.27 vs 3.35 ms (8, four
-        // blocks per CU: 3.83).  KMAN_RG_EI=12 / 8 select those for A/B.
-        const char *e = getenv("KMAN_RG_EI");
-        const int ei = e ? atoi(e) : 16;
-        if (p.rc) p.ei = ei == 16 ? 8u : 6u;  // two windows per item slot
-        else p.ei = ei == 16 ? 16u : (ei == 8 && !p.canon ? 8u : 12u);
-        const uint64_t win = (uint64_t)RT * p.ei;
-        p.n_tiles0 = (uint32_t)ceil_div(n_bases, win);
-        // RS = 64 look-back chains (KMAN_RG_NS=128 / 256: shorter chains, A/B
-        // only).  With the XCD-partitioned tickets and the segment prefixes
-        // held in registers (SPL per lane), one box, ms extract / pass: 64:
-        // 3.44 / 3.33, 128: 3.33 / 3.41, 256: 3.29 / 3.74-3.90 -- the step
-        // within 0.5 % at 128, so the default stays 64 (one prefix per lane)
-        const char *e2 = getenv("KMAN_RG_NS");
-        const uint32_t ns = e2 && (atoi(e2) == 128 || atoi(e2) == 256) ? (uint32_t)atoi(e2) : (uint32_t)RS;
-        p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, ns);
-        p.S = ns;
-    }
-    const uint64_t e0 = p.W / ((uint64_t)RADIX * p.S);
-    // (owned chains are longer than the look-back segments of small inputs:
-    // a 1024-item floor keeps a local repeat inside a region)
-    p.C0 = ceil_div(e0 + e0 / 2 + (p.own ? 1024 : 256), 64) * 64;
-    if ((uint64_t)RADIX * p.S * p.C0 >= (1ull << 32)) return KMAN_EFALLBACK;  // (32-bit item indices)
+    // windows per thread: 16 (8 with -r: two items per window) makes
+    // 8192-item tiles, 69 KiB of LDS, two blocks per CU: with the atomic
+    // region cursors a tile waits on nothing and the longer digit runs win
+    // (3.27 vs 3.35 ms with 12 windows, three blocks per CU; 8, four blocks:
+    // 3.83)
+    p.ei = p.rc ? 8u : 16u;
+    const uint64_t win = (uint64_t)RT * p.ei;
+    p.n_tiles0 = (uint32_t)ceil_div(n_bases, win);
+    p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, RS);
+    const uint64_t e0 = p.W / ((uint64_t)RADIX * RS);
+    p.C0 = ceil_div(e0 + e0 / 2 + 256, 64) * 64;
+    if ((uint64_t)RADIX * RS * p.C0 >= (1ull << 32)) return KMAN_EFALLBACK;  // (32-bit item indices)
     const uint64_t e1 = p.W >> (B1 + b2);
     uint64_t c1 = ceil_div(e1 + e1 / 2 + 512, 64) * 64;
     p.C1 = c1 < (uint64_t)FCAP ? c1 : (uint64_t)FCAP;
     // pass 1 runs H = 2 block-owned chains per bucket (its first and second
     // half of tiles) into H sub-regions per region that the finish
-    // concatenates: 512 chains for the 512 resident blocks
-    {
-        const char *e = getenv("KMAN_RG_H");  // A/B timing only
-        p.H = e && atoi(e) == 1 ? 1u : 2u;
-    }
+    // concatenates: 512 chains for the 256 resident blocks
+    p.H = 2;
     p.C1h = p.C1;  // either half may hold most of a region (position-skewed repeats)
-    p.maxt1 = (uint32_t)ceil_div((uint64_t)ceil_div(p.S, p.H) * p.C0, T1);
+    p.maxt1 = (uint32_t)ceil_div((uint64_t)ceil_div(RS, p.H) * p.C0, T1);
     const uint64_t nreg = 1ull << (B1 + b2);
-    p.off_r1 = (uint64_t)RADIX * p.S * p.C0 * 8;
+    p.off_r1 = (uint64_t)RADIX * RS * p.C0 * 8;
     p.off_c0 = p.off_r1 + nreg * p.H * p.C1h * 8;
-    p.off_c1 = p.off_c0 + (uint64_t)RADIX * p.S * 4;
+    p.off_c1 = p.off_c0 + (uint64_t)RADIX * RS * 4;
     p.off_lim = p.off_c1 + nreg * p.H * 4;
     p.bytes = p.off_lim + 64;
     *pl = p;
     return KMAN_OK;
 }
 
-template <int NT, int SI, bool PF, bool WC = false, bool BR = false, bool EPF = false>
-void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
-    if constexpr (BR) {  // no ordered LDS atomics needed
-        const void *fn = (const void *)rg_pass<true, NT, SI, PF, WC, BR, 64, EPF>;
-        const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, NT, (uint64_t)pa.nbk * pa.H);
-        hipLaunchKernelGGL((rg_pass<true, NT, SI, PF, WC, BR, 64, EPF>), dim3(grid), dim3(NT), 0, ctx->stream, pa, counter,
-                           ctx->d_err, dbg, stp);
-    } else {
-    const void *fn = ctx->lds_atomic_ordered ? (const void *)rg_pass<true, NT, SI, PF, WC>
-                                             : (const void *)rg_pass<false, NT, SI, PF, WC>;
-    const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, NT, (uint64_t)pa.nbk * pa.H);
-    if (ctx->lds_atomic_ordered)
-        hipLaunchKernelGGL((rg_pass<true, NT, SI, PF, WC>), dim3(grid), dim3(NT), 0, ctx->stream, pa, counter,
-                           ctx->d_err, dbg, stp);
-    else
-        hipLaunchKernelGGL((rg_pass<false, NT, SI, PF, WC>), dim3(grid), dim3(NT), 0, ctx->stream, pa, counter,
-                           ctx->d_err, dbg, stp);
-    }
-}
-
-// block shape of the digit pass: KMAN_RG_PASS = 0 (512 x 16, two blocks per
-// CU), 1 (the same with the next tile prefetched), 2 (1024 x 8, one block per
-// CU, prefetched), 3 (1024 x 8 with write combining), 4 (the same with
-// prefetch), 5 (4 with the block-wide rank), 6 (0 with the block-wide rank),
-// 7 (5 with 10 items per thread).  5 is the default.  One box, ms: 0 4.66,
-// 4 4.29, 5 3.78, 6 4.69; later boxes: 5 3.49-3.58 with per-digit store
-// parameters, 3.54 with 32-bit relative output indices (7: 3.56).
-void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint32_t dbg, uint64_t *stp) {
-    if (pa.nsg > 64) {  // 128 / 256 pass-0 chains, or the owned-chain pass 0's segments (<= 1024, no seg_base, no tag): shape 5
-        auto go = [&](auto nsg_c) {
-            constexpr int NSG = decltype(nsg_c)::value;
-            const void *fn = (const void *)rg_pass<true, 1024, 8, true, true, true, NSG>;
-            const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, 1024, (uint64_t)pa.nbk * pa.H);
-            hipLaunchKernelGGL((rg_pass<true, 1024, 8, true, true, true, NSG>), dim3(grid), dim3(1024), 0,
-                               ctx->stream, pa, counter, ctx->d_err, dbg, stp);
-        };
-        if (pa.nsg <= 128) go(std::integral_constant<int, 128>{});
-        else if (pa.nsg <= 256) go(std::integral_constant<int, 256>{});
-        else go(std::integral_constant<int, 1024>{});
-        return;
-    }
-    const char *e = getenv("KMAN_RG_PASS");
-    const int shape = e ? atoi(e) : 5;
-    // a few digits (pass 1b: 1-4 bits) rank by the same block-wide LDS
-    // atomics: config 4's shard 290.6 -> 277.4 ms per step, the skewed
-    // spectrum line's passes 3 ms faster, than ballots (rg_pass<false>:
-    // per-wave counters, one update per distinct digit of a row), which
-    // KMAN_RG_1B=0 keeps for A/B
-    static const char *e1b = getenv("KMAN_RG_1B");
-    if (pa.bits <= 4 && shape >= 3 && e1b && atoi(e1b) == 0) {
-        // (KMAN_RG_SMALL=0: 512-thread blocks without write combining, for
-        // A/B timing; pass 1b at world 1, ms: 8.7 vs 7.2 for the default)
-        const char *e2 = getenv("KMAN_RG_SMALL");
-        if (!e2 || atoi(e2) != 0) {
-            const void *fn = (const void *)rg_pass<false, 1024, 8, true, true, false>;
-            const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, 1024, (uint64_t)pa.nbk * pa.H);
-            hipLaunchKernelGGL((rg_pass<false, 1024, 8, true, true, false>), dim3(grid), dim3(1024), 0, ctx->stream,
-                               pa, counter, ctx->d_err, dbg, stp);
-        } else {
-            const void *fn = (const void *)rg_pass<false, RT, RSI, false, false, false>;
-            const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, RT, (uint64_t)pa.nbk * pa.H);
-            hipLaunchKernelGGL((rg_pass<false, RT, RSI, false, false, false>), dim3(grid), dim3(RT), 0, ctx->stream,
-                               pa, counter, ctx->d_err, dbg, stp);
-        }
-        return;
-    }
-    if (shape == 5) launch_pass_as<1024, 8, true, true, true>(ctx, pa, counter, dbg, stp);
-    else if (shape == 8) launch_pass_as<1024, 8, true, true, true, true>(ctx, pa, counter, dbg, stp);
-    else if (shape == 7) launch_pass_as<1024, 10, true, true, true>(ctx, pa, counter, dbg, stp);
-    else if (shape == 6) launch_pass_as<RT, RSI, false, false, true>(ctx, pa, counter, dbg, stp);
-    else if (shape == 4) launch_pass_as<1024, 8, true, true>(ctx, pa, counter, dbg, stp);
-    else if (shape == 3) launch_pass_as<1024, 8, false, true>(ctx, pa, counter, dbg, stp);
-    else if (shape == 2) launch_pass_as<1024, 8, true>(ctx, pa, counter, dbg, stp);
-    else if (shape == 1) launch_pass_as<RT, RSI, true>(ctx, pa, counter, dbg, stp);
-    else launch_pass_as<RT, RSI, false>(ctx, pa, counter, dbg, stp);
+void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint64_t *stp) {
+    const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, (const void *)rg_pass, PT_NT, (uint64_t)pa.nbk * pa.H);
+    hipLaunchKernelGGL(rg_pass, dim3(grid), dim3(PT_NT), 0, ctx->stream, pa, counter, ctx->d_err, stp);
 }
 
 struct FinishArgs {
@@ -1673,214 +972,112 @@ struct FinishArgs {
     uint8_t *freg = nullptr;  // per-region overflow flags (the round path), else null
 };
 
-template <int MODE, typename O, bool ATOMIC, bool PF, bool DB = false, typename T = uint64_t, bool PS = false>
+template <int MODE, typename O, bool ATOMIC, typename T = uint64_t, int CHK = 0>
 void launch_finish_as(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ovals, uint32_t epoch,
-                      uint32_t *counter, uint32_t dbg, uint64_t *stp) {
-    const void *fn = (const void *)rg_finish<MODE, O, ATOMIC, PF, DB, T, PS>;
-    constexpr int NT = DB ? 1024 : FT;
-    // (PS: the LDS-bound residency, 2 or 3 blocks per CU, times two -- the
-    // occupancy query under-reports these launch bounds; surplus blocks find
-    // no region left and leave)
-    const uint32_t ps_grid = (uint32_t)(2 * 256 * (sizeof(T) == 4 ? 3 : 2));
-    const uint32_t grid = PS ? (ps_grid < f.nreg ? ps_grid : f.nreg)
-                             : PF || DB ? (uint32_t)kman_persistent_grid(ctx, fn, NT, f.nreg) : f.nreg;
-    hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, PF, DB, T, PS>), dim3(grid), dim3(NT), 0, ctx->stream, f.in, f.C1, f.cnt, f.Q,
-                       f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status, counter, epoch,
-                       ctx->d_err, dbg, stp, f.nreg, f.freg);
+                      uint32_t *counter, uint32_t hook, uint64_t *stp) {
+    hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, T, CHK>), dim3(f.nreg), dim3(FT), 0, ctx->stream, f.in, f.C1, f.cnt,
+                       f.Q, f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status, counter,
+                       epoch, ctx->d_err, hook, stp, f.nreg, f.freg);
 }
 
-// one block per region; KMAN_RG_FIN=1: persistent blocks that prefetch the
-// next region while sorting this one (A/B only: the prefetch registers spill,
-// 11.1 vs 5.7 ms on the bench config); KMAN_RG_FIN=2: persistent 1024-thread
-// blocks, the next region streamed into a second LDS buffer by direct
-// global -> LDS loads (no registers held; parity green) -- 11.1-11.2 ms too:
-// with one block per CU the sort's barriers are exposed, where two blocks
-// per CU interleave them, so the loads were never the bound
+// The early-count check of the uniq finish (rg_finish CHK): KMAN_RG_CHECK=1
+// (or "hook=<region>": also one wrong mark in that region, the check's own
+// GPU test) selects the checked kernel; 0 / unset, the plain one.
+struct EarlyCheck {
+    int chk;
+    uint32_t hook;
+};
+EarlyCheck early_check() {
+    const char *e = getenv("KMAN_RG_CHECK");
+    if (!e || !*e || !strcmp(e, "0")) return {0, ~0u};
+    if (!strncmp(e, "hook=", 5)) return {2, (uint32_t)strtoul(e + 5, nullptr, 10)};
+    return {1, ~0u};
+}
+
+// one block per region; count rows whose key rest fits 32 bits hold 4-byte
+// items in LDS (three blocks per CU: count finish 5.95 -> 5.68 ms, config-4
+// shard 84.7 -> 78.3 ms).  Without the probed lane-ordered LDS atomics the
+// ranks are ballots (8-byte items: the ballot ranks overflow the 80 VGPRs of
+// three blocks per CU -- 2.5 KB of spills per lane -- so no narrow variant).
 template <int MODE, typename O>
 void launch_finish(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ovals, uint32_t epoch,
-                   uint32_t *counter, uint32_t dbg, uint64_t *stp) {
-    static const bool no_early = getenv("KMAN_RG_EARLY") && atoi(getenv("KMAN_RG_EARLY")) == 0;
-    if (no_early) dbg |= 16;  // (the uniq finish's early row count off: A/B)
-    static const char *e = getenv("KMAN_RG_FIN");
-    const bool pf = e && atoi(e) == 1;
-    const bool db = e && atoi(e) == 2;
-    const bool ps = e && atoi(e) == 3;  // (KMAN_RG_FIN=3: persistent blocks, A/B)
-    // count rows whose key rest fits 32 bits: 4-byte items in LDS
-    // (KMAN_RG_NARROW=0: the 8-byte items, for A/B)
-    static const char *en = getenv("KMAN_RG_NARROW");
+                   uint32_t *counter, uint64_t *stp) {
     if constexpr (MODE == RG_COUNT) {
-        // (atomic ranks only: the ballot ranks overflow the 80 VGPRs of three
-        // blocks per CU -- 2.5 KB of spills per lane, and results that were
-        // not the sort's: such code is not built)
-        if (!pf && !db && !ps && ctx->lds_atomic_ordered && f.rest <= 32 && f.Q == 0 && f.tag_shift == 0 &&
-            !(en && atoi(en) == 0)) {
-            launch_finish_as<MODE, O, true, false, false, uint32_t>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
+        if (ctx->lds_atomic_ordered && f.rest <= 32 && f.Q == 0 && f.tag_shift == 0) {
+            launch_finish_as<MODE, O, true, uint32_t>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
             return;
         }
     }
-    if (ctx->lds_atomic_ordered) {
-        if (db) launch_finish_as<MODE, O, true, false, true>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
-        else if (pf) launch_finish_as<MODE, O, true, true>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
-        else if (ps)
-            launch_finish_as<MODE, O, true, false, false, uint64_t, true>(ctx, f, okeys, ovals, epoch, counter, dbg,
-                                                                          stp);
-        else launch_finish_as<MODE, O, true, false>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
-    } else {  // (the ballot ranks need the registers the prefetch would take)
-        launch_finish_as<MODE, O, false, false>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
+    if (!ctx->lds_atomic_ordered) {
+        launch_finish_as<MODE, O, false>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
+        return;
     }
+    if constexpr (MODE == RG_UNIQ) {
+        const EarlyCheck ck = early_check();
+        if (ck.chk == 1) {
+            launch_finish_as<MODE, O, true, uint64_t, 1>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
+            return;
+        }
+        if (ck.chk == 2) {
+            launch_finish_as<MODE, O, true, uint64_t, 2>(ctx, f, okeys, ovals, epoch, counter, ck.hook, stp);
+            return;
+        }
+    }
+    launch_finish_as<MODE, O, true>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
 }
 
 int run_finish(kman_ctx *ctx, const FinishArgs &f, int mode, uint64_t *okeys, void *ovals, uint32_t oval_bytes,
-               uint32_t dbg, uint64_t *stp) {
+               uint64_t *stp) {
     uint32_t epoch, *counter;
     KMAN_TRY(kman_lookback_begin(ctx, f.nreg + 1, &epoch, &counter));
-    if (dbg & 4) HIP_TRY(ctx, hipMemsetAsync(ctx->d_status + f.nreg, 0, 8, ctx->stream));  // (the ablation's cursor)
     KTimer kt_(ctx, "region_finish");
     if (mode == KMAN_FINISH_UNIQ) {
-        if (oval_bytes == 4) launch_finish<RG_UNIQ, uint32_t>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
-        else launch_finish<RG_UNIQ, uint64_t>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
+        if (oval_bytes == 4) launch_finish<RG_UNIQ, uint32_t>(ctx, f, okeys, ovals, epoch, counter, stp);
+        else launch_finish<RG_UNIQ, uint64_t>(ctx, f, okeys, ovals, epoch, counter, stp);
     } else {
-        if (oval_bytes == 4) launch_finish<RG_COUNT, uint32_t>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
-        else launch_finish<RG_COUNT, uint64_t>(ctx, f, okeys, ovals, epoch, counter, dbg, stp);
+        if (oval_bytes == 4) launch_finish<RG_COUNT, uint32_t>(ctx, f, okeys, ovals, epoch, counter, stp);
+        else launch_finish<RG_COUNT, uint64_t>(ctx, f, okeys, ovals, epoch, counter, stp);
     }
     HIP_TRY(ctx, hipGetLastError());
     return KMAN_OK;
 }
 
-// XLB: predecessor status words per lane and look-back round -- each round
-// loads 2 * XLB words per digit (a 2 KB row per word), so the wide rounds of
-// the sort passes (LB = 8) cost rg_extract 4.6 GB of status reads per launch
-// (PMC: FETCH 2.27 GB raw, 8 GB of items out): 1 word per lane reads 2.6x
-// less at the same speed (3.69-3.73 vs 3.77-3.86 ms; KMAN_RG_XLB=2/4/8 for A/B)
-// rg_extract's tickets per XCD partition (XG): on by default; KMAN_RG_XG=0
-// takes one global ticket counter (A/B: 3.68 vs 3.75 ms, 10.35 vs 11.22 GB
-// per launch)
-static bool xcd_tickets() {
-    static const bool on = !(getenv("KMAN_RG_XG") && atoi(getenv("KMAN_RG_XG")) == 0);
-    return on;
+// The error word of the region kernels: ERR_REGION alone is not a fault (a
+// region that would overflow: the caller redoes the input, or its key ranges,
+// by another path); any other bit is, and each has its own message.
+int region_fault(kman_ctx *ctx, uint32_t e, const char *what) {
+    const uint32_t f = e & ~ERR_REGION;
+    if (f & ERR_EARLY)
+        return kman_fail(ctx, KMAN_EHIP,
+                         "%s: a region's early row count disagreed with the rows its sorted keys give (device "
+                         "check, error word %u)", what, e);
+    return kman_fail(ctx, KMAN_ETIMEOUT, "%s: device look-back wait exceeded its bound (error word %u)", what, e);
 }
 
-template <int EI, bool RC, int CANON, int NS, int XLB = 1>
-void launch_extract_ns(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
-                       uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp,
-                       uint32_t n_launch) {
-    if (NS == RS && XLB == 1) {
-        static const char *e = getenv("KMAN_RG_XLB");
-        const int x = e ? atoi(e) : 1;
-        if (x == 2) return launch_extract_ns<EI, RC, CANON, NS, 2>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter,
-                                                                    dbg, stp, n_launch);
-        if (x == 4) return launch_extract_ns<EI, RC, CANON, NS, 4>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter,
-                                                                    dbg, stp, n_launch);
-        if (x == 8) return launch_extract_ns<EI, RC, CANON, NS, 8>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter,
-                                                                    dbg, stp, n_launch);
-    }
-    // default: interleaved chains (tile = block ticket, so a launch can take
-    // a tile range: kman_groups_extract) with one lane per digit walking its
-    // chain -- 3.59 vs 3.61 ms and 10 % less FETCH than contiguous chains
-    // with two lanes per digit (KMAN_RG_IL=0, kept for A/B)
-    static const bool contiguous = getenv("KMAN_RG_IL") && atoi(getenv("KMAN_RG_IL")) == 0;
-    static const bool xg = xcd_tickets();
-    // atomic region cursors instead of the look-back (KMAN_RG_AT=0: the
-    // look-back chains, A/B)
-    static const bool at = !(getenv("KMAN_RG_AT") && atoi(getenv("KMAN_RG_AT")) == 0);
-    if (at && !contiguous && XLB == 1) {
-        if (!n_launch && xg && NS % 8 == 0)
-            hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS, 1, true, 1, true, true>),
-                               dim3(p.n_tiles0), dim3(RT), 0, ctx->stream, codes, n_bases, (int)k, p.Q, r0, p.C0,
-                               p.seg_tiles, p.n_tiles0, c0, ctx->d_status, ctx->d_xcounters + 8 * (epoch & 63u), epoch,
-                               ctx->d_err, dbg, stp, nullptr);
-        else
-            hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS, 1, true, 1, false, true>),
-                               dim3(n_launch ? n_launch : p.n_tiles0), dim3(RT), 0, ctx->stream, codes, n_bases,
-                               (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch,
-                               ctx->d_err, dbg, stp, nullptr);
-        return;
-    }
-    if (!n_launch && !contiguous && xg && NS % 8 == 0) {  // tickets per XCD partition (one launch, whole stream)
-        hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS, XLB, true, 1, true>), dim3(p.n_tiles0),
-                           dim3(RT), 0, ctx->stream, codes, n_bases, (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0,
-                           c0, ctx->d_status, ctx->d_xcounters + 8 * (epoch & 63u), epoch, ctx->d_err, dbg, stp,
-                           nullptr);
-        return;
-    }
-    if (n_launch || !contiguous) {
-        hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS, XLB, true, 1>),
-                           dim3(n_launch ? n_launch : p.n_tiles0), dim3(RT), 0, ctx->stream, codes, n_bases, (int)k,
-                           p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch, ctx->d_err, dbg,
-                           stp, nullptr);
-        return;
-    }
-    hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, false, NS, XLB>), dim3(NS * p.seg_tiles), dim3(RT), 0,
-                       ctx->stream, codes, n_bases, (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status,
-                       counter, epoch, ctx->d_err, dbg, stp);
-}
-
+// pass 0 over the whole stream (n_launch = 0: tickets per XCD partition) or
+// over the next n_launch tiles (the chunked loader: one global ticket
+// counter that carries the tile across launches)
 template <int EI, bool RC, int CANON = 0>
 void launch_extract(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
-                    uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp,
+                    uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint64_t *stp,
                     uint32_t n_launch) {
-    const uint32_t grid = RS * p.seg_tiles;
-    const char *e = getenv("KMAN_RG_EXTRACT");  // 1 (default): block-wide rank; 0: stable per-wave rank (RS chains)
-    if (p.S == 256)
-        launch_extract_ns<EI, RC, CANON, 256>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp,
-                                               n_launch);
-    else if (p.S == 128)
-        launch_extract_ns<EI, RC, CANON, 128>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp,
-                                               n_launch);
-    else if (!e || atoi(e) != 0 || n_launch)
-        launch_extract_ns<EI, RC, CANON, RS>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp,
-                                               n_launch);
-    else if (ctx->lds_atomic_ordered)
-        hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON>), dim3(grid), dim3(RT), 0, ctx->stream, codes, n_bases,
-                           (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch,
-                           ctx->d_err, dbg, stp);
+    if (!n_launch)
+        hipLaunchKernelGGL((rg_extract<EI, RC, CANON, false, true>), dim3(p.n_tiles0), dim3(RT), 0, ctx->stream, codes,
+                           n_bases, (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, c0,
+                           ctx->d_xcounters + 8 * (epoch & 63u), ctx->d_err, stp, nullptr);
     else
-        hipLaunchKernelGGL((rg_extract<EI, RC, false, CANON>), dim3(grid), dim3(RT), 0, ctx->stream, codes, n_bases,
-                           (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, ctx->d_status, counter, epoch,
-                           ctx->d_err, dbg, stp);
+        hipLaunchKernelGGL((rg_extract<EI, RC, CANON, false, false>), dim3(n_launch), dim3(RT), 0, ctx->stream, codes,
+                           n_bases, (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, c0, counter, ctx->d_err, stp,
+                           nullptr);
 }
 
-template <int EI, bool RC, int CANON = 0>
-void launch_xown(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
-                 uint64_t *r0, uint32_t *c0, uint32_t *counter, uint64_t *stp) {
-    if (p.xnt == 256) {  // four blocks per CU, write combining in 64-byte lines
-        const void *fn = (const void *)rg_xown<256, EI, RC, CANON, 8>;
-        const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, 256, p.S);
-        hipLaunchKernelGGL((rg_xown<256, EI, RC, CANON, 8>), dim3(grid), dim3(256), 0, ctx->stream, codes, n_bases,
-                           (int)k, p.Q, r0, p.C0, p.S, p.seg_tiles, p.n_tiles0, c0, counter, ctx->d_err, stp);
-    } else if (p.xnt == 1024) {
-        const void *fn = (const void *)rg_xown<1024, EI, RC, CANON>;
-        const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, 1024, p.S);
-        hipLaunchKernelGGL((rg_xown<1024, EI, RC, CANON>), dim3(grid), dim3(1024), 0, ctx->stream, codes, n_bases,
-                           (int)k, p.Q, r0, p.C0, p.S, p.seg_tiles, p.n_tiles0, c0, counter, ctx->d_err, stp);
-    } else {
-        const void *fn = (const void *)rg_xown<512, EI, RC, CANON>;
-        const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, fn, 512, p.S);
-        hipLaunchKernelGGL((rg_xown<512, EI, RC, CANON>), dim3(grid), dim3(512), 0, ctx->stream, codes, n_bases,
-                           (int)k, p.Q, r0, p.C0, p.S, p.seg_tiles, p.n_tiles0, c0, counter, ctx->d_err, stp);
-    }
-}
-
-// n_launch > 0: the next n_launch tiles of pass 0 (interleaved chains; the
-// epoch's ticket counter carries the tile across launches)
 void launch_extract_any(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
-                        uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint32_t dbg, uint64_t *stp,
+                        uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint64_t *stp,
                         uint32_t n_launch = 0) {
-    if (p.own) {
-        if (p.canon) launch_xown<8, false, 1>(ctx, p, codes, n_bases, k, r0, c0, counter, stp);
-        else if (p.rc) launch_xown<4, true>(ctx, p, codes, n_bases, k, r0, c0, counter, stp);
-        else launch_xown<8, false>(ctx, p, codes, n_bases, k, r0, c0, counter, stp);
-        return;
-    }
-    if (p.canon && p.mix && p.ei == 12) launch_extract<12, false, 2>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
-    else if (p.canon && p.mix) launch_extract<16, false, 2>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
-    else if (p.canon && p.ei == 12) launch_extract<12, false, 1>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
-    else if (p.canon) launch_extract<16, false, 1>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
-    else if (p.rc && p.ei == 6) launch_extract<6, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
-    else if (p.rc) launch_extract<8, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
-    else if (p.ei == 12) launch_extract<12, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
-    else if (p.ei == 8) launch_extract<8, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
-    else launch_extract<16, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, dbg, stp, n_launch);
+    if (p.canon && p.mix) launch_extract<16, false, 2>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
+    else if (p.canon) launch_extract<16, false, 1>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
+    else if (p.rc) launch_extract<8, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
+    else launch_extract<16, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
 }
 
 // mean phase durations (us) per kernel from the stamp rows; frees the buffers
@@ -2009,7 +1206,7 @@ int groups_outputs_ok(kman_ctx *ctx, const GroupsCall &g, int mode, const void *
 // region) and the results: output count (the last region's inclusive),
 // region-0 counts (k-mers), error word
 int groups_tail(kman_ctx *ctx, const GroupsCall &g, int mode, uint64_t *d_okeys, void *d_ovals, uint32_t oval_bytes,
-                uint32_t dbg, uint64_t **stamps, const uint64_t *stamp_rows, uint64_t *n_kmers, uint64_t *n_out) {
+                uint64_t **stamps, const uint64_t *stamp_rows, uint64_t *n_kmers, uint64_t *n_out) {
     const RegionPlan &p = g.p;
     uint32_t epoch, *counter;
     KMAN_TRY(kman_lookback_begin(ctx, 1, &epoch, &counter));  // (the chain counter only)
@@ -2021,7 +1218,7 @@ int groups_tail(kman_ctx *ctx, const GroupsCall &g, int mode, uint64_t *d_okeys,
         pa.seg_cnt = g.c0;
         pa.stride = p.C0;
         pa.nbk = RADIX;
-        pa.nsg = p.S;
+        pa.nsg = RS;
         pa.gsub = 1;
         pa.H = p.H;
         pa.shift = p.Q + p.rest;
@@ -2029,19 +1226,19 @@ int groups_tail(kman_ctx *ctx, const GroupsCall &g, int mode, uint64_t *d_okeys,
         pa.out = g.r1;
         pa.C1 = p.C1h;
         pa.cnt1 = g.c1;
-        launch_pass(ctx, pa, counter, dbg >> 4, stamps[1]);
+        launch_pass(ctx, pa, counter, stamps[1]);
         HIP_TRY(ctx, hipGetLastError());
     }
     {
         FinishArgs f{g.r1, p.C1h, g.c1, p.Q, p.rest, (uint32_t)p.rc, 0, 0, g.nreg};
         f.fsub = p.H;
-        KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, dbg & 15, stamps[2]));
+        KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, stamps[2]));
     }
     if (stamps[0]) KMAN_TRY(report_stamps(ctx, stamps, stamp_rows));
     uint64_t *h = ctx->h_small;
     HIP_TRY(ctx, hipMemcpyAsync(h + 4, ctx->d_status + (g.nreg - 1), 8, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(h + 8, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
-    std::vector<uint32_t> hc((size_t)RADIX * p.S);
+    std::vector<uint32_t> hc((size_t)RADIX * RS);
     HIP_TRY(ctx, hipMemcpyAsync(hc.data(), g.c0, hc.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     uint32_t e;
@@ -2049,14 +1246,10 @@ int groups_tail(kman_ctx *ctx, const GroupsCall &g, int mode, uint64_t *d_okeys,
     if (e) {
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_err, 0, sizeof(uint32_t), ctx->stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        if (e == ERR_REGION) return KMAN_EFALLBACK;  // a region overflowed: outputs invalid
-        return kman_fail(ctx, KMAN_ETIMEOUT, "device look-back wait exceeded its bound (code %u)", e);
+        if (e & ERR_REGION) return KMAN_EFALLBACK;  // a region overflowed: outputs invalid, redone elsewhere
+        return region_fault(ctx, e, "kman_groups");
     }
-    uint64_t wd = h[4];
-    if (dbg & 4) {  // (the unordered-output timing ablation: the total is its cursor)
-        HIP_TRY(ctx, hipMemcpy(&wd, ctx->d_status + g.nreg, 8, hipMemcpyDeviceToHost));
-        wd = ((uint64_t)ST_INCL << 62) | ((uint64_t)ctx->epoch << 56) | wd;
-    }
+    const uint64_t wd = h[4];
     if (((wd >> 56) & 63u) != ctx->epoch || (wd >> 62) != ST_INCL)
         return kman_fail(ctx, KMAN_EHIP, "region output total not published");
     uint64_t nk = 0;
@@ -2079,8 +1272,6 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
     if (!d_codes) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
     KMAN_TRY(groups_outputs_ok(ctx, g, mode, d_okeys, d_ovals, oval_bytes, n_bases));
     const RegionPlan &p = g.p;
-    const char *dbg_env = getenv("KMAN_RG_DBG");  // timing ablations (tools/regionbench.py)
-    const uint32_t dbg = dbg_env ? (uint32_t)atoi(dbg_env) : 0u;
     HIP_TRY(ctx, hipMemsetAsync(g.c0, 0, p.bytes - p.off_c0, ctx->stream));
     uint64_t *stamps[3] = {nullptr, nullptr, nullptr};
     const uint64_t stamp_rows[3] = {p.n_tiles0, (uint64_t)p.maxt1 * RADIX, g.nreg};
@@ -2091,13 +1282,13 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
         }
     uint32_t epoch, *counter;
     // pass 0: extraction by the top 8 bits
-    KMAN_TRY(kman_lookback_begin(ctx, p.own ? 1 : (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
+    KMAN_TRY(kman_lookback_begin(ctx, 1, &epoch, &counter));  // (the ticket counters only)
     {
         KTimer kt_(ctx, "region_extract");
-        launch_extract_any(ctx, p, d_codes, n_bases, k, g.r0, g.c0, epoch, counter, dbg >> 8, stamps[0]);
+        launch_extract_any(ctx, p, d_codes, n_bases, k, g.r0, g.c0, epoch, counter, stamps[0]);
         HIP_TRY(ctx, hipGetLastError());
     }
-    return groups_tail(ctx, g, mode, d_okeys, d_ovals, oval_bytes, dbg, stamps, stamp_rows, n_kmers, n_out);
+    return groups_tail(ctx, g, mode, d_okeys, d_ovals, oval_bytes, stamps, stamp_rows, n_kmers, n_out);
 }
 
 extern "C" int kman_groups_begin(kman_ctx *ctx, uint64_t n_bases, uint32_t k, uint32_t flags, int mode,
@@ -2110,13 +1301,12 @@ extern "C" int kman_groups_begin(kman_ctx *ctx, uint64_t n_bases, uint32_t k, ui
     const RegionPlan &p = g.p;
     HIP_TRY(ctx, hipMemsetAsync(g.c0, 0, p.bytes - p.off_c0, ctx->stream));
     uint32_t epoch, *counter;
-    KMAN_TRY(kman_lookback_begin(ctx, p.own ? 1 : (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
+    KMAN_TRY(kman_lookback_begin(ctx, 1, &epoch, &counter));
     ctx->grp_epoch = epoch;
     ctx->grp_next = 0;
     ctx->grp_tiles = p.n_tiles0;
-    // (the opt-in owned pass 0 walks whole chains: it runs at kman_groups_end)
-    *n_tiles = p.own ? 0u : p.n_tiles0;
-    *tile_bases = p.own ? 0u : (uint64_t)RT * p.ei;
+    *n_tiles = p.n_tiles0;
+    *tile_bases = (uint64_t)RT * p.ei;
     return KMAN_OK;
 }
 
@@ -2130,18 +1320,10 @@ int groups_extract_to(kman_ctx *ctx, const GroupsCall &g, const uint8_t *d_codes
     if (!d_codes) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
     if (tile_hi > p.n_tiles0) tile_hi = p.n_tiles0;
     uint32_t *counter = ctx->d_counters + ctx->grp_epoch;
-    if (p.own) {
-        if (tile_hi < p.n_tiles0 || ctx->grp_next) return KMAN_OK;
-        KTimer kt_(ctx, "region_extract");
-        launch_extract_any(ctx, p, d_codes, n_bases, k, g.r0, g.c0, ctx->grp_epoch, counter, 0, nullptr);
-        HIP_TRY(ctx, hipGetLastError());
-        ctx->grp_next = p.n_tiles0;
-        return KMAN_OK;
-    }
     if (tile_hi <= ctx->grp_next) return KMAN_OK;
     {
         KTimer kt_(ctx, "region_extract");
-        launch_extract_any(ctx, p, d_codes, n_bases, k, g.r0, g.c0, ctx->grp_epoch, counter, 0, nullptr,
+        launch_extract_any(ctx, p, d_codes, n_bases, k, g.r0, g.c0, ctx->grp_epoch, counter, nullptr,
                            tile_hi - ctx->grp_next);
         HIP_TRY(ctx, hipGetLastError());
     }
@@ -2171,7 +1353,7 @@ extern "C" int kman_groups_end(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n
     ctx->grp_epoch = 0;
     uint64_t *stamps[3] = {nullptr, nullptr, nullptr};
     const uint64_t stamp_rows[3] = {0, 0, 0};
-    return groups_tail(ctx, g, mode, d_okeys, d_ovals, oval_bytes, 0, stamps, stamp_rows, n_kmers, n_out);
+    return groups_tail(ctx, g, mode, d_okeys, d_ovals, oval_bytes, stamps, stamp_rows, n_kmers, n_out);
 }
 
 namespace {
@@ -2297,15 +1479,11 @@ int make_shard_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t f
     const uint64_t Wq = n_bases_q * (p.rc ? 2 : 1);
     p.Q = mode == KMAN_FINISH_UNIQ ? (bitlen(Wq - 1) ? bitlen(Wq - 1) : 1u) : 0u;
     if (p.K - B1 + p.Q > 64) return KMAN_EFALLBACK;
-    {
-        // the shard extraction's tiles (rg_hist counts in the same geometry):
-        // 12 windows per thread (6 with -r); KMAN_RG_XEI=16: 16 / 8 (A/B:
-        // config-4 shard extraction 80.0 vs 76.0 ms -- a round keeps 1/R of
-        // the windows, so the tiles' digit runs stay short either way)
-        const char *e = getenv("KMAN_RG_XEI");
-        const bool wide = e && atoi(e) == 16;
-        p.ei = p.rc ? (wide ? 8u : 6u) : (wide ? 16u : 12u);
-    }
+    // the shard extraction's tiles (rg_hist counts in the same geometry):
+    // 12 windows per thread (6 with -r): config-4 shard extraction 76.0 vs
+    // 80.0 ms with 16 -- a round keeps 1/R of the windows, so the tiles'
+    // digit runs stay short either way
+    p.ei = p.rc ? 6u : 12u;
     const uint64_t win = (uint64_t)RT * p.ei;
     p.n_tiles0 = (uint32_t)ceil_div(n_bases ? n_bases : 1, win);
     p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, RS);
@@ -2324,14 +1502,12 @@ struct RoundPlan {
     uint64_t off_c1, off_tab, off_fail, a_bytes, off_c2, b_bytes;
 };
 
-// Capacity of a region that expects e items: a fixed 1.5 x e (KMAN_DROUND_PAD=0,
-// A/B) or e + max(e / 8, 8 sd of a Poisson fill) -- the round path's arenas
-// are most of a rank's HBM, and at config 4's size (12.5 G k-mers per rank)
-// the 1.5 x slack cost one key round (a re-read and re-roll of the whole
-// shard).  A region that overflows anyway (a repeat) is redone by key range.
+// Capacity of a region that expects e items: e + max(e / 8, 8 sd of a
+// Poisson fill) -- the round path's arenas are most of a rank's HBM, and at
+// config 4's size (12.5 G k-mers per rank) a 1.5 x slack cost one key round (a
+// re-read and re-roll of the whole shard).  A region that overflows anyway (a
+// repeat) is redone by key range.
 uint64_t round_cap(uint64_t e, uint64_t extra) {
-    static const bool old = getenv("KMAN_DROUND_PAD") && atoi(getenv("KMAN_DROUND_PAD")) == 0;
-    if (old) return ceil_div(e + e / 2 + extra, 64) * 64;
     const uint64_t sd8 = (uint64_t)(8.0 * sqrt((double)e)) + 1;
     return ceil_div(e + (e / 8 > sd8 ? e / 8 : sd8) + extra, 64) * 64;
 }
@@ -2423,8 +1599,7 @@ int read_err(kman_ctx *ctx, uint32_t *e) {
     if (*e) {
         HIP_TRY(ctx, hipMemsetAsync(ctx->d_err, 0, 4, ctx->stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        if (*e != ERR_REGION)
-            return kman_fail(ctx, KMAN_ETIMEOUT, "device look-back wait exceeded its bound (code %u)", *e);
+        if (*e != ERR_REGION) return region_fault(ctx, *e, "kman_dround_finish");
     }
     return KMAN_OK;
 }
@@ -2439,27 +1614,12 @@ void launch_hist(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint6
 
 template <int EI, bool RC, int CANON>
 void launch_extract_ex(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
-                       uint64_t *out, uint32_t *cnt, const uint64_t *rtab, uint32_t epoch, uint32_t *counter) {
+                       uint64_t *out, const uint32_t *cnt, const uint64_t *rtab, uint32_t epoch) {
     const uint32_t grid = RS * p.seg_tiles;
-    // atomic region cursors instead of the look-back chains (KMAN_RG_AT=0: A/B)
-    static const bool at = !(getenv("KMAN_RG_AT") && atoi(getenv("KMAN_RG_AT")) == 0);
-    if (at && xcd_tickets()) {
-        (void)hipMemsetAsync(ctx->d_cursors, 0, (size_t)RADIX * RS * 4, ctx->stream);  // (errors: the caller's hipGetLastError)
-        hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, true, RS, 1, false, 0, true, true>), dim3(grid),
-                           dim3(RT), 0, ctx->stream, codes, n_bases, (int)k, p.Q, out, (uint64_t)0, p.seg_tiles,
-                           p.n_tiles0, cnt, (uint64_t *)ctx->d_cursors, ctx->d_xcounters + 8 * (epoch & 63u), epoch,
-                           ctx->d_err, 0u, nullptr, rtab);
-        return;
-    }
-    if (xcd_tickets()) {
-        hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, true, RS, 1, false, 0, true>), dim3(grid), dim3(RT), 0,
-                           ctx->stream, codes, n_bases, (int)k, p.Q, out, (uint64_t)0, p.seg_tiles, p.n_tiles0, cnt,
-                           ctx->d_status, ctx->d_xcounters + 8 * (epoch & 63u), epoch, ctx->d_err, 0u, nullptr, rtab);
-        return;
-    }
-    hipLaunchKernelGGL((rg_extract<EI, RC, true, CANON, true, true, RS, 1>), dim3(grid), dim3(RT), 0, ctx->stream, codes,
-                       n_bases, (int)k, p.Q, out, (uint64_t)0, p.seg_tiles, p.n_tiles0, cnt, ctx->d_status, counter,
-                       epoch, ctx->d_err, 0u, nullptr, rtab);
+    (void)hipMemsetAsync(ctx->d_cursors, 0, (size_t)RADIX * RS * 4, ctx->stream);  // (errors: the caller's hipGetLastError)
+    hipLaunchKernelGGL((rg_extract<EI, RC, CANON, true, true>), dim3(grid), dim3(RT), 0, ctx->stream, codes, n_bases,
+                       (int)k, p.Q, out, (uint64_t)0, p.seg_tiles, p.n_tiles0, cnt, ctx->d_cursors,
+                       ctx->d_xcounters + 8 * (epoch & 63u), ctx->d_err, nullptr, rtab);
 }
 
 // Pass 1b's width g, refitted from the pass-1 counts.  The plan takes g from
@@ -2573,19 +1733,19 @@ extern "C" int kman_dshard_extract(kman_ctx *ctx, const uint8_t *d_codes, uint64
     if (!d_codes || !d_hist || !d_rtab || !d_send) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
     uint32_t epoch, *counter;
-    KMAN_TRY(kman_lookback_begin(ctx, (uint64_t)p.n_tiles0 * RADIX, &epoch, &counter));
+    KMAN_TRY(kman_lookback_begin(ctx, 1, &epoch, &counter));  // (the XCD ticket counters only)
     {
         KTimer kt_(ctx, "region_extract");
-        uint32_t *cnt = const_cast<uint32_t *>(d_hist);  // read-only in EX mode
+        const uint32_t *cnt = d_hist;  // the exact region sizes (read-only)
         if (p.ei == 16 || p.ei == 8) {
-            if (p.canon && p.mix) launch_extract_ex<16, false, 2>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
-            else if (p.canon) launch_extract_ex<16, false, 1>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
-            else if (p.rc) launch_extract_ex<8, true, 0>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
-            else launch_extract_ex<16, false, 0>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
-        } else if (p.canon && p.mix) launch_extract_ex<12, false, 2>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
-        else if (p.canon) launch_extract_ex<12, false, 1>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
-        else if (p.rc) launch_extract_ex<6, true, 0>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
-        else launch_extract_ex<12, false, 0>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch, counter);
+            if (p.canon && p.mix) launch_extract_ex<16, false, 2>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch);
+            else if (p.canon) launch_extract_ex<16, false, 1>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch);
+            else if (p.rc) launch_extract_ex<8, true, 0>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch);
+            else launch_extract_ex<16, false, 0>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch);
+        } else if (p.canon && p.mix) launch_extract_ex<12, false, 2>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch);
+        else if (p.canon) launch_extract_ex<12, false, 1>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch);
+        else if (p.rc) launch_extract_ex<6, true, 0>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch);
+        else launch_extract_ex<12, false, 0>(ctx, p, d_codes, n_bases, k, d_send, cnt, d_rtab, epoch);
         HIP_TRY(ctx, hipGetLastError());
     }
     uint32_t e;
@@ -2673,7 +1833,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         pa.fail = freg;  // sub-region (b, d, src, h) -> flag (b, d) (spread over its 2^g regions below)
         pa.fail_div = G * d.H;
         pa.fail_shift = 0;
-        launch_pass(ctx, pa, counter, 0, nullptr);
+        launch_pass(ctx, pa, counter, nullptr);
         HIP_TRY(ctx, hipGetLastError());
     }
     KMAN_TRY(rg_check(ctx, "pass 1", c1, d.nsub));
@@ -2681,8 +1841,6 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         KMAN_TRY(refit_g(ctx, d, c1, freg, G));
         c2 = (uint32_t *)(wb + d.off_c2);
     }
-    const char *dbg_env = getenv("KMAN_RG_DBG");  // finish timing ablations only (bits 1, 2)
-    const uint32_t fdbg = dbg_env ? (uint32_t)atoi(dbg_env) & 3u : 0u;
     uint64_t *fst = nullptr;
 #ifdef KMAN_RG_STAMPS
     if (getenv("KMAN_RG_STAMPS")) {
@@ -2695,7 +1853,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         FinishArgs f{r1, d.C1s, c1, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << 9, 0u, (uint32_t)d.nreg};
         f.fsub = d.H;
         f.freg = freg;
-        KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, fdbg, fst));
+        KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, fst));
     } else {
     // (c2 may lie in the receive buffer: cleared only once pass 1 has read it)
     HIP_TRY(ctx, hipMemsetAsync(c2, 0, d.nreg * 4, ctx->stream));
@@ -2725,7 +1883,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         pa.fail = freg;
         pa.fail_div = 1;
         pa.fail_shift = 0;
-        launch_pass(ctx, pa, counter, 0, nullptr);
+        launch_pass(ctx, pa, counter, nullptr);
         HIP_TRY(ctx, hipGetLastError());
     }
     KMAN_TRY(rg_check(ctx, "pass 1b", c2, d.nreg));
@@ -2733,7 +1891,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         FinishArgs f{r2, d.C1, c2, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << (9 + d.g),
                      mode == KMAN_FINISH_UNIQ ? d.Q + d.rest + d.g : 0u, (uint32_t)d.nreg};
         f.freg = freg;
-        KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, fdbg, fst));
+        KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, fst));
     }
     }
     if (fst) KMAN_TRY(report_finish_stamps(ctx, fst, d.nreg));

@@ -105,9 +105,23 @@ class FileReader:
             self._fh = None
 
 
+def launch_nonce() -> str:
+    """Something every rank of ONE launch shares and the next launch does
+    not: the launcher's run id (KMAN_RUN_ID, set by bench.py's spawner), else
+    under torch.distributed.run the elastic agent's PID (every local worker
+    is its child; its TORCHELASTIC_RUN_ID is often the constant "none"), else
+    empty (other launchers: the start-time check in `rendezvous` only)."""
+    rid = os.environ.get("KMAN_RUN_ID")
+    if rid:
+        return rid
+    if "TORCHELASTIC_RUN_ID" in os.environ:
+        return "%s-%d" % (os.environ["TORCHELASTIC_RUN_ID"], os.getppid())
+    return ""
+
+
 def _id_path(tag: str, directory: Optional[str] = None) -> str:
-    key = "%s_%s_%s_%s" % (os.environ.get("MASTER_PORT", "0"), os.environ.get("TORCHELASTIC_RUN_ID", ""),
-                           os.environ.get("WORLD_SIZE", "1"), tag)
+    key = "%s_%s_%s_%s" % (os.environ.get("MASTER_PORT", "0"), launch_nonce(), os.environ.get("WORLD_SIZE", "1"),
+                           tag)
     return os.path.join(directory or tempfile.gettempdir(), "kman_rccl_id_" + key.replace(os.sep, "_"))
 
 

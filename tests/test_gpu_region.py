@@ -300,18 +300,34 @@ def test_skewed_input_takes_the_rounds(dev):
             assert fn(text, 21, dev=dev) == open(os.path.join(d, "w"), "rb").read()
 
 
-@pytest.mark.parametrize("xnt", ["256", "512"])
-@pytest.mark.parametrize("k,rc,mode", [(21, False, "count"), (21, False, "uniq"), (13, True, "uniq"),
-                                       (25, True, "count"), (31, False, "count")])
-def test_groups_owned_pass0(dev, golden_inputs, monkeypatch, xnt, k, rc, mode):
-    """The opt-in pass 0 by block-owned chains (KMAN_RG_OWN=1: rg_xown, no
-    look-back, write-combined lines) gives the same rows as the oracle."""
-    monkeypatch.setenv("KMAN_RG_OWN", "1")
-    monkeypatch.setenv("KMAN_RG_XNT", xnt)
+@pytest.mark.parametrize("k,rc", [(21, False), (13, True), (25, False), (9, False)])
+def test_groups_early_count_checked(dev, golden_inputs, monkeypatch, k, rc):
+    """The uniq finish under its early-count check (KMAN_RG_CHECK=1: every
+    thread compares the singleton marks of the early count with the rows its
+    sorted keys give) returns the oracle's rows and raises nothing."""
+    monkeypatch.setenv("KMAN_RG_CHECK", "1")
     for text in _texts(golden_inputs):
-        got = _groups(dev, text, k, rc, mode)
+        got = _groups(dev, text, k, rc, "uniq")
         if got is None:
             continue
-        want = _oracle(text, k, rc, mode)
+        want = _oracle(text, k, rc, "uniq")
         np.testing.assert_array_equal(got[0], want[0])
         np.testing.assert_array_equal(got[1].astype(np.uint64), want[1])
+
+
+def test_groups_early_count_check_catches_a_wrong_mark(dev, monkeypatch):
+    """One wrong singleton mark (KMAN_RG_CHECK=hook=<region>: the test hook
+    flips the early count's mark of one item in that region) fails the call
+    with the early-count error, not a look-back timeout; the next call on the
+    same context is correct again."""
+    import inputs
+
+    text = inputs.syn_numpy(3_000_000, 6, record_len=1 << 20)
+    monkeypatch.setenv("KMAN_RG_CHECK", "hook=3")
+    with pytest.raises(RuntimeError, match="early row count"):
+        _groups(dev, text, 21, False, "uniq")
+    monkeypatch.setenv("KMAN_RG_CHECK", "0")
+    got = _groups(dev, text, 21, False, "uniq")
+    want = _oracle(text, 21, False, "uniq")
+    np.testing.assert_array_equal(got[0], want[0])
+    np.testing.assert_array_equal(got[1].astype(np.uint64), want[1])

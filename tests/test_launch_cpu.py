@@ -100,6 +100,30 @@ def test_rendezvous_processes_and_stale_file(tmp_path):
     assert not os.path.exists(stale)
 
 
+def test_rendezvous_back_to_back_relaunch(tmp_path, monkeypatch):
+    """A launch that crashed seconds ago (its id file is fresh, so the
+    start-time check alone would take it) is keyed by its own run id: a new
+    launch on the same port never reads it."""
+    import struct
+
+    from kman_amd import launch
+
+    d = str(tmp_path)
+    monkeypatch.setenv("MASTER_PORT", "29500")
+    monkeypatch.setenv("KMAN_RUN_ID", "old")
+    stale = launch._id_path("t", d)
+    with open(stale, "wb") as fh:
+        fh.write(launch._MAGIC + struct.pack("<d", time.time()) + b"\0" * 8 + b"\x01" * 128)
+    monkeypatch.setenv("KMAN_RUN_ID", "new")
+    assert launch._id_path("t", d) != stale
+    with pytest.raises(RuntimeError):  # no rank 0 of the new launch: the old id is not taken
+        launch.rendezvous(1, 2, "t", make_uid=lambda: b"\2" * 128, directory=d, timeout=0.5)
+    # under torch.distributed.run the elastic agent's PID keys the launch
+    monkeypatch.delenv("KMAN_RUN_ID")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "none")
+    assert launch.launch_nonce() == "none-%d" % os.getppid()
+
+
 def test_cli_leaves_solo_work_to_rank_zero(tmp_path, monkeypatch):
     """Outside the multi-GPU domain (k > 32 here), ranks other than 0 leave
     without touching the GPU or the output; k <= 1 still raises everywhere."""
