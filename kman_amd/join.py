@@ -321,6 +321,14 @@ def join_vectors(batches: List[Batch], masked: bool, outpath: str) -> None:
     if emulate and not masked:
         # (the first group's add_count raises, abundance.py:60 via :123)
         raise NotImplementedError("AbundanceVector.add_count (the reference's VEC_COUNT)")
+    if emulate and (not all(isinstance(e[0], FastaSource) for e in entries) or entries[0][0].k > engine.MAX_K):
+        # reloaded batch files (-B) or word keys (k > 32): the same decision
+        # from the sorted union on the host side (bounded slices)
+        if groups_span_refs(entries):
+            raise NotImplementedError("AbundanceVector.add_count (the reference's VEC_COUNT_MASKED)")
+        print('Writing output in "%s"' % dirpath)  # abundance.py:160: no vector was added
+        os.makedirs(dirpath, exist_ok=True)
+        return
     if not all(isinstance(e[0], FastaSource) for e in entries):
         raise NotImplementedError("abundance vectors of reloaded batch files (-B)")
     if entries[0][0].k > engine.MAX_K:
@@ -413,6 +421,89 @@ def join_vectors(batches: List[Batch], masked: bool, outpath: str) -> None:
 
 
 _VEC_SLICE = 1 << 26  # u32 slots per host slice (256 MiB)
+_GROUP_SLICE = 1 << 24  # items per host slice of groups_span_refs
+
+
+def _record_refs(src, ref_ids: dict) -> Tuple[np.ndarray, np.ndarray]:
+    """(first base of each record, ref id of each record) of one source.
+    The ref is what SequenceCoords.from_str reads from the record's header
+    (join.py:311-335): a FASTA record's name, or the ref field of a batch
+    file record's title (seq.py:106-127; an incompatible title raises
+    AssertionError, as the reference does at that group)."""
+    from .seq import SequenceCoords
+    from .source import FastaSource
+
+    if isinstance(src, FastaSource):
+        names = [n.decode("utf-8", "surrogateescape") for n in src.parsed.names]
+    else:
+        names = [SequenceCoords.from_str(t).ref for t in src.titles]
+    ids = np.array([ref_ids.setdefault(nm, len(ref_ids)) for nm in names], np.int64)
+    return np.asarray(src.parsed.rec_seq, np.uint64), ids
+
+
+def groups_span_refs(entries) -> bool:
+    """True iff some group of equal k-mers of the joined batches holds
+    records of two different refs: exactly when the reference's
+    join_vector_count_masked reaches AbundanceVector.add_count
+    (join.py:318-335, which raises NotImplementedError, abundance.py:60 via
+    :123).  The union is sorted on the device (gather_sorted: any k, FASTA
+    or batch-file sources); groups and their min / max ref are found on the
+    host in bounded slices, a group open at a slice end carried over."""
+    from .source import gather_sorted
+
+    km, srcs, tagged = gather_sorted(entries, want_pos=True)
+    try:
+        dev, k = srcs[0].dev, srcs[0].k
+        ref_ids: dict = {}
+        recs = [_record_refs(s, ref_ids) for s in srcs]
+        if len(ref_ids) < 2:
+            return False
+        words = isinstance(km, engine.Words)
+        W = engine.nwords(k) if words else 1
+        pb = 8 if words else km.pos_bytes
+        mask = np.uint64((1 << (2 * k)) - 1) if k < 32 else np.uint64(0xFFFFFFFFFFFFFFFF)
+        low56 = np.uint64((1 << 56) - 1)
+        carry = None  # (key row, min ref, max ref) of the group open at the last slice's end
+        for lo in range(0, km.n, _GROUP_SLICE):
+            m = min(_GROUP_SLICE, km.n - lo)
+            if words:
+                keys = np.stack([dev.download(_Raw(km.plane(j)), m, np.uint64, 8 * lo) for j in range(W)], axis=1)
+            else:
+                keys = (dev.download(km.keys, m, np.uint64, 8 * lo) & mask)[:, None]
+            pos = dev.download(km.pos, m, np.uint64 if pb == 8 else np.uint32, pb * lo).astype(np.uint64)
+            base = (pos & low56) >> np.uint64(1)
+            src_of = (pos >> np.uint64(56)).astype(np.int64) if tagged else np.zeros(m, np.int64)
+            ref = np.empty(m, np.int64)
+            for si, (rs, ids) in enumerate(recs):
+                sel = src_of == si
+                if sel.any():
+                    ref[sel] = ids[np.searchsorted(rs, base[sel], side="right") - 1]
+            new = np.ones(m, bool)
+            new[1:] = (keys[1:] != keys[:-1]).any(axis=1)
+            if carry is not None and (keys[0] == carry[0]).all():
+                new[0] = False
+            starts = np.flatnonzero(new)
+            if not new[0]:  # the carried group continues into this slice
+                end0 = int(starts[0]) if len(starts) else m
+                carry = (carry[0], min(carry[1], int(ref[:end0].min())), max(carry[2], int(ref[:end0].max())))
+            if len(starts):
+                if carry is not None and carry[1] != carry[2]:
+                    return True
+                mins = np.minimum.reduceat(ref, starts)
+                maxs = np.maximum.reduceat(ref, starts)
+                if (mins[:-1] != maxs[:-1]).any():
+                    return True
+                carry = (keys[-1].copy(), int(mins[-1]), int(maxs[-1]))
+        return carry is not None and carry[1] != carry[2]
+    finally:
+        km.free()
+
+
+class _Raw:
+    """A raw device pointer for Device.download (no ownership)."""
+
+    def __init__(self, ptr: int):
+        self.ptr = ptr
 
 
 def _vector_len(dev, vec, first: int, end: int) -> int:

@@ -204,6 +204,21 @@ BATCH_CASES = [
     ("messy1", 70, ["-b", "300"]),
 ]
 
+# VEC_COUNT_MASKED (round 4): the reference's add_count raises
+# NotImplementedError at the first group whose records carry two names
+# (join.py:311-335, abundance.py:60 via :123), else it writes the empty
+# vector folder; k > 32 and k <= 32, with and without -r
+VEC_CASES = [
+    ("vecshare", 40, []),
+    ("vecshare", 40, ["-r"]),
+    ("vecshare", 21, []),
+    ("vecsame", 40, []),
+    ("vecsame", 21, ["-r"]),
+    ("messy1", 40, []),
+    ("messy2", 33, ["-r"]),
+    ("edge", 5, []),
+]
+
 ERROR_CASES = [
     ("empty", "count", 3, []),
     ("noheader", "count", 3, []),
@@ -231,12 +246,14 @@ def main() -> None:
 
     out_root = os.path.join(HERE, "ref_outputs")
     os.makedirs(out_root, exist_ok=True)
-    manifest = {"cases": [], "batch_cases": [], "error_cases": [], "config1": []}
+    manifest = {"cases": [], "batch_cases": [], "error_cases": [], "config1": [], "vec_cases": []}
     have = set()
     if args.only_new:
         with open(os.path.join(HERE, "manifest.json")) as fh:
             manifest = json.load(fh)
-        have = {e["name"] for part in ("cases", "batch_cases", "error_cases", "config1") for e in manifest[part]}
+        manifest.setdefault("vec_cases", [])
+        have = {e["name"] for part in ("cases", "batch_cases", "error_cases", "config1", "vec_cases")
+                for e in manifest[part]}
 
     def case_name(inp, cmd, k, extra):
         tag = "".join(x.strip("-") for x in extra)
@@ -275,6 +292,21 @@ def main() -> None:
             entry["files"] = sorted(contents)
         manifest["batch_cases"].append(entry)
         print(name, res, len(entry.get("files", [])), flush=True)
+
+    for inp, k, extra in VEC_CASES:
+        name = case_name(inp, "vecmasked", k, extra)
+        if name in have:
+            continue
+        work = os.path.join(scratch, "w_" + name)
+        os.makedirs(work)
+        out = os.path.join(work, "vec.out")
+        res = run_reference(standins, ["count", paths[inp], out, str(k), "--count-mode", "VEC_COUNT_MASKED"] + extra,
+                            work)
+        folder = os.path.join(work, "vec")
+        entry = {"name": name, "input": inp, "k": k, "flags": extra, "result": res,
+                 "folder": sorted(os.listdir(folder)) if os.path.isdir(folder) else None}
+        manifest["vec_cases"].append(entry)
+        print(name, res, entry["folder"], flush=True)
 
     for inp, cmd, k, extra in ERROR_CASES:
         name = case_name(inp, cmd, k, extra)

@@ -339,6 +339,16 @@ EDGE_FA = (
 )
 
 
+def vec_shared() -> bytes:
+    """Records a, b, c: b holds 60 bases of a (positions 20-79), c is its
+    own; lowercase in b (the reference upper-cases before the check)."""
+    rng = random.Random(77)
+    a = "".join(rng.choice("ACGT") for _ in range(120))
+    b = "".join(rng.choice("ACGT") for _ in range(30)) + a[20:80].lower() + "".join(rng.choice("ACGT") for _ in range(25))
+    c = "".join(rng.choice("ACGT") for _ in range(90))
+    return (">a one\n" + wrap(a) + ">b\ttwo\n" + wrap(b) + ">c\n" + wrap(c)).encode()
+
+
 def build_inputs(root: str) -> dict:
     files = {
         "edge": EDGE_FA,
@@ -351,6 +361,12 @@ def build_inputs(root: str) -> dict:
         "emptyname": b">chr1\nACGTAC\n> desc only\nACGTAC\n",
         "emptyname_short": b">chr1\nACGTAC\n> desc only\nACG\n",
         "syn1m": syn_python(10**6, 42),
+        # VEC_COUNT_MASKED (round 4): a 60-base segment of record a copied
+        # into record b (k-mers shared by two names), and one sequence under
+        # one name twice (shared by one name only)
+        "vecshare": vec_shared(),
+        "vecsame": (">same first\n" + wrap("".join(random.Random(5).choices("ACGT", k=90))) + ">same second\n"
+                    + wrap("".join(random.Random(5).choices("ACGT", k=90)))).encode(),
     }
     paths = {}
     for name, data in files.items():

@@ -191,3 +191,43 @@ def test_cli_hist_multi_gpu_path_world1(golden_inputs, tmp_path, monkeypatch):
     monkeypatch.setenv("KMAN_DIST_EXCHANGE", "1")
     _cli(["hist", golden_inputs["messy1"], out2, "21"])
     assert open(out1, "rb").read() == open(out2, "rb").read() and os.path.getsize(out1) > 0
+
+
+@pytest.mark.parametrize("case", _manifest().get("vec_cases", []), ids=lambda c: c["name"])
+def test_cli_vec_masked_matches_reference(case, golden_inputs, tmp_path, monkeypatch):
+    """`kmer count --count-mode VEC_COUNT_MASKED` (default: the reference's
+    behaviour) raises where the reference raised -- a group holding records
+    of two names reaches add_count, join.py:318-335 -- and otherwise leaves
+    the same (empty) vector folder; k > 32 through the word-key path."""
+    import builtins
+
+    monkeypatch.delenv("KMAN_VEC_COUNT", raising=False)
+    out = str(tmp_path / "vec.out")
+    argv = ["count", golden_inputs[case["input"]], out, str(case["k"]), "--count-mode", "VEC_COUNT_MASKED"] + case["flags"]
+    if case["result"]["ok"]:
+        _cli(argv)
+        assert sorted(os.listdir(str(tmp_path / "vec"))) == case["folder"]
+    else:
+        with pytest.raises(getattr(builtins, case["result"]["type"])):
+            _cli(argv)
+
+
+@pytest.mark.parametrize("k", [21, 40])
+def test_cli_vec_masked_previous_batches(k, golden_inputs, tmp_path, monkeypatch):
+    """-B: the VEC_COUNT_MASKED decision from reloaded batch files (refs read
+    from the batch records' titles) is the one the FASTA gives (the
+    reference's loader rejects every non-empty folder, SURVEY §A-5: evident
+    intent), at k <= 32 and k > 32."""
+    monkeypatch.delenv("KMAN_VEC_COUNT", raising=False)
+    want = {c["input"]: c["result"]["ok"] for c in _manifest()["vec_cases"] if c["k"] == 40 and not c["flags"]}
+    for inp in ("vecshare", "vecsame"):
+        outdir = str(tmp_path / ("b_%s" % inp))
+        _cli(["batch", golden_inputs[inp], outdir, str(k), "-b", "50"])
+        out = str(tmp_path / ("%s.out" % inp))
+        argv = ["count", golden_inputs[inp], out, str(k), "--count-mode", "VEC_COUNT_MASKED", "-B", outdir]
+        if want[inp]:
+            _cli(argv)
+            assert os.listdir(str(tmp_path / inp)) == []
+        else:
+            with pytest.raises(NotImplementedError):
+                _cli(argv)
