@@ -16,8 +16,11 @@ Reported beside it:
     pass of the previous chunk (shard.StreamedPipeline), beside the serial
     variant and the plain H2D time of the text;
   * ``output``: device text formatting and the file write of a bounded
-    slice of the rows, as rates and as ms extrapolated to all rows;
+    slice of the rows, as rates and as ms extrapolated to all rows, beside
+    the plain D2H rate (``output.d2h``) that bounds them;
   * ``file_to_file``: the CLI (`kmer count`) on a bounded FASTA file;
+    ``file_to_file_config2``: the CLI (`kmer uniq`) on config 2's whole 1 GB
+    FASTA into /dev/null and into a file;
   * ``roofline``: the dominant kernel of the step (largest stage), its
     algorithmic bytes per launch over its HIP-event duration, against the
     8 TB/s HBM peak; ``sort_pass_roofline``: the digit pass (the north star's
@@ -46,6 +49,7 @@ import argparse
 import json
 import os
 import re
+import shutil
 import subprocess
 import sys
 import tempfile
@@ -256,6 +260,68 @@ def file_to_file(k: int, nbases: int = 100_000_000):
                       "(includes interpreter + device init)" % (nbases, k)}
 
 
+def d2h_probe(dev, nbytes: int = 1 << 30) -> dict:
+    """One warm device -> pinned host copy of `nbytes` on the copy stream
+    (kman_copy_d2h_async, what the pipelined writer issues per slice): the
+    ceiling of any output line that leaves the GPU."""
+    from ctypes import byref, c_void_p
+
+    from kman_amd import _native as N
+
+    L = N.lib()
+    buf = dev.alloc(nbytes)
+    hp = c_void_p()
+    N.check(dev.ctx, L.kman_host_alloc(dev.ctx, byref(hp), nbytes), "kman_host_alloc")
+    try:
+        def once():
+            N.check(dev.ctx, L.kman_copy_d2h_async(dev.ctx, hp, c_void_p(buf.ptr), nbytes, 0), "kman_copy_d2h_async")
+            N.check(dev.ctx, L.kman_copy_d2h_wait(dev.ctx, 0), "kman_copy_d2h_wait")
+
+        once()  # (warm: maps the pages)
+        t0 = time.perf_counter()
+        for _ in range(3):
+            once()
+        dt = (time.perf_counter() - t0) / 3
+    finally:
+        L.kman_host_free(dev.ctx, hp)
+        buf.free()
+    return {"bytes": nbytes, "ms": dt * 1e3, "gbs": nbytes / dt / 1e9}
+
+
+def file_to_file_config2(path: str, k: int, mode: str, text_bytes_est: int) -> dict:
+    """`python -m kman_amd MODE IN OUT k` on config 2's whole 1 GB FASTA, what
+    a kmermaid user runs (kmer_uniq.py:73-92 / kmer_count.py): process start
+    to exit, into /dev/null (parse, sort, join, device formatting, D2H; no
+    disk) and into a file (+ the page cache; when the disk has room)."""
+    out = {}
+
+    def run(dst):
+        t0 = time.perf_counter()
+        subprocess.run([sys.executable, "-m", "kman_amd", mode, path, dst, str(k)], check=True, cwd=ROOT,
+                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        return time.perf_counter() - t0
+
+    s = run("/dev/null")
+    out["devnull"] = {"seconds": s}
+    d = os.environ.get("TMPDIR", "/tmp")
+    free = shutil.disk_usage(d).free
+    if free > 1.3 * text_bytes_est + (8 << 30):
+        dst = os.path.join(d, "kman_cfg2_out.txt")
+        try:
+            s2 = run(dst)
+            out["file"] = {"seconds": s2, "output_bytes": os.path.getsize(dst), "gbs": os.path.getsize(dst) / s2 / 1e9}
+        finally:
+            try:
+                os.remove(dst)
+            except OSError:
+                pass
+    else:
+        out["file"] = {"skipped": "%.1f GB free in %s for ~%.1f GB of text" % (free / 1e9, d, text_bytes_est / 1e9)}
+    out["note"] = ("`python -m kman_amd %s <1 GB FASTA> OUT %d`, process start to exit (interpreter, device init, "
+                   "file read, H2D, the step, device formatting, D2H, write)" % (mode, k))
+    return out
+
+
 def run_single(args):
     import numpy as np  # noqa: F401
     import inputs
@@ -303,10 +369,18 @@ def run_single(args):
     if not args.quick:
         try:
             out["output"] = output_lines(dev, pipe, args.k, args.mode)
+            d2h = d2h_probe(dev)
+            out["output"]["d2h"] = d2h
+            out["output"]["format_vs_d2h"] = out["output"]["format_gbs"] / d2h["gbs"]
         except Exception as e:  # reported, never fatal to the GPU number
             out["output"] = {"error": repr(e)}
     pipe.free()
+    cfg2_path = None
     if not args.quick:
+        # config 2's FASTA as a file, for the end-to-end CLI line below
+        fd, cfg2_path = tempfile.mkstemp(suffix=".fa", dir=os.environ.get("TMPDIR", "/tmp"))
+        with os.fdopen(fd, "wb") as fh:
+            fh.write(text)
         # the same step from pinned host bytes (chunked H2D overlapping the parse)
         rd = shard.PinnedReader(dev, text)
         del text
@@ -356,6 +430,18 @@ def run_single(args):
             out["file_to_file"] = file_to_file(args.k)
         except Exception as e:
             out["file_to_file"] = {"error": repr(e)}
+        try:
+            o = out.get("output") or {}
+            est = int(o.get("text_bytes", 0) * pipe.n_out / max(1, o.get("rows", 1))) if "rows" in o else 60 << 30
+            out["file_to_file_config2"] = file_to_file_config2(cfg2_path, args.k, args.mode, est)
+            f2 = out["file_to_file_config2"]
+            for key in ("devnull", "file"):
+                if "seconds" in f2.get(key, {}):
+                    f2[key]["kmers_per_s"] = out["config"]["kmers_per_step_per_gpu"] / f2[key]["seconds"]
+        except Exception as e:
+            out["file_to_file_config2"] = {"error": repr(e)}
+        finally:
+            os.remove(cfg2_path)
     if not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.k, args.mode)

@@ -81,9 +81,46 @@ class Device:
             )
         self.ctx = ctx.value
         self.index = device
+        self._fmt = None  # (cap, pinned stages, device slices) of the pipelined writer
+
+    def fmt_buffers(self, cap: int, nb: int):
+        """The pipelined writer's nb pinned host stages and nb device text
+        slices of >= cap bytes, kept across calls (a pinned allocation of a
+        few hundred MB costs tens of ms: per call it was a large part of a
+        bounded write)."""
+        if self._fmt is not None and self._fmt[0] >= cap and len(self._fmt[1]) >= nb:
+            return self._fmt[1], self._fmt[2]
+        self._free_fmt()
+        L = N.lib()
+        stages, dbufs = [], []
+        try:
+            for _ in range(nb):
+                hp = c_void_p()
+                N.check(self.ctx, L.kman_host_alloc(self.ctx, byref(hp), cap), "kman_host_alloc")
+                stages.append(hp)
+                dbufs.append(self.alloc(cap))
+        except Exception:
+            for hp in stages:
+                L.kman_host_free(self.ctx, hp)
+            for b in dbufs:
+                b.free()
+            raise
+        self._fmt = (cap, stages, dbufs)
+        return stages, dbufs
+
+    def _free_fmt(self) -> None:
+        if self._fmt is not None and self.ctx:
+            L = N.lib()
+            L.kman_copy_sync(self.ctx)
+            for hp in self._fmt[1]:
+                L.kman_host_free(self.ctx, hp)
+            for b in self._fmt[2]:
+                b.free()
+        self._fmt = None
 
     def close(self) -> None:
         if self.ctx:
+            self._free_fmt()
             N.lib().kman_destroy(c_void_p(self.ctx))
             self.ctx = None
 
@@ -718,6 +755,25 @@ _FMT_SLICE = 256 << 20  # text bytes per pipelined slice (_format_dev)
 _FMT_THREADS = int(os.environ.get("KMAN_FMT_THREADS", "8"))  # host copy threads
 
 
+def _pwrite_target(sink):
+    """(fd, offset) when the pipelined writer may put slices at computed
+    offsets with os.pwrite -- a regular file not opened for appending (pwrite
+    on an O_APPEND descriptor ignores the offset on Linux, and a pipe or a
+    terminal has no offsets) -- else (None, 0): the slices are then written
+    in order by the calling thread through sink.write."""
+    import fcntl
+    import stat
+
+    try:
+        sink.flush()
+        fd = sink.fileno()
+        if not stat.S_ISREG(os.fstat(fd).st_mode) or fcntl.fcntl(fd, fcntl.F_GETFL) & os.O_APPEND:
+            return None, 0
+        return fd, sink.tell()
+    except (AttributeError, OSError, ValueError):
+        return None, 0
+
+
 def _format_dev(dev: Device, n: int, row_bytes: int, call, sink=None):
     """Run a kman_format_*_dev call over row slices.  call(i0, rows, d_out,
     cap, used) formats rows [i0, i0 + rows); row_bytes bounds one row.
@@ -746,20 +802,11 @@ def _format_dev(dev: Device, n: int, row_bytes: int, call, sink=None):
         out = bytearray(int(used.value))
         dst0 = ctypes.addressof((ctypes.c_char * max(1, len(out))).from_buffer(out)) if len(out) else 0
     else:
-        try:
-            sink.flush()
-            fd, base = sink.fileno(), sink.tell()
-        except (AttributeError, OSError, ValueError):
-            fd = None  # (a sink without a file descriptor: written in order by this thread)
+        fd, base = _pwrite_target(sink)
     NB = 2
-    stages, dbufs = [], []
+    stages, dbufs = dev.fmt_buffers(cap, NB)
     pool = cf.ThreadPoolExecutor(max_workers=_FMT_THREADS)
     try:
-        for _ in range(NB):
-            hp = c_void_p()
-            N.check(dev.ctx, L.kman_host_alloc(dev.ctx, byref(hp), cap), "kman_host_alloc")
-            stages.append(hp)
-            dbufs.append(dev.alloc(cap))
         pending = [[] for _ in range(NB)]
         piece = max(1 << 20, cap // _FMT_THREADS + 1)
 
@@ -804,10 +851,6 @@ def _format_dev(dev: Device, n: int, row_bytes: int, call, sink=None):
     finally:
         pool.shutdown(wait=True)
         N.check(dev.ctx, L.kman_copy_sync(dev.ctx), "kman_copy_sync")
-        for x in dbufs:
-            x.free()
-        for hp in stages:
-            L.kman_host_free(dev.ctx, hp)
     if out is not None:
         assert at == len(out)
         return out

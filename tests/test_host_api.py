@@ -134,3 +134,28 @@ def test_joiner_modes(tmp_path):
     (tmp_path / "file").write_text("")
     with pytest.raises(AssertionError):  # the directory path is a file
         KJoiner(KJoiner.MODE.VEC_COUNT_MASKED).join([], str(tmp_path / "file.txt"))
+
+
+def test_pipelined_writer_pwrite_only_into_regular_non_append_files(tmp_path):
+    """The pipelined writer (engine._format_dev) puts slices at computed
+    offsets with os.pwrite only where that is the file's order: a regular
+    file opened without O_APPEND; an append-mode file, a pipe or a sink
+    without a descriptor are written in order by the calling thread."""
+    import io
+
+    from kman_amd import engine
+
+    with open(tmp_path / "w.txt", "wb") as fh:
+        fh.write(b"abc")
+        fd, base = engine._pwrite_target(fh)
+        assert fd == fh.fileno() and base == 3
+    with open(tmp_path / "a.txt", "ab") as fh:
+        assert engine._pwrite_target(fh) == (None, 0)
+    assert engine._pwrite_target(io.BytesIO()) == (None, 0)
+    r, w = os.pipe()
+    try:
+        with os.fdopen(w, "wb", closefd=False) as fh:
+            assert engine._pwrite_target(fh) == (None, 0)
+    finally:
+        os.close(r)
+        os.close(w)
