@@ -73,8 +73,13 @@ def _groups(dev, text, k, rc, mode):
 @pytest.mark.parametrize("k", [5, 9, 13, 21, 25])
 @pytest.mark.parametrize("rc", [False, True])
 @pytest.mark.parametrize("mode", ["count", "uniq"])
-def test_groups_matches_oracle(dev, golden_inputs, k, rc, mode):
+@pytest.mark.parametrize("check", ["0", "1"])
+def test_groups_matches_oracle(dev, golden_inputs, monkeypatch, k, rc, mode, check):
+    """(check: the uniq finish without / with the early-count device check,
+    the product default and the GPU test session's setting)"""
     from kman_amd import _native as N
+
+    monkeypatch.setenv("KMAN_RG_CHECK", check)
 
     for text in _texts(golden_inputs):
         n_bases = sum(len(s) for _, s in __import__("np_oracle").parse_fasta(text))
