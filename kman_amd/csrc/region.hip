@@ -46,9 +46,12 @@ constexpr int RT = 512;           // threads of passes 0 and 1
 constexpr int RS = 64;            // position segments of pass 0 (one wave of counts)
 constexpr int RSI = 16;           // items per thread, pass 1
 constexpr uint64_t T1 = (uint64_t)RT * RSI;  // pass-1 tile
-constexpr int FT = 512;           // finish threads (two blocks per CU)
-constexpr int FIPT = 17;          // finish items per thread
-constexpr int FCAP = FT * FIPT;   // 8704 items = 68 KiB: largest region
+#ifndef RG_FT64
+#define RG_FT64 512
+#endif
+constexpr int FT = 512;           // finish threads, 4-byte items (three blocks per CU)
+constexpr int FCAP = 8704;        // largest region: 68 KiB of 8-byte items
+constexpr int FT64 = RG_FT64;     // finish threads, 8-byte items (two blocks per CU)
 constexpr int FBITS = 9;          // finish LSD digit (26 bits: 3 passes)
 constexpr int FRAD = 1 << FBITS;
 constexpr int FWORD = FRAD / 2;   // per-wave counters: two u16 per word
@@ -544,15 +547,20 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
 // flips one mark of region `hook` (a test of the check itself).
 enum { RG_COUNT = 1, RG_UNIQ = 2 };
 
+// threads per block: FT for 4-byte items and for the ballot ranks (their
+// registers), FT64 for 8-byte items with the atomic ranks
+template <typename T, bool ATOMIC>
+constexpr int fin_threads() { return sizeof(T) == 4 || !ATOMIC ? FT : FT64; }
+
 template <int MODE, typename O, bool ATOMIC, typename T = uint64_t, int CHK = 0>
-__global__ __launch_bounds__(FT, (sizeof(T) == 4 ? 6 : 4)) void rg_finish(
+__global__ __launch_bounds__((fin_threads<T, ATOMIC>()), (sizeof(T) == 4 ? 6 : (fin_threads<T, ATOMIC>()) / 128)) void rg_finish(
     const uint64_t *__restrict__ in, uint64_t C1, const uint32_t *__restrict__ cnt1, uint32_t Q, uint32_t rest,
     uint32_t rc, uint64_t rbase, uint32_t tag_shift, uint32_t fsub, uint64_t *__restrict__ okeys,
     O *__restrict__ ovals, uint64_t *__restrict__ status, uint32_t *__restrict__ counter, uint32_t epoch,
     uint32_t *__restrict__ err, uint32_t hook, uint64_t *__restrict__ stp, uint32_t nreg,
     uint8_t *__restrict__ freg) {
-    constexpr int NT = FT, NW_ = NT / 64;
-    constexpr int IPT = FIPT;  // items per thread
+    constexpr int NT = fin_threads<T, ATOMIC>(), NW_ = NT / 64;
+    constexpr int IPT = (FCAP + NT - 1) / NT;  // items per thread
     constexpr bool NARROW = sizeof(T) == 4;
     static_assert(!NARROW || MODE == RG_COUNT, "narrow items: count mode");
     static_assert(CHK == 0 || MODE == RG_UNIQ, "the early count is uniq's");
@@ -604,7 +612,7 @@ __global__ __launch_bounds__(FT, (sizeof(T) == 4 ? 6 : 4)) void rg_finish(
     RSTAMP(r, 1);
 
     // stable LSD passes of <= 9 bits.  Ranks: per-wave u16 counters packed two
-    // to a word (a wave ranks <= 64 * FIPT items), same-word LDS atomics of one
+    // to a word (a wave ranks <= 64 * IPT items), same-word LDS atomics of one
     // wave return in lane order (probed: ATOMIC), else ballot match-any.
     const uint32_t np = (rest + FBITS - 1) / FBITS;
     // EARLY (uniq): the region's row count is found after the second-to-last
@@ -771,7 +779,7 @@ __global__ __launch_bounds__(FT, (sizeof(T) == 4 ? 6 : 4)) void rg_finish(
     }
 
     RSTAMP(r, 2);
-    // ---- run-length pass (thread t: sorted positions t*FIPT ..)
+    // ---- run-length pass (thread t: sorted positions t*IPT ..)
     const uint32_t q0 = (uint32_t)t * IPT;
     uint32_t heads = 0, tails = 0;
 #define RKEY(v) (((v) >> Q) & rmask)
@@ -975,7 +983,8 @@ struct FinishArgs {
 template <int MODE, typename O, bool ATOMIC, typename T = uint64_t, int CHK = 0>
 void launch_finish_as(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ovals, uint32_t epoch,
                       uint32_t *counter, uint32_t hook, uint64_t *stp) {
-    hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, T, CHK>), dim3(f.nreg), dim3(FT), 0, ctx->stream, f.in, f.C1, f.cnt,
+    hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, T, CHK>), dim3(f.nreg), dim3(fin_threads<T, ATOMIC>()), 0,
+                       ctx->stream, f.in, f.C1, f.cnt,
                        f.Q, f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status, counter,
                        epoch, ctx->d_err, hook, stp, f.nreg, f.freg);
 }
