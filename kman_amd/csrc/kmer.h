@@ -101,15 +101,22 @@ KMAN_DEV uint32_t roll_seq(const uint8_t *s, int base, int k, uint64_t mask, uin
     return valid;
 }
 
-// The same windows bit-parallel (rollfast.h): aligned 32-bit LDS reads packed
+// The same windows bit-parallel (rollfast.h): aligned LDS word reads packed
 // four codes per multiply, each window a funnel shift of the packed stream.
+// base = threadIdx.x * EI at every call site and s is 16-byte aligned, so the
+// words are read as 16- or 8-byte vectors when EI is a multiple of 16 / 8.
 template <int EI, int CANON>
 KMAN_DEV uint32_t roll(const uint8_t *s, int base, int k, uint64_t mask, uint64_t p0, uint64_t n_bases,
                        uint64_t (&kf)[EI], uint64_t (&kr)[EI]) {
 #ifdef KMAN_ROLL_SEQ
     return roll_seq<EI, CANON>(s, base, k, mask, p0, n_bases, kf, kr);
 #else
-    return roll_fast<EI, CANON>(s, base, k, mask, p0, n_bases, kf, kr);
+#ifdef KMAN_ROLL_A4
+    constexpr int A = 4;  // (A/B: 4-byte word reads)
+#else
+    constexpr int A = EI % 16 == 0 ? 16 : (EI % 8 == 0 ? 8 : 4);
+#endif
+    return roll_fast<EI, CANON, A>(s, base, k, mask, p0, n_bases, kf, kr);
 #endif
 }
 

@@ -46,18 +46,27 @@ constexpr int RT = 512;           // threads of passes 0 and 1
 constexpr int RS = 64;            // position segments of pass 0 (one wave of counts)
 constexpr int RSI = 16;           // items per thread, pass 1
 constexpr uint64_t T1 = (uint64_t)RT * RSI;  // pass-1 tile
-#ifndef RG_FT64
-#define RG_FT64 512
-#endif
-constexpr int FT = 512;           // finish threads, 4-byte items (three blocks per CU)
-constexpr int FCAP = 8704;        // largest region: 68 KiB of 8-byte items
-constexpr int FT64 = RG_FT64;     // finish threads, 8-byte items (two blocks per CU)
+constexpr int FT = 512;           // finish threads (more threads per region, e.g. 640 or 576: a
+                                  // second block no longer fits the CU's SIMDs, 9.5 / 11.5 vs 5.7 ms)
+constexpr int FCAP = 8704;        // round-path finish capacity: 68 KiB of 8-byte items
 constexpr int FBITS = 9;          // finish LSD digit (26 bits: 3 passes)
 constexpr int FRAD = 1 << FBITS;
 constexpr int FWORD = FRAD / 2;   // per-wave counters: two u16 per word
 constexpr uint32_t ERR_REGION = 1u << 8;  // a region would overflow (not an engine fault)
 constexpr uint32_t ERR_EARLY = 1u << 9;   // the uniq finish's early row count was not its rows'
-constexpr uint32_t B1 = 8;        // pass-0 digit = top 8 key bits
+constexpr uint32_t B1 = 8;        // pass-0 digit: top 8 key bits
+// kman_groups' pass-0 bits.  (9, with 9 more in pass 1, leaves regions of ~3.8
+// K items per 1 G k-mers that a GCAP finish holds in 40 KiB -- three blocks
+// per CU -- but the finish's per-region costs dominate there: 5.96 vs 5.62
+// ms, and the 512-bucket pass 0 4.0 vs 3.6 ms)
+constexpr uint32_t G1 = B1;
+// finish capacities (items): FCAP (68 KiB of 8-byte items, two blocks per
+// CU) and GCAP (40 KiB, three blocks per CU) for the round path's small
+// regions (a pass 1b over many ranks' items leaves ~4 K per region)
+constexpr int GCAP = 5120;
+// expected region fills the plans aim at (<= T) and accept (<= M): M keeps
+// > 10 sd of a uniform fill below the capacity
+constexpr uint64_t FFILL_T = 6144, FFILL_M = 7800;
 
 // phase stamps (s_memrealtime, 100 MHz) per tile, thread 0, into `stp`: only
 // in diagnostic builds (make EXTRA=-DKMAN_RG_STAMPS OUT=../lib_stamps,
@@ -124,7 +133,7 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 // the 128-byte line two of them share meets in that XCD's L2 instead of
 // leaving two partial lines.  Placement changes only speed; a block leaves
 // only when every partition is dealt out.
-template <int EI, bool RC, int CANON, bool EX, bool XG>
+template <int EI, bool RC, int CANON, bool EX, bool XG, int P0B = (int)(EX ? B1 : G1)>
 __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI == 8 ? 8 : 4)))) void rg_extract(
     const uint8_t *__restrict__ codes, uint64_t n_bases, int k, uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
     uint32_t seg_tiles, uint32_t n_tiles, const uint32_t *__restrict__ cnt0, uint32_t *__restrict__ cursor,
@@ -138,59 +147,56 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     constexpr bool IL = !EX;
     static_assert(WIN + 64 <= TILE * 8, "codes fit in the key staging area");
     static_assert(RS % 8 == 0, "XCD partitions of whole segments");
+    constexpr uint32_t R0 = 1u << P0B;  // pass-0 radix
+    static_assert(R0 <= (uint32_t)NT && (!EX || R0 == RADIX), "a thread per digit; the round path's 256 buckets");
     __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
-    __shared__ uint32_t thist[RADIX];
-    __shared__ uint32_t lstart[RADIX];
-    __shared__ uint64_t gexcl[RADIX];
+    __shared__ uint32_t thist[R0];
+    __shared__ uint32_t lstart[R0];
+    __shared__ uint64_t gexcl[R0];
     __shared__ uint32_t lds_scan[NWAVE];
-    __shared__ uint32_t lds_tile;
-    __shared__ uint32_t keep[EX ? RADIX / 32 : 1];
+    __shared__ uint32_t keep[EX ? R0 / 32 : 1];
 
-    uint32_t cid;
-    if (XG) {
-        if (threadIdx.x == 0) {
+    // one tile per block: a ticket of a tile that exists (thread 0 only),
+    // ~0u when every partition is dealt out (XG) or past the tiles / a
+    // segment's end.  (Persistent blocks that load the next tile's codes
+    // into registers while this one is worked measured slower: 3.97-4.19 vs
+    // 3.64-3.83 ms, the loop costs registers and spills.)
+    __shared__ uint32_t lds_tile;
+    auto take = [&]() -> uint32_t {
+        uint32_t c = ~0u;
+        if (XG) {
             constexpr uint32_t CPG = RS / 8;  // segments per partition
             const uint32_t x = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // hwreg(HW_REG_XCC_ID, 0, 4)
-            uint32_t got = ~0u;
-            for (uint32_t a = 0; a < 8 && got == ~0u; a++) {
+            for (uint32_t a = 0; a < 8 && c == ~0u; a++) {
                 const uint32_t pp = (x + a) & 7u;
                 const uint32_t j = atomicAdd(counter + pp, 1u);
                 const uint64_t tt = (uint64_t)(j / CPG) * RS + pp * CPG + j % CPG;
-                if (tt < (IL ? (uint64_t)n_tiles : (uint64_t)RS * seg_tiles)) got = (uint32_t)tt;
+                if (tt < (IL ? (uint64_t)n_tiles : (uint64_t)RS * seg_tiles)) c = (uint32_t)tt;
             }
-            lds_tile = got;
+        } else {
+            c = atomicAdd(counter, 1u);
         }
-        __syncthreads();
-        cid = lds_tile;
-        __syncthreads();
-        if (cid == ~0u) return;  // (block-uniform: every partition dealt out)
-    } else {
-        cid = (uint32_t)grab_tile(counter, &lds_tile);
-    }
-    uint32_t sgi;
-    int64_t tile;
-    if (IL) {
-        tile = cid;
-        if (tile >= (int64_t)n_tiles) return;  // (block-uniform)
-        sgi = (uint32_t)(tile % RS);
-    } else {
-        sgi = cid % RS;
-        const uint32_t jj = cid / RS;
-        const uint32_t t0 = sgi * seg_tiles;
-        const uint32_t t1 = t0 + seg_tiles < n_tiles ? t0 + seg_tiles : n_tiles;
-        if (t0 + jj >= t1) return;  // (block-uniform) past a segment's end
-        tile = (int64_t)t0 + jj;
-    }
+        if (c == ~0u) return ~0u;
+        if (IL) return c < n_tiles ? c : ~0u;
+        const uint32_t s_ = c % RS, jj = c / RS, t0 = s_ * seg_tiles;
+        return t0 + jj < (t0 + seg_tiles < n_tiles ? t0 + seg_tiles : n_tiles) ? c : ~0u;
+    };
+    if (threadIdx.x == 0) lds_tile = take();
+    __syncthreads();
+    const uint32_t cid = lds_tile;
+    if (cid == ~0u) return;  // (block-uniform)
+    const int64_t tile = IL ? (int64_t)cid : (int64_t)(cid % RS) * seg_tiles + cid / RS;
+    const uint32_t sgi = cid % RS;
     RSTAMP(tile, 0);
     const uint32_t kb = 2u * (uint32_t)k;
-    const uint32_t shift = kb - B1;
+    const uint32_t shift = kb - P0B;
     const uint64_t keymask = kb >= 64 ? ~0ull : ((1ull << kb) - 1);
     const uint64_t restmask = (1ull << shift) - 1;
-    const uint64_t wb = (uint64_t)tile * WIN;
     uint8_t *scodes = reinterpret_cast<uint8_t *>(skeys);
+    const uint64_t wb = (uint64_t)tile * WIN;
     stage_codes<NT, EI>(codes, n_bases, wb, scodes);
-    if (threadIdx.x < RADIX) thist[threadIdx.x] = 0;
-    if (EX && threadIdx.x < RADIX) {  // (one table load per thread, a ballot per wave)
+    if (threadIdx.x < R0) thist[threadIdx.x] = 0;
+    if (EX && threadIdx.x < R0) {  // (one table load per thread, a ballot per wave)
         const uint64_t bal = __ballot(rtab[(uint64_t)threadIdx.x * RS + sgi] != ~0ull);
         if ((threadIdx.x & 63) == 0) {
             keep[threadIdx.x / 32] = (uint32_t)bal;
@@ -241,16 +247,16 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     for (int i = 0; i < SI; i++) rank[i] = (vmask >> i) & 1u ? atomicAdd(&thist[XDIGIT(key[i])], 1u) : 0u;
     __syncthreads();  // (also: every roll read of the staged codes before the scatter below)
     RSTAMP(tile, 2);
-    if (threadIdx.x < RADIX) {  // the tile's place in each region, claimed now
+    if (threadIdx.x < R0) {  // the tile's place in each region, claimed now
         const uint32_t c = thist[threadIdx.x];
         at_base = c ? atomicAdd(cursor + threadIdx.x * RS + sgi, c) : 0u;
     }
     RSTAMP(tile, 3);
     const uint32_t d0 = threadIdx.x;
-    const uint32_t tot = d0 < RADIX ? thist[d0] : 0u;
+    const uint32_t tot = d0 < R0 ? thist[d0] : 0u;
     uint32_t tcnt;
     const uint32_t ls = block_exclusive_scan1<NT>(tot, SumU32(), 0u, lds_scan, &tcnt);
-    if (d0 < RADIX) lstart[d0] = ls;
+    if (d0 < R0) lstart[d0] = ls;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < SI; i++) {
@@ -259,7 +265,8 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
             skeys[lstart[d] + rank[i]] = key[i];
         }
     }
-    if (threadIdx.x < RADIX) {
+
+    if (threadIdx.x < R0) {
         const uint32_t d = threadIdx.x;
         const uint64_t incl = (uint64_t)at_base + thist[d];
         if (EX) {  // (digits not kept this round have no items)
@@ -347,13 +354,17 @@ struct PassArgs {
 //   * write combining: each digit's last partial 128-byte line (< 16 items)
 //     stays in LDS until a later tile completes it, so only whole lines leave
 //     the CU, each written within one tile's store phase (64 KiB of LDS).
+// (512-thread blocks, two per CU, with 64-byte write-combining lines --
+// 32 KiB each -- measured slower: 4.32 vs 3.48 ms)
 constexpr int PT_NT = 1024, PT_SI = 8, PT = PT_NT * PT_SI;
+constexpr uint32_t PT_WLB = 4, PT_WL = 1u << PT_WLB;  // items per write-combining line (128 bytes)
 __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
                                                    uint32_t *__restrict__ err, uint64_t *__restrict__ stp) {
     constexpr int NT = PT_NT, SI = PT_SI, TILE = PT, NWAVE = NT / 64;
-    static_assert(NT >= R1 && NT / 16 <= R1, "a thread per digit");
+    constexpr uint32_t WL = PT_WL, WM = WL - 1;
+    static_assert(NT >= R1 && NT / WL <= R1, "a thread per digit");
     __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
-    __shared__ uint64_t wcb[R1][16];  // the pending items of digit d at wcb[d][pos % 16]
+    __shared__ uint64_t wcb[R1][WL];  // the pending items of digit d at wcb[d][pos % WL]
     // per digit for the store loop: qpar[d] = (q bound of the whole-line
     // items << 32) | the output index of tile item 0 relative to the chain's
     // first sub-region (digit d's sub-region is d * gsub * H after it, and
@@ -439,6 +450,8 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
         };
         if (ra < rb) load_tile(ra);
         for (uint32_t r = ra; r < rb; r++) {
+            // (double-buffered counts, so that neither this clear nor the
+            // update below needs its barrier: no faster, 3.50 vs 3.41-3.50 ms)
             if (threadIdx.x < R1) thist[threadIdx.x] = 0;
             __syncthreads();
             const uint32_t t0 = r * TILE;
@@ -471,9 +484,9 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
             // items go out first, 16 lanes per digit (one line per quarter
             // wave, so a store covers 4 lines)
 #pragma unroll
-            for (uint32_t d = threadIdx.x >> 4; d < (uint32_t)R1; d += NT / 16) {
-                const uint32_t j = threadIdx.x & 15u, rn = run[d], p = rn & 15u;
-                if (j < p && ((rn + thist[d]) >> 4) > (rn >> 4) && rn - p + j < C1)
+            for (uint32_t d = threadIdx.x >> PT_WLB; d < (uint32_t)R1; d += NT / WL) {
+                const uint32_t j = threadIdx.x & WM, rn = run[d], p = rn & WM;
+                if (j < p && ((rn + thist[d]) >> PT_WLB) > (rn >> PT_WLB) && rn - p + j < C1)
                     obase0[d * dstride + rn - p + j] = wcb[d][j];
             }
             if (threadIdx.x < R1) {
@@ -481,7 +494,7 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
                 // end at fe; positions >= C1 are dropped (an overflowing
                 // region raises ERR_REGION, so where its items go is moot)
                 const uint32_t d = threadIdx.x, rn = run[d], off = rn - lstart[d];
-                const int32_t fe = (int32_t)((rn + thist[d]) & ~15u);
+                const int32_t fe = (int32_t)((rn + thist[d]) & ~WM);
                 const int32_t qlim = (fe < (int32_t)C1 ? fe : (int32_t)C1) - (int32_t)off;
                 qpar[d] = ((uint64_t)(uint32_t)qlim << 32) | (d * dstride + off);
             }
@@ -496,7 +509,7 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
                     const uint64_t qp = qpar[d];
                     const uint32_t rel = (uint32_t)qp + q;
                     if ((int32_t)q < (int32_t)(qp >> 32)) obase0[rel] = kk;
-                    else wcb[d][rel & 15u] = kk;
+                    else wcb[d][rel & WM] = kk;
                 }
             }
             // the next tile's loads behind the stores (issued before the
@@ -512,8 +525,8 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
         __syncthreads();
         // the last partial lines, 16 lanes per digit
 #pragma unroll
-        for (uint32_t d = threadIdx.x >> 4; d < (uint32_t)R1; d += NT / 16) {
-            const uint32_t j = threadIdx.x & 15u, rn = run[d], p = rn & 15u;
+        for (uint32_t d = threadIdx.x >> PT_WLB; d < (uint32_t)R1; d += NT / WL) {
+            const uint32_t j = threadIdx.x & WM, rn = run[d], p = rn & WM;
             if (j < p && rn - p + j < C1) pa.out[SUBREG(d) * C1 + rn - p + j] = wcb[d][j];
         }
         if (threadIdx.x < R1) {
@@ -547,24 +560,30 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
 // flips one mark of region `hook` (a test of the check itself).
 enum { RG_COUNT = 1, RG_UNIQ = 2 };
 
-// threads per block: FT for 4-byte items and for the ballot ranks (their
-// registers), FT64 for 8-byte items with the atomic ranks
-template <typename T, bool ATOMIC>
-constexpr int fin_threads() { return sizeof(T) == 4 || !ATOMIC ? FT : FT64; }
+// waves per SIMD the launch bounds ask for: 8-byte items of a GCAP region
+// (40 KiB) and 4-byte items: three blocks per CU; 8-byte items of an FCAP
+// region (68 KiB) and the ballot ranks (their registers): two
+template <typename T, bool ATOMIC, int CAP>
+constexpr int fin_waves() {
+    // (4-byte items of a GCAP region, 28 KiB: four blocks per CU in 64
+    // VGPRs, 6.46 vs 7.07 ms per 1 G k-mers at three)
+    if (sizeof(T) == 4 && CAP <= GCAP) return 8;
+    return sizeof(T) == 4 || (ATOMIC && CAP <= GCAP) ? 6 : 4;
+}
 
-template <int MODE, typename O, bool ATOMIC, typename T = uint64_t, int CHK = 0>
-__global__ __launch_bounds__((fin_threads<T, ATOMIC>()), (sizeof(T) == 4 ? 6 : (fin_threads<T, ATOMIC>()) / 128)) void rg_finish(
+template <int MODE, typename O, bool ATOMIC, typename T = uint64_t, int CHK = 0, int CAP = FCAP>
+__global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     const uint64_t *__restrict__ in, uint64_t C1, const uint32_t *__restrict__ cnt1, uint32_t Q, uint32_t rest,
     uint32_t rc, uint64_t rbase, uint32_t tag_shift, uint32_t fsub, uint64_t *__restrict__ okeys,
     O *__restrict__ ovals, uint64_t *__restrict__ status, uint32_t *__restrict__ counter, uint32_t epoch,
     uint32_t *__restrict__ err, uint32_t hook, uint64_t *__restrict__ stp, uint32_t nreg,
     uint8_t *__restrict__ freg) {
-    constexpr int NT = fin_threads<T, ATOMIC>(), NW_ = NT / 64;
-    constexpr int IPT = (FCAP + NT - 1) / NT;  // items per thread
+    constexpr int NT = FT, NW_ = NT / 64;
+    constexpr int IPT = (CAP + NT - 1) / NT;  // items per thread
     constexpr bool NARROW = sizeof(T) == 4;
     static_assert(!NARROW || MODE == RG_COUNT, "narrow items: count mode");
     static_assert(CHK == 0 || MODE == RG_UNIQ, "the early count is uniq's");
-    __shared__ __attribute__((aligned(16))) T s[FCAP];
+    __shared__ __attribute__((aligned(16))) T s[CAP];
     __shared__ uint32_t wh[NW_][FWORD];  // per-wave digit counters, u16 pairs
     __shared__ uint32_t lds_scan[NW_], lds_scan2[NW_];
     __shared__ uint32_t s_tile;
@@ -573,38 +592,46 @@ __global__ __launch_bounds__((fin_threads<T, ATOMIC>()), (sizeof(T) == 4 ? 6 : (
     const int t = threadIdx.x, lane = lane_id(), w = t >> 6;
     const uint64_t rmask = (1ull << rest) - 1;
     const uint32_t pw = (uint32_t)w * (IPT * 64) + (uint32_t)lane;  // wave-striped positions
+    // region rr's size m0 (first sub-region) and m (0: emits nothing), and
+    // its items into v (wave-striped positions)
+    auto region_size = [&](uint32_t rr, uint32_t &m0_) -> uint32_t {
+        m0_ = cnt1[(uint64_t)rr * fsub];
+        const uint32_t m1_ = fsub > 1 ? cnt1[(uint64_t)rr * fsub + 1] : 0u;
+        // freg (the round path): a region flagged by a pass (a sub-region
+        // overflowed) or here (more than the LDS holds) emits nothing
+        const uint32_t mm = m0_ + m1_;
+        if (freg && freg[rr]) return 0u;  // (block-uniform)
+        if (mm > (uint32_t)CAP) {
+            if (t == 0) {
+                atomicOr(err, ERR_REGION);  // (block-uniform) more than the LDS holds
+                if (freg) freg[rr] = 1;
+            }
+            return 0u;
+        }
+        return mm;
+    };
+    auto load_items = [&](uint32_t rr, uint32_t m0_, uint32_t mm, T (&v)[IPT]) {
+        // (a uniform base and one 32-bit offset per item: few address VGPRs)
+        const uint64_t *src = in + (uint64_t)rr * fsub * C1;
+        const uint32_t skip = (uint32_t)C1 - m0_;
+#pragma unroll
+        for (int i = 0; i < IPT; i++) {
+            const uint32_t p = pw + i * 64;
+            v[i] = p < mm ? (T)src[p < m0_ ? p : p + skip] : (T)0;
+        }
+    };
+    // one region per block.  (Persistent blocks that load the next region's
+    // items into registers while this one is written: 15 vs 6 ms, spilled at
+    // three blocks per CU; round 2's at two: 11.1 vs 5.7 ms.)
     if (t == 0) s_tile = atomicAdd(counter, 1u);
     __syncthreads();
     const uint32_t r = __builtin_amdgcn_readfirstlane(s_tile);
     if (r >= nreg) return;
-    RSTAMP(r, 0);
-    // a region r = fsub (1 or 2 ...) sub-regions of capacity C1, concatenated:
-    // position p < m0 at in[r * fsub * C1 + p], p >= m0 at .. + C1 - m0 + p
-    const uint32_t m0 = cnt1[(uint64_t)r * fsub];
-    const uint32_t m1 = fsub > 1 ? cnt1[(uint64_t)r * fsub + 1] : 0u;
-    // freg (the round path): a region flagged by a pass (a sub-region
-    // overflowed) or here (more than the LDS holds) emits nothing
-    uint32_t m = m0 + m1;
-    if (freg && freg[r]) {
-        m = 0;  // (block-uniform)
-    } else if (m > (uint32_t)FCAP) {
-        if (t == 0) {
-            atomicOr(err, ERR_REGION);  // (block-uniform) more than the LDS holds
-            if (freg) freg[r] = 1;
-        }
-        m = 0;
-    }
+    uint32_t m0;
+    const uint32_t m = region_size(r, m0);
     T x[IPT];
-    {
-        // (a uniform base and one 32-bit offset per item: few address VGPRs)
-        const uint64_t *src = in + (uint64_t)r * fsub * C1;
-        const uint32_t skip = (uint32_t)C1 - m0;
-#pragma unroll
-        for (int i = 0; i < IPT; i++) {
-            const uint32_t p = pw + i * 64;
-            x[i] = p < m ? (T)src[p < m0 ? p : p + skip] : (T)0;
-        }
-    }
+    load_items(r, m0, m, x);
+    RSTAMP(r, 0);
 #ifdef KMAN_RG_STAMPS
     __builtin_amdgcn_s_waitcnt(0);  // (diagnostic build: phase 1 = the wait for the region's items)
     if (stp && t == 0) stp[(uint64_t)r * 8 + 7] = m;  // (the region's items, beside its phase stamps)
@@ -923,15 +950,15 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     p.K = 2 * k;
     p.W = n_bases * (p.rc ? 2 : 1);
     p.Q = mode == KMAN_FINISH_UNIQ ? (bitlen(p.W - 1) ? bitlen(p.W - 1) : 1u) : 0u;
-    if (p.K - B1 + p.Q > 64) return KMAN_EFALLBACK;
-    // B2: fewest bits with an expected region fill <= 6144 (at most 9); up
-    // to 7800 expected keeps > 10 sd (uniform data) below the LDS capacity
+    if (p.K - G1 + p.Q > 64) return KMAN_EFALLBACK;
+    // B2: fewest bits with an expected region fill <= FFILL_T (at most 9); up
+    // to FFILL_M expected keeps > 10 sd (uniform data) below the capacity
     uint32_t b2 = 1;
-    while (b2 < 9 && (p.W >> (B1 + b2)) > 6144) b2++;
-    if ((p.W >> (B1 + b2)) > 7800) return KMAN_EFALLBACK;
-    if (p.K < B1 + b2 + 1) return KMAN_EFALLBACK;
+    while (b2 < 9 && (p.W >> (G1 + b2)) > FFILL_T) b2++;
+    if ((p.W >> (G1 + b2)) > FFILL_M) return KMAN_EFALLBACK;
+    if (p.K < G1 + b2 + 1) return KMAN_EFALLBACK;
     p.B2 = b2;
-    p.rest = p.K - B1 - b2;
+    p.rest = p.K - G1 - b2;
     // windows per thread: 16 (8 with -r: two items per window) makes
     // 8192-item tiles, 69 KiB of LDS, two blocks per CU: with the atomic
     // region cursors a tile waits on nothing and the longer digit runs win
@@ -941,10 +968,11 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     const uint64_t win = (uint64_t)RT * p.ei;
     p.n_tiles0 = (uint32_t)ceil_div(n_bases, win);
     p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, RS);
-    const uint64_t e0 = p.W / ((uint64_t)RADIX * RS);
+    const uint64_t nb0 = 1ull << G1;  // pass-0 buckets
+    const uint64_t e0 = p.W / (nb0 * RS);
     p.C0 = ceil_div(e0 + e0 / 2 + 256, 64) * 64;
-    if ((uint64_t)RADIX * RS * p.C0 >= (1ull << 32)) return KMAN_EFALLBACK;  // (32-bit item indices)
-    const uint64_t e1 = p.W >> (B1 + b2);
+    if (nb0 * RS * p.C0 >= (1ull << 32)) return KMAN_EFALLBACK;  // (32-bit item indices)
+    const uint64_t e1 = p.W >> (G1 + b2);
     uint64_t c1 = ceil_div(e1 + e1 / 2 + 512, 64) * 64;
     p.C1 = c1 < (uint64_t)FCAP ? c1 : (uint64_t)FCAP;
     // pass 1 runs H = 2 block-owned chains per bucket (its first and second
@@ -953,10 +981,10 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     p.H = 2;
     p.C1h = p.C1;  // either half may hold most of a region (position-skewed repeats)
     p.maxt1 = (uint32_t)ceil_div((uint64_t)ceil_div(RS, p.H) * p.C0, T1);
-    const uint64_t nreg = 1ull << (B1 + b2);
-    p.off_r1 = (uint64_t)RADIX * RS * p.C0 * 8;
+    const uint64_t nreg = 1ull << (G1 + b2);
+    p.off_r1 = nb0 * RS * p.C0 * 8;
     p.off_c0 = p.off_r1 + nreg * p.H * p.C1h * 8;
-    p.off_c1 = p.off_c0 + (uint64_t)RADIX * RS * 4;
+    p.off_c1 = p.off_c0 + nb0 * RS * 4;
     p.off_lim = p.off_c1 + nreg * p.H * 4;
     p.bytes = p.off_lim + 64;
     *pl = p;
@@ -978,15 +1006,15 @@ struct FinishArgs {
     uint32_t nreg;
     uint32_t fsub = 1;  // sub-regions per region (cnt and in indexed per sub-region)
     uint8_t *freg = nullptr;  // per-region overflow flags (the round path), else null
+    int cap = FCAP;  // the finish's region capacity: GCAP (kman_groups) or FCAP (the round path)
 };
 
-template <int MODE, typename O, bool ATOMIC, typename T = uint64_t, int CHK = 0>
+template <int MODE, typename O, int CAP, bool ATOMIC, typename T = uint64_t, int CHK = 0>
 void launch_finish_as(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ovals, uint32_t epoch,
                       uint32_t *counter, uint32_t hook, uint64_t *stp) {
-    hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, T, CHK>), dim3(f.nreg), dim3(fin_threads<T, ATOMIC>()), 0,
-                       ctx->stream, f.in, f.C1, f.cnt,
-                       f.Q, f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status, counter,
-                       epoch, ctx->d_err, hook, stp, f.nreg, f.freg);
+    hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, T, CHK, CAP>), dim3(f.nreg), dim3(FT), 0, ctx->stream, f.in, f.C1,
+                       f.cnt, f.Q, f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status,
+                       counter, epoch, ctx->d_err, hook, stp, f.nreg, f.freg);
 }
 
 // The early-count check of the uniq finish (rg_finish CHK): KMAN_RG_CHECK=1
@@ -1008,31 +1036,43 @@ EarlyCheck early_check() {
 // shard 84.7 -> 78.3 ms).  Without the probed lane-ordered LDS atomics the
 // ranks are ballots (8-byte items: the ballot ranks overflow the 80 VGPRs of
 // three blocks per CU -- 2.5 KB of spills per lane -- so no narrow variant).
-template <int MODE, typename O>
+template <int MODE, typename O, int CAP>
 void launch_finish(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ovals, uint32_t epoch,
                    uint32_t *counter, uint64_t *stp) {
     if constexpr (MODE == RG_COUNT) {
         if (ctx->lds_atomic_ordered && f.rest <= 32 && f.Q == 0 && f.tag_shift == 0) {
-            launch_finish_as<MODE, O, true, uint32_t>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
+            launch_finish_as<MODE, O, CAP, true, uint32_t>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
             return;
         }
     }
     if (!ctx->lds_atomic_ordered) {
-        launch_finish_as<MODE, O, false>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
+        launch_finish_as<MODE, O, CAP, false>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
         return;
     }
     if constexpr (MODE == RG_UNIQ) {
         const EarlyCheck ck = early_check();
         if (ck.chk == 1) {
-            launch_finish_as<MODE, O, true, uint64_t, 1>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
+            launch_finish_as<MODE, O, CAP, true, uint64_t, 1>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
             return;
         }
         if (ck.chk == 2) {
-            launch_finish_as<MODE, O, true, uint64_t, 2>(ctx, f, okeys, ovals, epoch, counter, ck.hook, stp);
+            launch_finish_as<MODE, O, CAP, true, uint64_t, 2>(ctx, f, okeys, ovals, epoch, counter, ck.hook, stp);
             return;
         }
     }
-    launch_finish_as<MODE, O, true>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
+    launch_finish_as<MODE, O, CAP, true>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
+}
+
+template <int CAP>
+void launch_finish_cap(kman_ctx *ctx, const FinishArgs &f, int mode, uint64_t *okeys, void *ovals,
+                       uint32_t oval_bytes, uint32_t epoch, uint32_t *counter, uint64_t *stp) {
+    if (mode == KMAN_FINISH_UNIQ) {
+        if (oval_bytes == 4) launch_finish<RG_UNIQ, uint32_t, CAP>(ctx, f, okeys, ovals, epoch, counter, stp);
+        else launch_finish<RG_UNIQ, uint64_t, CAP>(ctx, f, okeys, ovals, epoch, counter, stp);
+    } else {
+        if (oval_bytes == 4) launch_finish<RG_COUNT, uint32_t, CAP>(ctx, f, okeys, ovals, epoch, counter, stp);
+        else launch_finish<RG_COUNT, uint64_t, CAP>(ctx, f, okeys, ovals, epoch, counter, stp);
+    }
 }
 
 int run_finish(kman_ctx *ctx, const FinishArgs &f, int mode, uint64_t *okeys, void *ovals, uint32_t oval_bytes,
@@ -1040,13 +1080,8 @@ int run_finish(kman_ctx *ctx, const FinishArgs &f, int mode, uint64_t *okeys, vo
     uint32_t epoch, *counter;
     KMAN_TRY(kman_lookback_begin(ctx, f.nreg + 1, &epoch, &counter));
     KTimer kt_(ctx, "region_finish");
-    if (mode == KMAN_FINISH_UNIQ) {
-        if (oval_bytes == 4) launch_finish<RG_UNIQ, uint32_t>(ctx, f, okeys, ovals, epoch, counter, stp);
-        else launch_finish<RG_UNIQ, uint64_t>(ctx, f, okeys, ovals, epoch, counter, stp);
-    } else {
-        if (oval_bytes == 4) launch_finish<RG_COUNT, uint32_t>(ctx, f, okeys, ovals, epoch, counter, stp);
-        else launch_finish<RG_COUNT, uint64_t>(ctx, f, okeys, ovals, epoch, counter, stp);
-    }
+    if (f.cap == GCAP) launch_finish_cap<GCAP>(ctx, f, mode, okeys, ovals, oval_bytes, epoch, counter, stp);
+    else launch_finish_cap<FCAP>(ctx, f, mode, okeys, ovals, oval_bytes, epoch, counter, stp);
     HIP_TRY(ctx, hipGetLastError());
     return KMAN_OK;
 }
@@ -1071,7 +1106,8 @@ void launch_extract(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, ui
                     uint64_t *r0, uint32_t *c0, uint32_t epoch, uint32_t *counter, uint64_t *stp,
                     uint32_t n_launch) {
     if (!n_launch)
-        hipLaunchKernelGGL((rg_extract<EI, RC, CANON, false, true>), dim3(p.n_tiles0), dim3(RT), 0, ctx->stream, codes,
+        hipLaunchKernelGGL((rg_extract<EI, RC, CANON, false, true>),
+                           dim3(p.n_tiles0), dim3(RT), 0, ctx->stream, codes,
                            n_bases, (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, c0,
                            ctx->d_xcounters + 8 * (epoch & 63u), ctx->d_err, stp, nullptr);
     else
@@ -1198,7 +1234,7 @@ int groups_setup(kman_ctx *ctx, uint64_t n_bases, uint32_t k, uint32_t flags, in
     g->r1 = (uint64_t *)((char *)d_work + p.off_r1);
     g->c0 = (uint32_t *)((char *)d_work + p.off_c0);
     g->c1 = (uint32_t *)((char *)d_work + p.off_c1);
-    g->nreg = 1u << (B1 + p.B2);
+    g->nreg = 1u << (G1 + p.B2);
     return KMAN_OK;
 }
 
@@ -1226,7 +1262,7 @@ int groups_tail(kman_ctx *ctx, const GroupsCall &g, int mode, uint64_t *d_okeys,
         pa.seg_base = nullptr;
         pa.seg_cnt = g.c0;
         pa.stride = p.C0;
-        pa.nbk = RADIX;
+        pa.nbk = 1u << G1;
         pa.nsg = RS;
         pa.gsub = 1;
         pa.H = p.H;
@@ -1247,7 +1283,7 @@ int groups_tail(kman_ctx *ctx, const GroupsCall &g, int mode, uint64_t *d_okeys,
     uint64_t *h = ctx->h_small;
     HIP_TRY(ctx, hipMemcpyAsync(h + 4, ctx->d_status + (g.nreg - 1), 8, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(h + 8, ctx->d_err, 4, hipMemcpyDeviceToHost, ctx->stream));
-    std::vector<uint32_t> hc((size_t)RADIX * RS);
+    std::vector<uint32_t> hc((size_t)RS << G1);
     HIP_TRY(ctx, hipMemcpyAsync(hc.data(), g.c0, hc.size() * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     uint32_t e;
@@ -1283,7 +1319,7 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
     const RegionPlan &p = g.p;
     HIP_TRY(ctx, hipMemsetAsync(g.c0, 0, p.bytes - p.off_c0, ctx->stream));
     uint64_t *stamps[3] = {nullptr, nullptr, nullptr};
-    const uint64_t stamp_rows[3] = {p.n_tiles0, (uint64_t)p.maxt1 * RADIX, g.nreg};
+    const uint64_t stamp_rows[3] = {p.n_tiles0, (uint64_t)p.maxt1 << G1, g.nreg};
     if (getenv("KMAN_RG_STAMPS"))
         for (int q = 0; q < 3; q++) {
             HIP_TRY(ctx, hipMalloc((void **)&stamps[q], stamp_rows[q] * 64));
@@ -1505,6 +1541,7 @@ struct RoundPlan {
     uint32_t H;           // pass-1 chains per (bucket, source)
     bool rc;
     uint64_t C1s, C1;     // pass-1 sub-region / pass-1b region capacities
+    int cap;              // the finish's capacity: GCAP when the planned regions fit it (three blocks per CU)
     uint64_t nsub, nreg;
     // arena A: r1 | c1 | pass-1 segment bases (u64) + counts (u32) | region
     // overflow flags (u8); arena B: r2 | c2
@@ -1566,8 +1603,8 @@ int make_rplan(uint32_t k, uint32_t flags, int mode, uint32_t world, uint64_t n_
             }
         }
     }
-    // pass 1b bits g: until a final region expects <= 6144 items (the LDS
-    // finish holds FCAP = 8704).  g = 0 (no pass 1b, the finish reads the
+    // pass 1b bits g: until a final region expects <= FFILL_T items (the
+    // LDS finish holds FCAP = 8704).  g = 0 (no pass 1b, the finish reads the
     // pass-1 sub-regions) when one rank's 9-bit regions already fit: with one
     // source and two chains (N > 1 needs pass 1b anyway, to tag each item with
     // its source rank for uniq and to merge the ranks' sub-regions)
@@ -1577,9 +1614,9 @@ int make_rplan(uint32_t k, uint32_t flags, int mode, uint32_t world, uint64_t n_
         g = e ? (uint32_t)atoi(e) : 0u;
         g = g <= 9 ? g : 9;
     }
-    if (g == 0 && (world * d.H > 2 || (maxb >> 9) > 7800)) g = 1;  // (7800: the single-GPU path's bound)
-    while (g > 0 && g < 9 && ((maxb >> 9) >> g) > 6144) g++;
-    if (((maxb >> 9) >> g) > 7800) return KMAN_EFALLBACK;
+    if (g == 0 && (world * d.H > 2 || (maxb >> 9) > FFILL_M)) g = 1;
+    while (g > 0 && g < 9 && ((maxb >> 9) >> g) > FFILL_T) g++;
+    if (((maxb >> 9) >> g) > FFILL_M) return KMAN_EFALLBACK;
     if (d.K < B1 + 9 + g + 1) return KMAN_EFALLBACK;
     d.g = g;
     d.rest = d.K - B1 - 9 - g;
@@ -1589,6 +1626,10 @@ int make_rplan(uint32_t k, uint32_t flags, int mode, uint32_t world, uint64_t n_
     const uint64_t e2 = (maxb >> 9) >> g;
     const uint64_t c2 = round_cap(e2, 512);
     d.C1 = c2 < (uint64_t)FCAP ? c2 : (uint64_t)FCAP;
+    // the finish at GCAP (40 KiB, three blocks per CU) when the regions the
+    // plan expects fit it with the same margin; else FCAP (68 KiB, two)
+    d.cap = round_cap(e2, 512) <= (uint64_t)GCAP ? GCAP : FCAP;
+    if (d.cap == GCAP) d.C1 = d.C1 < (uint64_t)GCAP ? d.C1 : (uint64_t)GCAP;
     d.nsub = (uint64_t)nb * 512 * world * d.H;
     d.nreg = (uint64_t)nb * 512 << g;
     d.off_c1 = d.nsub * d.C1s * 8;
@@ -1656,7 +1697,7 @@ int refit_g(kman_ctx *ctx, RoundPlan &d, const uint32_t *c1, uint8_t *freg, uint
         for (uint64_t q = 0; q < gh; q++) t += hc[j * gh + q];
         size[j] = t;
         uint32_t g = gmin;
-        while (g < 9 && (t >> g) > 6144) g++;
+        while (g < 9 && (t >> g) > FFILL_T) g++;
         need[j] = (uint8_t)g;
     }
     std::vector<uint64_t> ss(size);
@@ -1677,6 +1718,7 @@ int refit_g(kman_ctx *ctx, RoundPlan &d, const uint32_t *c1, uint8_t *freg, uint
             d.rest = d.K - B1 - 9 - g;
             d.nreg = nreg;
             d.C1 = C1;
+            d.cap = C1 <= (uint64_t)GCAP ? GCAP : FCAP;
             d.off_c2 = off_c2;
         }
     }
@@ -1862,6 +1904,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         FinishArgs f{r1, d.C1s, c1, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << 9, 0u, (uint32_t)d.nreg};
         f.fsub = d.H;
         f.freg = freg;
+        f.cap = d.cap;
         KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, fst));
     } else {
     // (c2 may lie in the receive buffer: cleared only once pass 1 has read it)
@@ -1900,6 +1943,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         FinishArgs f{r2, d.C1, c2, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << (9 + d.g),
                      mode == KMAN_FINISH_UNIQ ? d.Q + d.rest + d.g : 0u, (uint32_t)d.nreg};
         f.freg = freg;
+        f.cap = d.cap;
         KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, fst));
     }
     }

@@ -44,16 +44,44 @@ KMAN_RF_HD uint64_t mix_key(uint64_t x, int k) {
     return (x * 0xBF58476D1CE4E5B9ull) & m;
 }
 
-template <int EI, int CANON>
+// ALIGN (16 or 8): s + base is that aligned (base = thread * EI with EI a
+// multiple of it), so the words are read as 16- / 8-byte LDS vectors --
+// with consecutive threads EI bytes apart, ds_read_b128 / ds_read_b64 hit
+// every bank once per lane group, where ds_read_b32 at a 16-byte stride is
+// 4-way conflicted
+template <int EI, int CANON, int ALIGN = 4>
 KMAN_RF_HD uint32_t roll_fast(const uint8_t *s, int base, int k, uint64_t mask, uint64_t p0, uint64_t n_bases,
                               uint64_t (&kf)[EI], uint64_t (&kr)[EI]) {
     // words covering (base & 3) + k - 1 + EI codes for any k <= 32
     constexpr int NW = (3 + 31 + EI + 3) / 4;
     static_assert(NW <= 16, "at most 64 codes");
-    const int b4 = base & ~3, dl = base & 3;
+    static_assert(ALIGN == 4 || ALIGN == 8 || ALIGN == 16, "4-, 8- or 16-byte word reads");
+    const int b4 = base & ~3, dl = ALIGN > 4 ? 0 : base & 3;
     uint32_t w[NW];
+    if constexpr (ALIGN == 16) {
+        const uint32_t *p = reinterpret_cast<const uint32_t *>(s + base);
 #pragma unroll
-    for (int i = 0; i < NW; i++) w[i] = *reinterpret_cast<const uint32_t *>(s + b4 + 4 * i);
+        for (int q = 0; q < (NW + 3) / 4; q++) {
+            uint32_t v[4];
+            __builtin_memcpy(v, __builtin_assume_aligned(p + 4 * q, 16), 16);
+#pragma unroll
+            for (int e = 0; e < 4; e++)
+                if (4 * q + e < NW) w[4 * q + e] = v[e];
+        }
+    } else if constexpr (ALIGN == 8) {
+        const uint32_t *p = reinterpret_cast<const uint32_t *>(s + base);
+#pragma unroll
+        for (int q = 0; q < (NW + 1) / 2; q++) {
+            uint32_t v[2];
+            __builtin_memcpy(v, __builtin_assume_aligned(p + 2 * q, 8), 8);
+#pragma unroll
+            for (int e = 0; e < 2; e++)
+                if (2 * q + e < NW) w[2 * q + e] = v[e];
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < NW; i++) w[i] = *reinterpret_cast<const uint32_t *>(s + b4 + 4 * i);
+    }
     // code c (0 .. 4 * NW) of the thread's words: BE stream be0:be1 (code 0 at
     // the top of be0), LE stream le0:le1 (code 0 at the bottom of le0); the
     // not-ACGT and record-start flags, one bit per code

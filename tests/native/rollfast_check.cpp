@@ -34,7 +34,9 @@ static uint32_t roll_ref(const uint8_t *s, int base, int k, uint64_t mask, uint6
     return valid;
 }
 
-template <int EI, bool CANON>
+// A: the word-read width roll() picks for base = thread * EI (16- / 8-byte
+// vectors when EI is a multiple of 16 / 8), or 4 (any base)
+template <int EI, bool CANON, int A = 4>
 static int check(std::mt19937_64 &g, long &n) {
     alignas(16) uint8_t s[4096 + 128];
     for (int trial = 0; trial < 300; trial++) {
@@ -53,10 +55,10 @@ static int check(std::mt19937_64 &g, long &n) {
                 uint64_t a[EI], b[EI], c[EI], d[EI];
                 memset(b, 0, sizeof b);
                 memset(d, 0, sizeof d);
-                const uint32_t va = roll_fast<EI, CANON>(s, base, k, mask, p0, nb, a, b);
+                const uint32_t va = roll_fast<EI, CANON, A>(s, base, k, mask, p0, nb, a, b);
                 const uint32_t vb = roll_ref<EI, CANON>(s, base, k, mask, p0, nb, c, d);
                 if (va != vb) {
-                    printf("valid mismatch EI=%d canon=%d k=%d base=%d: %x vs %x\n", EI, CANON, k, base, va, vb);
+                    printf("valid mismatch EI=%d canon=%d A=%d k=%d base=%d: %x vs %x\n", EI, CANON, A, k, base, va, vb);
                     return 1;
                 }
                 for (int j = 0; j < EI; j++) {
@@ -79,7 +81,9 @@ int main() {
     std::mt19937_64 g(7);
     long n = 0;
     if (check<4, false>(g, n) || check<6, false>(g, n) || check<8, false>(g, n) || check<12, false>(g, n) ||
-        check<16, false>(g, n) || check<8, true>(g, n) || check<12, true>(g, n) || check<16, true>(g, n))
+        check<16, false>(g, n) || check<8, true>(g, n) || check<12, true>(g, n) || check<16, true>(g, n) ||
+        check<8, false, 8>(g, n) || check<16, false, 16>(g, n) || check<16, false, 8>(g, n) ||
+        check<16, true, 16>(g, n) || check<8, true, 8>(g, n))
         return 1;
     printf("ok %ld\n", n);
     return 0;

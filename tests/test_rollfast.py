@@ -1,6 +1,7 @@
 """The bit-parallel window roll (kman_amd/csrc/rollfast.h, used by every
 extraction kernel) against a per-base roll, on the host: random codes with
-not-ACGT and record-start flags, k = 2..32, all four word alignments."""
+not-ACGT and record-start flags, k = 2..32, all four word alignments, and
+the 8- and 16-byte vector reads roll() uses when the base is that aligned."""
 import os
 import shutil
 import subprocess
