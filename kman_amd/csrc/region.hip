@@ -46,9 +46,11 @@ constexpr int RT = 512;           // threads of passes 0 and 1
 constexpr int RS = 64;            // position segments of pass 0 (one wave of counts)
 constexpr int RSI = 16;           // items per thread, pass 1
 constexpr uint64_t T1 = (uint64_t)RT * RSI;  // pass-1 tile
-constexpr int FT = 512;           // finish threads (more threads per region, e.g. 640 or 576: a
-                                  // second block no longer fits the CU's SIMDs, 9.5 / 11.5 vs 5.7 ms)
-constexpr int FCAP = 8704;        // round-path finish capacity: 68 KiB of 8-byte items
+constexpr int FT = 512;           // finish threads (more threads per region: 640 or 576 -- a second
+                                  // block no longer fits the CU's SIMDs, 9.5 / 11.5 vs 5.7 ms; 768,
+                                  // two blocks at 80 VGPRs -- 6.7 ms, the sort phase's barriers over
+                                  // 12 waves cost more than the waves gain)
+constexpr int FCAP = 8704;        // finish capacity: 68 KiB of 8-byte items
 constexpr int FBITS = 9;          // finish LSD digit (26 bits: 3 passes)
 constexpr int FRAD = 1 << FBITS;
 constexpr int FWORD = FRAD / 2;   // per-wave counters: two u16 per word
