@@ -505,6 +505,12 @@ def run_dist(args, world: int, rank: int, local: int):
             stages[tag] = round(ms / args.steps, 3)
     if rank == 0:
         dom, sp = dist_roofline(pipe, args.steps, args.mode, args.k, per, world, canon)
+        stage_alg = {}
+        for tag, (kern, alg_step) in dist_stage_bytes(pipe, args.steps, args.mode).items():
+            c, _ = pipe.timed(tag)
+            if c:
+                stage_alg[tag] = {"kernel": kern, "alg_bytes_per_launch": alg_step / max(1, c // args.steps),
+                                  "launches_per_step": c // args.steps}
         out = {
             "metric": METRIC, "value": total / elapsed, "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -526,7 +532,7 @@ def run_dist(args, world: int, rank: int, local: int):
                        "path": pipe.path, "rounds": pipe.rounds, "fallback_rounds": pipe.fallback_rounds,
                        "partial_rounds": pipe.partial_rounds,
                        "memory_plan": getattr(pipe, "plan_info", None),
-                       "stages_ms_per_step_rank0": stages},
+                       "stages_ms_per_step_rank0": stages, "stage_alg_bytes_rank0": stage_alg},
             "roofline": dom, "sort_pass_roofline": sp, "cpu_baseline": None,
         }
     comm.allreduce(np.zeros(1, np.uint64))  # every rank is done
