@@ -1,11 +1,10 @@
-# round-end GPU call: every gpu test + smoke, the default bench line (CPU baseline included), rocprofv3 stats + PMC passes, dist lines, GRCh38-shaped lines
+# what the round-end driver runs, in one call: every GPU test, smoke(), the
+# default bench line
 set -e
-TAG=${1:-r03}
+TAG=${1:-final}
 mkdir -p gpurun_out
-bash tools/gpu_tests_bench.sh $TAG
-timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
-timeout -k 10 300 python bench.py > gpurun_out/bench_default_$TAG.json 2> gpurun_out/bench_default_$TAG.err
-python3 -c "import json; d=json.load(open('gpurun_out/bench_default_$TAG.json')); print('default', d['value']/1e9, d['ms_per_step'], d['roofline']['frac'], d.get('cpu_baseline'))"
-bash tools/gpu_profile.sh $TAG
-timeout -k 10 500 python -u tools/widebench.py grch38s_spectrum --steps 3 > gpurun_out/g5_$TAG.json 2> gpurun_out/g5_$TAG.err
-cat gpurun_out/g5_$TAG.json
+timeout -k 10 900 python -u -m pytest tests -q -m gpu -x --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 || { tail -40 gpurun_out/pytest_gpu_$TAG.log; exit 1; }
+echo tests-ok; tail -1 gpurun_out/pytest_gpu_$TAG.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke-ok')"
+timeout -k 10 600 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail gpurun_out/bench_$TAG.err; exit 1; }
+python3 -c "import json; d=json.load(open('gpurun_out/bench_$TAG.json')); print('bench', d['value']/1e9, d['ms_per_step'], d['roofline']['frac'], d['cpu_baseline']['value'])"
