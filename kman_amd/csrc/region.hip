@@ -892,10 +892,14 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     __syncthreads();
     RSTAMP(r, 4);
     const uint64_t ob = s_out;
+    // the rows leave with non-temporal stores (a stream of GBs that no cache
+    // keeps until it is read): 5.52-5.58 vs 5.58-5.62 ms (`r04k_nt_ab.txt`;
+    // on the passes' scattered line stores they lose L2's write combining:
+    // rg_pass 6.3-8.0 vs 3.5 ms)
     const uint64_t qmask = Q ? ((1ull << Q) - 1) : 0ull;
     for (uint32_t q = t; q < total; q += NT) {
         const uint64_t v = s[q];
-        okeys[ob + q] = ((uint64_t)(r + rbase) << rest) | RKEY(v);
+        __builtin_nontemporal_store(((uint64_t)(r + rbase) << rest) | RKEY(v), okeys + ob + q);
     }
     if constexpr (NARROW) {
         __syncthreads();  // (every key read before the sizes overwrite them)
@@ -910,11 +914,11 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
             // N > 1: the source rank (tagged into the item by the pass after
             // the exchange) in bits 56-63, as DistPipeline's payloads
             // (ranks < 256: 8 tag bits, so bit 63 -- the early count's mark -- is not read)
-            ovals[ob + q] = (O)(tag_shift ? pos | (((v >> tag_shift) & 0xffull) << 56) : pos);
+            __builtin_nontemporal_store((O)(tag_shift ? pos | (((v >> tag_shift) & 0xffull) << 56) : pos), ovals + ob + q);
         } else if constexpr (NARROW) {
-            ovals[ob + q] = (O)v;
+            __builtin_nontemporal_store((O)v, ovals + ob + q);
         } else {
-            ovals[ob + q] = (O)(v >> rest);
+            __builtin_nontemporal_store((O)(v >> rest), ovals + ob + q);
         }
     }
 #undef RKEY
