@@ -283,6 +283,11 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     }
     __syncthreads();
     RSTAMP(tile, 4);
+    // vmcnt(0) once, on every path: the region-cursor atomic's return (issued
+    // only by the waves of threads < R0) is otherwise still pending, as far
+    // as the compiler can tell, in the waves that skipped it, and it puts a
+    // vmcnt(0) before every store below -- each store waiting for the last
+    __builtin_amdgcn_s_waitcnt(0x0f70);
     constexpr int RQ = (TILE + NT - 1) / NT;
 #pragma unroll
     for (int r = 0; r < RQ; r++) {
