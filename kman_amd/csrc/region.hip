@@ -260,13 +260,11 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     const uint32_t ls = block_exclusive_scan1<NT>(tot, SumU32(), 0u, lds_scan, &tcnt);
     if (d0 < R0) lstart[d0] = ls;
     __syncthreads();
+    // (the slot reads issued first, back to back, then the writes: 3.23 vs
+    // 3.12 ms, the same with the store loop's reads -- `r04o_pipe_ab.txt`)
 #pragma unroll
-    for (int i = 0; i < SI; i++) {
-        if ((vmask >> i) & 1u) {
-            const uint32_t d = XDIGIT(key[i]);
-            skeys[lstart[d] + rank[i]] = key[i];
-        }
-    }
+    for (int i = 0; i < SI; i++)
+        if ((vmask >> i) & 1u) skeys[lstart[XDIGIT(key[i])] + rank[i]] = key[i];
 
     if (threadIdx.x < R0) {
         const uint32_t d = threadIdx.x;
@@ -490,6 +488,8 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
             // a digit whose partial line completes in this tile: its pending
             // items go out first, 16 lanes per digit (one line per quarter
             // wave, so a store covers 4 lines)
+            // (the LDS reads of this loop and the store loop below issued
+            // first, back to back: 3.39 vs 3.31 ms, `r04o_pipe_ab.txt`)
 #pragma unroll
             for (uint32_t d = threadIdx.x >> PT_WLB; d < (uint32_t)R1; d += NT / WL) {
                 const uint32_t j = threadIdx.x & WM, rn = run[d], p = rn & WM;
@@ -589,9 +589,15 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     constexpr int IPT = (CAP + NT - 1) / NT;  // items per thread
     constexpr bool NARROW = sizeof(T) == 4;
     static_assert(!NARROW || MODE == RG_COUNT, "narrow items: count mode");
+    // PIPE: the rank atomics and slot reads of a pass issue back to back
+    // (8-byte items of an FCAP region, 128 VGPRs; the 80- and 64-VGPR
+    // instances spill so, and keep one round trip at a time)
+    constexpr bool PIPE = ATOMIC && !NARROW && CAP == FCAP;
     static_assert(CHK == 0 || MODE == RG_UNIQ, "the early count is uniq's");
     __shared__ __attribute__((aligned(16))) T s[CAP];
-    __shared__ uint32_t wh[NW_][FWORD];  // per-wave digit counters, u16 pairs
+    // per-wave digit counters, u16 pairs; words FWORD + lane: where the
+    // lanes without an item add (so every rank atomic is unconditional)
+    __shared__ uint32_t wh[NW_][FWORD + 64];
     __shared__ uint32_t lds_scan[NW_], lds_scan2[NW_];
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_out;
@@ -676,7 +682,12 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
             const bool valid = pw + i * 64 < m;
             const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
             const uint32_t hs = (d & 1u) * 16u;
-            if (ATOMIC) {
+            if (PIPE) {
+                // (no branch around the atomic: in a branch its return is
+                // waited for before the next item's atomic issues, 17 LDS
+                // round trips in a row per pass)
+                rk[i] = (atomicAdd(&wh[w][valid ? d >> 1 : (uint32_t)FWORD + lane], 1u << hs) >> hs) & 0xffffu;
+            } else if (ATOMIC) {
                 rk[i] = valid ? (atomicAdd(&wh[w][d >> 1], 1u << hs) >> hs) & 0xffffu : 0u;
             } else {
                 uint64_t peers = __ballot(valid);
@@ -718,11 +729,25 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
             }
         }
         __syncthreads();
+        if (PIPE) {
+            // every item's slot first (unconditional reads, issued back to
+            // back; an item past m reads a slot it does not use), then the
+            // writes
 #pragma unroll
-        for (int i = 0; i < IPT; i++) {
-            if (pw + i * 64 < m) {
+            for (int i = 0; i < IPT; i++) {
                 const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
-                s[((wh[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rk[i]] = x[i];
+                rk[i] += (wh[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu;
+            }
+#pragma unroll
+            for (int i = 0; i < IPT; i++)
+                if (pw + i * 64 < m) s[rk[i]] = x[i];
+        } else {
+#pragma unroll
+            for (int i = 0; i < IPT; i++) {
+                if (pw + i * 64 < m) {
+                    const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
+                    s[((wh[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rk[i]] = x[i];
+                }
             }
         }
         __syncthreads();
@@ -902,17 +927,33 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     // on the passes' scattered line stores they lose L2's write combining:
     // rg_pass 6.3-8.0 vs 3.5 ms)
     const uint64_t qmask = Q ? ((1ull << Q) - 1) : 0ull;
-    for (uint32_t q = t; q < total; q += NT) {
-        const uint64_t v = s[q];
+    // OB rows per trip, their LDS reads first, back to back (rows past total
+    // read slot 0 and are not written)
+    constexpr uint32_t OB = 4;
+    auto each_row = [&](auto &&put) {
+        for (uint32_t q0 = t; q0 < total; q0 += OB * NT) {
+            uint64_t v4[OB];
+#pragma unroll
+            for (uint32_t u = 0; u < OB; u++) {
+                const uint32_t q = q0 + u * NT;
+                v4[u] = (uint64_t)s[q < total ? q : 0u];
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < OB; u++) {
+                const uint32_t q = q0 + u * NT;
+                if (q < total) put(q, v4[u]);
+            }
+        }
+    };
+    each_row([&](uint32_t q, uint64_t v) {
         __builtin_nontemporal_store(((uint64_t)(r + rbase) << rest) | RKEY(v), okeys + ob + q);
-    }
+    });
     if constexpr (NARROW) {
         __syncthreads();  // (every key read before the sizes overwrite them)
         stage(true);
         __syncthreads();
     }
-    for (uint32_t q = t; q < total; q += NT) {
-        const uint64_t v = s[q];
+    each_row([&](uint32_t q, uint64_t v) {
         if constexpr (MODE == RG_UNIQ) {
             const uint64_t idx = v & qmask;
             const uint64_t pos = rc ? idx : (idx << 1);
@@ -925,7 +966,7 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
         } else {
             __builtin_nontemporal_store((O)(v >> rest), ovals + ob + q);
         }
-    }
+    });
 #undef RKEY
     RSTAMP(r, 5);
 }

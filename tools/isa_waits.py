@@ -19,7 +19,7 @@ def kernel_waits(src: str, extra=()) -> dict:
     with tempfile.TemporaryDirectory() as td:
         asm = os.path.join(td, "k.s")
         subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950",
-                        "--cuda-device-only", "-S", src, "-o", asm] + list(extra),
+                        "--cuda-device-only", "-S", os.path.abspath(src), "-o", asm] + list(extra),
                        check=True, capture_output=True, cwd=os.path.dirname(os.path.abspath(src)))
         lines = open(asm).read().split("\n")
     res, kern, after = {}, None, False
