@@ -284,6 +284,20 @@ struct SumU32 {
 };
 
 // ------------------------------------------------------ decoupled look-back
+// the wave's sum (OP 0) or max (OP 1) of v in every lane: DPP row shifts and
+// broadcasts, then lane 63's by readlane (no LDS round trips; the xor
+// butterfly through ds_bpermute took six, two per step for 64 bits)
+template <int OP>
+KMAN_DEV uint64_t wave_reduce_lb(uint64_t v) {
+    struct MaxU64 {
+        KMAN_DEV uint64_t operator()(uint64_t a, uint64_t b) const { return a > b ? a : b; }
+    };
+    if (OP == 0) v = wave_inclusive_scan(v, SumU64(), (uint64_t)0);
+    else v = wave_inclusive_scan(v, MaxU64(), (uint64_t)0);
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), 63) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+}
+
 // Called by ONE full wave of the tile (all 64 lanes active).  Publishes the
 // tile aggregate, looks back over up to 64 predecessors per round (one status
 // word per lane, sc1 loads), publishes the inclusive prefix and returns the
@@ -319,11 +333,7 @@ KMAN_DEV uint64_t wave_lookback(uint64_t *status, int64_t tile, uint64_t agg, ui
         }
         uint64_t v = (j >= 0 && (need >> lane) & 1ull) ? (w & ST_VMASK) : 0ull;
         // wave reduce
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            uint64_t o = shfl_any(v, lane ^ d);
-            v = OP == 0 ? v + o : (v > o ? v : o);
-        }
+        v = wave_reduce_lb<OP>(v);
         excl = OP == 0 ? excl + v : (excl > v ? excl : v);
         if (first_incl < 64 || end - 64 <= 0) break;
         end -= 64;
@@ -364,11 +374,7 @@ KMAN_DEV uint64_t wave_lookback_published(uint64_t *status, int64_t tile, uint64
             continue;
         }
         uint64_t v = (j >= 0 && (need >> lane) & 1ull) ? (w & ST_VMASK) : 0ull;
-#pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) {
-            uint64_t o = shfl_any(v, lane ^ d);
-            v = OP == 0 ? v + o : (v > o ? v : o);
-        }
+        v = wave_reduce_lb<OP>(v);
         excl = OP == 0 ? excl + v : (excl > v ? excl : v);
         if (first_incl < 64 || end - 64 <= 0) break;
         end -= 64;

@@ -590,8 +590,11 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     constexpr bool NARROW = sizeof(T) == 4;
     static_assert(!NARROW || MODE == RG_COUNT, "narrow items: count mode");
     // PIPE: the rank atomics and slot reads of a pass issue back to back
-    // (8-byte items of an FCAP region, 128 VGPRs; the 80- and 64-VGPR
-    // instances spill so, and keep one round trip at a time)
+    // (8-byte items of an FCAP region, 128 VGPRs).  The 80- and 64-VGPR
+    // instances spill so: their ranks stay one round trip at a time and
+    // their slot reads go four at a time (count finish 5.34 -> 5.27 ms);
+    // the GCAP instance with 3 dwords of spills was no faster on the round
+    // path (`r04q_ab.txt`)
     constexpr bool PIPE = ATOMIC && !NARROW && CAP == FCAP;
     static_assert(CHK == 0 || MODE == RG_UNIQ, "the early count is uniq's");
     __shared__ __attribute__((aligned(16))) T s[CAP];
@@ -743,11 +746,17 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
                 if (pw + i * 64 < m) s[rk[i]] = x[i];
         } else {
 #pragma unroll
-            for (int i = 0; i < IPT; i++) {
-                if (pw + i * 64 < m) {
+            for (int i0 = 0; i0 < IPT; i0 += 4) {
+                uint32_t sl[4];
+#pragma unroll
+                for (int i = i0; i < i0 + 4 && i < IPT; i++) {
                     const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
-                    s[((wh[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rk[i]] = x[i];
+                    sl[i - i0] = ((wh[w][d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rk[i];
                 }
+#pragma unroll
+                for (int i = i0; i < i0 + 4 && i < IPT; i++)
+                    if (pw + i * 64 < m) s[sl[i - i0]] = x[i];
+                __builtin_amdgcn_sched_barrier(0);
             }
         }
         __syncthreads();
