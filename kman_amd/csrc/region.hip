@@ -936,20 +936,25 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     // on the passes' scattered line stores they lose L2's write combining:
     // rg_pass 6.3-8.0 vs 3.5 ms)
     const uint64_t qmask = Q ? ((1ull << Q) - 1) : 0ull;
-    // OB rows per trip, their LDS reads first, back to back (rows past total
-    // read slot 0 and are not written)
+    // OB rows per trip, their LDS reads first, back to back (rows outside
+    // the region's read slot 0 and are not written).  Lane l of a wave
+    // writes a global row = l mod 64 (the region's first row shifted by
+    // ob % 64), so a wave's store covers whole 128-byte lines: non-temporal
+    // stores of part lines are not merged in L2 (finish writes 12.35 GB per
+    // launch unaligned, 11.74 aligned, `r04s_ab.txt`; same time)
+    const uint32_t mis = (uint32_t)(ob & 63);
     constexpr uint32_t OB = 4;
     auto each_row = [&](auto &&put) {
-        for (uint32_t q0 = t; q0 < total; q0 += OB * NT) {
+        for (uint32_t q0 = t; q0 < total + mis; q0 += OB * NT) {
             uint64_t v4[OB];
 #pragma unroll
             for (uint32_t u = 0; u < OB; u++) {
-                const uint32_t q = q0 + u * NT;
+                const uint32_t q = q0 + u * NT - mis;
                 v4[u] = (uint64_t)s[q < total ? q : 0u];
             }
 #pragma unroll
             for (uint32_t u = 0; u < OB; u++) {
-                const uint32_t q = q0 + u * NT;
+                const uint32_t q = q0 + u * NT - mis;
                 if (q < total) put(q, v4[u]);
             }
         }
