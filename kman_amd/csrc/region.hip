@@ -154,7 +154,11 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
     __shared__ uint32_t thist[R0];
     __shared__ uint32_t lstart[R0];
+    // the output index of the tile's item q (a digit-d item) is gexcl[d] + q,
+    // stored when q < qlim[d] (a digit not kept, or the items past a
+    // region's capacity: none)
     __shared__ uint64_t gexcl[R0];
+    __shared__ uint32_t qlim[R0];
     __shared__ uint32_t lds_scan[NWAVE];
     __shared__ uint32_t keep[EX ? R0 / 32 : 1];
 
@@ -267,15 +271,17 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
         if ((vmask >> i) & 1u) skeys[lstart[XDIGIT(key[i])] + rank[i]] = key[i];
 
     if (threadIdx.x < R0) {
-        const uint32_t d = threadIdx.x;
-        const uint64_t incl = (uint64_t)at_base + thist[d];
+        const uint32_t d = threadIdx.x, ls = lstart[d], c = thist[d];
+        const uint64_t incl = (uint64_t)at_base + c;
         if (EX) {  // (digits not kept this round have no items)
             const uint64_t rb = rtab[(uint64_t)d * RS + sgi];
-            const bool over = thist[d] && incl > cnt0[d * RS + sgi];
+            const bool over = c && incl > cnt0[d * RS + sgi];
             if (over && rb != ~0ull) atomicOr(err, ERR_REGION);  // (the input changed under the plan)
-            gexcl[d] = rb == ~0ull || over ? ~0ull : rb + at_base;
+            gexcl[d] = rb + at_base - ls;
+            qlim[d] = rb == ~0ull || over ? 0u : ls + c;
         } else {
-            gexcl[d] = at_base;
+            gexcl[d] = ((uint64_t)d * RS + sgi) * C0 + at_base - ls;
+            qlim[d] = ls + (incl <= C0 ? c : at_base < C0 ? (uint32_t)(C0 - at_base) : 0u);
             if (incl > C0) atomicOr(err, ERR_REGION);
         }
     }
@@ -293,7 +299,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
         if (q < tcnt) {
             const uint64_t kk = skeys[q];
             const uint32_t d = XDIGIT(kk);
-            const uint64_t at = gexcl[d] + (q - lstart[d]);
+            if (q >= qlim[d]) continue;
             uint64_t v = kk & restmask;
             if (Q) {
                 const uint64_t f = kk >> kb;  // tile-local (window << 1 | strand)
@@ -301,11 +307,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
                 const uint64_t idx = RC ? ((win << 1) | (f & 1u)) : win;
                 v = (v << Q) | idx;
             }
-            if (EX) {
-                if (gexcl[d] != ~0ull) out[at] = v;
-            } else if (at < C0) {
-                out[((uint64_t)d * RS + sgi) * C0 + at] = v;
-            }
+            out[gexcl[d] + q] = v;
         }
     }
     RSTAMP(tile, 5);
