@@ -154,11 +154,13 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
     __shared__ uint32_t thist[R0];
     __shared__ uint32_t lstart[R0];
-    // the output index of the tile's item q (a digit-d item) is gexcl[d] + q,
-    // stored when q < qlim[d] (a digit not kept, or the items past a
-    // region's capacity: none)
+    // !EX: the output index of the tile's item q (a digit-d item) is
+    // gexcl[d] + q, stored when q < qlim[d] (the items past a region's
+    // capacity are not).  EX: gexcl[d] + q - lstart[d], ~0 for a digit not
+    // kept (the !EX form measured slower there: config 4's extraction 87 vs
+    // 75 ms, `r04x_extract_ex_ab.txt`)
     __shared__ uint64_t gexcl[R0];
-    __shared__ uint32_t qlim[R0];
+    __shared__ uint32_t qlim[EX ? 1 : R0];
     __shared__ uint32_t lds_scan[NWAVE];
     __shared__ uint32_t keep[EX ? R0 / 32 : 1];
 
@@ -277,8 +279,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
             const uint64_t rb = rtab[(uint64_t)d * RS + sgi];
             const bool over = c && incl > cnt0[d * RS + sgi];
             if (over && rb != ~0ull) atomicOr(err, ERR_REGION);  // (the input changed under the plan)
-            gexcl[d] = rb + at_base - ls;
-            qlim[d] = rb == ~0ull || over ? 0u : ls + c;
+            gexcl[d] = rb == ~0ull || over ? ~0ull : rb + at_base;
         } else {
             gexcl[d] = ((uint64_t)d * RS + sgi) * C0 + at_base - ls;
             qlim[d] = ls + (incl <= C0 ? c : at_base < C0 ? (uint32_t)(C0 - at_base) : 0u);
@@ -299,7 +300,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
         if (q < tcnt) {
             const uint64_t kk = skeys[q];
             const uint32_t d = XDIGIT(kk);
-            if (q >= qlim[d]) continue;
+            if (!EX && q >= qlim[d]) continue;
             uint64_t v = kk & restmask;
             if (Q) {
                 const uint64_t f = kk >> kb;  // tile-local (window << 1 | strand)
@@ -307,7 +308,11 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
                 const uint64_t idx = RC ? ((win << 1) | (f & 1u)) : win;
                 v = (v << Q) | idx;
             }
-            out[gexcl[d] + q] = v;
+            if (EX) {
+                if (gexcl[d] != ~0ull) out[gexcl[d] + (q - lstart[d])] = v;
+            } else {
+                out[gexcl[d] + q] = v;
+            }
         }
     }
     RSTAMP(tile, 5);
