@@ -127,14 +127,12 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 //     is written at rtab[b * RS + s] (exact sizes from rg_hist in cnt0, which
 //     is read-only); buckets with rtab == ~0 are not kept this round, and
 //     their windows are dropped before the rank (keep bitmap).
-// XG (a whole-stream launch): tickets per XCD partition -- segments
-// [p * RS / 8, (p + 1) * RS / 8) form partition p, counter[p] deals its tiles
-// in stream order, and a block takes tickets from its own XCD's partition
-// first (HW_REG_XCC_ID), then from the others once that one is dealt out.  So
-// the tiles that claim consecutive slots of a region usually run on one XCD:
-// the 128-byte line two of them share meets in that XCD's L2 instead of
-// leaving two partial lines.  Placement changes only speed; a block leaves
-// only when every partition is dealt out.
+// XG (a whole-stream launch): tiles by XCD partition -- segments
+// [p * RS / 8, (p + 1) * RS / 8) form partition p, whose tiles the blocks on
+// XCD p take in stream order (block id -> tile, no ticket).  So the tiles
+// that claim consecutive slots of a region usually run on one XCD: the
+// 128-byte line two of them share meets in that XCD's L2 instead of leaving
+// two partial lines.  Placement changes only speed.
 template <int EI, bool RC, int CANON, bool EX, bool XG, int P0B = (int)(EX ? B1 : G1)>
 __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI == 8 ? 8 : 4)))) void rg_extract(
     const uint8_t *__restrict__ codes, uint64_t n_bases, int k, uint32_t Q, uint64_t *__restrict__ out, uint64_t C0,
@@ -164,23 +162,23 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     __shared__ uint32_t lds_scan[NWAVE];
     __shared__ uint32_t keep[EX ? R0 / 32 : 1];
 
-    // one tile per block: a ticket of a tile that exists (thread 0 only),
-    // ~0u when every partition is dealt out (XG) or past the tiles / a
-    // segment's end.  (Persistent blocks that load the next tile's codes
+    // one tile per block: the block's tile (XG: from the block id), or a
+    // ticket (thread 0 only); ~0u past the tiles / a segment's end.  (Persistent blocks that load the next tile's codes
     // into registers while this one is worked measured slower: 3.97-4.19 vs
     // 3.64-3.83 ms, the loop costs registers and spills.)
     __shared__ uint32_t lds_tile;
     auto take = [&]() -> uint32_t {
         uint32_t c = ~0u;
         if (XG) {
-            constexpr uint32_t CPG = RS / 8;  // segments per partition
-            const uint32_t x = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;  // hwreg(HW_REG_XCC_ID, 0, 4)
-            for (uint32_t a = 0; a < 8 && c == ~0u; a++) {
-                const uint32_t pp = (x + a) & 7u;
-                const uint32_t j = atomicAdd(counter + pp, 1u);
-                const uint64_t tt = (uint64_t)(j / CPG) * RS + pp * CPG + j % CPG;
-                if (tt < (IL ? (uint64_t)n_tiles : (uint64_t)RS * seg_tiles)) c = (uint32_t)tt;
-            }
+            // block b runs on XCD b % 8 (workgroups are dealt to the XCDs
+            // round robin): within each 64 blocks, b = 8 c + x takes tile
+            // 8 x + c, so XCD x works through the segments of partition x in
+            // stream order.  (Tickets from a per-partition atomic counter,
+            // the XCD read from HW_REG_XCC_ID, cost a round trip before the
+            // codes load: 2.92 vs 2.75 ms, config 4's extraction 75.4 vs 68.7
+            // ms, `r04ad_static_tiles_ab.txt`)
+            const uint32_t b = blockIdx.x;
+            c = (b & ~63u) | ((b & 7u) << 3) | ((b >> 3) & 7u);
         } else {
             c = atomicAdd(counter, 1u);
         }
@@ -189,9 +187,14 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
         const uint32_t s_ = c % RS, jj = c / RS, t0 = s_ * seg_tiles;
         return t0 + jj < (t0 + seg_tiles < n_tiles ? t0 + seg_tiles : n_tiles) ? c : ~0u;
     };
-    if (threadIdx.x == 0) lds_tile = take();
-    __syncthreads();
-    const uint32_t cid = lds_tile;
+    uint32_t cid;
+    if (XG) {
+        cid = take();  // (block-uniform)
+    } else {
+        if (threadIdx.x == 0) lds_tile = take();
+        __syncthreads();
+        cid = lds_tile;
+    }
     if (cid == ~0u) return;  // (block-uniform)
     const int64_t tile = IL ? (int64_t)cid : (int64_t)(cid % RS) * seg_tiles + cid / RS;
     const uint32_t sgi = cid % RS;
@@ -1180,7 +1183,7 @@ void launch_extract(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, ui
                     uint32_t n_launch) {
     if (!n_launch)
         hipLaunchKernelGGL((rg_extract<EI, RC, CANON, false, true>),
-                           dim3(p.n_tiles0), dim3(RT), 0, ctx->stream, codes,
+                           dim3((p.n_tiles0 + RS - 1) / RS * RS), dim3(RT), 0, ctx->stream, codes,
                            n_bases, (int)k, p.Q, r0, p.C0, p.seg_tiles, p.n_tiles0, c0, c0,
                            ctx->d_xcounters + 8 * (epoch & 63u), ctx->d_err, stp, nullptr);
     else
