@@ -1,0 +1,11 @@
+# rg_extract: static XCD-aware tile order by block id (base) vs per-partition ticket atomics (ftix); tests on base first
+set -e
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_region.py tests/test_gpu_parity.py tests/test_gpu_dist_region.py tests/test_gpu_canonical.py tests/test_gpu_dist.py tests/test_gpu_config3.py -q -x -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_r04ae.log 2>&1 || { tail -40 gpurun_out/pytest_r04ae.log; exit 1; }
+echo tests-ok; tail -1 gpurun_out/pytest_r04ae.log
+bash tools/ab/gpu_libab.sh r04ae 3 base ftix
+for v in base ftix; do
+  if [ $v = base ]; then L=$PWD/kman_amd/lib/libkman.so; else L=$PWD/kman_amd/lib_ab_$v/libkman.so; fi
+  KMAN_LIB=$L timeout -k 10 300 python bench.py --gpus 1 --dist --mode count --shard-gb 12.5 --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/labc_r04ae.json 2> gpurun_out/labc_r04ae.err || { tail gpurun_out/labc_r04ae.err; exit 1; }
+  python3 -c "import json; d=json.load(open('gpurun_out/labc_r04ae.json')); print('cfg4 $v', round(d['ms_per_step'],1), d['config']['stages_ms_per_step_rank0'])"
+done
