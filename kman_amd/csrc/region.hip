@@ -1607,11 +1607,14 @@ int make_shard_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t f
     const uint64_t Wq = n_bases_q * (p.rc ? 2 : 1);
     p.Q = mode == KMAN_FINISH_UNIQ ? (bitlen(Wq - 1) ? bitlen(Wq - 1) : 1u) : 0u;
     if (p.K - B1 + p.Q > 64) return KMAN_EFALLBACK;
-    // the shard extraction's tiles (rg_hist counts in the same geometry):
-    // 12 windows per thread (6 with -r): config-4 shard extraction 76.0 vs
-    // 80.0 ms with 16 -- a round keeps 1/R of the windows, so the tiles'
-    // digit runs stay short either way
-    p.ei = p.rc ? 6u : 12u;
+    // the shard extraction's tiles (rg_hist counts in the same geometry): 16
+    // windows per thread (8 with -r) for shards that one key round takes
+    // (1 GB per rank: 2.80-2.88 vs 3.05-3.45 ms with 12), 12 (6) for the big
+    // ones, whose rounds keep 1/R of the windows each (config 4's 12.5 GB:
+    // 63.8-64.2 vs 71.8-72.2 ms with 16, `r04aj_tiles_ab.txt`); decided on
+    // the common bound, so every rank takes the same
+    const bool wide = n_bases_q <= (4ull << 30);
+    p.ei = p.rc ? (wide ? 8u : 6u) : (wide ? 16u : 12u);
     const uint64_t win = (uint64_t)RT * p.ei;
     p.n_tiles0 = (uint32_t)ceil_div(n_bases ? n_bases : 1, win);
     p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, RS);
