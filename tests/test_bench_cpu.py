@@ -117,3 +117,13 @@ def test_dist_roofline_picks_the_dominant_stage():
     alg = 8.0 * 10 ** 9 + 16.0 * 9 * 10 ** 8
     assert abs(dom["algorithmic_bytes_per_launch"] - alg) < 1 and abs(dom["avg_launch_ms"] - 6.0) < 1e-9
     assert abs(dom["achieved"] - alg / 6e-3 / 1e9) < 1e-6 and abs(sp["achieved"] - 16e9 / 3.5e-3 / 1e9) < 1e-6
+
+
+def test_committed_pmc_summary_matches_the_default_workload():
+    """bench.py's roofline `traffic` comes from profiles/pmc_current.json only
+    when its metadata names the default workload (uniq, k 21, 1 G bases): a
+    copy without it silently turns the field into null."""
+    import bench
+    for kern in ("rg_finish", "rg_pass", "rg_extract"):
+        t = bench.pmc_traffic(kern, "uniq", 21, 1_000_000_000)
+        assert t is not None and t > 0, kern
