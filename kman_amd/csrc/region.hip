@@ -653,6 +653,12 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
             v[i] = p < mm ? (T)src[p < m0_ ? p : p + skip] : (T)0;
         }
     };
+    // NARROW (three blocks per CU): wave priority 2 while a region's loads and
+    // row stores issue, 0 while it sorts, so the memory phases go ahead of
+    // the other blocks' sorting (count finish 5.17 -> 5.08 ms; the uniq
+    // instance, two blocks per CU, slows down with it: 5.29 vs 5.21,
+    // `r04am_prio_ab.txt`)
+    if (NARROW) __builtin_amdgcn_s_setprio(2);
     // one region per block.  (Persistent blocks that load the next region's
     // items into registers while this one is written: 15 vs 6 ms, spilled at
     // three blocks per CU; round 2's at two: 11.1 vs 5.7 ms.)
@@ -665,6 +671,7 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     T x[IPT];
     load_items(r, m0, m, x);
     RSTAMP(r, 0);
+    if (NARROW) __builtin_amdgcn_s_setprio(0);  // (the sort)
 #ifdef KMAN_RG_STAMPS
     __builtin_amdgcn_s_waitcnt(0);  // (diagnostic build: phase 1 = the wait for the region's items)
     if (stp && t == 0) stp[(uint64_t)r * 8 + 7] = m;  // (the region's items, beside its phase stamps)
@@ -947,6 +954,7 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     stage(false);
     __syncthreads();
     RSTAMP(r, 4);
+    if (NARROW) __builtin_amdgcn_s_setprio(2);  // (the row stores)
     const uint64_t ob = s_out;
     // the rows leave with non-temporal stores (a stream of GBs that no cache
     // keeps until it is read): 5.52-5.58 vs 5.58-5.62 ms (`r04k_nt_ab.txt`;
