@@ -451,17 +451,86 @@ def run_single(args):
     dev.close()
 
 
-def run_dist(args, world: int, rank: int, local: int):
+def dist_line(args, dev, world: int, rank: int, per: int, mode: str, canon: bool, reparse: bool, steps: int,
+              warmup: int, tag: str):
+    """One multi-GPU measurement: ONE global synthetic FASTA of `per` bytes
+    per rank, byte-range sharded; `warmup` untimed steps, then `steps` timed
+    ones between barriers, max over ranks.  Returns rank 0's line (None on
+    the other ranks); the pipeline is freed before it returns."""
     import numpy as np
     import inputs
-    from kman_amd import dist, engine, launch, shard
+    from kman_amd import dist, launch, shard
+
+    lay = inputs.SynthLayout(per * world, 1)
+    rd = shard.SynthReader(lay)
+    uid = launch.rendezvous(rank, world, tag)
+    t_setup = time.time()
+    pipe = dist.DistPipeline(dev, rd, args.k, mode, world, rank, uid, chunk_bytes=1 << 30, reparse=reparse,
+                             canonical=canon, ordered=not canon)
+    if rank == 0:
+        launch.remove_id(tag)  # (every rank has joined the communicator)
+    comm = pipe.comm
+    rccl_ranks, rccl_rank = comm.count()
+    log("rank %d (RCCL rank %d of %d): shard %d..%d (%.2f GB) generated + parsed on the device, setup %.1f s"
+        % (rank, rccl_rank, rccl_ranks, pipe.spec.start, pipe.spec.own_end, (pipe.spec.own_end - pipe.spec.start) / 1e9,
+           time.time() - t_setup))
+    hist = [None]
+
+    def one_step():
+        n = pipe.step()
+        if canon:  # config 5: the abundance spectrum of the global canonical counts, all-reduced
+            hist[0] = comm.run(pipe.hist_gen(10001))
+        return n
+
+    try:
+        for _ in range(warmup):
+            one_step()
+        setup_s = time.time() - t_setup
+        pipe.timing(True)
+        comm.allreduce(np.zeros(1, np.uint64))  # barrier
+        dev.sync()
+        t0 = time.perf_counter()
+        kmers = 0
+        for _ in range(steps):
+            kmers += one_step()
+        dev.sync()
+        elapsed = time.perf_counter() - t0
+        el = comm.allgather(np.array([int(elapsed * 1e9)], np.uint64))
+        tot = comm.allreduce(np.array([kmers], np.uint64))
+        elapsed, total = float(el.max()) / 1e9, int(tot[0])
+        out = None
+        if rank == 0:
+            stages = {}
+            for st in ("parse", "shard_hist", "region_extract", "region_pass", "region_pass1b", "region_finish",
+                       "extract", "sort_pass", "finish"):
+                c, ms = pipe.timed(st)
+                if c:
+                    stages[st] = round(ms / steps, 3)
+            dom, sp = dist_roofline(pipe, steps, mode, args.k, per, world, canon)
+            stage_alg = {}
+            for st, (kern, alg_step) in dist_stage_bytes(pipe, steps, mode).items():
+                c, _ = pipe.timed(st)
+                if c:
+                    stage_alg[st] = {"kernel": kern, "alg_bytes_per_launch": alg_step / max(1, c // steps),
+                                     "launches_per_step": c // steps}
+            out = {"value": total / elapsed, "ms_per_step": elapsed / steps * 1e3, "steps": steps, "warmup": warmup,
+                   "kmers_per_step": total // max(steps, 1), "rccl_ranks": rccl_ranks, "setup_s": round(setup_s, 2),
+                   "fasta_bytes": lay.size, "fasta_bytes_per_rank": per, "path": pipe.path, "rounds": pipe.rounds,
+                   "fallback_rounds": pipe.fallback_rounds, "partial_rounds": pipe.partial_rounds,
+                   "memory_plan": getattr(pipe, "plan_info", None), "stages_ms_per_step_rank0": stages,
+                   "stage_alg_bytes_rank0": stage_alg, "roofline": dom, "sort_pass_roofline": sp,
+                   "spectrum_distinct": int(hist[0].sum()) if canon else None}
+        comm.allreduce(np.zeros(1, np.uint64))  # every rank is done with this line
+        return out
+    finally:
+        pipe.free()
+
+
+def run_dist(args, world: int, rank: int, local: int):
+    from kman_amd import engine
 
     dev = engine.Device(local)
     per = int(args.shard_gb * 1e9) if args.shard_gb else args.bases
-    lay = inputs.SynthLayout(per * world, 1)
-    rd = shard.SynthReader(lay)
-    uid = launch.rendezvous(rank, world, "bench")
-    t0 = time.time()
     # the 1 GB-per-rank line keeps each rank's text in HBM and parses it in
     # every step (the single-GPU step's scope); config 4's 12.5 GB shards
     # stream through two 1 GiB staging buffers, parsed once at setup
@@ -469,76 +538,44 @@ def run_dist(args, world: int, rank: int, local: int):
     canon = args.canonical
     if canon and args.mode != "count":
         raise SystemExit("--canonical counts (config 5): use --mode count")
-    pipe = dist.DistPipeline(dev, rd, args.k, args.mode, world, rank, uid, chunk_bytes=1 << 30, reparse=reparse,
-                             canonical=canon, ordered=not canon)
+    ln = dist_line(args, dev, world, rank, per, args.mode, canon, reparse, args.steps, args.warmup, "bench")
+    # BASELINE config 4 (100 GB synthetic FASTA, k=21, N GPUs): after the
+    # weak-scaling line, the same job at 100 / N GB per rank, count mode,
+    # parsed at setup -- so the driver's plain `--gpus N` run measures it too
+    sub = None
+    if world > 1 and args.config4 and args.shard_gb is None and not canon:
+        per4 = int(100e9 / world)
+        sub = dist_line(args, dev, world, rank, per4, "count", False, False, args.config4_steps, 1, "bench4")
+    dev.close()
     if rank == 0:
-        launch.remove_id("bench")  # (every rank has joined the communicator)
-    log("rank %d: shard %d..%d (%.2f GB) generated + parsed on the device, setup %.1f s"
-        % (rank, pipe.spec.start, pipe.spec.own_end, (pipe.spec.own_end - pipe.spec.start) / 1e9, time.time() - t0))
-    comm = pipe.comm
-
-    def one_step():
-        n = pipe.step()
-        if canon:  # config 5: the abundance spectrum of the global canonical counts, all-reduced
-            one_step.hist = comm.run(pipe.hist_gen(10001))
-        return n
-
-    for _ in range(args.warmup):
-        one_step()
-    pipe.timing(True)
-    comm.allreduce(np.zeros(1, np.uint64))  # barrier
-    dev.sync()
-    t0 = time.perf_counter()
-    kmers = 0
-    for _ in range(args.steps):
-        kmers += one_step()
-    dev.sync()
-    elapsed = time.perf_counter() - t0
-    el = comm.allgather(np.array([int(elapsed * 1e9)], np.uint64))
-    tot = comm.allreduce(np.array([kmers], np.uint64))
-    elapsed, total = float(el.max()) / 1e9, int(tot[0])
-    stages = {}
-    for tag in ("parse", "shard_hist", "region_extract", "region_pass", "region_pass1b", "region_finish",
-                "extract", "sort_pass", "finish"):
-        c, ms = pipe.timed(tag)
-        if c:
-            stages[tag] = round(ms / args.steps, 3)
-    if rank == 0:
-        dom, sp = dist_roofline(pipe, args.steps, args.mode, args.k, per, world, canon)
-        stage_alg = {}
-        for tag, (kern, alg_step) in dist_stage_bytes(pipe, args.steps, args.mode).items():
-            c, _ = pipe.timed(tag)
-            if c:
-                stage_alg[tag] = {"kernel": kern, "alg_bytes_per_launch": alg_step / max(1, c // args.steps),
-                                  "launches_per_step": c // args.steps}
         out = {
-            "metric": METRIC, "value": total / elapsed, "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "metric": METRIC, "value": ln["value"], "unit": "k-mers/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ln["ms_per_step"], "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u64",
             "data": "synthetic: ONE global FASTA (kman_synth_fasta seed 1, uniform ACGT, 80 col) of %d x %.2f GB, "
                     "byte-range sharded, each rank's bytes generated in its HBM; a step = %s shard histogram + key "
                     "rounds" % (world, per / 1e9, "parse of the resident text +" if reparse else "(parsed at setup)"),
             "config": {"workload": "%.2f GB synthetic FASTA in %d byte-range shards of %.2f GB per rank, k=%d, "
                                    "extract+radix-sort+%s, key rounds + one RCCL all-to-all per round%s"
-                                   % (lay.size / 1e9, world, per / 1e9, args.k,
+                                   % (ln["fasta_bytes"] / 1e9, world, per / 1e9, args.k,
                                       "canonical count + all-reduced abundance spectrum (config 5's pipeline)"
                                       if canon else args.mode,
                                       "" if not canon else "; the synthetic input stands in for GRCh38"),
-                       "canonical": canon,
-                       "spectrum_distinct": int(one_step.hist.sum()) if canon else None,
-                       "fasta_bytes": lay.size, "fasta_bytes_per_rank": per,
-                       "kmers_per_step": total // max(args.steps, 1), "k": args.k,
+                       "canonical": canon, "spectrum_distinct": ln["spectrum_distinct"],
+                       "fasta_bytes": ln["fasta_bytes"], "fasta_bytes_per_rank": per,
+                       "kmers_per_step": ln["kmers_per_step"], "k": args.k,
                        "mode": args.mode, "parallelism": "dp%d: top-8-bit bucket parts + RCCL all-to-all" % world,
-                       "path": pipe.path, "rounds": pipe.rounds, "fallback_rounds": pipe.fallback_rounds,
-                       "partial_rounds": pipe.partial_rounds,
-                       "memory_plan": getattr(pipe, "plan_info", None),
-                       "stages_ms_per_step_rank0": stages, "stage_alg_bytes_rank0": stage_alg},
-            "roofline": dom, "sort_pass_roofline": sp, "cpu_baseline": None,
+                       "rccl_ranks": ln["rccl_ranks"], "setup_s": ln["setup_s"],
+                       "path": ln["path"], "rounds": ln["rounds"], "fallback_rounds": ln["fallback_rounds"],
+                       "partial_rounds": ln["partial_rounds"], "memory_plan": ln["memory_plan"],
+                       "stages_ms_per_step_rank0": ln["stages_ms_per_step_rank0"],
+                       "stage_alg_bytes_rank0": ln["stage_alg_bytes_rank0"]},
+            "roofline": ln["roofline"], "sort_pass_roofline": ln["sort_pass_roofline"], "cpu_baseline": None,
         }
-    comm.allreduce(np.zeros(1, np.uint64))  # every rank is done
-    pipe.free()
-    dev.close()
-    if rank == 0:
+        if sub is not None:
+            out["config4"] = dict(sub, metric=METRIC, unit="k-mers/s", n_gpus=world,
+                                  workload="BASELINE config 4: 100 GB synthetic FASTA, k=21, count, %d x %.2f GB "
+                                           "byte-range shards, key rounds + RCCL all-to-all" % (world, 100.0 / world))
         # the C port on the host's cores, after every rank has left the GPU
         # work (the other ranks exit; the GPUs are idle while it runs)
         if not args.no_cpu_baseline:
@@ -631,11 +668,7 @@ def emit(out: dict) -> None:
         os.write(_RESULT_FD, line)
 
 
-def main() -> None:
-    global _RESULT_FD
-    sys.stdout.flush()
-    _RESULT_FD = os.dup(1)
-    os.dup2(2, 1)  # everything else printed to fd 1 (ours or a library's) goes to stderr
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -651,10 +684,21 @@ def main() -> None:
     ap.add_argument("--path", choices=["region", "split", "full"], default="region",
                     help="single-GPU engine path (region falls back to split outside its domain)")
     ap.add_argument("--dist", action="store_true", help="run the multi-GPU pipeline even at world size 1")
+    ap.add_argument("--no-config4", dest="config4", action="store_false",
+                    help="N > 1: skip the config-4 sub-line (100 GB / N per rank, count) after the main line")
+    ap.add_argument("--config4-steps", type=int, default=3, help="timed steps of the config-4 sub-line")
     ap.add_argument("--canonical", action="store_true",
                     help="multi-GPU path: canonical k-mers + the all-reduced abundance spectrum (config 5; "
                          "with --mode count)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def main() -> None:
+    global _RESULT_FD
+    sys.stdout.flush()
+    _RESULT_FD = os.dup(1)
+    os.dup2(2, 1)  # everything else printed to fd 1 (ours or a library's) goes to stderr
+    args = parse_args()
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ and (args.gpus > 1 or args.dist or args.canonical):

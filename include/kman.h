@@ -453,6 +453,8 @@ int kman_rle_uniq(kman_ctx *ctx, const uint64_t *d_keys, const void *d_vals, uin
  * splits the global join by prefix range.
  *   kman_comm_unique_id  rank 0 creates the 128-byte id, the launcher shares it
  *   kman_comm_init       ncclCommInitRank on the context's device
+ *   kman_comm_count      the ranks and this rank as the communicator counts
+ *                        them (ncclCommCount / ncclCommUserRank)
  *   kman_prefix_hist     d_hist[(key >> shift) & (2^bits - 1)] += 1 (bits <= 14)
  *   kman_allreduce_u64   in-place sum (histograms)
  *   kman_allgather_u64   per-rank counts
@@ -462,6 +464,7 @@ int kman_rle_uniq(kman_ctx *ctx, const uint64_t *d_keys, const void *d_vals, uin
  *                        onesweep pass; bucket_counts is a host array */
 int kman_comm_unique_id(uint8_t *out128);
 int kman_comm_init(kman_ctx *ctx, const uint8_t *id128, int nranks, int rank);
+int kman_comm_count(kman_ctx *ctx, int *nranks, int *rank);
 int kman_comm_destroy(kman_ctx *ctx);
 int kman_prefix_hist(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint32_t shift, uint32_t bits,
                      uint64_t *d_hist);

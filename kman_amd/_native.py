@@ -164,6 +164,7 @@ SIGNATURES = {
     ),
     "kman_comm_unique_id": (c_int, [c_void_p]),
     "kman_comm_init": (c_int, [c_void_p, c_void_p, c_int, c_int]),
+    "kman_comm_count": (c_int, [c_void_p, c_void_p, c_void_p]),
     "kman_comm_destroy": (c_int, [c_void_p]),
     "kman_prefix_hist": (c_int, [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_void_p]),
     "kman_allreduce_u64": (c_int, [c_void_p, c_void_p, c_uint64]),

@@ -89,6 +89,15 @@ extern "C" int kman_comm_init(kman_ctx *ctx, const uint8_t *id128, int nranks, i
     return KMAN_OK;
 }
 
+extern "C" int kman_comm_count(kman_ctx *ctx, int *nranks, int *rank) {
+    if (!ctx || !nranks || !rank) return KMAN_EINVAL;
+    Comm *c = comm_of(ctx);
+    if (!c) return kman_fail(ctx, KMAN_EINVAL, "no communicator");
+    NCCL_TRY(ctx, ncclCommCount(c->comm, nranks));
+    NCCL_TRY(ctx, ncclCommUserRank(c->comm, rank));
+    return KMAN_OK;
+}
+
 extern "C" int kman_comm_destroy(kman_ctx *ctx) {
     if (!ctx) return KMAN_EINVAL;
     Comm *c = comm_of(ctx);

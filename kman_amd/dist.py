@@ -264,6 +264,13 @@ class RcclComm:
             self.d_vec = self.dev.alloc(8 * self.cap)
             self.d_mat = self.dev.alloc(8 * self.cap * self.world)
 
+    def count(self) -> Tuple[int, int]:
+        """(ranks, this rank) as the RCCL communicator counts them."""
+        n, r = ctypes.c_int(0), ctypes.c_int(0)
+        N.check(self.dev.ctx, N.lib().kman_comm_count(self.dev.ctx, ctypes.byref(n), ctypes.byref(r)),
+                "kman_comm_count")
+        return int(n.value), int(r.value)
+
     def allreduce(self, x: np.ndarray) -> np.ndarray:
         x = np.ascontiguousarray(x, np.uint64)
         self._bufs(len(x))
@@ -325,6 +332,9 @@ class LocalComm:
 
     def __init__(self, dev: engine.Device):
         self.dev = dev
+
+    def count(self) -> Tuple[int, int]:
+        return 1, 0
 
     def run(self, gen):
         try:

@@ -106,16 +106,20 @@ class FileReader:
 
 
 def launch_nonce() -> str:
-    """Something every rank of ONE launch shares and the next launch does
-    not: the launcher's run id (KMAN_RUN_ID, set by bench.py's spawner), else
-    under torch.distributed.run the elastic agent's PID (every local worker
-    is its child; its TORCHELASTIC_RUN_ID is often the constant "none"), else
-    empty (other launchers: the start-time check in `rendezvous` only)."""
+    """Something every rank of ONE launch shares (and, where the launcher
+    offers it, the next launch does not), taken from the environment only:
+    the launcher's run id (KMAN_RUN_ID, set by bench.py's spawner), else
+    torch.distributed.run's TORCHELASTIC_RUN_ID with its restart count when
+    the id is not the constant "none", else empty -- the start-time check in
+    `rendezvous` then tells launches apart.  (Not the parent PID: a worker
+    wrapped in a shell or launcher has a parent of its own, and its peers
+    would wait on another file.)"""
     rid = os.environ.get("KMAN_RUN_ID")
     if rid:
         return rid
-    if "TORCHELASTIC_RUN_ID" in os.environ:
-        return "%s-%d" % (os.environ["TORCHELASTIC_RUN_ID"], os.getppid())
+    tid = os.environ.get("TORCHELASTIC_RUN_ID", "")
+    if tid and tid != "none":
+        return "%s-%s" % (tid, os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
     return ""
 
 

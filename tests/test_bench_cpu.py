@@ -127,3 +127,58 @@ def test_committed_pmc_summary_matches_the_default_workload():
     for kern in ("rg_finish", "rg_pass", "rg_extract"):
         t = bench.pmc_traffic(kern, "uniq", 21, 1_000_000_000)
         assert t is not None and t > 0, kern
+
+
+def _fake_line(calls):
+    def line(args, dev, world, rank, per, mode, canon, reparse, steps, warmup, tag):
+        calls.append({"per": per, "mode": mode, "canon": canon, "reparse": reparse, "steps": steps,
+                      "warmup": warmup, "tag": tag})
+        if rank:
+            return None
+        return {"value": 1e9 * world, "ms_per_step": 10.0, "steps": steps, "warmup": warmup,
+                "kmers_per_step": per * world, "rccl_ranks": world, "setup_s": 1.0, "fasta_bytes": per * world,
+                "fasta_bytes_per_rank": per, "path": "region", "rounds": 3 if mode == "count" else 1,
+                "fallback_rounds": 0, "partial_rounds": 0, "memory_plan": None, "stages_ms_per_step_rank0": {},
+                "stage_alg_bytes_rank0": {}, "roofline": {"frac": 0.5}, "sort_pass_roofline": {"frac": 0.6},
+                "spectrum_distinct": None}
+    return line
+
+
+class _Dev:
+    def __init__(self, i):
+        pass
+
+    def close(self):
+        pass
+
+
+def test_multi_gpu_line_carries_config4_and_rccl_ranks(monkeypatch, capsys):
+    """`bench.py --gpus N` (N > 1, the driver's plain run): after the
+    1 GB-per-rank weak-scaling line, a config4 sub-line of BASELINE config 4
+    (100 GB over N ranks: 100/N GB per rank, count, parsed at setup), each with
+    the RCCL communicator's own rank count."""
+    from kman_amd import engine
+
+    calls = []
+    monkeypatch.setattr(bench, "dist_line", _fake_line(calls))
+    monkeypatch.setattr(engine, "Device", _Dev)
+    args = bench.parse_args(["--gpus", "8", "--steps", "4", "--warmup", "1", "--no-cpu-baseline"])
+    bench.run_dist(args, 8, 0, 0)
+    out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert out["n_gpus"] == 8 and out["config"]["rccl_ranks"] == 8 and out["steps"] == 4
+    c4 = out["config4"]
+    assert c4["rccl_ranks"] == 8 and c4["fasta_bytes_per_rank"] == int(100e9 / 8) and c4["rounds"] == 3
+    assert "roofline" in c4 and c4["ms_per_step"] > 0 and c4["setup_s"] >= 0
+    assert [(c["mode"], c["per"], c["reparse"], c["tag"]) for c in calls] == [
+        ("uniq", 10 ** 9, True, "bench"), ("count", int(100e9 / 8), False, "bench4")]
+    # the other ranks run both lines and print nothing
+    calls.clear()
+    bench.run_dist(args, 8, 3, 3)
+    assert capsys.readouterr().out.strip() == "" and len(calls) == 2
+    # --no-config4, an explicit --shard-gb and world 1 run the main line only
+    for argv, world in ((["--gpus", "2", "--no-config4"], 2), (["--gpus", "2", "--shard-gb", "12.5"], 2),
+                        (["--dist"], 1)):
+        calls.clear()
+        bench.run_dist(bench.parse_args(argv + ["--no-cpu-baseline"]), world, 0, 0)
+        out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+        assert len(calls) == 1 and "config4" not in out and out["config"]["rccl_ranks"] == world

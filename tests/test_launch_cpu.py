@@ -118,10 +118,46 @@ def test_rendezvous_back_to_back_relaunch(tmp_path, monkeypatch):
     assert launch._id_path("t", d) != stale
     with pytest.raises(RuntimeError):  # no rank 0 of the new launch: the old id is not taken
         launch.rendezvous(1, 2, "t", make_uid=lambda: b"\2" * 128, directory=d, timeout=0.5)
-    # under torch.distributed.run the elastic agent's PID keys the launch
+    # under torch.distributed.run: its run id and restart count when the id
+    # is a real one; the constant "none" keys nothing (start-time check only)
     monkeypatch.delenv("KMAN_RUN_ID")
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "abc")
+    monkeypatch.setenv("TORCHELASTIC_RESTART_COUNT", "2")
+    assert launch.launch_nonce() == "abc-2"
     monkeypatch.setenv("TORCHELASTIC_RUN_ID", "none")
-    assert launch.launch_nonce() == "none-%d" % os.getppid()
+    assert launch.launch_nonce() == ""
+
+
+def _wrapped_rank(rank, world, d, q, delay):
+    # one more process between the "launcher" and the rank (a shell or a
+    # wrapper script): every rank then has a parent of its own
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_rank, args=(rank, world, d, q, delay))
+    p.start()
+    p.join(timeout=60)
+
+
+def test_rendezvous_ranks_with_different_parents(tmp_path, monkeypatch):
+    """torchrun with a wrapper between the agent and Python
+    (TORCHELASTIC_RUN_ID "none"): the ranks' parents differ, and they still
+    meet on one id file."""
+    from kman_amd import launch
+
+    monkeypatch.delenv("KMAN_RUN_ID", raising=False)
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "none")
+    monkeypatch.setenv("MASTER_PORT", "29501")
+    d = str(tmp_path)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    world = 3
+    ps = [ctx.Process(target=_wrapped_rank, args=(r, world, d, q, 0.0 if r else 0.5)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = dict(q.get(timeout=90) for _ in range(world))
+    for p in ps:
+        p.join(timeout=30)
+    assert len(got) == world and len(set(got.values())) == 1
+    launch.remove_id("t", d)
 
 
 def test_cli_leaves_solo_work_to_rank_zero(tmp_path, monkeypatch):
