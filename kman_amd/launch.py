@@ -74,11 +74,20 @@ def solo_rank() -> bool:
 
 class FileReader:
     """A shard.py reader over a FASTA file: plain files memory-mapped (a rank
-    touches only its byte range and the cuts around it), gzip input
-    (batcher.py:480 opens ``.gz`` with gzip.open) decompressed in memory."""
+    touches only its byte range and the cuts around it).  Gzip input
+    (batcher.py:480 opens ``.gz`` with gzip.open): one rank decompresses it
+    in memory; under a multi-GPU launch rank 0 decompresses it ONCE, as a
+    stream, into a temp file that every rank then memory-maps like a plain
+    one (so no rank holds the whole text, and the file is inflated once, not
+    once per rank).  Rank 0 removes the temp file when it closes the reader
+    (the peers' maps stay valid) or at exit."""
 
-    def __init__(self, path: str):
+    def __init__(self, path: str, world: int = 1, rank: int = 0, directory: Optional[str] = None,
+                 timeout: float = 3600.0):
         self._fh = self._mm = None
+        self._tmp = None
+        if path.endswith(".gz") and world > 1:
+            path = self._gunzip_shared(path, world, rank, directory, timeout)
         if path.endswith(".gz"):
             with gzip.open(path, "rb") as fh:
                 self._mv = memoryview(fh.read())
@@ -92,6 +101,66 @@ class FileReader:
                 self._mv = memoryview(b"")
         self.size = len(self._mv)
 
+    def _gunzip_shared(self, path: str, world: int, rank: int, directory: Optional[str], timeout: float,
+                       skew: float = 30.0) -> str:
+        """The plain text of `path` in a temp file shared by the ranks of this
+        launch (keyed like the RCCL id file, plus the input's identity); rank 0
+        writes it and then a marker holding its start time, a peer accepts
+        only a marker written by a rank 0 that started no earlier than `skew`
+        seconds before itself."""
+        import atexit
+        import shutil
+        import zlib
+
+        st = os.stat(path)
+        ident = "%08x" % (zlib.crc32(("%s|%d|%d" % (os.path.abspath(path), st.st_size, st.st_mtime_ns)).encode())
+                          & 0xffffffff)
+        plain = _id_path("gz" + ident, directory) + ".fa"
+        done = plain + ".done"
+        if rank == 0:
+            for q in (done, plain):
+                try:
+                    os.remove(q)
+                except OSError:
+                    pass
+            part = plain + ".part%d" % os.getpid()
+            try:
+                with gzip.open(path, "rb") as src, open(part, "wb") as dst:
+                    shutil.copyfileobj(src, dst, 16 << 20)
+                os.replace(part, plain)
+            finally:
+                try:
+                    os.remove(part)
+                except OSError:
+                    pass
+            self._tmp = (plain, done)
+            atexit.register(self._remove_tmp)
+            with open(done + ".tmp", "wb") as fh:
+                fh.write(_MAGIC + struct.pack("<d", _START))
+            os.replace(done + ".tmp", done)
+            return plain
+        t0 = time.time()
+        while True:
+            try:
+                with open(done, "rb") as fh:
+                    blob = fh.read()
+                if blob[:8] == _MAGIC and len(blob) >= 16 and struct.unpack("<d", blob[8:16])[0] >= _START - skew:
+                    return plain
+            except OSError:
+                pass
+            if time.time() - t0 > timeout:
+                raise RuntimeError("rank %d: rank 0 did not decompress %s into %s" % (rank, path, plain))
+            time.sleep(0.05)
+
+    def _remove_tmp(self) -> None:
+        if self._tmp:
+            for q in self._tmp:
+                try:
+                    os.remove(q)
+                except OSError:
+                    pass
+            self._tmp = None
+
     def read(self, lo: int, hi: int) -> bytes:
         return bytes(self._mv[max(0, lo):max(0, min(hi, self.size))])
 
@@ -103,6 +172,7 @@ class FileReader:
         if self._fh is not None:
             self._fh.close()
             self._fh = None
+        self._remove_tmp()
 
 
 def launch_nonce() -> str:
@@ -195,7 +265,7 @@ class ShardedSource:
         engine._check_k(k)
         self.world, self.rank, self.local = world_env()
         self.dev, self.k, self.rc, self.path = dev, k, rc, path
-        self.reader = FileReader(path)
+        self.reader = FileReader(path, self.world, self.rank)
         self.spec = S.shard_specs(self.reader, self.world, k)[self.rank]
         self.loader = S.ShardLoader(dev, self.reader, self.spec, k)
         self.shard = self.loader.load()

@@ -180,3 +180,67 @@ def test_cli_leaves_solo_work_to_rank_zero(tmp_path, monkeypatch):
     assert r.exit_code == 0 and not (tmp_path / "bd").exists()
     r = CliRunner().invoke(main, ["count", str(src), str(out), "1"])
     assert isinstance(r.exception, AssertionError)
+
+
+def _gz_rank(rank, world, path, d, q, chunk):
+    import hashlib
+    import resource
+
+    from kman_amd import launch, shard
+
+    rss0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024
+    rd = launch.FileReader(path, world, rank, directory=d, timeout=120)
+    spec = shard.shard_specs(rd, world, 21)[rank]
+    h = hashlib.sha256()
+    for lo in range(spec.start, spec.halo_end, chunk):  # the loader's chunked reads
+        h.update(rd.read(lo, min(spec.halo_end, lo + chunk)))
+    peak = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss * 1024 - rss0
+    q.put((rank, spec.start, spec.halo_end, h.hexdigest(), peak, rd.size))
+    # rank 0 keeps its reader (and the temp file) until every peer has read
+    time.sleep(3.0 if rank == 0 else 0.0)
+    rd.close()
+
+
+def test_gzip_input_inflated_once_and_memory_mapped_by_every_rank(tmp_path):
+    """A gzipped FASTA under a 4-rank launch: rank 0 inflates it once into a
+    shared temp file, every rank maps it and reads only its byte range; each
+    rank's peak RSS grows by at most 1.5x its shard, the shards are the plain
+    file's bytes, and the temp file is gone once rank 0 closes its reader."""
+    import hashlib
+
+    import numpy as np
+
+    from kman_amd import shard
+
+    rng = np.random.default_rng(5)
+    recs = []
+    for r in range(24):  # ~10 MB records of 80-column lines
+        seq = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, 10_000_000)].tobytes()
+        recs.append(b">rec%d some description\n" % r + b"\n".join(seq[i:i + 80] for i in range(0, len(seq), 80)) + b"\n")
+    text = b"".join(recs)
+    gz = tmp_path / "big.fa.gz"
+    with gzip.open(gz, "wb", compresslevel=1) as fh:
+        fh.write(text)
+    world, chunk = 4, 16 << 20
+    specs = shard.shard_specs(shard.BytesReader(text), world, 21)
+    d = str(tmp_path / "tmp")
+    os.mkdir(d)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_gz_rank, args=(r, world, str(gz), d, q, chunk)) for r in range(world)]
+    for p in ps:
+        p.start()
+    got = {}
+    for _ in range(world):
+        rank, lo, hi, digest, peak, size = q.get(timeout=300)
+        got[rank] = (lo, hi, digest, peak, size)
+    for p in ps:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    del recs
+    for r, s in enumerate(specs):
+        lo, hi, digest, peak, size = got[r]
+        assert size == len(text) and (lo, hi) == (s.start, s.halo_end)
+        assert digest == hashlib.sha256(text[lo:hi]).hexdigest()
+        assert peak <= 1.5 * (hi - lo), (r, peak, hi - lo)
+    assert os.listdir(d) == []
