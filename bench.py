@@ -260,32 +260,68 @@ def file_to_file(k: int, nbases: int = 100_000_000):
                       "(includes interpreter + device init)" % (nbases, k)}
 
 
-def d2h_probe(dev, nbytes: int = 1 << 30) -> dict:
-    """One warm device -> pinned host copy of `nbytes` on the copy stream
-    (kman_copy_d2h_async, what the pipelined writer issues per slice): the
-    ceiling of any output line that leaves the GPU."""
+def d2h_probe(dev, total: int = 8 << 30) -> dict:
+    """Device -> pinned host copies in the pipelined writer's own pattern
+    (engine._format_dev without the formatting): slices of _FMT_SLICE bytes
+    through two pinned stages on the copy stream (kman_copy_d2h_async into
+    stage i % 2, then the wait for slice i - 1), `total` bytes, warm: the
+    ceiling of any output line that leaves the GPU.  Also one whole 1 GiB
+    copy, as earlier rounds reported it."""
     from ctypes import byref, c_void_p
 
     from kman_amd import _native as N
+    from kman_amd import engine
 
     L = N.lib()
-    buf = dev.alloc(nbytes)
+    sl = engine._FMT_SLICE
+    bufs = [dev.alloc(sl) for _ in range(2)]
+    stages = []
+    try:
+        for _ in range(2):
+            hp = c_void_p()
+            N.check(dev.ctx, L.kman_host_alloc(dev.ctx, byref(hp), sl), "kman_host_alloc")
+            stages.append(hp)
+
+        def sliced():
+            last = None
+            for i in range(total // sl):
+                b = i % 2
+                N.check(dev.ctx, L.kman_copy_d2h_async(dev.ctx, stages[b], c_void_p(bufs[b].ptr), sl, b),
+                        "kman_copy_d2h_async")
+                if last is not None:
+                    N.check(dev.ctx, L.kman_copy_d2h_wait(dev.ctx, last), "kman_copy_d2h_wait")
+                last = b
+            N.check(dev.ctx, L.kman_copy_d2h_wait(dev.ctx, last), "kman_copy_d2h_wait")
+
+        sliced()  # (warm: maps the pages)
+        t0 = time.perf_counter()
+        sliced()
+        dt = time.perf_counter() - t0
+    finally:
+        for hp in stages:
+            L.kman_host_free(dev.ctx, hp)
+        for b_ in bufs:
+            b_.free()
+    nb1 = 1 << 30
+    buf = dev.alloc(nb1)
     hp = c_void_p()
-    N.check(dev.ctx, L.kman_host_alloc(dev.ctx, byref(hp), nbytes), "kman_host_alloc")
+    N.check(dev.ctx, L.kman_host_alloc(dev.ctx, byref(hp), nb1), "kman_host_alloc")
     try:
         def once():
-            N.check(dev.ctx, L.kman_copy_d2h_async(dev.ctx, hp, c_void_p(buf.ptr), nbytes, 0), "kman_copy_d2h_async")
+            N.check(dev.ctx, L.kman_copy_d2h_async(dev.ctx, hp, c_void_p(buf.ptr), nb1, 0), "kman_copy_d2h_async")
             N.check(dev.ctx, L.kman_copy_d2h_wait(dev.ctx, 0), "kman_copy_d2h_wait")
 
-        once()  # (warm: maps the pages)
+        once()
         t0 = time.perf_counter()
         for _ in range(3):
             once()
-        dt = (time.perf_counter() - t0) / 3
+        d1 = (time.perf_counter() - t0) / 3
     finally:
         L.kman_host_free(dev.ctx, hp)
         buf.free()
-    return {"bytes": nbytes, "ms": dt * 1e3, "gbs": nbytes / dt / 1e9}
+    return {"bytes": total, "slice_bytes": sl, "ms": dt * 1e3, "gbs": total / dt / 1e9,
+            "single_1gib_gbs": nb1 / d1 / 1e9,
+            "note": "the writer's pattern: %d MiB slices through two pinned stages on the copy stream" % (sl >> 20)}
 
 
 def file_to_file_config2(path: str, k: int, mode: str, text_bytes_est: int) -> dict:
@@ -295,21 +331,38 @@ def file_to_file_config2(path: str, k: int, mode: str, text_bytes_est: int) -> d
     disk) and into a file (+ the page cache; when the disk has room)."""
     out = {}
 
-    def run(dst):
-        t0 = time.perf_counter()
-        subprocess.run([sys.executable, "-m", "kman_amd", mode, path, dst, str(k)], check=True, cwd=ROOT,
-                       stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
-        return time.perf_counter() - t0
+    def run(dst, phases_out=None):
+        from kman_amd import phases
 
-    s = run("/dev/null")
-    out["devnull"] = {"seconds": s}
+        fd_, ph = tempfile.mkstemp(suffix=".json")
+        os.close(fd_)
+        try:
+            t0 = time.perf_counter()
+            env = dict(os.environ, KMAN_PHASES=ph, KMAN_T0=repr(time.time()))
+            subprocess.run([sys.executable, "-m", "kman_amd", mode, path, dst, str(k)], check=True, cwd=ROOT,
+                           stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, env=env)
+            dt = time.perf_counter() - t0
+            if phases_out is not None:
+                try:
+                    phases_out.update(phases.breakdown(ph))
+                except (OSError, ValueError, KeyError):
+                    pass
+            return dt
+        finally:
+            os.remove(ph)
+
+    ph = {}
+    s = run("/dev/null", ph)
+    out["devnull"] = {"seconds": s, "phases_s": ph}
     d = os.environ.get("TMPDIR", "/tmp")
     free = shutil.disk_usage(d).free
     if free > 1.3 * text_bytes_est + (8 << 30):
         dst = os.path.join(d, "kman_cfg2_out.txt")
         try:
-            s2 = run(dst)
-            out["file"] = {"seconds": s2, "output_bytes": os.path.getsize(dst), "gbs": os.path.getsize(dst) / s2 / 1e9}
+            ph2 = {}
+            s2 = run(dst, ph2)
+            out["file"] = {"seconds": s2, "output_bytes": os.path.getsize(dst), "gbs": os.path.getsize(dst) / s2 / 1e9,
+                           "phases_s": ph2}
         finally:
             try:
                 os.remove(dst)
@@ -318,8 +371,79 @@ def file_to_file_config2(path: str, k: int, mode: str, text_bytes_est: int) -> d
     else:
         out["file"] = {"skipped": "%.1f GB free in %s for ~%.1f GB of text" % (free / 1e9, d, text_bytes_est / 1e9)}
     out["note"] = ("`python -m kman_amd %s <1 GB FASTA> OUT %d`, process start to exit (interpreter, device init, "
-                   "file read, H2D, the step, device formatting, D2H, write)" % (mode, k))
+                   "file read, H2D, the step, device formatting, D2H, write); phases_s: wall seconds from one mark "
+                   "to the next (kman_amd/phases.py, KMAN_PHASES)" % (mode, k))
     return out
+
+
+def extra_lines(args, dev, pipe, out, text, cfg2_path):
+    """The non-quick lines after the headline: the same step from pinned host
+    bytes, the 100 Mbp and config-2 file-to-file CLI lines (each recorded in
+    `out`, an error string when it fails)."""
+    from kman_amd import shard
+
+    # the same step from pinned host bytes (chunked H2D overlapping the parse)
+    rd = None
+    try:
+        rd = shard.PinnedReader(dev, text)
+        buf = dev.alloc(rd.size + 64)
+        from ctypes import c_void_p as _vp
+
+        from kman_amd import _native as _N
+
+        def _copy():  # one async copy on the copy stream (what the chunked loader issues)
+            _N.check(dev.ctx, _N.lib().kman_copy_h2d_async(dev.ctx, _vp(buf.ptr), _vp(rd.ptr(0)), rd.size, 0),
+                     "kman_copy_h2d_async")
+            _N.check(dev.ctx, _N.lib().kman_copy_sync(dev.ctx), "kman_copy_sync")
+
+        _copy()  # (warm: the first copy also maps the pages)
+        t0 = time.perf_counter()
+        _copy()
+        h2d = time.perf_counter() - t0
+        buf.free()
+        lines = {}
+        for ov in (True, False):
+            sp_ = shard.StreamedPipeline(dev, rd, args.k, args.mode, chunk_bytes=args.chunk_mb << 20, overlap=ov)
+            for _ in range(args.warmup):
+                sp_.step()
+            dev.sync()
+            t0 = time.perf_counter()
+            n = 0
+            for _ in range(args.steps):
+                n += sp_.step()
+            dev.sync()
+            lines[ov] = (n / (time.perf_counter() - t0), (time.perf_counter() - t0) / args.steps * 1e3)
+            sp_.free()
+        out["pinned_host"] = {"value": lines[True][0], "unit": "k-mers/s", "ms_per_step": lines[True][1],
+                              "serial_value": lines[False][0], "serial_ms_per_step": lines[False][1],
+                              "h2d_ms": h2d * 1e3, "h2d_gbs": rd.size / h2d / 1e9, "chunk_mb": args.chunk_mb,
+                              "note": "step from pinned host bytes: %d MiB chunks copied on a copy stream; the "
+                                      "parse and the region path's first pass (kman_groups_begin / _extract) "
+                                      "of chunk i run behind the copy of chunk i + 1, pass 1 + finish after "
+                                      "the last chunk (kman_groups_end); serial_* = the whole load, then "
+                                      "kman_groups; h2d_ms = one warm async copy of the whole text on the "
+                                      "copy stream" % args.chunk_mb}
+    except Exception as e:
+        out["pinned_host"] = {"error": repr(e)}
+    finally:
+        if rd is not None:
+            rd.free()
+    try:
+        out["file_to_file"] = file_to_file(args.k)
+    except Exception as e:
+        out["file_to_file"] = {"error": repr(e)}
+    try:
+        o = out.get("output") or {}
+        est = int(o.get("text_bytes", 0) * pipe.n_out / max(1, o.get("rows", 1))) if "rows" in o else 60 << 30
+        if cfg2_path is None:
+            raise RuntimeError("no room in TMPDIR for config 2's FASTA")
+        out["file_to_file_config2"] = file_to_file_config2(cfg2_path, args.k, args.mode, est)
+        f2 = out["file_to_file_config2"]
+        for key in ("devnull", "file"):
+            if "seconds" in f2.get(key, {}):
+                f2[key]["kmers_per_s"] = out["config"]["kmers_per_step_per_gpu"] / f2[key]["seconds"]
+    except Exception as e:
+        out["file_to_file_config2"] = {"error": repr(e)}
 
 
 def run_single(args):
@@ -377,71 +501,22 @@ def run_single(args):
     pipe.free()
     cfg2_path = None
     if not args.quick:
-        # config 2's FASTA as a file, for the end-to-end CLI line below
-        fd, cfg2_path = tempfile.mkstemp(suffix=".fa", dir=os.environ.get("TMPDIR", "/tmp"))
-        with os.fdopen(fd, "wb") as fh:
-            fh.write(text)
-        # the same step from pinned host bytes (chunked H2D overlapping the parse)
-        rd = shard.PinnedReader(dev, text)
-        del text
         try:
-            buf = dev.alloc(rd.size + 64)
-            from ctypes import c_void_p as _vp
-
-            from kman_amd import _native as _N
-
-            def _copy():  # one async copy on the copy stream (what the chunked loader issues)
-                _N.check(dev.ctx, _N.lib().kman_copy_h2d_async(dev.ctx, _vp(buf.ptr), _vp(rd.ptr(0)), rd.size, 0),
-                         "kman_copy_h2d_async")
-                _N.check(dev.ctx, _N.lib().kman_copy_sync(dev.ctx), "kman_copy_sync")
-
-            _copy()  # (warm: the first copy also maps the pages)
-            t0 = time.perf_counter()
-            _copy()
-            h2d = time.perf_counter() - t0
-            buf.free()
-            lines = {}
-            for ov in (True, False):
-                sp_ = shard.StreamedPipeline(dev, rd, args.k, args.mode, chunk_bytes=args.chunk_mb << 20, overlap=ov)
-                for _ in range(args.warmup):
-                    sp_.step()
-                dev.sync()
-                t0 = time.perf_counter()
-                n = 0
-                for _ in range(args.steps):
-                    n += sp_.step()
-                dev.sync()
-                lines[ov] = (n / (time.perf_counter() - t0), (time.perf_counter() - t0) / args.steps * 1e3)
-                sp_.free()
-            out["pinned_host"] = {"value": lines[True][0], "unit": "k-mers/s", "ms_per_step": lines[True][1],
-                                  "serial_value": lines[False][0], "serial_ms_per_step": lines[False][1],
-                                  "h2d_ms": h2d * 1e3, "h2d_gbs": rd.size / h2d / 1e9, "chunk_mb": args.chunk_mb,
-                                  "note": "step from pinned host bytes: %d MiB chunks copied on a copy stream; the "
-                                          "parse and the region path's first pass (kman_groups_begin / _extract) "
-                                          "of chunk i run behind the copy of chunk i + 1, pass 1 + finish after "
-                                          "the last chunk (kman_groups_end); serial_* = the whole load, then "
-                                          "kman_groups; h2d_ms = one warm async copy of the whole text on the "
-                                          "copy stream" % args.chunk_mb}
-        except Exception as e:
-            out["pinned_host"] = {"error": repr(e)}
+            # config 2's FASTA as a file, for the end-to-end CLI line below
+            # (never fatal to the GPU number: any failure is reported in the
+            # line, and the file is removed whatever happens)
+            tdir = os.environ.get("TMPDIR", "/tmp")
+            if shutil.disk_usage(tdir).free > 2 * len(text) + (1 << 30):
+                fd, cfg2_path = tempfile.mkstemp(suffix=".fa", dir=tdir)
+                with os.fdopen(fd, "wb") as fh:
+                    fh.write(text)
+            extra_lines(args, dev, pipe, out, text, cfg2_path)
         finally:
-            rd.free()
-        try:
-            out["file_to_file"] = file_to_file(args.k)
-        except Exception as e:
-            out["file_to_file"] = {"error": repr(e)}
-        try:
-            o = out.get("output") or {}
-            est = int(o.get("text_bytes", 0) * pipe.n_out / max(1, o.get("rows", 1))) if "rows" in o else 60 << 30
-            out["file_to_file_config2"] = file_to_file_config2(cfg2_path, args.k, args.mode, est)
-            f2 = out["file_to_file_config2"]
-            for key in ("devnull", "file"):
-                if "seconds" in f2.get(key, {}):
-                    f2[key]["kmers_per_s"] = out["config"]["kmers_per_step_per_gpu"] / f2[key]["seconds"]
-        except Exception as e:
-            out["file_to_file_config2"] = {"error": repr(e)}
-        finally:
-            os.remove(cfg2_path)
+            if cfg2_path is not None:
+                try:
+                    os.remove(cfg2_path)
+                except OSError:
+                    pass
     if not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.k, args.mode)

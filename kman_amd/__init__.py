@@ -8,4 +8,8 @@ include/kman.h (libkman.so, loaded by ``_native``).
 
 __version__ = "0.1.0"
 
+from . import phases as _phases  # noqa: E402
+
+_phases.mark("interpreter+import")
+
 __all__ = ["__version__", "batch", "batcher", "engine", "io", "join", "seq", "source"]

@@ -30,6 +30,7 @@ from typing import List, Optional, Tuple
 import numpy as np
 
 from . import _native as N
+from . import phases
 
 MAX_K = 32       # 2-bit keys in one u64 (the region / prefix-split paths)
 MAX_K_WIDE = 64  # k <= 64: kman_extract_wide rolls the two words of a key; beyond, kman_extract_words
@@ -82,6 +83,7 @@ class Device:
         self.ctx = ctx.value
         self.index = device
         self._fmt = None  # (cap, pinned stages, device slices) of the pipelined writer
+        phases.mark("device_init")
 
     def fmt_buffers(self, cap: int, nb: int):
         """The pipelined writer's nb pinned host stages and nb device text
@@ -216,6 +218,7 @@ def parse(dev: Device, text: bytes) -> Parsed:
     codes = dev.alloc(n + 64)
     try:
         dev.upload(d_text, text)
+        phases.mark("h2d")
         # record capacity: one record per 2 bytes at most ('>' + terminator)
         cap = n // 2 + 1
         d_hdr = dev.alloc(8 * cap)
@@ -235,6 +238,7 @@ def parse(dev: Device, text: bytes) -> Parsed:
     name_off = np.zeros(R + 1, dtype=np.uint64)
     if R:
         name_off[1:] = np.cumsum([len(x) for x in names], dtype=np.uint64)
+    phases.mark("parse")
     return Parsed(dev, codes, int(info.n_bases), R, rec_hdr, rec_seq, names, b"".join(names), name_off)
 
 
@@ -1001,9 +1005,12 @@ def read_input(path: str) -> bytes:
         import gzip
 
         with gzip.open(path, "rb") as fh:
-            return fh.read()
-    with open(path, "rb") as fh:
-        return fh.read()
+            text = fh.read()
+    else:
+        with open(path, "rb") as fh:
+            text = fh.read()
+    phases.mark("file_read")
+    return text
 
 
 def count_groups(p: Parsed, k: int, rc: bool = False, canonical: bool = False, ordered: bool = True) -> CountResult:

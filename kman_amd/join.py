@@ -41,7 +41,7 @@ from typing import Dict, Iterator, List, Tuple
 
 import numpy as np
 
-from . import engine
+from . import engine, phases
 from .batch import Batch
 
 
@@ -232,6 +232,7 @@ def join_bytes(batches: List[Batch], count: bool, sink=None):
         # one batch does not fit the HBM, else the general path (no copy of a
         # cached extraction either way)
         r = engine.join_groups(whole.parsed, whole.k, whole.rc, "count" if count else "uniq")
+        phases.mark("step")
         if r is None:
             return None if sink is not None else b""
         try:
@@ -241,6 +242,7 @@ def join_bytes(batches: List[Batch], count: bool, sink=None):
                 return engine.emit_count(whole.dev, r, sink)
             return engine.emit_uniq(whole.parsed, r, sink)
         finally:
+            phases.mark("format+d2h+write")
             engine.free_result(r)
     km, srcs, tagged = gather_sorted(entries, want_pos=not count)
     dev = srcs[0].dev

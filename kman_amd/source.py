@@ -21,7 +21,7 @@ from typing import List, Optional
 import numpy as np
 
 from . import _native as N
-from . import engine
+from . import engine, phases
 
 
 class FastaSource:
@@ -32,6 +32,7 @@ class FastaSource:
         engine.check_empty_names(self.parsed, k)
         self.n_kmers = engine.count_kmers(self.parsed, k, rc)
         self._km = {}  # want_pos -> engine.Kmers (stream order)
+        phases.mark("count_kmers")
 
     # ------------------------------------------------------------ extraction
     def kmers(self, want_pos: bool):

@@ -92,11 +92,40 @@ def test_dist_shards_match_oracle(G, mode, k, name):
         _close(pipes)
 
 
+# the finish kernels a round can run: the product uniq finish (early count
+# unchecked, KMAN_RG_CHECK=0: what bench.py and the CLI run), the checked one
+# the GPU session defaults to, and the LSD passes every region takes when a
+# bucket is large (KMAN_RG_LSD=1 forces them everywhere)
+FINISH_VARIANTS = {"plain": {"KMAN_RG_CHECK": "0"}, "checked": {"KMAN_RG_CHECK": "1"},
+                   "lsd": {"KMAN_RG_CHECK": "1", "KMAN_RG_LSD": "1"}}
+
+
+@pytest.mark.parametrize("variant", sorted(FINISH_VARIANTS))
+@pytest.mark.parametrize("G", [1, 3])
+@pytest.mark.parametrize("mode", ["count", "uniq"])
+@pytest.mark.parametrize("name", ["synth", "messy"])
+def test_dist_finish_variants(monkeypatch, variant, G, mode, name):
+    for k_, v_ in FINISH_VARIANTS[variant].items():
+        monkeypatch.setenv(k_, v_)
+    text = _texts()[name]
+    outs, pipes, _ = _run(text, 21, mode, G)
+    try:
+        wk, wv = _oracle(text, 21, mode)
+        for keys, vals in outs:
+            np.testing.assert_array_equal(keys, wk)
+            np.testing.assert_array_equal(vals, wv)
+    finally:
+        _close(pipes)
+
+
+@pytest.mark.parametrize("variant", ["plain", "checked"])
 @pytest.mark.parametrize("G", [2, 8])
 @pytest.mark.parametrize("mode", ["count", "uniq"])
-def test_dist_streamed_rounds(G, mode):
+def test_dist_streamed_rounds(monkeypatch, variant, G, mode):
     """R >= 3 key rounds forced by a small per-round budget: each rank's
     rounds append its key range in order."""
+    for k_, v_ in FINISH_VARIANTS[variant].items():
+        monkeypatch.setenv(k_, v_)
     text = _texts()["synth"]
     outs, pipes, _ = _run(text, 21, mode, G, max_round_items=120_000 // G)
     try:

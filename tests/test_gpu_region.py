@@ -73,13 +73,16 @@ def _groups(dev, text, k, rc, mode):
 @pytest.mark.parametrize("k", [5, 9, 13, 21, 25])
 @pytest.mark.parametrize("rc", [False, True])
 @pytest.mark.parametrize("mode", ["count", "uniq"])
-@pytest.mark.parametrize("check", ["0", "1"])
+@pytest.mark.parametrize("check", ["0", "1", "lsd"])
 def test_groups_matches_oracle(dev, golden_inputs, monkeypatch, k, rc, mode, check):
     """(check: the uniq finish without / with the early-count device check,
-    the product default and the GPU test session's setting)"""
+    the product default and the GPU test session's setting; lsd: every region
+    through the finish's LSD passes, which regions with a large bucket take)"""
     from kman_amd import _native as N
 
-    monkeypatch.setenv("KMAN_RG_CHECK", check)
+    monkeypatch.setenv("KMAN_RG_CHECK", "1" if check == "lsd" else check)
+    if check == "lsd":
+        monkeypatch.setenv("KMAN_RG_LSD", "1")
 
     for text in _texts(golden_inputs):
         n_bases = sum(len(s) for _, s in __import__("np_oracle").parse_fasta(text))
@@ -108,8 +111,9 @@ def test_groups_matches_oracle(dev, golden_inputs, monkeypatch, k, rc, mode, che
 @pytest.mark.parametrize("mode", ["count", "uniq"])
 @pytest.mark.parametrize("copies", [3, 100, 1000])
 def test_groups_repeats(dev, mode, copies):
-    """Repeated segments: equal keys share a finish bin; past BINMAX (64)
-    the region takes the in-kernel LSD passes instead of the bin sort."""
+    """Repeated segments: equal keys share a finish bucket; past BIGB (16)
+    items in one bucket the region takes the in-kernel LSD passes instead of
+    the bucket sort."""
     import inputs
 
     rng = np.random.default_rng(copies)
@@ -193,13 +197,18 @@ def test_pipeline_region_equals_split(dev, mode, rc):
     np.testing.assert_array_equal(outs[0][3], outs[1][3])
 
 
-def test_full_size_region(dev):
+@pytest.mark.parametrize("check", ["0", "1"])
+def test_full_size_region(dev, monkeypatch, check):
     """BASELINE config 2 (1 GB synthetic FASTA, k=21) on the region path:
     uniq keys are exactly the count-1 keys of the count run, counts sum to
     the k-mer count, keys strictly increase, the key checksum of the stream
-    is preserved, and every uniq pos decodes (from the codes) to its key."""
+    is preserved, and every uniq pos decodes (from the codes) to its key.
+    check 0: the uniq finish the bench times (no device check of its early
+    row count); 1: the checked one."""
     import inputs
     from kman_amd import engine
+
+    monkeypatch.setenv("KMAN_RG_CHECK", check)
 
     text = inputs.syn_numpy(1_000_000_000, 1)
     pu = engine.ResidentPipeline(dev, text, 21, mode="uniq")
