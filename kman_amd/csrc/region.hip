@@ -76,7 +76,7 @@ constexpr uint64_t FFILL_T = 6144, FFILL_M = 7800;
 #ifdef KMAN_RG_STAMPS
 #define RSTAMP(id, i)                                                                                 \
     do {                                                                                              \
-        if (stp && threadIdx.x == 0) stp[(uint64_t)(id) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+        if (stp && threadIdx.x == 0) stp[(uint64_t)(id) * 16 + (i)] = __builtin_amdgcn_s_memrealtime(); \
     } while (0)
 #else
 #define RSTAMP(id, i) \
@@ -681,7 +681,7 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     if (NARROW) __builtin_amdgcn_s_setprio(0);  // (the sort)
 #ifdef KMAN_RG_STAMPS
     __builtin_amdgcn_s_waitcnt(0);  // (diagnostic build: phase 1 = the wait for the region's items)
-    if (stp && t == 0) stp[(uint64_t)r * 8 + 7] = m;  // (the region's items, beside its phase stamps)
+    if (stp && t == 0) stp[(uint64_t)r * 16 + 15] = m;  // (the region's items, beside its phase stamps)
 #endif
     RSTAMP(r, 1);
 
@@ -1104,7 +1104,7 @@ struct FinishArgs {
     uint32_t nreg;
     uint32_t fsub = 1;  // sub-regions per region (cnt and in indexed per sub-region)
     uint8_t *freg = nullptr;  // per-region overflow flags (the round path), else null
-    int cap = FCAP;  // the finish's region capacity: GCAP (kman_groups) or FCAP (the round path)
+    int cap = FCAP;  // the finish's region capacity: FCAP (kman_groups) or GCAP / FCAP chosen by the round plan
 };
 
 template <int MODE, typename O, int CAP, bool ATOMIC, typename T = uint64_t, int CHK = 0>
@@ -1228,21 +1228,21 @@ void launch_extract_any(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes
 // the spread of per-region times and of the look-back wait, by region size
 int report_finish_stamps(kman_ctx *ctx, uint64_t *st, uint64_t nreg) {
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    std::vector<uint64_t> h(nreg * 8);
+    std::vector<uint64_t> h(nreg * 16);
     HIP_TRY(ctx, hipMemcpy(h.data(), st, h.size() * 8, hipMemcpyDeviceToHost));
     HIP_TRY(ctx, hipFree(st));
     std::vector<double> tot, wait;
     double ph[7] = {0}, sz_t[4] = {0};
     uint64_t n = 0, sz_n[4] = {0}, t0 = ~0ull, t1 = 0;
     for (uint64_t r = 0; r < nreg; r++) {
-        const uint64_t *x = &h[r * 8];
+        const uint64_t *x = &h[r * 16];
         if (!x[0] || !x[5]) continue;
         t0 = x[0] < t0 ? x[0] : t0;
         t1 = x[5] > t1 ? x[5] : t1;
         for (int i = 1; i < 6; i++) ph[i] += (double)(x[i] - x[i - 1]) / 100.0;
         tot.push_back((double)(x[5] - x[0]) / 100.0);
         wait.push_back((double)(x[4] - x[3]) / 100.0);
-        const int b = x[7] < 2048 ? 0 : x[7] < 4096 ? 1 : x[7] < 6144 ? 2 : 3;
+        const int b = x[15] < 2048 ? 0 : x[15] < 4096 ? 1 : x[15] < 6144 ? 2 : 3;
         sz_t[b] += tot.back();
         sz_n[b]++;
         n++;
@@ -1269,15 +1269,15 @@ int report_stamps(kman_ctx *ctx, uint64_t **st, const uint64_t *rows) {
     static const char *names[3] = {"rg_extract", "rg_pass", "rg_finish"};
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     for (int q = 0; q < 3; q++) {
-        std::vector<uint64_t> h(rows[q] * 8);
+        std::vector<uint64_t> h(rows[q] * 16);
         HIP_TRY(ctx, hipMemcpy(h.data(), st[q], h.size() * 8, hipMemcpyDeviceToHost));
         HIP_TRY(ctx, hipFree(st[q]));
-        double sum[8] = {0}, tot = 0;
-        uint64_t n[8] = {0}, nt = 0;
+        double sum[16] = {0}, tot = 0;
+        uint64_t n[16] = {0}, nt = 0;
         for (uint64_t r = 0; r < rows[q]; r++) {
-            const uint64_t *x = &h[r * 8];
+            const uint64_t *x = &h[r * 16];
             int last = 0;
-            for (int i = 1; i < 8; i++)
+            for (int i = 1; i < 15; i++)
                 if (x[i] && x[i - 1]) {
                     sum[i] += (double)(x[i] - x[i - 1]) / 100.0;
                     n[i]++;
@@ -1290,7 +1290,7 @@ int report_stamps(kman_ctx *ctx, uint64_t **st, const uint64_t *rows) {
         }
         fprintf(stderr, "stamps %-10s tiles %8llu  mean us/tile %.2f  phases:", names[q], (unsigned long long)nt,
                 nt ? tot / nt : 0.0);
-        for (int i = 1; i < 8; i++)
+        for (int i = 1; i < 15; i++)
             if (n[i]) fprintf(stderr, " %d:%.2f", i, sum[i] / n[i]);
         fprintf(stderr, "\n");
     }
@@ -1420,8 +1420,8 @@ extern "C" int kman_groups(kman_ctx *ctx, const uint8_t *d_codes, uint64_t n_bas
     const uint64_t stamp_rows[3] = {p.n_tiles0, (uint64_t)p.maxt1 << G1, g.nreg};
     if (getenv("KMAN_RG_STAMPS"))
         for (int q = 0; q < 3; q++) {
-            HIP_TRY(ctx, hipMalloc((void **)&stamps[q], stamp_rows[q] * 64));
-            HIP_TRY(ctx, hipMemsetAsync(stamps[q], 0, stamp_rows[q] * 64, ctx->stream));
+            HIP_TRY(ctx, hipMalloc((void **)&stamps[q], stamp_rows[q] * 128));
+            HIP_TRY(ctx, hipMemsetAsync(stamps[q], 0, stamp_rows[q] * 128, ctx->stream));
         }
     uint32_t epoch, *counter;
     // pass 0: extraction by the top 8 bits
@@ -1996,8 +1996,8 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     uint64_t *fst = nullptr;
 #ifdef KMAN_RG_STAMPS
     if (getenv("KMAN_RG_STAMPS")) {
-        HIP_TRY(ctx, hipMalloc((void **)&fst, d.nreg * 64));
-        HIP_TRY(ctx, hipMemsetAsync(fst, 0, d.nreg * 64, ctx->stream));
+        HIP_TRY(ctx, hipMalloc((void **)&fst, d.nreg * 128));
+        HIP_TRY(ctx, hipMemsetAsync(fst, 0, d.nreg * 128, ctx->stream));
     }
 #endif
     if (d.g == 0) {

@@ -93,11 +93,9 @@ def test_dist_shards_match_oracle(G, mode, k, name):
 
 
 # the finish kernels a round can run: the product uniq finish (early count
-# unchecked, KMAN_RG_CHECK=0: what bench.py and the CLI run), the checked one
-# the GPU session defaults to, and the LSD passes every region takes when a
-# bucket is large (KMAN_RG_LSD=1 forces them everywhere)
-FINISH_VARIANTS = {"plain": {"KMAN_RG_CHECK": "0"}, "checked": {"KMAN_RG_CHECK": "1"},
-                   "lsd": {"KMAN_RG_CHECK": "1", "KMAN_RG_LSD": "1"}}
+# unchecked, KMAN_RG_CHECK=0: what bench.py and the CLI run) and the checked
+# one the GPU session defaults to
+FINISH_VARIANTS = {"plain": {"KMAN_RG_CHECK": "0"}, "checked": {"KMAN_RG_CHECK": "1"}}
 
 
 @pytest.mark.parametrize("variant", sorted(FINISH_VARIANTS))

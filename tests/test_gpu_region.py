@@ -73,16 +73,13 @@ def _groups(dev, text, k, rc, mode):
 @pytest.mark.parametrize("k", [5, 9, 13, 21, 25])
 @pytest.mark.parametrize("rc", [False, True])
 @pytest.mark.parametrize("mode", ["count", "uniq"])
-@pytest.mark.parametrize("check", ["0", "1", "lsd"])
+@pytest.mark.parametrize("check", ["0", "1"])
 def test_groups_matches_oracle(dev, golden_inputs, monkeypatch, k, rc, mode, check):
     """(check: the uniq finish without / with the early-count device check,
-    the product default and the GPU test session's setting; lsd: every region
-    through the finish's LSD passes, which regions with a large bucket take)"""
+    the product default and the GPU test session's setting)"""
     from kman_amd import _native as N
 
-    monkeypatch.setenv("KMAN_RG_CHECK", "1" if check == "lsd" else check)
-    if check == "lsd":
-        monkeypatch.setenv("KMAN_RG_LSD", "1")
+    monkeypatch.setenv("KMAN_RG_CHECK", check)
 
     for text in _texts(golden_inputs):
         n_bases = sum(len(s) for _, s in __import__("np_oracle").parse_fasta(text))
@@ -111,9 +108,8 @@ def test_groups_matches_oracle(dev, golden_inputs, monkeypatch, k, rc, mode, che
 @pytest.mark.parametrize("mode", ["count", "uniq"])
 @pytest.mark.parametrize("copies", [3, 100, 1000])
 def test_groups_repeats(dev, mode, copies):
-    """Repeated segments: equal keys share a finish bucket; past BIGB (16)
-    items in one bucket the region takes the in-kernel LSD passes instead of
-    the bucket sort."""
+    """Repeated segments: runs of equal keys inside a finish region (and, at
+    1000 copies, a region past its capacity: the general path)."""
     import inputs
 
     rng = np.random.default_rng(copies)
