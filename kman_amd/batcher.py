@@ -203,7 +203,7 @@ class FastaBatcher(BatcherThreading):
             n = src.n_kmers
             self.feed_collection([Batch.from_source(src, 0, n, max(1, n), self.tmp)], feedMode)
             return self
-        src = FastaSource(dev, engine.read_input(fasta), k, self.doReverseComplement)
+        src = FastaSource(dev, None, k, self.doReverseComplement, path=fasta)
         self.source = src
         for name in src.parsed.names:
             logging.info("Batching record '%s'..." % name.decode("utf-8", "surrogateescape"))

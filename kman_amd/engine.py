@@ -82,33 +82,30 @@ class Device:
             )
         self.ctx = ctx.value
         self.index = device
-        self._fmt = None  # (cap, pinned stages, device slices) of the pipelined writer
+        self._fmt = None  # (cap, pinned stages) of the pipelined writer and the file loader
         phases.mark("device_init")
 
-    def fmt_buffers(self, cap: int, nb: int):
-        """The pipelined writer's nb pinned host stages and nb device text
-        slices of >= cap bytes, kept across calls (a pinned allocation of a
-        few hundred MB costs tens of ms: per call it was a large part of a
-        bounded write)."""
+    def pinned_stages(self, cap: int, nb: int):
+        """nb pinned host stages of >= cap bytes, kept across calls (a pinned
+        allocation of a few hundred MB costs tens of ms: per call it was a
+        large part of a bounded write): the pipelined writer's D2H stages and
+        the chunked file loader's H2D stages.  Device memory is not held."""
         if self._fmt is not None and self._fmt[0] >= cap and len(self._fmt[1]) >= nb:
-            return self._fmt[1], self._fmt[2]
+            return self._fmt[1]
         self._free_fmt()
         L = N.lib()
-        stages, dbufs = [], []
+        stages = []
         try:
             for _ in range(nb):
                 hp = c_void_p()
                 N.check(self.ctx, L.kman_host_alloc(self.ctx, byref(hp), cap), "kman_host_alloc")
                 stages.append(hp)
-                dbufs.append(self.alloc(cap))
         except Exception:
             for hp in stages:
                 L.kman_host_free(self.ctx, hp)
-            for b in dbufs:
-                b.free()
             raise
-        self._fmt = (cap, stages, dbufs)
-        return stages, dbufs
+        self._fmt = (cap, stages)
+        return stages
 
     def _free_fmt(self) -> None:
         if self._fmt is not None and self.ctx:
@@ -116,8 +113,6 @@ class Device:
             L.kman_copy_sync(self.ctx)
             for hp in self._fmt[1]:
                 L.kman_host_free(self.ctx, hp)
-            for b in self._fmt[2]:
-                b.free()
         self._fmt = None
 
     def close(self) -> None:
@@ -235,6 +230,76 @@ def parse(dev: Device, text: bytes) -> Parsed:
     finally:
         d_text.free()
     names = [_title_name(text, int(h)) for h in rec_hdr]
+    name_off = np.zeros(R + 1, dtype=np.uint64)
+    if R:
+        name_off[1:] = np.cumsum([len(x) for x in names], dtype=np.uint64)
+    phases.mark("parse")
+    return Parsed(dev, codes, int(info.n_bases), R, rec_hdr, rec_seq, names, b"".join(names), name_off)
+
+
+def parse_file(dev: Device, path: str) -> Parsed:
+    """kman_parse_fasta of a FASTA file (batcher.py:480 reads it whole).  A
+    plain file is read in _FMT_SLICE chunks straight into two pinned stages,
+    each chunk's H2D (on the copy stream) running while the next chunk is
+    read, so the text crosses host memory once and no pageable copy is made;
+    the record names come from the file's header lines (mmap).  Gzip input
+    is inflated into memory and parsed from there (read_input + parse)."""
+    if path.endswith(".gz"):
+        return parse(dev, read_input(path))
+    import mmap
+
+    L = N.lib()
+    with open(path, "rb", buffering=0) as fh:
+        n = os.fstat(fh.fileno()).st_size
+        if n == 0:
+            raise AssertionError("premature end of file or empty file")
+        d_text = dev.alloc(n + 64)
+        codes = dev.alloc(n + 64)
+        try:
+            stages = dev.pinned_stages(_FMT_SLICE + 16, 2)
+            at, i = 0, 0
+            while at < n:
+                b, m = i % 2, min(_FMT_SLICE, n - at)
+                mv = memoryview((ctypes.c_char * m).from_address(stages[b].value)).cast("B")
+                got = 0
+                while got < m:
+                    r = fh.readinto(mv[got:])
+                    if not r:
+                        raise OSError("%s: short read at byte %d of %d" % (path, at + got, n))
+                    got += r
+                # the chunk before this one is out of its stage (and stage b's
+                # previous chunk long since): then this chunk's copy is queued
+                N.check(dev.ctx, L.kman_copy_sync(dev.ctx), "kman_copy_sync")
+                N.check(dev.ctx, L.kman_copy_h2d_async(dev.ctx, c_void_p(d_text.ptr + at), stages[b], m, b),
+                        "kman_copy_h2d_async")
+                at += m
+                i += 1
+            N.check(dev.ctx, L.kman_copy_sync(dev.ctx), "kman_copy_sync")
+            phases.mark("file_read+h2d")
+            cap = n // 2 + 1
+            d_hdr = dev.alloc(8 * cap)
+            d_seq = dev.alloc(8 * cap)
+            try:
+                info = N.ParseInfo()
+                N.check(dev.ctx, L.kman_parse_fasta(dev.ctx, c_void_p(d_text.ptr), n, c_void_p(codes.ptr),
+                                                    c_void_p(d_hdr.ptr), c_void_p(d_seq.ptr), cap, byref(info)),
+                        "kman_parse_fasta")
+                R = int(info.n_records)
+                rec_hdr = dev.download(d_hdr, R, np.uint64)
+                rec_seq = dev.download(d_seq, R, np.uint64)
+            finally:
+                d_hdr.free()
+                d_seq.free()
+        except BaseException:
+            codes.free()
+            raise
+        finally:
+            d_text.free()
+        mm = mmap.mmap(fh.fileno(), 0, access=mmap.ACCESS_READ)
+        try:
+            names = [_title_name(mm, int(h)) for h in rec_hdr]
+        finally:
+            mm.close()
     name_off = np.zeros(R + 1, dtype=np.uint64)
     if R:
         name_off[1:] = np.cumsum([len(x) for x in names], dtype=np.uint64)
@@ -502,12 +567,14 @@ def groups(p: Parsed, k: int, rc: bool, mode: str, canonical: bool = False, mixe
     work = dev.alloc(int(wb.value))
     okeys = dev.alloc(8 * cap)
     ovals = dev.alloc(vb * cap)
+    phases.mark("groups_alloc")
     nk, no = c_uint64(0), c_uint64(0)
     try:
         rc_ = L.kman_groups(dev.ctx, c_void_p(p.codes.ptr), p.n_bases, k, flags, m, c_void_p(work.ptr), wb.value,
                             c_void_p(okeys.ptr), c_void_p(ovals.ptr), vb, byref(nk), byref(no))
     finally:
         work.free()
+    phases.mark("groups_kernels")
     if rc_ == N.KMAN_EFALLBACK:
         okeys.free()
         ovals.free()
@@ -757,6 +824,13 @@ def format_fasta(keys: np.ndarray, pos: np.ndarray, k: int, p: Parsed) -> bytes:
 _FMT_CHUNK = 1 << 31
 _FMT_SLICE = 256 << 20  # text bytes per pipelined slice (_format_dev)
 _FMT_THREADS = int(os.environ.get("KMAN_FMT_THREADS", "8"))  # host copy threads
+# the format kernels write the pinned stages directly (zero-copy over PCIe)
+# instead of a device slice + a copy-engine D2H: the copy engine ran a fresh
+# process's first ~2 s at ~31 GB/s (8.2 ms per 256 MiB slice, then 4.2 once
+# warm), the kernels' own writes reach ~54 GB/s from the first slice
+# (tools/fmtcold.py: 49 GB of uniq text 1.02 s cold vs 1.76; warm 0.92 vs
+# 0.88).  KMAN_FMT_ZC=0: the copy-engine pipeline.
+_FMT_ZC = os.environ.get("KMAN_FMT_ZC", "1") != "0"
 
 
 def _pwrite_target(sink):
@@ -784,12 +858,13 @@ def _format_dev(dev: Device, n: int, row_bytes: int, call, sink=None):
     Returns the text (a bytearray), or, with a sink (a binary file), writes
     it there and returns None.
 
-    Pipelined over slices of <= _FMT_SLICE text bytes, two of everything:
-    slice i is formatted on the device while slice i - 1 crosses PCIe on the
-    copy stream into a pinned stage (kman_copy_d2h_async) and slice i - 2 is
-    copied out of its stage by a pool of host threads -- pwrite at its file
-    offset, or memmove into the result -- so the device, the copy engine and
-    the host copies run at once instead of one after another."""
+    Pipelined over slices of <= _FMT_SLICE text bytes through two pinned
+    stages: the format kernel writes slice i straight into stage i % 2 over
+    PCIe (_FMT_ZC, the default) while a pool of host threads copies slice
+    i - 1 out of the other stage -- pwrite at its file offset, or memmove
+    into the result.  (KMAN_FMT_ZC=0: slice i formatted into a device slice
+    while slice i - 1 crosses PCIe on the copy stream, kman_copy_d2h_async,
+    and slice i - 2 leaves its stage.)"""
     if n == 0:
         return None if sink is not None else bytearray()
     import concurrent.futures as cf
@@ -808,8 +883,13 @@ def _format_dev(dev: Device, n: int, row_bytes: int, call, sink=None):
     else:
         fd, base = _pwrite_target(sink)
     NB = 2
-    stages, dbufs = dev.fmt_buffers(cap, NB)
+    stages = dev.pinned_stages(max(cap, _FMT_SLICE + 16), NB)
+    # (the device text slices live for this call only: held across calls
+    # they would hide 2 x 256 MiB from later mem_info-based plans)
+    dbufs = [] if _FMT_ZC else [dev.alloc(cap) for _ in range(NB)]
+    phases.mark("fmt_buffers")
     pool = cf.ThreadPoolExecutor(max_workers=_FMT_THREADS)
+    wpool = cf.ThreadPoolExecutor(max_workers=1)
     try:
         pending = [[] for _ in range(NB)]
         piece = max(1 << 20, cap // _FMT_THREADS + 1)
@@ -833,28 +913,58 @@ def _format_dev(dev: Device, n: int, row_bytes: int, call, sink=None):
                           for o in range(0, u, piece)]
 
         at, last = 0, None
-        for i, i0 in enumerate(range(0, n, rows)):
-            b = i % NB
-            for f in pending[b]:  # slice i - 2 out of stage b (its D2H finished before)
-                f.result()
-            pending[b] = []
-            m = min(rows, n - i0)
-            N.check(dev.ctx, call(i0, m, c_void_p(dbufs[b].ptr), cap, used), "kman_format_*_dev")
-            u = int(used.value)
-            N.check(dev.ctx, L.kman_copy_d2h_async(dev.ctx, stages[b], c_void_p(dbufs[b].ptr), u, b),
-                    "kman_copy_d2h_async")
+        if _FMT_ZC:
+            # zero-copy: the format kernel writes slice i straight into pinned
+            # stage b over PCIe (no copy engine); the host drains stage b while
+            # slice i + 1 is formatted into the other stage
+            for i, i0 in enumerate(range(0, n, rows)):
+                b = i % NB
+                for f in pending[b]:
+                    f.result()
+                pending[b] = []
+                m = min(rows, n - i0)
+                N.check(dev.ctx, call(i0, m, stages[b], cap, used), "kman_format_*_dev")
+                u = int(used.value)
+                if out is None and fd is None:  # a stream: one writer thread keeps the slices in order
+                    mv = memoryview((ctypes.c_char * u).from_address(stages[b].value)).cast("B")
+                    pending[b] = [wpool.submit(sink.write, mv)]
+                else:
+                    pending[b] = [pool.submit(copy_piece, stages[b].value + o, at + o, min(piece, u - o))
+                                  for o in range(0, u, piece)]
+                if i == 0:
+                    phases.mark("fmt_first_slice")
+                at += u
+            for pb in pending:
+                for f in pb:
+                    f.result()
+        else:
+            for i, i0 in enumerate(range(0, n, rows)):
+                b = i % NB
+                for f in pending[b]:  # slice i - 2 out of stage b (its D2H finished before)
+                    f.result()
+                pending[b] = []
+                m = min(rows, n - i0)
+                N.check(dev.ctx, call(i0, m, c_void_p(dbufs[b].ptr), cap, used), "kman_format_*_dev")
+                u = int(used.value)
+                N.check(dev.ctx, L.kman_copy_d2h_async(dev.ctx, stages[b], c_void_p(dbufs[b].ptr), u, b),
+                        "kman_copy_d2h_async")
+                if last is not None:
+                    drain(*last)
+                    if i == 1:
+                        phases.mark("fmt_first_slice")
+                last = (b, at, u)
+                at += u
             if last is not None:
                 drain(*last)
-            last = (b, at, u)
-            at += u
-        if last is not None:
-            drain(*last)
-        for pb in pending:
-            for f in pb:
-                f.result()
+            for pb in pending:
+                for f in pb:
+                    f.result()
     finally:
         pool.shutdown(wait=True)
+        wpool.shutdown(wait=True)
         N.check(dev.ctx, L.kman_copy_sync(dev.ctx), "kman_copy_sync")
+        for b_ in dbufs:
+            b_.free()
     if out is not None:
         assert at == len(out)
         return out

@@ -25,10 +25,12 @@ from . import engine, phases
 
 
 class FastaSource:
-    def __init__(self, dev: engine.Device, text: bytes, k: int, rc: bool):
+    def __init__(self, dev: engine.Device, text: Optional[bytes], k: int, rc: bool, path: Optional[str] = None):
+        """The k-mer stream of FASTA bytes (`text`), or of the file at `path`
+        (engine.parse_file: chunked pinned reads overlapping the H2D)."""
         engine._check_k(k, wide=True)
         self.dev, self.k, self.rc = dev, k, rc
-        self.parsed = engine.parse(dev, text)
+        self.parsed = engine.parse_file(dev, path) if text is None else engine.parse(dev, text)
         engine.check_empty_names(self.parsed, k)
         self.n_kmers = engine.count_kmers(self.parsed, k, rc)
         self._km = {}  # want_pos -> engine.Kmers (stream order)
