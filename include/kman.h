@@ -74,6 +74,10 @@ extern "C" {
                              * 2k-bit keys (odd multiply, xorshift, odd multiply mod 2^2k), so the top
                              * bits are uniform; the multiset of counts is unchanged -- for abundance
                              * spectra (kman_groups, kman_dshard_*, kman_extract_marked / _range) */
+#define KMAN_ONCE 16u       /* kman_dshard_hist / _extract: the shard is extracted ONCE for all key rounds
+                             * (every window kept; the rounds' items in one buffer, round-major), so
+                             * both use the tiles of a shard that one round takes (16 windows per
+                             * thread, 8 with KMAN_RC); the same flags on both calls */
 /* kman_extract: accumulate d_hist for the passes over bits [b, 2k) only
  * (the prefix passes of kman_split_bits); default b = 0, every bit */
 #define KMAN_HIST_LO(b) (((uint32_t)(b) & 0x7fu) << 8)

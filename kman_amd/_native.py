@@ -34,6 +34,7 @@ KMAN_RC = 1
 KMAN_WANT_POS = 2
 KMAN_CANONICAL = 4
 KMAN_MIXED = 8
+KMAN_ONCE = 16
 KMAN_FINISH_SORT = 0
 KMAN_FINISH_COUNT = 1
 KMAN_FINISH_UNIQ = 2

@@ -623,8 +623,18 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     static_assert(CHK == 0 || MODE == RG_UNIQ, "the early count is uniq's");
     __shared__ __attribute__((aligned(16))) T s[CAP];
     // per-wave digit counters, u16 pairs; words FWORD + lane: where the
-    // lanes without an item add (so every rank atomic is unconditional)
-    __shared__ uint32_t wh[NW_][FWORD + 64];
+    // lanes without an item add (so every rank atomic is unconditional).
+    // TWO (4-byte count items, rest <= 21 bits: the round path's regions):
+    // two passes instead of three -- the first by up to 11 bits on ONE
+    // block-wide counter array (an LSD sort's first pass need not be stable),
+    // the second by up to 10 bits on per-wave counters of 512 words
+#ifdef KMAN_NO_TWO
+    constexpr bool TWO_OK = false;  // (A/B builds: the three-pass finish everywhere)
+#else
+    constexpr bool TWO_OK = NARROW;
+#endif
+    constexpr uint32_t WSTR = TWO_OK ? 512 + 64 : FWORD + 64;
+    __shared__ uint32_t wh[NW_][WSTR];
     __shared__ uint32_t lds_scan[NW_], lds_scan2[NW_];
     __shared__ uint32_t s_tile;
     __shared__ uint64_t s_out;
@@ -688,7 +698,9 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     // stable LSD passes of <= 9 bits.  Ranks: per-wave u16 counters packed two
     // to a word (a wave ranks <= 64 * IPT items), same-word LDS atomics of one
     // wave return in lane order (probed: ATOMIC), else ballot match-any.
-    const uint32_t np = (rest + FBITS - 1) / FBITS;
+    const bool two = TWO_OK && rest >= 2 && rest <= 21;
+    const uint32_t np = two ? 2u : (rest + FBITS - 1) / FBITS;
+    const uint32_t bw_two = rest / 2;  // (two: the stable second pass's bits, <= 10)
     // EARLY (uniq): the region's row count is found after the second-to-last
     // pass, when equal keys already share a run of equal low bits (a run of
     // one item almost always), and published then, so the look-back after the
@@ -703,12 +715,67 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     const bool early = MODE == RG_UNIQ && (!tag_shift || tag_shift + 8 <= 63) && np >= 2;
     uint32_t etot = 0;
     uint32_t at = 0;
-    for (uint32_t p = 0; p < np; p++) {
-        const uint32_t bw = (rest - at + (np - p) - 1) / (np - p);
+    uint32_t p0 = 0;
+    if constexpr (TWO_OK) {
+        if (two) {
+            // the first pass, by the low rest - bw_two bits on one block-wide
+            // counter array (u16 pairs; the waves' adds interleave, so the
+            // pass is not stable, which a first LSD pass need not be)
+            uint32_t *const flat = &wh[0][0];
+            const uint32_t bw = rest - bw_two, dm = (1u << bw) - 1, nwd = 1u << (bw - 1);
+            for (uint32_t q = t; q < nwd; q += NT) flat[q] = 0;
+            __syncthreads();
+            uint32_t rk[IPT];
+#pragma unroll
+            for (int i = 0; i < IPT; i++) {
+                const uint32_t d = (uint32_t)(x[i] >> Q) & dm, hs = (d & 1u) * 16u;
+                rk[i] = pw + i * 64 < m ? (atomicAdd(&flat[d >> 1], 1u << hs) >> hs) & 0xffffu : 0u;
+            }
+            __syncthreads();
+            {
+                // thread t: words 2t, 2t+1 (digits 4t .. 4t+3) -> their starts
+                // (the scan's barrier orders every word read before the writes)
+                const uint32_t c0 = 2 * t < nwd ? flat[2 * t] : 0u, c1 = 2 * t + 1 < nwd ? flat[2 * t + 1] : 0u;
+                const uint32_t a0 = c0 & 0xffffu, a1 = c0 >> 16, a2 = c1 & 0xffffu, a3 = c1 >> 16;
+                const uint32_t ls =
+                    block_exclusive_scan1<NT>(a0 + a1 + a2 + a3, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
+                if (2 * t < nwd) flat[2 * t] = ls | ((ls + a0) << 16);
+                if (2 * t + 1 < nwd) flat[2 * t + 1] = (ls + a0 + a1) | ((ls + a0 + a1 + a2) << 16);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i0 = 0; i0 < IPT; i0 += 4) {
+                uint32_t sl[4];
+#pragma unroll
+                for (int i = i0; i < i0 + 4 && i < IPT; i++) {
+                    const uint32_t d = (uint32_t)(x[i] >> Q) & dm;
+                    sl[i - i0] = ((flat[d >> 1] >> ((d & 1u) * 16u)) & 0xffffu) + rk[i];
+                }
+#pragma unroll
+                for (int i = i0; i < i0 + 4 && i < IPT; i++)
+                    if (pw + i * 64 < m) s[sl[i - i0]] = x[i];
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < IPT; i++)
+                if (pw + i * 64 < m) x[i] = s[pw + i * 64];
+            at = bw;
+            p0 = 1;
+        }
+    }
+    for (uint32_t p = p0; p < np; p++) {
+        const uint32_t bw = two ? bw_two : (rest - at + (np - p) - 1) / (np - p);
         const uint32_t sh = Q + at, dm = (1u << bw) - 1;
         at += bw;
+        // (two: the second pass's per-wave counters, 2^(bw - 1) <= 512 words)
+        const uint32_t nwd = two ? 1u << (bw - 1) : (uint32_t)FWORD;
+        if (TWO_OK && two) {
+            for (uint32_t q = lane; q < nwd; q += 64) wh[w][q] = 0;
+        } else {
 #pragma unroll
-        for (int q = 0; q < FWORD / 64; q++) wh[w][lane + 64 * q] = 0;
+            for (int q = 0; q < FWORD / 64; q++) wh[w][lane + 64 * q] = 0;
+        }
         __builtin_amdgcn_wave_barrier();
         uint32_t rk[IPT];
 #pragma unroll
@@ -739,27 +806,30 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
             }
         }
         __syncthreads();
-        // thread t < FWORD: digits 2t, 2t+1 -> their totals, block scan of the
-        // totals -> digit starts, then each wave's first slot per digit
-        // (digit start + the earlier waves' counts, < 2^16) in place of its
-        // counters, so the scatter reads one word per item
-        uint32_t tlo = 0, thi = 0, cw[NW_];
-        if (t < FWORD) {
+        {
+            // thread t < words: digits 2t, 2t+1 -> their totals, block scan
+            // of the totals -> digit starts, then each wave's first slot per
+            // digit (digit start + the earlier waves' counts, < 2^16) in place
+            // of its counters, so the scatter reads one word per item
+            const uint32_t nw_ = nwd;
+            uint32_t tlo = 0, thi = 0, cw[NW_];
+            if (t < nw_) {
 #pragma unroll
-            for (int ww = 0; ww < NW_; ww++) {
-                cw[ww] = wh[ww][t];
-                tlo += cw[ww] & 0xffffu;
-                thi += cw[ww] >> 16;
+                for (int ww = 0; ww < NW_; ww++) {
+                    cw[ww] = wh[ww][t];
+                    tlo += cw[ww] & 0xffffu;
+                    thi += cw[ww] >> 16;
+                }
             }
-        }
-        const uint32_t ls = block_exclusive_scan1<NT>(tlo + thi, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
-        if (t < FWORD) {
-            uint32_t plo = ls, phi = ls + tlo;
+            const uint32_t ls = block_exclusive_scan1<NT>(tlo + thi, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
+            if (t < nw_) {
+                uint32_t plo = ls, phi = ls + tlo;
 #pragma unroll
-            for (int ww = 0; ww < NW_; ww++) {
-                wh[ww][t] = plo | (phi << 16);
-                plo += cw[ww] & 0xffffu;
-                phi += cw[ww] >> 16;
+                for (int ww = 0; ww < NW_; ww++) {
+                    wh[ww][t] = plo | (phi << 16);
+                    plo += cw[ww] & 0xffffu;
+                    phi += cw[ww] >> 16;
+                }
             }
         }
         __syncthreads();
@@ -1628,7 +1698,9 @@ int make_shard_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t f
     // ones, whose rounds keep 1/R of the windows each (config 4's 12.5 GB:
     // 63.8-64.2 vs 71.8-72.2 ms with 16, `r04aj_tiles_ab.txt`); decided on
     // the common bound, so every rank takes the same
-    const bool wide = n_bases_q <= (4ull << 30);
+    // (KMAN_ONCE: every window of the shard is kept by one extraction for all
+    // rounds, so the 16-window tiles as well)
+    const bool wide = n_bases_q <= (4ull << 30) || (flags & KMAN_ONCE);
     p.ei = p.rc ? (wide ? 8u : 6u) : (wide ? 16u : 12u);
     const uint64_t win = (uint64_t)RT * p.ei;
     p.n_tiles0 = (uint32_t)ceil_div(n_bases ? n_bases : 1, win);

@@ -624,10 +624,16 @@ class DistPipeline:
             self.phase_ms[tag] = self.phase_ms.get(tag, 0.0) + (t - tick[0]) * 1e3
             tick[0] = t
 
+        # once: no exchange (one rank), so the shard is extracted ONCE for all
+        # key rounds, round-major into the output-key buffer, instead of
+        # re-rolled every round (KMAN_ONCE: the same tiles for the histogram)
+        xch = self.exchange and not isinstance(self.comm, LocalComm)
+        once = self.path == "region" and not xch and not self.overlap and os.environ.get("KMAN_DIST_ONCE", "1") != "0"
+        fl = self.flags | (N.KMAN_ONCE if once else 0)
         # 1. (bucket, segment) counts of the shard, bucket totals all-gathered
         H = np.zeros(NB * RS, np.uint32)
         if self.path == "region":
-            N.check(ctx, L.kman_dshard_hist(ctx, c_void_p(sh.codes.ptr), sh.n_eff, self.n_bases_q, self.k, self.flags,
+            N.check(ctx, L.kman_dshard_hist(ctx, c_void_p(sh.codes.ptr), sh.n_eff, self.n_bases_q, self.k, fl,
                                             self.fmode, c_void_p(self.d_hist.ptr), H.ctypes.data_as(c_void_p)),
                     "kman_dshard_hist")
             c_local = H.reshape(NB, RS).sum(axis=1).astype(np.uint64)
@@ -658,6 +664,29 @@ class DistPipeline:
         S_ = self.pieces
         use_ov = (self.path == "region" and self.overlap and R == 1
                   and (a_need + b_need) * (1 + 2.0 / S_) + out_bytes <= self.budget)
+        # once (R > 1): every round's items extracted by one pass into the
+        # output-key buffer, round r's regions (b, s) at x_off[r] + their
+        # round_send offsets.  Round r's rows are written from n_out on, and
+        # n_out + rows <= x_off[r + 1] (a row is a distinct key of the round's
+        # items), so they only ever overwrite rounds already consumed
+        x_off = None
+        if once and R > 1:
+            rtab_all = np.full(NB * RS, np.uint64(0xFFFFFFFFFFFFFFFF), dtype=np.uint64)
+            x_off, off = [], 0
+            for r in range(R):
+                rtab, sc, _ = round_send(H, cuts, G, R, r)
+                m = rtab != np.uint64(0xFFFFFFFFFFFFFFFF)
+                rtab_all[m] = rtab[m] + np.uint64(off)
+                x_off.append(off)
+                off += int(sc.sum())
+            x_off.append(off)
+            if 8 * off > ok_.nbytes:
+                raise RuntimeError("rank %d: %d items exceed the output-key buffer" % (me, off))
+            dev.upload(self.d_rtab, rtab_all)
+            N.check(ctx, L.kman_dshard_extract(ctx, c_void_p(sh.codes.ptr), sh.n_eff, self.n_bases_q, self.k, fl,
+                                               self.fmode, c_void_p(self.d_hist.ptr), c_void_p(self.d_rtab.ptr),
+                                               c_void_p(ok_.ptr)), "kman_dshard_extract")
+            lap("extract")
         for r in range(R):
             if use_ov:
                 got_ = yield from self._overlapped_round(C, cuts, R, r, H, c_local, a_need, b_need, ok_, ov_, n_out, vb)
@@ -667,22 +696,25 @@ class DistPipeline:
                     continue
             if self.path == "region":
                 A, B = self.arena_a.get(a_need), self.arena_b.get(b_need)
-                rtab, sc, so = round_send(H, cuts, G, R, r)
-                dev.upload(self.d_rtab, rtab)
-                # the send buffer is arena A; one rank extracts straight into
-                # its receive buffer B (no exchange at all)
-                xch = self.exchange and not isinstance(self.comm, LocalComm)
-                N.check(ctx, L.kman_dshard_extract(ctx, c_void_p(sh.codes.ptr), sh.n_eff, self.n_bases_q, self.k,
-                                                   self.flags, self.fmode, c_void_p(self.d_hist.ptr),
-                                                   c_void_p(self.d_rtab.ptr), c_void_p((A if xch else B).ptr)),
-                        "kman_dshard_extract")
+                if x_off is None:
+                    rtab, sc, so = round_send(H, cuts, G, R, r)
+                    dev.upload(self.d_rtab, rtab)
+                    # the send buffer is arena A; one rank extracts straight
+                    # into its receive buffer B (no exchange at all)
+                    N.check(ctx, L.kman_dshard_extract(ctx, c_void_p(sh.codes.ptr), sh.n_eff, self.n_bases_q, self.k,
+                                                       fl, self.fmode, c_void_p(self.d_hist.ptr),
+                                                       c_void_p(self.d_rtab.ptr), c_void_p((A if xch else B).ptr)),
+                            "kman_dshard_extract")
+                    rin = B.ptr
+                else:
+                    rin = ok_.ptr + 8 * x_off[r]  # (extracted above, with every round)
                 lo, nb, counts, rcnt, roff = round_recv(C, cuts, R, me, r)
                 lap("extract")
                 if xch:
                     yield ("alltoallv", (A.ptr, sc, so, B.ptr, rcnt, roff, 8))
                     lap("exchange")
                 got = c_uint64(0)
-                ret = L.kman_dround_finish(ctx, c_void_p(B.ptr), self.k, self.flags, self.fmode, G, self.n_bases_q,
+                ret = L.kman_dround_finish(ctx, c_void_p(rin), self.k, self.flags, self.fmode, G, self.n_bases_q,
                                            lo, nb, _u64p(np.ascontiguousarray(counts.reshape(-1))),
                                            c_void_p(A.ptr), A.nbytes, c_void_p(B.ptr), B.nbytes,
                                            c_void_p(ok_.ptr + 8 * n_out), c_void_p(ov_.ptr + vb * n_out), vb,

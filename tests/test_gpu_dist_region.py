@@ -117,13 +117,16 @@ def test_dist_finish_variants(monkeypatch, variant, G, mode, name):
 
 
 @pytest.mark.parametrize("variant", ["plain", "checked"])
-@pytest.mark.parametrize("G", [2, 8])
+@pytest.mark.parametrize("G,once", [(1, "1"), (1, "0"), (2, "1"), (8, "1")])
 @pytest.mark.parametrize("mode", ["count", "uniq"])
-def test_dist_streamed_rounds(monkeypatch, variant, G, mode):
+def test_dist_streamed_rounds(monkeypatch, variant, G, once, mode):
     """R >= 3 key rounds forced by a small per-round budget: each rank's
-    rounds append its key range in order."""
+    rounds append its key range in order.  One rank (no exchange) extracts
+    the shard once for every round into its output-key buffer (KMAN_DIST_ONCE,
+    the default), or round by round (0)."""
     for k_, v_ in FINISH_VARIANTS[variant].items():
         monkeypatch.setenv(k_, v_)
+    monkeypatch.setenv("KMAN_DIST_ONCE", once)
     text = _texts()["synth"]
     outs, pipes, _ = _run(text, 21, mode, G, max_round_items=120_000 // G)
     try:
