@@ -19,7 +19,7 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 # The uniq finish's early row count is checked on the device in every GPU
 # test (KMAN_RG_CHECK=1: each singleton mark against the rows its sorted keys
 # give; a disagreement fails the call).  The check costs 0.25-0.3 ms per 1 GB
-# step (profiles/r04a_check_ab.txt), so the product default is off; tests
+# step (profiles/archive/r04a_check_ab.txt), so the product default is off; tests
 # that pin the default kernel set KMAN_RG_CHECK=0 themselves.
 os.environ.setdefault("KMAN_RG_CHECK", "1")
 
