@@ -1636,41 +1636,84 @@ namespace {
 constexpr uint32_t HIST_BLOCKS_PER_SEG = 32;
 
 // exact (bucket, segment) counts of rg_extract's items: block (j, s) rolls
-// the tiles j, j + J, ... of segment s
+// the tiles j, j + J, ... of segment s.  The counters are lane-private: lane l
+// of every wave adds to column l mod 32 of a [bucket][32] table, so the 32
+// lanes of a ds_add lane group hit 32 distinct banks whatever their buckets
+// (a per-wave [bucket] table takes random buckets: ~3-way bank conflicts and
+// same-address serialisation on every add; A/B: -DKMAN_HIST_WAVE)
 template <int EI, bool RC, int CANON>
 __global__ __launch_bounds__(RT) void rg_hist(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
                                              uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ hist) {
-    constexpr int NT = RT, NWAVE = NT / 64, WIN = NT * EI;
+    constexpr int NT = RT, WIN = NT * EI;
     __shared__ __attribute__((aligned(16))) uint8_t scodes[WIN + 64];
+#ifdef KMAN_HIST_WAVE
+    constexpr int NWAVE = NT / 64;
     __shared__ uint32_t wh[NWAVE][RADIX];
+    const int w = threadIdx.x >> 6;
+#define HSLOT(d) wh[w][d]
+#else
+    __shared__ uint32_t wh[RADIX * 32];
+    const uint32_t col = threadIdx.x & 31u;
+#define HSLOT(d) wh[(d) * 32u + col]
+#endif
     const uint32_t sgi = blockIdx.y;
     const uint32_t t0 = sgi * seg_tiles;
     const uint32_t t1 = t0 + seg_tiles < n_tiles ? t0 + seg_tiles : n_tiles;
-    const int w = threadIdx.x >> 6;
-    for (int i = threadIdx.x; i < NWAVE * RADIX; i += NT) (&wh[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < (int)(sizeof(wh) / 4); i += NT) reinterpret_cast<uint32_t *>(wh)[i] = 0;
     const uint32_t kb = 2u * (uint32_t)k, shift = kb - B1;
     const uint64_t keymask = kb >= 64 ? ~0ull : ((1ull << kb) - 1);
     const uint32_t w0 = threadIdx.x * EI;
-    for (uint32_t t = t0 + blockIdx.x; t < t1; t += gridDim.x) {
+    // the next tile's codes are loaded into registers while this tile rolls:
+    // one 8 KiB tile per block in flight alone leaves the CU ~24 KiB of reads
+    // to hide HBM latency with
+    CodeVecs<NT, EI> cv;
+    uint32_t t = t0 + blockIdx.x;
+    if (t < t1) load_codes<NT, EI>(codes, n_bases, (uint64_t)t * WIN, cv);
+    for (; t < t1; t += gridDim.x) {
         const uint64_t wb = (uint64_t)t * WIN;
         __syncthreads();  // the previous tile's rolls read scodes
-        stage_codes<NT, EI>(codes, n_bases, wb, scodes);
+        store_codes<NT, EI>(cv, codes, n_bases, wb, scodes);
+        if (t + gridDim.x < t1) load_codes<NT, EI>(codes, n_bases, (uint64_t)(t + gridDim.x) * WIN, cv);
         __syncthreads();
+#ifndef KMAN_HIST_FULL
+        if constexpr (!CANON && EI % 4 == 0) {
+            // (only the keys' top bytes: roll_top, a third of the full roll's
+            // VALU work -- the full roll made this kernel VALU-bound)
+            constexpr int A = EI % 16 == 0 ? 16 : (EI % 8 == 0 ? 8 : 4);
+            uint32_t bf[EI], br[EI];
+            const uint32_t valid = roll_top<EI, RC, A>(scodes, (int)w0, k, wb + w0, n_bases, bf, br);
+#pragma unroll
+            for (int j = 0; j < EI; j++) {
+                if ((valid >> j) & 1u) {
+                    atomicAdd(&HSLOT(bf[j]), 1u);
+                    if (RC) atomicAdd(&HSLOT(br[j]), 1u);
+                }
+            }
+            continue;
+        }
+#endif
         uint64_t kf[EI], kr[EI];
         const uint32_t valid = roll<EI, CANON>(scodes, w0, k, keymask, wb + w0, n_bases, kf, kr);
 #pragma unroll
         for (int j = 0; j < EI; j++) {
             if ((valid >> j) & 1u) {
-                atomicAdd(&wh[w][(uint32_t)(kf[j] >> shift)], 1u);
-                if (RC) atomicAdd(&wh[w][(uint32_t)(kr[j] >> shift)], 1u);
+                atomicAdd(&HSLOT((uint32_t)(kf[j] >> shift)), 1u);
+                if (RC) atomicAdd(&HSLOT((uint32_t)(kr[j] >> shift)), 1u);
             }
         }
     }
+#undef HSLOT
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < (uint32_t)RADIX; d += NT) {
         uint32_t c = 0;
+#ifdef KMAN_HIST_WAVE
 #pragma unroll
         for (int ww = 0; ww < NWAVE; ww++) c += wh[ww][d];
+#else
+        // (column (c + d) mod 32: the lanes of a read spread over the banks)
+#pragma unroll 8
+        for (uint32_t q = 0; q < 32; q++) c += wh[d * 32u + ((q + d) & 31u)];
+#endif
         if (c) atomicAdd(&hist[d * RS + sgi], c);
     }
 }
@@ -1830,7 +1873,8 @@ int read_err(kman_ctx *ctx, uint32_t *e) {
 template <int EI, bool RC, int CANON>
 void launch_hist(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                  uint32_t *hist) {
-    const uint32_t gx = p.seg_tiles < HIST_BLOCKS_PER_SEG ? p.seg_tiles : HIST_BLOCKS_PER_SEG;
+    static const uint32_t bps = getenv("KMAN_HIST_GX") ? (uint32_t)atoi(getenv("KMAN_HIST_GX")) : HIST_BLOCKS_PER_SEG;
+    const uint32_t gx = p.seg_tiles < bps ? p.seg_tiles : (bps ? bps : 1u);
     hipLaunchKernelGGL((rg_hist<EI, RC, CANON>), dim3(gx, RS), dim3(RT), 0, ctx->stream, codes, n_bases, (int)k,
                        p.seg_tiles, p.n_tiles0, hist);
 }

@@ -122,3 +122,69 @@ KMAN_RF_HD uint32_t roll_fast(const uint8_t *s, int base, int k, uint64_t mask, 
     }
     return valid;
 }
+
+// Only the top 8 key bits (the region passes' bucket) of each window, and
+// its validity -- what the shard histogram counts: bf[j] = the window's first
+// four codes (the forward key's top byte), br[j] (RC) = the reverse
+// complement's top byte (the complements of its last four codes, the last
+// one highest).  Validity bit-parallel for all EI windows: with y = not-ACGT
+// | record start, window j is bad when code j is not ACGT or any of codes
+// j+1 .. j+k-1 is flagged, an OR over a (k-1)-wide window of y built by
+// doubling (widths 1, 2, 4, 8, 16, then two overlapping ones).  base is a
+// multiple of 4 and of ALIGN (window j starts at code j of the thread's
+// words); k >= 4 (a key of 8 bits or more).
+template <int EI, bool RC, int ALIGN>
+KMAN_RF_HD uint32_t roll_top(const uint8_t *s, int base, int k, uint64_t p0, uint64_t n_bases,
+                             uint32_t (&bf)[EI], uint32_t (&br)[EI]) {
+    static_assert(ALIGN == 4 || ALIGN == 8 || ALIGN == 16, "4-, 8- or 16-byte word reads");
+    static_assert(EI % 4 == 0 && EI <= 16, "windows start at word boundaries, within 64 flag bits");
+    constexpr int NW = (31 + EI + 3) / 4;  // codes 0 .. EI + 30
+    constexpr int AW = ALIGN / 4;
+    uint32_t w[(NW + AW - 1) / AW * AW];
+    const uint32_t *p = reinterpret_cast<const uint32_t *>(s + base);
+#pragma unroll
+    for (int q = 0; q < (NW + AW - 1) / AW; q++) {
+        uint32_t v[AW];
+        __builtin_memcpy(v, __builtin_assume_aligned(p + AW * q, ALIGN), ALIGN);
+#pragma unroll
+        for (int e = 0; e < AW; e++) w[AW * q + e] = v[e];
+    }
+    uint64_t inv = 0, y = 0;
+#pragma unroll
+    for (int i = 0; i < NW; i++) {
+        inv |= (uint64_t)rf_bit4(w[i], 2) << (4 * i);
+        y |= (uint64_t)rf_bit4(w[i] | (w[i] >> 1), 2) << (4 * i);
+    }
+    // forward: codes 0 .. EI + 2 as a big-endian 2-bit stream
+    constexpr int NF = (EI + 3 + 3) / 4;
+    uint64_t be = 0;
+#pragma unroll
+    for (int i = 0; i < NF; i++) be |= (uint64_t)rf_be8(w[i]) << (56 - 8 * i);
+#pragma unroll
+    for (int j = 0; j < EI; j++) bf[j] = (uint32_t)(be >> (56 - 2 * j)) & 0xffu;
+    if constexpr (RC) {
+        // codes 0 .. 63 as a little-endian 2-bit stream le0:le1; window j's
+        // last four codes start at code j + k - 4
+        uint64_t le0 = 0, le1 = 0;
+#pragma unroll
+        for (int i = 0; i < NW; i++) {
+            if (i < 8) le0 |= (uint64_t)rf_le8(w[i]) << (8 * i);
+            else le1 |= (uint64_t)rf_le8(w[i]) << (8 * (i - 8));
+        }
+#pragma unroll
+        for (int j = 0; j < EI; j++) {
+            const int sh = 2 * (j + k - 4);  // 0 .. 86
+            const uint64_t u = sh >= 64 ? le1 >> (sh - 64) : sh ? (le0 >> sh) | (le1 << (64 - sh)) : le0;
+            br[j] = ~(uint32_t)u & 0xffu;
+        }
+    }
+    // windows of width k - 1 over y, one code after each window's first
+    const int wd = k - 1;  // 3 .. 31
+    const uint64_t y2 = y | (y >> 1), y4 = y2 | (y2 >> 2), y8 = y4 | (y4 >> 4), y16 = y8 | (y8 >> 8);
+    const int m = wd >= 16 ? 16 : wd >= 8 ? 8 : wd >= 4 ? 4 : 2;
+    const uint64_t ym = m == 16 ? y16 : m == 8 ? y8 : m == 4 ? y4 : y2;
+    const uint64_t yw = ym | (ym >> (wd - m));
+    uint32_t valid = ~(uint32_t)(inv | (yw >> 1)) & (uint32_t)((1ull << EI) - 1);
+    if (p0 + EI > n_bases) valid &= p0 >= n_bases ? 0u : (uint32_t)((1ull << (n_bases - p0)) - 1);
+    return valid;
+}
