@@ -348,7 +348,7 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
 // loaded (the source rank on N > 1).
 constexpr int R1 = 512;  // pass-1 radix bound
 struct PassArgs {
-    const uint64_t *in;
+    const void *in;  // items of TI (rg_pass's template): 8 bytes, or 4 (narrow count items)
     const uint64_t *seg_base;
     const uint32_t *seg_cnt;
     uint64_t stride;
@@ -357,7 +357,7 @@ struct PassArgs {
     uint32_t tag_div;  // tag = segment index / tag_div
     uint32_t shift, bits;
     uint32_t tag, tag_shift, tag_bits;
-    uint64_t *out;
+    void *out;  // items of TO
     uint64_t C1;
     uint32_t *cnt1;
     // optional: a sub-region that overflows C1 flags the finish regions
@@ -385,15 +385,35 @@ struct PassArgs {
 //     the CU, each written within one tile's store phase (64 KiB of LDS).
 // (512-thread blocks, two per CU, with 64-byte write-combining lines --
 // 32 KiB each -- measured slower: 4.32 vs 3.48 ms)
+// TI / TO: the items read / written, 8 bytes or 4.  Count items whose key
+// bits below this pass's digit fit 32 bits (no window index, no tag: k <= 24
+// after pass 0 + 1's 17 bits) are written as 4 bytes -- the digit and the
+// bits above it are implied by the sub-region -- so the next pass and the
+// finish read half the bytes.
 constexpr int PT_NT = 1024, PT_SI = 8, PT = PT_NT * PT_SI;
-constexpr uint32_t PT_WLB = 4, PT_WL = 1u << PT_WLB;  // items per write-combining line (128 bytes)
+template <typename TI, typename TO>
 __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
                                                    uint32_t *__restrict__ err, uint64_t *__restrict__ stp) {
     constexpr int NT = PT_NT, SI = PT_SI, TILE = PT, NWAVE = NT / 64;
-    constexpr uint32_t WL = PT_WL, WM = WL - 1;
+    // items per write-combining line (128 bytes)
+    constexpr uint32_t WLB = sizeof(TO) == 8 ? 4 : 5, WL = 1u << WLB, WM = WL - 1;
     static_assert(NT >= R1 && NT / WL <= R1, "a thread per digit");
-    __shared__ __attribute__((aligned(16))) uint64_t skeys[TILE];
-    __shared__ uint64_t wcb[R1][WL];  // the pending items of digit d at wcb[d][pos % WL]
+    __shared__ __attribute__((aligned(16))) TI skeys[TILE];
+    __shared__ __attribute__((aligned(16))) uint64_t wcb_[R1 * 16];  // 128 bytes per digit
+    TO(*const wcb)[WL] = reinterpret_cast<TO(*)[WL]>(wcb_);  // the pending items of digit d at wcb[d][pos % WL]
+    // pending items leave 16 lanes per digit (one line per quarter wave), EPL
+    // items per lane: a 4-byte item's lane stores two as one 8-byte store
+    // (its slot j is even and lines are 128-byte aligned)
+    constexpr uint32_t EPL = WL / 16;
+    auto put_pending = [](TO *dst, const TO *src, bool both) {
+        if constexpr (EPL == 2) {
+            if (both) {
+                *reinterpret_cast<uint2 *>(dst) = *reinterpret_cast<const uint2 *>(src);
+                return;
+            }
+        }
+        *dst = *src;
+    };
     // per digit for the store loop: qpar[d] = (q bound of the whole-line
     // items << 32) | the output index of tile item 0 relative to the chain's
     // first sub-region (digit d's sub-region is d * gsub * H after it, and
@@ -440,10 +460,10 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
         const uint64_t reg0 = (uint64_t)(b / pa.gsub) << bits, rsub = b % pa.gsub;
 #define SUBREG(d) (((reg0 | (d)) * pa.gsub + rsub) * H + h)
         // digit d's sub-region is d * dstride items after digit 0's
-        uint64_t *const obase0 = pa.out + SUBREG(0u) * C1;
+        TO *const obase0 = static_cast<TO *>(pa.out) + SUBREG(0u) * C1;
         const uint32_t dstride = pa.gsub * H * (uint32_t)C1;
         const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
-        uint64_t key[SI];
+        TI key[SI];
         uint32_t sgp[(SI + 3) / 4];  // the items' segments, 8 bits each (for the tag)
         auto load_tile = [&](uint32_t rt) {
             const uint32_t tt0 = rt * TILE;
@@ -474,7 +494,9 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
                     }
                 }
                 sgp[i >> 2] |= sg << (8 * (i & 3));
-                key[i] = ib + i * 64 < nn ? pa.in[bs + (li - po)] : 0;
+                // (kept as TI: a 4-byte load zero-extended in the branch
+                // was waited for inside it, one load at a time)
+                key[i] = ib + i * 64 < nn ? static_cast<const TI *>(pa.in)[bs + (li - po)] : (TI)0;
             }
         };
         if (ra < rb) load_tile(ra);
@@ -493,7 +515,7 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
 #pragma unroll
                 for (int i = 0; i < SI; i++) {
                     const uint32_t sg = (sgp[i >> 2] >> (8 * (i & 3))) & 0xffu;
-                    key[i] = (key[i] & ~tm) | ((uint64_t)(sg / pa.tag_div) << pa.tag_shift);
+                    key[i] = (TI)((key[i] & ~tm) | ((uint64_t)(sg / pa.tag_div) << pa.tag_shift));
                 }
             }
 #define PDIGIT(x) ((uint32_t)((x) >> shift) & dmask)
@@ -515,10 +537,11 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
             // (the LDS reads of this loop and the store loop below issued
             // first, back to back: 3.39 vs 3.31 ms, `r04o_pipe_ab.txt`)
 #pragma unroll
-            for (uint32_t d = threadIdx.x >> PT_WLB; d < (uint32_t)R1; d += NT / WL) {
-                const uint32_t j = threadIdx.x & WM, rn = run[d], p = rn & WM;
-                if (j < p && ((rn + thist[d]) >> PT_WLB) > (rn >> PT_WLB) && rn - p + j < C1)
-                    obase0[d * dstride + rn - p + j] = wcb[d][j];
+            for (uint32_t it = 0; it < R1 / (NT / 16); it++) {  // (a constant trip count: unrolled)
+                const uint32_t d = (threadIdx.x >> 4) + it * (NT / 16);
+                const uint32_t j = (threadIdx.x & 15u) * EPL, rn = run[d], p = rn & WM;
+                if (j < p && ((rn + thist[d]) >> WLB) > (rn >> WLB) && rn - p + j < C1)
+                    put_pending(obase0 + d * dstride + rn - p + j, &wcb[d][j], j + 1 < p && rn - p + j + 1 < C1);
             }
             if (threadIdx.x < R1) {
                 // item q of digit d goes to position at = q + off; whole lines
@@ -539,8 +562,8 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
                     const uint32_t d = PDIGIT(kk);
                     const uint64_t qp = qpar[d];
                     const uint32_t rel = (uint32_t)qp + q;
-                    if ((int32_t)q < (int32_t)(qp >> 32)) obase0[rel] = kk;
-                    else wcb[d][rel & WM] = kk;
+                    if ((int32_t)q < (int32_t)(qp >> 32)) obase0[rel] = (TO)kk;
+                    else wcb[d][rel & WM] = (TO)kk;
                 }
             }
             // the next tile's loads behind the stores (issued before the
@@ -556,9 +579,12 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
         __syncthreads();
         // the last partial lines, 16 lanes per digit
 #pragma unroll
-        for (uint32_t d = threadIdx.x >> PT_WLB; d < (uint32_t)R1; d += NT / WL) {
-            const uint32_t j = threadIdx.x & WM, rn = run[d], p = rn & WM;
-            if (j < p && rn - p + j < C1) pa.out[SUBREG(d) * C1 + rn - p + j] = wcb[d][j];
+        for (uint32_t it = 0; it < R1 / (NT / 16); it++) {
+            const uint32_t d = (threadIdx.x >> 4) + it * (NT / 16);
+            const uint32_t j = (threadIdx.x & 15u) * EPL, rn = run[d], p = rn & WM;
+            if (j < p && rn - p + j < C1)
+                put_pending(static_cast<TO *>(pa.out) + SUBREG(d) * C1 + rn - p + j, &wcb[d][j],
+                            j + 1 < p && rn - p + j + 1 < C1);
         }
         if (threadIdx.x < R1) {
             const uint32_t d = threadIdx.x;
@@ -608,7 +634,7 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     uint32_t rc, uint64_t rbase, uint32_t tag_shift, uint32_t fsub, uint64_t *__restrict__ okeys,
     O *__restrict__ ovals, uint64_t *__restrict__ status, uint32_t *__restrict__ counter, uint32_t epoch,
     uint32_t *__restrict__ err, uint32_t hook, uint64_t *__restrict__ stp, uint32_t nreg,
-    uint8_t *__restrict__ freg) {
+    uint8_t *__restrict__ freg, uint32_t in4) {
     constexpr int NT = FT, NW_ = NT / 64;
     constexpr int IPT = (CAP + NT - 1) / NT;  // items per thread
     constexpr bool NARROW = sizeof(T) == 4;
@@ -662,8 +688,17 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     };
     auto load_items = [&](uint32_t rr, uint32_t m0_, uint32_t mm, T (&v)[IPT]) {
         // (a uniform base and one 32-bit offset per item: few address VGPRs)
-        const uint64_t *src = in + (uint64_t)rr * fsub * C1;
         const uint32_t skip = (uint32_t)C1 - m0_;
+        if (NARROW && in4) {  // (4-byte count items from the pass: rg_pass<.., uint32_t>)
+            const uint32_t *src = reinterpret_cast<const uint32_t *>(in) + (uint64_t)rr * fsub * C1;
+#pragma unroll
+            for (int i = 0; i < IPT; i++) {
+                const uint32_t p = pw + i * 64;
+                v[i] = p < mm ? (T)src[p < m0_ ? p : p + skip] : (T)0;
+            }
+            return;
+        }
+        const uint64_t *src = in + (uint64_t)rr * fsub * C1;
 #pragma unroll
         for (int i = 0; i < IPT; i++) {
             const uint32_t p = pw + i * 64;
@@ -1159,9 +1194,20 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     return KMAN_OK;
 }
 
-void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint64_t *stp) {
-    const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, (const void *)rg_pass, PT_NT, (uint64_t)pa.nbk * pa.H);
-    hipLaunchKernelGGL(rg_pass, dim3(grid), dim3(PT_NT), 0, ctx->stream, pa, counter, ctx->d_err, stp);
+template <typename TI, typename TO>
+void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint64_t *stp) {
+    const uint32_t grid =
+        (uint32_t)kman_persistent_grid(ctx, (const void *)rg_pass<TI, TO>, PT_NT, (uint64_t)pa.nbk * pa.H);
+    hipLaunchKernelGGL((rg_pass<TI, TO>), dim3(grid), dim3(PT_NT), 0, ctx->stream, pa, counter, ctx->d_err, stp);
+}
+
+// in4 / out4: the pass reads / writes 4-byte items (out4 only when every key
+// bit below the digit fits 32 bits: pa.shift <= 32, and no tag)
+void launch_pass(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint64_t *stp, bool in4 = false,
+                 bool out4 = false) {
+    if (in4) launch_pass_as<uint32_t, uint32_t>(ctx, pa, counter, stp);
+    else if (out4) launch_pass_as<uint64_t, uint32_t>(ctx, pa, counter, stp);
+    else launch_pass_as<uint64_t, uint64_t>(ctx, pa, counter, stp);
 }
 
 struct FinishArgs {
@@ -1175,6 +1221,7 @@ struct FinishArgs {
     uint32_t fsub = 1;  // sub-regions per region (cnt and in indexed per sub-region)
     uint8_t *freg = nullptr;  // per-region overflow flags (the round path), else null
     int cap = FCAP;  // the finish's region capacity: FCAP (kman_groups) or GCAP / FCAP chosen by the round plan
+    bool in4 = false;  // 4-byte items (the pass wrote them narrow: only with the narrow finish, narrow_ok)
 };
 
 template <int MODE, typename O, int CAP, bool ATOMIC, typename T = uint64_t, int CHK = 0>
@@ -1182,7 +1229,7 @@ void launch_finish_as(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void 
                       uint32_t *counter, uint32_t hook, uint64_t *stp) {
     hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, T, CHK, CAP>), dim3(f.nreg), dim3(FT), 0, ctx->stream, f.in, f.C1,
                        f.cnt, f.Q, f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status,
-                       counter, epoch, ctx->d_err, hook, stp, f.nreg, f.freg);
+                       counter, epoch, ctx->d_err, hook, stp, f.nreg, f.freg, (uint32_t)f.in4);
 }
 
 // The early-count check of the uniq finish (rg_finish CHK): KMAN_RG_CHECK=1
@@ -1204,11 +1251,17 @@ EarlyCheck early_check() {
 // shard 84.7 -> 78.3 ms).  Without the probed lane-ordered LDS atomics the
 // ranks are ballots (8-byte items: the ballot ranks overflow the 80 VGPRs of
 // three blocks per CU -- 2.5 KB of spills per lane -- so no narrow variant).
+// the narrow (4-byte) count finish's condition -- also when the pass before
+// it writes 4-byte items (FinishArgs::in4)
+bool narrow_ok(const kman_ctx *ctx, int mode, uint32_t Q, uint32_t rest, uint32_t tag_shift) {
+    return mode == KMAN_FINISH_COUNT && ctx->lds_atomic_ordered && rest <= 32 && Q == 0 && tag_shift == 0;
+}
+
 template <int MODE, typename O, int CAP>
 void launch_finish(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ovals, uint32_t epoch,
                    uint32_t *counter, uint64_t *stp) {
     if constexpr (MODE == RG_COUNT) {
-        if (ctx->lds_atomic_ordered && f.rest <= 32 && f.Q == 0 && f.tag_shift == 0) {
+        if (narrow_ok(ctx, KMAN_FINISH_COUNT, f.Q, f.rest, f.tag_shift)) {
             launch_finish_as<MODE, O, CAP, true, uint32_t>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
             return;
         }
@@ -1423,6 +1476,9 @@ int groups_tail(kman_ctx *ctx, const GroupsCall &g, int mode, uint64_t *d_okeys,
     const RegionPlan &p = g.p;
     uint32_t epoch, *counter;
     KMAN_TRY(kman_lookback_begin(ctx, 1, &epoch, &counter));  // (the chain counter only)
+    // count items leave pass 1 as 4 bytes when the narrow finish takes them
+    // (KMAN_WIDE_ITEMS=1: 8 bytes, for A/B)
+    const bool narrow4 = narrow_ok(ctx, mode, p.Q, p.rest, 0) && !getenv("KMAN_WIDE_ITEMS");
     {
         KTimer kt_(ctx, "region_pass");
         PassArgs pa{};
@@ -1439,12 +1495,13 @@ int groups_tail(kman_ctx *ctx, const GroupsCall &g, int mode, uint64_t *d_okeys,
         pa.out = g.r1;
         pa.C1 = p.C1h;
         pa.cnt1 = g.c1;
-        launch_pass(ctx, pa, counter, stamps[1]);
+        launch_pass(ctx, pa, counter, stamps[1], false, narrow4);
         HIP_TRY(ctx, hipGetLastError());
     }
     {
         FinishArgs f{g.r1, p.C1h, g.c1, p.Q, p.rest, (uint32_t)p.rc, 0, 0, g.nreg};
         f.fsub = p.H;
+        f.in4 = narrow4;
         KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, stamps[2]));
     }
     if (stamps[0]) KMAN_TRY(report_stamps(ctx, stamps, stamp_rows));
@@ -2080,6 +2137,9 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     HIP_TRY(ctx, hipMemsetAsync(c1, 0, d.nsub * 4, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(freg, 0, d.nreg, ctx->stream));
     uint32_t epoch, *counter;
+    // 4-byte count items out of pass 1 when the key bits below its digit
+    // (rest + g, whatever refit_g makes of the split) fit 32 bits
+    const bool narrow1 = narrow_ok(ctx, mode, d.Q, d.K - B1 - 9, 0) && !getenv("KMAN_WIDE_ITEMS");
     // pass 1: by the 9 bits below the bucket, H chains per (b, src) into
     // sub-regions (b, d, src, h)
     {
@@ -2101,7 +2161,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         pa.fail = freg;  // sub-region (b, d, src, h) -> flag (b, d) (spread over its 2^g regions below)
         pa.fail_div = G * d.H;
         pa.fail_shift = 0;
-        launch_pass(ctx, pa, counter, nullptr);
+        launch_pass(ctx, pa, counter, nullptr, false, narrow1);
         HIP_TRY(ctx, hipGetLastError());
     }
     KMAN_TRY(rg_check(ctx, "pass 1", c1, d.nsub));
@@ -2121,11 +2181,15 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         FinishArgs f{r1, d.C1s, c1, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << 9, 0u, (uint32_t)d.nreg};
         f.fsub = d.H;
         f.freg = freg;
+        f.in4 = narrow1;
         f.cap = d.cap;
         KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, fst));
     } else {
     // (c2 may lie in the receive buffer: cleared only once pass 1 has read it)
     HIP_TRY(ctx, hipMemsetAsync(c2, 0, d.nreg * 4, ctx->stream));
+    // pass 1b's items: 4 bytes out when the narrow finish takes them (always
+    // when pass 1's were: rest <= rest + g)
+    const bool narrow1b = narrow1 || (narrow_ok(ctx, mode, d.Q, d.rest, 0) && !getenv("KMAN_WIDE_ITEMS"));
     // pass 1b: per (b, d), its 2G sub-regions concatenated, by g more bits;
     // the source rank (segment index / 2) goes into the d field
     {
@@ -2152,7 +2216,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         pa.fail = freg;
         pa.fail_div = 1;
         pa.fail_shift = 0;
-        launch_pass(ctx, pa, counter, nullptr);
+        launch_pass(ctx, pa, counter, nullptr, narrow1, narrow1b);
         HIP_TRY(ctx, hipGetLastError());
     }
     KMAN_TRY(rg_check(ctx, "pass 1b", c2, d.nreg));
@@ -2160,6 +2224,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         FinishArgs f{r2, d.C1, c2, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << (9 + d.g),
                      mode == KMAN_FINISH_UNIQ ? d.Q + d.rest + d.g : 0u, (uint32_t)d.nreg};
         f.freg = freg;
+        f.in4 = narrow1b;
         f.cap = d.cap;
         KMAN_TRY(run_finish(ctx, f, mode, d_okeys, d_ovals, oval_bytes, fst));
     }
