@@ -44,6 +44,25 @@ KMAN_RF_HD uint64_t mix_key(uint64_t x, int k) {
     return (x * 0xBF58476D1CE4E5B9ull) & m;
 }
 
+// Validity of windows 0 .. EI-1 starting at codes 0 .. EI-1 (EI <= 16): with
+// inv = not-ACGT flags and y = inv | record-start flags (one bit per code),
+// window j is bad when code j is not ACGT or any of codes j+1 .. j+k-1 is
+// flagged -- an OR over a (k-1)-wide window of y, built by doubling (widths
+// 2, 4, 8, 16, then two overlapping ones); past n_bases nothing is valid.
+// 2 <= k <= 32.
+template <int EI>
+KMAN_RF_HD uint32_t rf_valid_bits(uint64_t inv, uint64_t y, int k, uint64_t p0, uint64_t n_bases) {
+    static_assert(EI <= 16, "windows within the first 64 flag bits");
+    const int wd = k - 1;  // 1 .. 31
+    const uint64_t y2 = y | (y >> 1), y4 = y2 | (y2 >> 2), y8 = y4 | (y4 >> 4), y16 = y8 | (y8 >> 8);
+    const int m = wd >= 16 ? 16 : wd >= 8 ? 8 : wd >= 4 ? 4 : wd >= 2 ? 2 : 1;
+    const uint64_t ym = m == 16 ? y16 : m == 8 ? y8 : m == 4 ? y4 : m == 2 ? y2 : y;
+    const uint64_t yw = ym | (ym >> (wd - m));
+    uint32_t valid = ~(uint32_t)(inv | (yw >> 1)) & (uint32_t)((1ull << EI) - 1);
+    if (p0 + EI > n_bases) valid &= p0 >= n_bases ? 0u : (uint32_t)((1ull << (n_bases - p0)) - 1);
+    return valid;
+}
+
 // ALIGN (16 or 8): s + base is that aligned (base = thread * EI with EI a
 // multiple of it), so the words are read as 16- / 8-byte LDS vectors --
 // with consecutive threads EI bytes apart, ds_read_b128 / ds_read_b64 hit
@@ -117,8 +136,15 @@ KMAN_RF_HD uint32_t roll_fast(const uint8_t *s, int base, int k, uint64_t mask, 
             kf[j] = fwd;
             kr[j] = rc;
         }
-        const bool ok = !((inv >> o) & km) && !((rst >> (o + 1)) & (km >> 1)) && p0 + j < n_bases;
-        valid |= (uint32_t)ok << j;
+        if constexpr (ALIGN == 4 || EI > 16) {
+            const bool ok = !((inv >> o) & km) && !((rst >> (o + 1)) & (km >> 1)) && p0 + j < n_bases;
+            valid |= (uint32_t)ok << j;
+        }
+    }
+    if constexpr (ALIGN > 4 && EI <= 16) {
+        // (window j at code j: the validity of all EI windows bit-parallel,
+        // as roll_top below -- an OR over a (k-1)-wide window of flags)
+        valid = rf_valid_bits<EI>(inv, inv | rst, k, p0, n_bases);
     }
     return valid;
 }
@@ -127,12 +153,9 @@ KMAN_RF_HD uint32_t roll_fast(const uint8_t *s, int base, int k, uint64_t mask, 
 // its validity -- what the shard histogram counts: bf[j] = the window's first
 // four codes (the forward key's top byte), br[j] (RC) = the reverse
 // complement's top byte (the complements of its last four codes, the last
-// one highest).  Validity bit-parallel for all EI windows: with y = not-ACGT
-// | record start, window j is bad when code j is not ACGT or any of codes
-// j+1 .. j+k-1 is flagged, an OR over a (k-1)-wide window of y built by
-// doubling (widths 1, 2, 4, 8, 16, then two overlapping ones).  base is a
-// multiple of 4 and of ALIGN (window j starts at code j of the thread's
-// words); k >= 4 (a key of 8 bits or more).
+// one highest); validity by rf_valid_bits.  base is a multiple of 4 and of
+// ALIGN (window j starts at code j of the thread's words); k >= 4 (a key of
+// 8 bits or more).
 template <int EI, bool RC, int ALIGN>
 KMAN_RF_HD uint32_t roll_top(const uint8_t *s, int base, int k, uint64_t p0, uint64_t n_bases,
                              uint32_t (&bf)[EI], uint32_t (&br)[EI]) {
@@ -178,13 +201,5 @@ KMAN_RF_HD uint32_t roll_top(const uint8_t *s, int base, int k, uint64_t p0, uin
             br[j] = ~(uint32_t)u & 0xffu;
         }
     }
-    // windows of width k - 1 over y, one code after each window's first
-    const int wd = k - 1;  // 3 .. 31
-    const uint64_t y2 = y | (y >> 1), y4 = y2 | (y2 >> 2), y8 = y4 | (y4 >> 4), y16 = y8 | (y8 >> 8);
-    const int m = wd >= 16 ? 16 : wd >= 8 ? 8 : wd >= 4 ? 4 : 2;
-    const uint64_t ym = m == 16 ? y16 : m == 8 ? y8 : m == 4 ? y4 : y2;
-    const uint64_t yw = ym | (ym >> (wd - m));
-    uint32_t valid = ~(uint32_t)(inv | (yw >> 1)) & (uint32_t)((1ull << EI) - 1);
-    if (p0 + EI > n_bases) valid &= p0 >= n_bases ? 0u : (uint32_t)((1ull << (n_bases - p0)) - 1);
-    return valid;
+    return rf_valid_bits<EI>(inv, y, k, p0, n_bases);
 }
