@@ -109,7 +109,7 @@ KMAN_DEV uint32_t ballot_rank(uint32_t *hist, uint32_t d, bool valid, uint32_t b
 // two strands with RC; tile-local (window << 1 | strand) packed above the 2k
 // key bits), LDS-staged coalesced scatter into region (b, s).
 // A tile takes its place in region (b, s) by one atomic add per digit on the
-// region's cursor (cursor[b * RS + s], zeroed before the launch; it ends as the
+// region's cursor (cursor[s * 256 + b], zeroed before the launch; it ends as the
 // region's count), issued right after the rank so its round trip overlaps the
 // digit scan and the LDS scatter.  A region's items are then in no particular
 // order, which nothing downstream needs: pass 1 ranks unstably and the finish
@@ -273,7 +273,10 @@ __global__ __launch_bounds__(RT, (RC ? (EI == 6 ? 6 : 4) : (EI == 12 ? 6 : (EI =
     RSTAMP(tile, 2);
     if (threadIdx.x < R0) {  // the tile's place in each region, claimed now
         const uint32_t c = thist[threadIdx.x];
-        at_base = c ? atomicAdd(cursor + threadIdx.x * RS + sgi, c) : 0u;
+        // (cursor[s * 256 + b]: a wave's 64 adds are 256 contiguous bytes,
+        // which leave L2 as four 64-byte requests to the memory-side atomic
+        // units -- at cursor[b * RS + s] they were 64 requests, one per lane)
+        at_base = c ? atomicAdd(cursor + (uint64_t)sgi * R0 + threadIdx.x, c) : 0u;
     }
     RSTAMP(tile, 3);
     const uint32_t d0 = threadIdx.x;
@@ -351,6 +354,7 @@ struct PassArgs {
     const void *in;  // items of TI (rg_pass's template): 8 bytes, or 4 (narrow count items)
     const uint64_t *seg_base;
     const uint32_t *seg_cnt;
+    uint32_t cnt_sb;  // seg_cnt indexed [segment][bucket] (pass 0's cursors), else [bucket][segment]
     uint64_t stride;
     uint32_t nbk, nsg, gsub, maxt;
     uint32_t H;        // chains (parts) per bucket: outputs are H sub-regions per region
@@ -443,7 +447,7 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
         {
             const uint32_t sgl = (uint32_t)lane;
             const uint64_t gi = (uint64_t)b * nsg + sgl;
-            uint32_t c = sgl < nsg ? pa.seg_cnt[gi] : 0u;
+            uint32_t c = sgl < nsg ? pa.seg_cnt[pa.cnt_sb ? (uint64_t)sgl * pa.nbk + b : gi] : 0u;
             if (!pa.seg_base && c > pa.stride) c = (uint32_t)pa.stride;  // (an overflowed atomic cursor)
             const uint32_t inc = wave_inclusive_scan(c, SumU32());
             spre_l = inc - c;
@@ -1168,6 +1172,10 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     // (3.27 vs 3.35 ms with 12 windows, three blocks per CU; 8, four blocks:
     // 3.83)
     p.ei = p.rc ? 8u : 16u;
+    if (!p.rc && getenv("KMAN_EXTRACT_EI")) {  // (A/B: 12 or 8 windows per thread, three / four blocks per CU)
+        const uint32_t e = (uint32_t)atoi(getenv("KMAN_EXTRACT_EI"));
+        p.ei = e == 12 || e == 8 ? e : 16u;
+    }
     const uint64_t win = (uint64_t)RT * p.ei;
     p.n_tiles0 = (uint32_t)ceil_div(n_bases, win);
     p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, RS);
@@ -1343,6 +1351,8 @@ void launch_extract_any(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes
     if (p.canon && p.mix) launch_extract<16, false, 2>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
     else if (p.canon) launch_extract<16, false, 1>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
     else if (p.rc) launch_extract<8, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
+    else if (p.ei == 12) launch_extract<12, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
+    else if (p.ei == 8) launch_extract<8, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
     else launch_extract<16, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
 }
 
@@ -1485,6 +1495,7 @@ int groups_tail(kman_ctx *ctx, const GroupsCall &g, int mode, uint64_t *d_okeys,
         pa.in = g.r0;
         pa.seg_base = nullptr;
         pa.seg_cnt = g.c0;
+        pa.cnt_sb = 1;  // (rg_extract's cursors: [segment][bucket])
         pa.stride = p.C0;
         pa.nbk = 1u << G1;
         pa.nsg = RS;
