@@ -61,7 +61,11 @@ constexpr uint32_t B1 = 8;        // pass-0 digit: top 8 key bits
 // K items per 1 G k-mers that a GCAP finish holds in 40 KiB -- three blocks
 // per CU -- but the finish's per-region costs dominate there: 5.96 vs 5.62
 // ms, and the 512-bucket pass 0 4.0 vs 3.6 ms)
+#ifndef KMAN_G1
 constexpr uint32_t G1 = B1;
+#else
+constexpr uint32_t G1 = KMAN_G1;  // (A/B builds: pass 0 by 9 bits, pass 1 by 8)
+#endif
 // finish capacities (items): FCAP (68 KiB of 8-byte items, two blocks per
 // CU) and GCAP (40 KiB, three blocks per CU) for the round path's small
 // regions (a pass 1b over many ranks' items leaves ~4 K per region)
@@ -394,16 +398,20 @@ struct PassArgs {
 // after pass 0 + 1's 17 bits) are written as 4 bytes -- the digit and the
 // bits above it are implied by the sub-region -- so the next pass and the
 // finish read half the bytes.
+// NT_ / RB: 1024 threads and digits up to 9 bits (141 KiB of LDS, one block
+// per CU), or 512 threads and up to 8 bits (4096-item tiles and 256 digits'
+// lines, ~69 KiB: two blocks per CU, so one block's loads, rank and scatter
+// run while the other's stores stream)
 constexpr int PT_NT = 1024, PT_SI = 8, PT = PT_NT * PT_SI;
-template <typename TI, typename TO>
-__global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
-                                                   uint32_t *__restrict__ err, uint64_t *__restrict__ stp) {
-    constexpr int NT = PT_NT, SI = PT_SI, TILE = PT, NWAVE = NT / 64;
+template <typename TI, typename TO, int NT_ = PT_NT, int RB = R1>
+__global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
+                                                 uint32_t *__restrict__ err, uint64_t *__restrict__ stp) {
+    constexpr int NT = NT_, SI = PT_SI, TILE = NT * SI, NWAVE = NT / 64;
     // items per write-combining line (128 bytes)
     constexpr uint32_t WLB = sizeof(TO) == 8 ? 4 : 5, WL = 1u << WLB, WM = WL - 1;
-    static_assert(NT >= R1 && NT / WL <= R1, "a thread per digit");
+    static_assert(NT >= RB && NT / WL <= RB, "a thread per digit");
     __shared__ __attribute__((aligned(16))) TI skeys[TILE];
-    __shared__ __attribute__((aligned(16))) uint64_t wcb_[R1 * 16];  // 128 bytes per digit
+    __shared__ __attribute__((aligned(16))) uint64_t wcb_[RB * 16];  // 128 bytes per digit
     TO(*const wcb)[WL] = reinterpret_cast<TO(*)[WL]>(wcb_);  // the pending items of digit d at wcb[d][pos % WL]
     // pending items leave 16 lanes per digit (one line per quarter wave), EPL
     // items per lane: a 4-byte item's lane stores two as one 8-byte store
@@ -422,10 +430,10 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
     // items << 32) | the output index of tile item 0 relative to the chain's
     // first sub-region (digit d's sub-region is d * gsub * H after it, and
     // C1 is a multiple of 16, so the low 4 bits are the line slot)
-    __shared__ uint64_t qpar[R1];
-    __shared__ uint32_t thist[R1];
-    __shared__ uint32_t lstart[R1];
-    __shared__ uint32_t run[R1];  // the chain's running count per digit
+    __shared__ uint64_t qpar[RB];
+    __shared__ uint32_t thist[RB];
+    __shared__ uint32_t lstart[RB];
+    __shared__ uint32_t run[RB];  // the chain's running count per digit
     __shared__ uint32_t lds_scan[NWAVE];
     __shared__ uint32_t s_items;
     __shared__ uint32_t lds_tile;
@@ -454,7 +462,7 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
             sbase_l = sgl < nsg ? (pa.seg_base ? pa.seg_base[gi] : gi * pa.stride) : 0ull;
             if (threadIdx.x == 63) s_items = inc;
         }
-        if (threadIdx.x < R1) run[threadIdx.x] = 0;
+        if (threadIdx.x < RB) run[threadIdx.x] = 0;
         __syncthreads();
         const uint32_t items = s_items;
         const uint32_t tiles = (items + TILE - 1) / TILE;
@@ -507,7 +515,7 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
         for (uint32_t r = ra; r < rb; r++) {
             // (double-buffered counts, so that neither this clear nor the
             // update below needs its barrier: no faster, 3.50 vs 3.41-3.50 ms)
-            if (threadIdx.x < R1) thist[threadIdx.x] = 0;
+            if (threadIdx.x < RB) thist[threadIdx.x] = 0;
             __syncthreads();
             const uint32_t t0 = r * TILE;
             const uint32_t n = items - t0 < (uint32_t)TILE ? items - t0 : (uint32_t)TILE;
@@ -526,9 +534,9 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
 #pragma unroll
             for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < n ? atomicAdd(&thist[PDIGIT(key[i])], 1u) : 0u;
             __syncthreads();
-            const uint32_t ls = block_exclusive_scan1<NT>(threadIdx.x < R1 ? thist[threadIdx.x] : 0u, SumU32(), 0u,
+            const uint32_t ls = block_exclusive_scan1<NT>(threadIdx.x < RB ? thist[threadIdx.x] : 0u, SumU32(), 0u,
                                                           lds_scan, (uint32_t *)nullptr);
-            if (threadIdx.x < R1) lstart[threadIdx.x] = ls;
+            if (threadIdx.x < RB) lstart[threadIdx.x] = ls;
             __syncthreads();
 #pragma unroll
             for (int i = 0; i < SI; i++)
@@ -541,13 +549,13 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
             // (the LDS reads of this loop and the store loop below issued
             // first, back to back: 3.39 vs 3.31 ms, `r04o_pipe_ab.txt`)
 #pragma unroll
-            for (uint32_t it = 0; it < R1 / (NT / 16); it++) {  // (a constant trip count: unrolled)
+            for (uint32_t it = 0; it < RB / (NT / 16); it++) {  // (a constant trip count: unrolled)
                 const uint32_t d = (threadIdx.x >> 4) + it * (NT / 16);
                 const uint32_t j = (threadIdx.x & 15u) * EPL, rn = run[d], p = rn & WM;
                 if (j < p && ((rn + thist[d]) >> WLB) > (rn >> WLB) && rn - p + j < C1)
                     put_pending(obase0 + d * dstride + rn - p + j, &wcb[d][j], j + 1 < p && rn - p + j + 1 < C1);
             }
-            if (threadIdx.x < R1) {
+            if (threadIdx.x < RB) {
                 // item q of digit d goes to position at = q + off; whole lines
                 // end at fe; positions >= C1 are dropped (an overflowing
                 // region raises ERR_REGION, so where its items go is moot)
@@ -575,7 +583,7 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
             // 6.2 vs 4.9 ms; issued right after the LDS scatter: 3.80 vs 3.43)
             if (r + 1 < rb) load_tile(r + 1);
             __syncthreads();  // every read of run[] above before its update
-            if (threadIdx.x < R1) run[threadIdx.x] += thist[threadIdx.x];
+            if (threadIdx.x < RB) run[threadIdx.x] += thist[threadIdx.x];
             RSTAMP(r, 2);
 #undef PDIGIT
         }
@@ -583,14 +591,14 @@ __global__ __launch_bounds__(PT_NT, 4) void rg_pass(PassArgs pa, uint32_t *__res
         __syncthreads();
         // the last partial lines, 16 lanes per digit
 #pragma unroll
-        for (uint32_t it = 0; it < R1 / (NT / 16); it++) {
+        for (uint32_t it = 0; it < RB / (NT / 16); it++) {
             const uint32_t d = (threadIdx.x >> 4) + it * (NT / 16);
             const uint32_t j = (threadIdx.x & 15u) * EPL, rn = run[d], p = rn & WM;
             if (j < p && rn - p + j < C1)
                 put_pending(static_cast<TO *>(pa.out) + SUBREG(d) * C1 + rn - p + j, &wcb[d][j],
                             j + 1 < p && rn - p + j + 1 < C1);
         }
-        if (threadIdx.x < R1) {
+        if (threadIdx.x < RB) {
             const uint32_t d = threadIdx.x;
             if (run[d] > C1 && d < radix) {
                 atomicOr(err, ERR_REGION);
@@ -1162,6 +1170,9 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     // to FFILL_M expected keeps > 10 sd (uniform data) below the capacity
     uint32_t b2 = 1;
     while (b2 < 9 && (p.W >> (G1 + b2)) > FFILL_T) b2++;
+#ifdef KMAN_G1
+    if (G1 + b2 > 17 && (p.W >> 17) <= FFILL_M) b2 = 17 - G1;  // (A/B: the same 2^17 regions as G1 = 8)
+#endif
     if ((p.W >> (G1 + b2)) > FFILL_M) return KMAN_EFALLBACK;
     if (p.K < G1 + b2 + 1) return KMAN_EFALLBACK;
     p.B2 = b2;
@@ -1204,6 +1215,15 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
 
 template <typename TI, typename TO>
 void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint64_t *stp) {
+    // radix <= 256: the 512-thread instance, two blocks per CU (KMAN_PASS_SMALL=0: the 1024-thread one)
+    static const bool small_ok = !getenv("KMAN_PASS_SMALL") || strcmp(getenv("KMAN_PASS_SMALL"), "0") != 0;
+    if (small_ok && pa.bits <= 8) {
+        const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, (const void *)rg_pass<TI, TO, 512, 256>, 512,
+                                                             (uint64_t)pa.nbk * pa.H);
+        hipLaunchKernelGGL((rg_pass<TI, TO, 512, 256>), dim3(grid), dim3(512), 0, ctx->stream, pa, counter,
+                           ctx->d_err, stp);
+        return;
+    }
     const uint32_t grid =
         (uint32_t)kman_persistent_grid(ctx, (const void *)rg_pass<TI, TO>, PT_NT, (uint64_t)pa.nbk * pa.H);
     hipLaunchKernelGGL((rg_pass<TI, TO>), dim3(grid), dim3(PT_NT), 0, ctx->stream, pa, counter, ctx->d_err, stp);
