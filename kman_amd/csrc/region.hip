@@ -477,33 +477,53 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
         const uint32_t ib = (uint32_t)(w * (SI * 64) + lane);
         TI key[SI];
         uint32_t sgp[(SI + 3) / 4];  // the items' segments, 8 bits each (for the tag)
+        auto rl64 = [](uint64_t v, int l) -> uint64_t {
+            return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+                   (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+        };
         auto load_tile = [&](uint32_t rt) {
             const uint32_t tt0 = rt * TILE;
             const uint32_t nn = items - tt0 < (uint32_t)TILE ? items - tt0 : (uint32_t)TILE;
 #pragma unroll
             for (int i = 0; i < (SI + 3) / 4; i++) sgp[i] = 0;
+            // a wave's rows are consecutive items: the segment of its first
+            // row, its base and where the next segment starts, once per tile
+            // (wave-uniform, from readlanes); only a row that reaches the
+            // next segment takes the per-row ballots
+            const uint32_t wfirst = tt0 + (uint32_t)w * (SI * 64);
+            uint32_t c_sg, c_po, c_nx;
+            uint64_t c_bs;
+            auto seg_at = [&](uint32_t li0) {
+                const int s0 = __popcll(__ballot(spre_l <= li0) & ~1ull);  // lane 0 (prefix 0) not counted
+                c_sg = (uint32_t)s0;
+                c_po = (uint32_t)__builtin_amdgcn_readlane((int)spre_l, s0);
+                c_bs = rl64(sbase_l, s0);
+                c_nx = s0 < 63 ? (uint32_t)__builtin_amdgcn_readlane((int)spre_l, s0 + 1) : ~0u;
+            };
+            seg_at(wfirst);
 #pragma unroll
             for (int i = 0; i < SI; i++) {
-                const uint32_t li0 = tt0 + (uint32_t)w * (SI * 64) + (uint32_t)i * 64;
+                const uint32_t li0 = wfirst + (uint32_t)i * 64;
                 const uint32_t li = li0 + (uint32_t)lane;
-                // the row start's segment is wave-uniform: its base and
-                // prefix come from readlanes (scalar), not LDS permutes
-                const int sg0 = __popcll(__ballot(spre_l <= li0) & ~1ull);  // lane 0 (prefix 0) not counted
-                uint32_t sg = (uint32_t)sg0;
-                uint64_t bs = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(sbase_l >> 32), sg0) << 32) |
-                              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sbase_l, sg0);
-                uint32_t po = (uint32_t)__builtin_amdgcn_readlane((int)spre_l, sg0);
-                uint64_t inrow = __ballot(spre_l > li0 && spre_l <= li0 + 63);
-                while (inrow) {  // (wave-uniform)
-                    const int s2 = __ffsll((unsigned long long)inrow) - 1;
-                    inrow &= inrow - 1;
-                    const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)spre_l, s2);
-                    if (li >= p2) {
-                        sg = (uint32_t)s2;
-                        po = p2;
-                        bs = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(sbase_l >> 32), s2) << 32) |
-                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)sbase_l, s2);
+                uint32_t sg = c_sg, po = c_po;
+                uint64_t bs = c_bs;
+                if (li0 + 63 >= c_nx) {  // (wave-uniform, rare: the row reaches the next segment)
+                    const int sg0 = __popcll(__ballot(spre_l <= li0) & ~1ull);
+                    sg = (uint32_t)sg0;
+                    bs = rl64(sbase_l, sg0);
+                    po = (uint32_t)__builtin_amdgcn_readlane((int)spre_l, sg0);
+                    uint64_t inrow = __ballot(spre_l > li0 && spre_l <= li0 + 63);
+                    while (inrow) {  // (wave-uniform)
+                        const int s2 = __ffsll((unsigned long long)inrow) - 1;
+                        inrow &= inrow - 1;
+                        const uint32_t p2 = (uint32_t)__builtin_amdgcn_readlane((int)spre_l, s2);
+                        if (li >= p2) {
+                            sg = (uint32_t)s2;
+                            po = p2;
+                            bs = rl64(sbase_l, s2);
+                        }
                     }
+                    seg_at(li0 + 64);
                 }
                 sgp[i >> 2] |= sg << (8 * (i & 3));
                 // (kept as TI: a 4-byte load zero-extended in the branch
