@@ -61,11 +61,9 @@ constexpr uint32_t B1 = 8;        // pass-0 digit: top 8 key bits
 // K items per 1 G k-mers that a GCAP finish holds in 40 KiB -- three blocks
 // per CU -- but the finish's per-region costs dominate there: 5.96 vs 5.62
 // ms, and the 512-bucket pass 0 4.0 vs 3.6 ms)
-#ifndef KMAN_G1
+// (Round 5, with the cursor adds cheap: 9 + 8 bits measured equal to 8 + 9,
+// `r05xy_pass_geometry_ab.txt`)
 constexpr uint32_t G1 = B1;
-#else
-constexpr uint32_t G1 = KMAN_G1;  // (A/B builds: pass 0 by 9 bits, pass 1 by 8)
-#endif
 // finish capacities (items): FCAP (68 KiB of 8-byte items, two blocks per
 // CU) and GCAP (40 KiB, three blocks per CU) for the round path's small
 // regions (a pass 1b over many ranks' items leaves ~4 K per region)
@@ -377,7 +375,7 @@ struct PassArgs {
 
 // Persistent 1024-thread blocks (one per CU; 141 KiB of LDS), block-owned
 // chains: a block takes a whole chain (bucket b, part h: the h-th of H runs of
-// the bucket's PT-item tiles) and walks its tiles in order, carrying each
+// the bucket's tiles of PT_NT * PT_SI items) and walks its tiles in order, carrying each
 // digit's running count in LDS, so no tile ever waits on another block (no
 // look-back, no status words).  Per tile:
 //   * loads: logical item -> (segment, offset) by ballots over the lanes'
@@ -402,7 +400,7 @@ struct PassArgs {
 // per CU), or 512 threads and up to 8 bits (4096-item tiles and 256 digits'
 // lines, ~69 KiB: two blocks per CU, so one block's loads, rank and scatter
 // run while the other's stores stream)
-constexpr int PT_NT = 1024, PT_SI = 8, PT = PT_NT * PT_SI;
+constexpr int PT_NT = 1024, PT_SI = 8;
 template <typename TI, typename TO, int NT_ = PT_NT, int RB = R1>
 __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
                                                  uint32_t *__restrict__ err, uint64_t *__restrict__ stp) {
@@ -1190,9 +1188,6 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     // to FFILL_M expected keeps > 10 sd (uniform data) below the capacity
     uint32_t b2 = 1;
     while (b2 < 9 && (p.W >> (G1 + b2)) > FFILL_T) b2++;
-#ifdef KMAN_G1
-    if (G1 + b2 > 17 && (p.W >> 17) <= FFILL_M) b2 = 17 - G1;  // (A/B: the same 2^17 regions as G1 = 8)
-#endif
     if ((p.W >> (G1 + b2)) > FFILL_M) return KMAN_EFALLBACK;
     if (p.K < G1 + b2 + 1) return KMAN_EFALLBACK;
     p.B2 = b2;
@@ -1203,10 +1198,6 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     // (3.27 vs 3.35 ms with 12 windows, three blocks per CU; 8, four blocks:
     // 3.83)
     p.ei = p.rc ? 8u : 16u;
-    if (!p.rc && getenv("KMAN_EXTRACT_EI")) {  // (A/B: 12 or 8 windows per thread, three / four blocks per CU)
-        const uint32_t e = (uint32_t)atoi(getenv("KMAN_EXTRACT_EI"));
-        p.ei = e == 12 || e == 8 ? e : 16u;
-    }
     const uint64_t win = (uint64_t)RT * p.ei;
     p.n_tiles0 = (uint32_t)ceil_div(n_bases, win);
     p.seg_tiles = (uint32_t)ceil_div(p.n_tiles0, RS);
@@ -1391,8 +1382,6 @@ void launch_extract_any(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes
     if (p.canon && p.mix) launch_extract<16, false, 2>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
     else if (p.canon) launch_extract<16, false, 1>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
     else if (p.rc) launch_extract<8, true>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
-    else if (p.ei == 12) launch_extract<12, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
-    else if (p.ei == 8) launch_extract<8, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
     else launch_extract<16, false>(ctx, p, codes, n_bases, k, r0, c0, epoch, counter, stp, n_launch);
 }
 
@@ -1747,27 +1736,19 @@ constexpr uint32_t HIST_BLOCKS_PER_SEG = 32;
 // the tiles j, j + J, ... of segment s.  The counters are lane-private: lane l
 // of every wave adds to column l mod 32 of a [bucket][32] table, so the 32
 // lanes of a ds_add lane group hit 32 distinct banks whatever their buckets
-// (a per-wave [bucket] table takes random buckets: ~3-way bank conflicts and
-// same-address serialisation on every add; A/B: -DKMAN_HIST_WAVE)
+// (per-wave [bucket] tables: 4.80 vs 4.36 ms per 12.5 G bases with roll_top,
+// `r05mn_hist_ab.txt`)
 template <int EI, bool RC, int CANON>
 __global__ __launch_bounds__(RT) void rg_hist(const uint8_t *__restrict__ codes, uint64_t n_bases, int k,
                                              uint32_t seg_tiles, uint32_t n_tiles, uint32_t *__restrict__ hist) {
     constexpr int NT = RT, WIN = NT * EI;
     __shared__ __attribute__((aligned(16))) uint8_t scodes[WIN + 64];
-#ifdef KMAN_HIST_WAVE
-    constexpr int NWAVE = NT / 64;
-    __shared__ uint32_t wh[NWAVE][RADIX];
-    const int w = threadIdx.x >> 6;
-#define HSLOT(d) wh[w][d]
-#else
     __shared__ uint32_t wh[RADIX * 32];
     const uint32_t col = threadIdx.x & 31u;
-#define HSLOT(d) wh[(d) * 32u + col]
-#endif
     const uint32_t sgi = blockIdx.y;
     const uint32_t t0 = sgi * seg_tiles;
     const uint32_t t1 = t0 + seg_tiles < n_tiles ? t0 + seg_tiles : n_tiles;
-    for (int i = threadIdx.x; i < (int)(sizeof(wh) / 4); i += NT) reinterpret_cast<uint32_t *>(wh)[i] = 0;
+    for (int i = threadIdx.x; i < RADIX * 32; i += NT) wh[i] = 0;
     const uint32_t kb = 2u * (uint32_t)k, shift = kb - B1;
     const uint64_t keymask = kb >= 64 ? ~0ull : ((1ull << kb) - 1);
     const uint32_t w0 = threadIdx.x * EI;
@@ -1783,45 +1764,38 @@ __global__ __launch_bounds__(RT) void rg_hist(const uint8_t *__restrict__ codes,
         store_codes<NT, EI>(cv, codes, n_bases, wb, scodes);
         if (t + gridDim.x < t1) load_codes<NT, EI>(codes, n_bases, (uint64_t)(t + gridDim.x) * WIN, cv);
         __syncthreads();
-#ifndef KMAN_HIST_FULL
         if constexpr (!CANON && EI % 4 == 0) {
-            // (only the keys' top bytes: roll_top, a third of the full roll's
-            // VALU work -- the full roll made this kernel VALU-bound)
+            // only the keys' top bytes: roll_top, a third of the full roll's
+            // VALU work (the full roll made this kernel VALU-bound: 8.4 vs 4.4
+            // ms per 12.5 G bases)
             constexpr int A = EI % 16 == 0 ? 16 : (EI % 8 == 0 ? 8 : 4);
             uint32_t bf[EI], br[EI];
             const uint32_t valid = roll_top<EI, RC, A>(scodes, (int)w0, k, wb + w0, n_bases, bf, br);
 #pragma unroll
             for (int j = 0; j < EI; j++) {
                 if ((valid >> j) & 1u) {
-                    atomicAdd(&HSLOT(bf[j]), 1u);
-                    if (RC) atomicAdd(&HSLOT(br[j]), 1u);
+                    atomicAdd(&wh[bf[j] * 32u + col], 1u);
+                    if (RC) atomicAdd(&wh[br[j] * 32u + col], 1u);
                 }
             }
-            continue;
-        }
-#endif
-        uint64_t kf[EI], kr[EI];
-        const uint32_t valid = roll<EI, CANON>(scodes, w0, k, keymask, wb + w0, n_bases, kf, kr);
+        } else {
+            uint64_t kf[EI], kr[EI];
+            const uint32_t valid = roll<EI, CANON>(scodes, w0, k, keymask, wb + w0, n_bases, kf, kr);
 #pragma unroll
-        for (int j = 0; j < EI; j++) {
-            if ((valid >> j) & 1u) {
-                atomicAdd(&HSLOT((uint32_t)(kf[j] >> shift)), 1u);
-                if (RC) atomicAdd(&HSLOT((uint32_t)(kr[j] >> shift)), 1u);
+            for (int j = 0; j < EI; j++) {
+                if ((valid >> j) & 1u) {
+                    atomicAdd(&wh[(uint32_t)(kf[j] >> shift) * 32u + col], 1u);
+                    if (RC) atomicAdd(&wh[(uint32_t)(kr[j] >> shift) * 32u + col], 1u);
+                }
             }
         }
     }
-#undef HSLOT
     __syncthreads();
     for (uint32_t d = threadIdx.x; d < (uint32_t)RADIX; d += NT) {
         uint32_t c = 0;
-#ifdef KMAN_HIST_WAVE
-#pragma unroll
-        for (int ww = 0; ww < NWAVE; ww++) c += wh[ww][d];
-#else
         // (column (c + d) mod 32: the lanes of a read spread over the banks)
 #pragma unroll 8
         for (uint32_t q = 0; q < 32; q++) c += wh[d * 32u + ((q + d) & 31u)];
-#endif
         if (c) atomicAdd(&hist[d * RS + sgi], c);
     }
 }
@@ -1981,8 +1955,7 @@ int read_err(kman_ctx *ctx, uint32_t *e) {
 template <int EI, bool RC, int CANON>
 void launch_hist(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes, uint64_t n_bases, uint32_t k,
                  uint32_t *hist) {
-    static const uint32_t bps = getenv("KMAN_HIST_GX") ? (uint32_t)atoi(getenv("KMAN_HIST_GX")) : HIST_BLOCKS_PER_SEG;
-    const uint32_t gx = p.seg_tiles < bps ? p.seg_tiles : (bps ? bps : 1u);
+    const uint32_t gx = p.seg_tiles < HIST_BLOCKS_PER_SEG ? p.seg_tiles : HIST_BLOCKS_PER_SEG;
     hipLaunchKernelGGL((rg_hist<EI, RC, CANON>), dim3(gx, RS), dim3(RT), 0, ctx->stream, codes, n_bases, (int)k,
                        p.seg_tiles, p.n_tiles0, hist);
 }
