@@ -27,7 +27,7 @@ import tempfile
 from enum import Enum
 from typing import List, Optional, Type
 
-from . import engine
+from . import engine, phases
 from .batch import Batch
 from .seq import NATYPES, KMer
 
@@ -216,6 +216,7 @@ class FastaBatcher(BatcherThreading):
         else:
             batches = self._record_batches(src)
         self.feed_collection(batches, feedMode)
+        phases.mark("batches")
         return self
 
     def _record_batches(self, src) -> List[Batch]:
