@@ -427,6 +427,14 @@ typedef struct {
 int kman_merge_runs(kman_ctx *ctx, const kman_run *runs, int nruns, uint32_t val_bytes, uint64_t *d_okeys,
                     void *d_ovals, uint64_t *d_tmp_keys, void *d_tmp_vals);
 int kman_count_descents(kman_ctx *ctx, const uint64_t *d_keys, uint64_t n, uint64_t *descents);
+/* kman_row_digest: a checksum of n result rows (keys + 0 / 4 / 8-byte values)
+ * for comparing two joins' outputs without moving them to the host (the
+ * at-size tests): out4 = {sum, xor} of h_i = mix(key_i ^ mix(val_i + (first +
+ * i) * 0x9E3779B97F4A7C15)) (mix = the murmur3 finaliser), the sum of the
+ * values, and the number of i >= 1 with keys[i] <= keys[i-1].  Sums are mod
+ * 2^64; slices [a, b) digested with first = a combine by sum / xor / sum. */
+int kman_row_digest(kman_ctx *ctx, const uint64_t *d_keys, const void *d_vals, uint32_t val_bytes, uint64_t n,
+                    uint64_t first_index, uint64_t *out4);
 
 /* Abundance vectors, KJoiner VEC_COUNT / VEC_COUNT_MASKED (join.py:288-335 ->
  * AbundanceVector.add_count, abundance.py:103-130; the reference's base-class

@@ -245,6 +245,7 @@ SIGNATURES = {
     ),
     "kman_merge_runs": (c_int, [c_void_p, c_void_p, c_int, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p]),
     "kman_count_descents": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
+    "kman_row_digest": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_uint64, c_uint64, POINTER(c_uint64)]),
     "kman_format_vector": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p, c_size_t, POINTER(c_size_t), c_int]),
     "kman_vec_fill": (
         c_int,

@@ -689,6 +689,10 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
 #else
     constexpr bool TWO_OK = NARROW;
 #endif
+    // the two-pass scans cover their counter words with one word pair per
+    // thread (first pass: <= 11 bits, 1024 words) and one word per thread
+    // (second pass: <= 10 bits, 512 words)
+    static_assert(!TWO_OK || (2 * NT >= 1024 && NT >= 512), "the two-pass finish needs >= 512 threads");
     constexpr uint32_t WSTR = TWO_OK ? 512 + 64 : FWORD + 64;
     __shared__ uint32_t wh[NW_][WSTR];
     __shared__ uint32_t lds_scan[NW_], lds_scan2[NW_];

@@ -478,6 +478,53 @@ __global__ __launch_bounds__(256) void descents_kernel(const uint64_t *__restric
     if (c) atomicAdd(out, (unsigned long long)c);
 }
 
+// a position-keyed digest of n rows (key, value): sum and xor of
+// mix(key ^ mix(value + (first + i) * PHI)), the values' sum and the number of
+// i >= 1 with keys[i] <= keys[i-1]; sums mod 2^64 and xors combine over slices
+KMAN_DEV uint64_t dg_mix(uint64_t x) {
+    x ^= x >> 33;
+    x *= 0xFF51AFD7ED558CCDull;
+    x ^= x >> 33;
+    x *= 0xC4CEB9FE1A85EC53ull;
+    return x ^ (x >> 33);
+}
+
+template <typename V>
+__global__ __launch_bounds__(256) void digest_kernel(const uint64_t *__restrict__ k, const V *__restrict__ v,
+                                                     uint64_t n, uint64_t first, unsigned long long *__restrict__ out) {
+    uint64_t hs = 0, hx = 0, vs = 0;
+    uint32_t nd = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256) {
+        const uint64_t key = k[i], val = v ? (uint64_t)v[i] : 0;
+        const uint64_t h = dg_mix(key ^ dg_mix(val + (first + i) * 0x9E3779B97F4A7C15ull));
+        hs += h;
+        hx ^= h;
+        vs += val;
+        nd += i && key <= k[i - 1];
+    }
+    __shared__ uint64_t r[4][256];
+    r[0][threadIdx.x] = hs;
+    r[1][threadIdx.x] = hx;
+    r[2][threadIdx.x] = vs;
+    r[3][threadIdx.x] = nd;
+    __syncthreads();
+    for (uint32_t s = 128; s; s >>= 1) {
+        if (threadIdx.x < s) {
+            r[0][threadIdx.x] += r[0][threadIdx.x + s];
+            r[1][threadIdx.x] ^= r[1][threadIdx.x + s];
+            r[2][threadIdx.x] += r[2][threadIdx.x + s];
+            r[3][threadIdx.x] += r[3][threadIdx.x + s];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        atomicAdd(&out[0], (unsigned long long)r[0][0]);
+        atomicXor(&out[1], (unsigned long long)r[1][0]);
+        atomicAdd(&out[2], (unsigned long long)r[2][0]);
+        atomicAdd(&out[3], (unsigned long long)r[3][0]);
+    }
+}
+
 }  // namespace
 
 // ================================================================ vectors
@@ -609,6 +656,32 @@ extern "C" int kman_count_descents(kman_ctx *ctx, const uint64_t *d_keys, uint64
     HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small, scr, 8, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     *descents = ctx->h_small[0];
+    return KMAN_OK;
+}
+
+extern "C" int kman_row_digest(kman_ctx *ctx, const uint64_t *d_keys, const void *d_vals, uint32_t val_bytes, uint64_t n,
+                               uint64_t first_index, uint64_t *out4) {
+    if (!ctx || !out4) return KMAN_EINVAL;
+    if (val_bytes != 0 && val_bytes != 4 && val_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "val_bytes 0, 4 or 8");
+    out4[0] = out4[1] = out4[2] = out4[3] = 0;
+    if (n == 0) return KMAN_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    void *scr;
+    KMAN_TRY(kman_scratch(ctx, 256, &scr));
+    HIP_TRY(ctx, hipMemsetAsync(scr, 0, 32, ctx->stream));
+    const uint64_t b = ceil_div(n, 256 * 16);
+    const dim3 g((uint32_t)(b < 4096 ? b : 4096));
+    if (val_bytes == 8)
+        hipLaunchKernelGGL(digest_kernel<uint64_t>, g, dim3(256), 0, ctx->stream, d_keys, (const uint64_t *)d_vals, n,
+                           first_index, (unsigned long long *)scr);
+    else
+        hipLaunchKernelGGL(digest_kernel<uint32_t>, g, dim3(256), 0, ctx->stream, d_keys,
+                           val_bytes ? (const uint32_t *)d_vals : (const uint32_t *)nullptr, n, first_index,
+                           (unsigned long long *)scr);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipMemcpyAsync(ctx->h_small, scr, 32, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    for (int i = 0; i < 4; i++) out4[i] = ctx->h_small[i];
     return KMAN_OK;
 }
 

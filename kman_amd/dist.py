@@ -392,6 +392,8 @@ class SimGroup:
                 outs = [None for _ in live]
             else:  # alltoallv (async: done right away, which any later wait allows)
                 L = N.lib()
+                for src in live:  # (every send buffer complete on its own rank's stream)
+                    self.pipes[src].dev.sync()
                 for dst in live:
                     pd = self.pipes[dst]
                     _, _, _, recv, rcnt, roff, eb = reqs[dst][1][:7]
@@ -521,6 +523,7 @@ class DistPipeline:
         self.fallback_rounds = 0
         self.partial_rounds = 0
         self.redone_kmers = 0
+        self.exchanged_items = self.max_message = 0
         self.phase_ms = {}
         self.ready = False
         if self.comm is not None:
@@ -660,6 +663,8 @@ class DistPipeline:
         self.partial_rounds = 0
         self.redone_kmers = 0
         self.overlapped_rounds = 0
+        self.exchanged_items = 0  # items this rank sent through kman_alltoallv (its rounds)
+        self.max_message = 0  # bytes of its largest message to one peer
         # overlapped rounds need two more scratch arenas (a piece's a and b)
         S_ = self.pieces
         use_ov = (self.path == "region" and self.overlap and R == 1
@@ -712,6 +717,8 @@ class DistPipeline:
                 lap("extract")
                 if xch:
                     yield ("alltoallv", (A.ptr, sc, so, B.ptr, rcnt, roff, 8))
+                    self.exchanged_items += int(np.asarray(sc, np.uint64).sum())
+                    self.max_message = max(self.max_message, 8 * int(np.asarray(sc, np.uint64).max()))
                     lap("exchange")
                 got = c_uint64(0)
                 ret = L.kman_dround_finish(ctx, c_void_p(rin), self.k, self.flags, self.fmode, G, self.n_bases_q,
@@ -727,6 +734,7 @@ class DistPipeline:
                 f = yield ("allreduce", np.array([fb, part], np.uint64))
                 if int(f[0]) == 0 and int(f[1]) == 0:
                     n_out += int(got.value)
+                    self._check_once_bound(x_off, r, n_out)
                     continue
                 if int(f[0]) == 0:
                     # regions overflowed (a repeat far beyond its region's
@@ -735,16 +743,26 @@ class DistPipeline:
                     self.partial_rounds += 1
                     mine = self._failed_ranges() if part else np.zeros((0, 2), np.uint64)
                     n_out += yield from self._redo_ranges(mine, int(got.value), A, B, ok_, ov_, n_out, vb)
+                    self._check_once_bound(x_off, r, n_out)
                     lap("partial_redo")
                     continue
                 self.fallback_rounds += 1
             # the general path for this round (every rank together)
             n_out += yield from self._general_round(C, cuts, R, r, ok_, ov_, n_out, vb)
+            self._check_once_bound(x_off, r, n_out)
             lap("general_round")
         self.n_out = n_out
         self.n_recv = cap
         self._out = (ok_, ov_, vb)
         return self.n_local
+
+    def _check_once_bound(self, x_off, r: int, n_out: int) -> None:
+        """Extract-once rounds (x_off): round r's rows must end before the
+        items of round r + 1 (a row is a distinct key of round r's items), or
+        they have overwritten input of a later round -- fail loudly."""
+        if x_off is not None and r + 1 < len(x_off) and n_out > x_off[r + 1]:
+            raise RuntimeError("rank %d round %d: %d rows overran the next round's items at %d"
+                               % (self.rank, r, n_out, x_off[r + 1]))
 
     def _overlapped_round(self, C, cuts, R, r, H, c_local, a_need, b_need, ok_, ov_, n_out, vb):
         """Round r with its exchange overlapped: one extraction (destination-
@@ -805,6 +823,8 @@ class DistPipeline:
             recv_at.append(at)
             at += int(rc_s.sum())
             yield ("alltoallv_async", (A.ptr, ssc, sso, B.ptr, rc_s, ro_s, 8, s_))
+            self.exchanged_items += int(ssc.sum())
+            self.max_message = max(self.max_message, 8 * int(ssc.max()))
         start, mine = n_out, []
         for s_ in range(S_):
             yield ("comm_wait", s_)

@@ -83,9 +83,15 @@ class FileReader:
     (the peers' maps stay valid) or at exit."""
 
     def __init__(self, path: str, world: int = 1, rank: int = 0, directory: Optional[str] = None,
-                 timeout: float = 3600.0):
+                 timeout: Optional[float] = None):
         self._fh = self._mm = None
         self._tmp = None
+        # where rank 0 inflates a gzip input, and how long the peers wait for
+        # it (rank 0 marks a failure at once, so the wait only bounds a rank 0
+        # that died without a word)
+        directory = directory or os.environ.get("KMAN_GZ_DIR") or None
+        if timeout is None:
+            timeout = float(os.environ.get("KMAN_GZ_TIMEOUT", "1800"))
         if path.endswith(".gz") and world > 1:
             path = self._gunzip_shared(path, world, rank, directory, timeout)
         if path.endswith(".gz"):
@@ -117,6 +123,11 @@ class FileReader:
                           & 0xffffffff)
         plain = _id_path("gz" + ident, directory) + ".fa"
         done = plain + ".done"
+        def mark(status: bytes) -> None:  # MAGIC | rank 0's start | status (b"ok" or b"!" + error text)
+            with open(done + ".tmp", "wb") as fh:
+                fh.write(_MAGIC + struct.pack("<d", _START) + status)
+            os.replace(done + ".tmp", done)
+
         if rank == 0:
             for q in (done, plain):
                 try:
@@ -124,20 +135,36 @@ class FileReader:
                 except OSError:
                     pass
             part = plain + ".part%d" % os.getpid()
+            self._tmp = (plain, done)
+            atexit.register(self._remove_tmp)
             try:
+                # the inflated size (gzip's ISIZE trailer: the size mod 2^32, so
+                # at least that much) must fit the directory's free space
+                with open(path, "rb") as fh:
+                    fh.seek(-4, os.SEEK_END)
+                    (isize,) = struct.unpack("<I", fh.read(4))
+                free = shutil.disk_usage(os.path.dirname(plain)).free
+                if isize > free:
+                    raise OSError("inflating %s needs >= %d bytes in %s, %d free (set KMAN_GZ_DIR)"
+                                  % (path, isize, os.path.dirname(plain), free))
                 with gzip.open(path, "rb") as src, open(part, "wb") as dst:
                     shutil.copyfileobj(src, dst, 16 << 20)
                 os.replace(part, plain)
+            except BaseException as e:
+                # the peers read the failure at once instead of waiting out
+                # their timeout
+                try:
+                    mark(b"!" + ("%s: %s" % (type(e).__name__, e)).encode("utf-8", "replace")[:4000])
+                    self._tmp = (plain,)  # (the marker outlives this process: a peer may start polling later)
+                except OSError:
+                    pass
+                raise
             finally:
                 try:
                     os.remove(part)
                 except OSError:
                     pass
-            self._tmp = (plain, done)
-            atexit.register(self._remove_tmp)
-            with open(done + ".tmp", "wb") as fh:
-                fh.write(_MAGIC + struct.pack("<d", _START))
-            os.replace(done + ".tmp", done)
+            mark(b"ok")
             return plain
         t0 = time.time()
         while True:
@@ -145,11 +172,15 @@ class FileReader:
                 with open(done, "rb") as fh:
                     blob = fh.read()
                 if blob[:8] == _MAGIC and len(blob) >= 16 and struct.unpack("<d", blob[8:16])[0] >= _START - skew:
+                    if blob[16:17] == b"!":
+                        raise RuntimeError("rank %d: rank 0 failed to decompress %s: %s"
+                                           % (rank, path, blob[17:].decode("utf-8", "replace")))
                     return plain
             except OSError:
                 pass
             if time.time() - t0 > timeout:
-                raise RuntimeError("rank %d: rank 0 did not decompress %s into %s" % (rank, path, plain))
+                raise RuntimeError("rank %d: rank 0 did not decompress %s into %s within %.0f s (KMAN_GZ_TIMEOUT)"
+                                   % (rank, path, plain, timeout))
             time.sleep(0.05)
 
     def _remove_tmp(self) -> None:
@@ -190,6 +221,15 @@ def launch_nonce() -> str:
     tid = os.environ.get("TORCHELASTIC_RUN_ID", "")
     if tid and tid != "none":
         return "%s-%s" % (tid, os.environ.get("TORCHELASTIC_RESTART_COUNT", "0"))
+    # torch.distributed.run with the default run id "none": its per-launch log
+    # directory (<tmp>/torchelastic_<random>/<run id>_<random>/attempt_<n>/<local
+    # rank>/error.json) is shared by the workers of one launch and by no other
+    ef = os.environ.get("TORCHELASTIC_ERROR_FILE", "")
+    if ef and ef != os.devnull:
+        import zlib
+
+        attempt = os.path.dirname(os.path.dirname(ef))
+        return "te%08x" % (zlib.crc32(attempt.encode()) & 0xffffffff)
     return ""
 
 

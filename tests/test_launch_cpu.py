@@ -244,3 +244,60 @@ def test_gzip_input_inflated_once_and_memory_mapped_by_every_rank(tmp_path):
         assert digest == hashlib.sha256(text[lo:hi]).hexdigest()
         assert peak <= 1.5 * (hi - lo), (r, peak, hi - lo)
     assert os.listdir(d) == []
+
+
+def test_nonce_from_torchrun_log_dir(monkeypatch):
+    """torch.distributed.run with the default run id "none": the workers of one
+    launch share its per-launch log directory (TORCHELASTIC_ERROR_FILE =
+    <dir>/<run id>_<random>/attempt_<n>/<local rank>/error.json), so the id
+    file is keyed by it -- and a later launch has another."""
+    from kman_amd import launch
+
+    monkeypatch.delenv("KMAN_RUN_ID", raising=False)
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "none")
+    base = "/tmp/torchelastic_ab12/none_x9y8/attempt_0/%d/error.json"
+    monkeypatch.setenv("TORCHELASTIC_ERROR_FILE", base % 0)
+    n0 = launch.launch_nonce()
+    monkeypatch.setenv("TORCHELASTIC_ERROR_FILE", base % 3)
+    assert launch.launch_nonce() == n0 and n0
+    monkeypatch.setenv("TORCHELASTIC_ERROR_FILE", "/tmp/torchelastic_cd34/none_q1w2/attempt_0/3/error.json")
+    assert launch.launch_nonce() != n0
+    monkeypatch.setenv("TORCHELASTIC_ERROR_FILE", "")  # (logs to /dev/null: nothing to key on)
+    assert launch.launch_nonce() == ""
+
+
+def _gz_peer(path, d, q):
+    from kman_amd import launch
+
+    t0 = time.time()
+    try:
+        launch.FileReader(path, 2, 1, directory=d, timeout=120)
+        q.put(("ok", time.time() - t0))
+    except RuntimeError as e:
+        q.put((str(e), time.time() - t0))
+
+
+def test_gzip_failure_reaches_the_peers_at_once(tmp_path, monkeypatch):
+    """A corrupt gzip: rank 0 raises and writes a failure marker, so its peer
+    raises with rank 0's error within seconds instead of waiting out its
+    timeout (120 s here)."""
+    from kman_amd import launch
+
+    monkeypatch.setattr(launch, "_START", time.time())  # (this process plays a rank 0 started with its peer)
+
+    gz = tmp_path / "bad.fa.gz"
+    good = gzip.compress(b">a\n" + b"ACGT" * 100000 + b"\n")
+    gz.write_bytes(good[:len(good) // 2] + b"\0" * 64 + good[-8:])  # truncated body, intact ISIZE trailer
+    d = str(tmp_path / "tmp")
+    os.mkdir(d)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_gz_peer, args=(str(gz), d, q))
+    p.start()
+    time.sleep(1.0)
+    with pytest.raises(Exception):
+        launch.FileReader(str(gz), 2, 0, directory=d, timeout=120)
+    msg, dt = q.get(timeout=60)
+    p.join(timeout=30)
+    assert msg != "ok" and "failed to decompress" in msg and dt < 30
+    assert not [f for f in os.listdir(d) if not f.endswith(".done")]
