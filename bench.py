@@ -527,11 +527,15 @@ def run_single(args):
 
 
 def dist_line(args, dev, world: int, rank: int, per: int, mode: str, canon: bool, reparse: bool, steps: int,
-              warmup: int, tag: str):
+              warmup: int, tag: str, also_overlap: bool = False):
     """One multi-GPU measurement: ONE global synthetic FASTA of `per` bytes
     per rank, byte-range sharded; `warmup` untimed steps, then `steps` timed
-    ones between barriers, max over ranks.  Returns rank 0's line (None on
-    the other ranks); the pipeline is freed before it returns."""
+    ones between barriers, max over ranks.  also_overlap: then the same
+    pipeline with overlapped rounds (each round's all-to-all in pieces on the
+    communication stream, piece s sorted while piece s + 1 is exchanged), one
+    untimed step and `steps` timed ones -- the line's "overlapped" entry, so
+    one N > 1 run settles which default is faster.  Returns rank 0's line
+    (None on the other ranks); the pipeline is freed before it returns."""
     import numpy as np
     import inputs
     from kman_amd import dist, launch, shard
@@ -541,7 +545,7 @@ def dist_line(args, dev, world: int, rank: int, per: int, mode: str, canon: bool
     uid = launch.rendezvous(rank, world, tag)
     t_setup = time.time()
     pipe = dist.DistPipeline(dev, rd, args.k, mode, world, rank, uid, chunk_bytes=1 << 30, reparse=reparse,
-                             canonical=canon, ordered=not canon)
+                             canonical=canon, ordered=not canon, exchange=args.exchange == "on")
     if rank == 0:
         launch.remove_id(tag)  # (every rank has joined the communicator)
     comm = pipe.comm
@@ -557,27 +561,31 @@ def dist_line(args, dev, world: int, rank: int, per: int, mode: str, canon: bool
             hist[0] = comm.run(pipe.hist_gen(10001))
         return n
 
-    try:
-        for _ in range(warmup):
-            one_step()
-        setup_s = time.time() - t_setup
-        pipe.timing(True)
+    def timed_steps(n):
+        """n steps between barriers: (max elapsed over ranks, k-mers of all ranks)"""
         comm.allreduce(np.zeros(1, np.uint64))  # barrier
         dev.sync()
         t0 = time.perf_counter()
         kmers = 0
-        for _ in range(steps):
+        for _ in range(n):
             kmers += one_step()
         dev.sync()
         elapsed = time.perf_counter() - t0
         el = comm.allgather(np.array([int(elapsed * 1e9)], np.uint64))
         tot = comm.allreduce(np.array([kmers], np.uint64))
-        elapsed, total = float(el.max()) / 1e9, int(tot[0])
+        return float(el.max()) / 1e9, int(tot[0])
+
+    try:
+        for _ in range(warmup):
+            one_step()
+        setup_s = time.time() - t_setup
+        pipe.timing(True)
+        elapsed, total = timed_steps(steps)
         out = None
         if rank == 0:
             stages = {}
-            for st in ("parse", "shard_hist", "region_extract", "region_pass", "region_pass1b", "region_finish",
-                       "extract", "sort_pass", "finish"):
+            for st in ("parse", "shard_hist", "region_extract", "exchange", "region_pass", "region_pass1b",
+                       "region_finish", "extract", "sort_pass", "finish"):
                 c, ms = pipe.timed(st)
                 if c:
                     stages[st] = round(ms / steps, 3)
@@ -594,7 +602,28 @@ def dist_line(args, dev, world: int, rank: int, per: int, mode: str, canon: bool
                    "fallback_rounds": pipe.fallback_rounds, "partial_rounds": pipe.partial_rounds,
                    "memory_plan": getattr(pipe, "plan_info", None), "stages_ms_per_step_rank0": stages,
                    "stage_alg_bytes_rank0": stage_alg, "roofline": dom, "sort_pass_roofline": sp,
-                   "spectrum_distinct": int(hist[0].sum()) if canon else None}
+                   "spectrum_distinct": int(hist[0].sum()) if canon else None,
+                   # the data path: the all-to-all runs on every rank at N > 1;
+                   # at world 1 only with --exchange on (RCCL send/recv to self,
+                   # the per-rank step the N > 1 run takes), else the rank
+                   # extracts straight into its receive buffer / once for all
+                   # rounds (a one-GPU-only shortcut)
+                   "exchange": bool(pipe.exchanged_items),
+                   "exchanged_bytes_per_step": 8 * pipe.exchanged_items,
+                   "max_message_bytes": pipe.max_message,
+                   "exchange_gbs_rank0": (8 * pipe.exchanged_items / (stages["exchange"] / 1e3) / 1e9
+                                          if stages.get("exchange") else None)}
+        if also_overlap:
+            pipe.timing(False)
+            pipe.overlap = True
+            one_step()  # (untimed: the overlapped plan's arenas grow here)
+            e2, t2 = timed_steps(steps)
+            if rank == 0:
+                out["overlapped"] = {"value": t2 / e2, "ms_per_step": e2 / steps * 1e3, "steps": steps,
+                                     "overlapped_rounds": pipe.overlapped_rounds, "rounds": pipe.rounds,
+                                     "pieces": pipe.pieces,
+                                     "vs_sequential": (elapsed / steps) / (e2 / steps)}
+            pipe.overlap = False
         comm.allreduce(np.zeros(1, np.uint64))  # every rank is done with this line
         return out
     finally:
@@ -613,14 +642,19 @@ def run_dist(args, world: int, rank: int, local: int):
     canon = args.canonical
     if canon and args.mode != "count":
         raise SystemExit("--canonical counts (config 5): use --mode count")
-    ln = dist_line(args, dev, world, rank, per, args.mode, canon, reparse, args.steps, args.warmup, "bench")
+    # N > 1: each line also timed with overlapped rounds (opt-in in the
+    # product until an N > 1 run shows which is faster)
+    ov = world > 1 and not canon
+    ln = dist_line(args, dev, world, rank, per, args.mode, canon, reparse, args.steps, args.warmup, "bench",
+                   also_overlap=ov)
     # BASELINE config 4 (100 GB synthetic FASTA, k=21, N GPUs): after the
     # weak-scaling line, the same job at 100 / N GB per rank, count mode,
     # parsed at setup -- so the driver's plain `--gpus N` run measures it too
     sub = None
     if world > 1 and args.config4 and args.shard_gb is None and not canon:
         per4 = int(100e9 / world)
-        sub = dist_line(args, dev, world, rank, per4, "count", False, False, args.config4_steps, 1, "bench4")
+        sub = dist_line(args, dev, world, rank, per4, "count", False, False, args.config4_steps, 1, "bench4",
+                        also_overlap=ov)
     dev.close()
     if rank == 0:
         out = {
@@ -631,11 +665,17 @@ def run_dist(args, world: int, rank: int, local: int):
                     "byte-range sharded, each rank's bytes generated in its HBM; a step = %s shard histogram + key "
                     "rounds" % (world, per / 1e9, "parse of the resident text +" if reparse else "(parsed at setup)"),
             "config": {"workload": "%.2f GB synthetic FASTA in %d byte-range shards of %.2f GB per rank, k=%d, "
-                                   "extract+radix-sort+%s, key rounds + one RCCL all-to-all per round%s"
+                                   "extract+radix-sort+%s, key rounds%s%s"
                                    % (ln["fasta_bytes"] / 1e9, world, per / 1e9, args.k,
                                       "canonical count + all-reduced abundance spectrum (config 5's pipeline)"
                                       if canon else args.mode,
+                                      " + one RCCL all-to-all per round" if ln.get("exchange") else
+                                      " without an exchange (one rank, --exchange off: a one-GPU-only shortcut, "
+                                      "not the per-rank step of an N > 1 run)",
                                       "" if not canon else "; the synthetic input stands in for GRCh38"),
+                       "exchange": ln.get("exchange"), "exchanged_bytes_per_step": ln.get("exchanged_bytes_per_step"),
+                       "max_message_bytes": ln.get("max_message_bytes"),
+                       "exchange_gbs_rank0": ln.get("exchange_gbs_rank0"), "overlapped": ln.get("overlapped"),
                        "canonical": canon, "spectrum_distinct": ln["spectrum_distinct"],
                        "fasta_bytes": ln["fasta_bytes"], "fasta_bytes_per_rank": per,
                        "kmers_per_step": ln["kmers_per_step"], "k": args.k,
@@ -762,6 +802,11 @@ def parse_args(argv=None):
     ap.add_argument("--no-config4", dest="config4", action="store_false",
                     help="N > 1: skip the config-4 sub-line (100 GB / N per rank, count) after the main line")
     ap.add_argument("--config4-steps", type=int, default=3, help="timed steps of the config-4 sub-line")
+    ap.add_argument("--exchange", choices=["on", "off"], default="on",
+                    help="multi-GPU path at world 1: on (default) runs each round's all-to-all (RCCL send/recv to "
+                         "self), i.e. the per-rank step of an N > 1 run; off extracts straight into the receive "
+                         "buffer (for R > 1 rounds once for all of them: a one-GPU-only shortcut).  N > 1 always "
+                         "exchanges")
     ap.add_argument("--canonical", action="store_true",
                     help="multi-GPU path: canonical k-mers + the all-reduced abundance spectrum (config 5; "
                          "with --mode count)")

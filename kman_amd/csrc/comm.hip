@@ -172,6 +172,7 @@ extern "C" int kman_alltoallv(kman_ctx *ctx, const void *d_send, const uint64_t 
                               const uint64_t *send_offsets, void *d_recv, const uint64_t *recv_counts,
                               const uint64_t *recv_offsets, uint32_t elem_bytes) {
     if (!ctx) return KMAN_EINVAL;
+    KTimer kt_(ctx, "exchange");  // (the grouped send/recv on the compute stream, between HIP events)
     return alltoallv_on(ctx, ctx->stream, false, d_send, send_counts, send_offsets, d_recv, recv_counts, recv_offsets,
                         elem_bytes);
 }

@@ -649,7 +649,11 @@ class DistPipeline:
         pl = RoundPlanner(self.k, self.flags, self.fmode, G, self.n_bases_q)
         tot = int(np.asarray(C, np.uint64).sum())
         out_bytes = (8 + self._vb(C)) * (tot if G == 1 else int(tot * 1.1 / G) + (1 << 20))
-        R, cuts, a_need, b_need = pl.plan(C, max(1, self.budget - out_bytes), self.max_round_items)
+        S_ = self.pieces
+        # overlapped rounds hold a piece's two scratch arenas beside A and B
+        # (about 2 / S of them): their plan leaves room for those
+        ov_scale = 1.0 + 2.0 / S_ if (self.overlap and self.path == "region") else 1.0
+        R, cuts, a_need, b_need = pl.plan(C, max(1, int((self.budget - out_bytes) / ov_scale)), self.max_round_items)
         self.rounds = R
         self.plan_info = {"budget_gb": self.budget / 1e9, "out_gb": out_bytes / 1e9, "arena_a_gb": a_need / 1e9,
                           "arena_b_gb": b_need / 1e9, "rounds": R}
@@ -665,10 +669,11 @@ class DistPipeline:
         self.overlapped_rounds = 0
         self.exchanged_items = 0  # items this rank sent through kman_alltoallv (its rounds)
         self.max_message = 0  # bytes of its largest message to one peer
-        # overlapped rounds need two more scratch arenas (a piece's a and b)
-        S_ = self.pieces
-        use_ov = (self.path == "region" and self.overlap and R == 1
-                  and (a_need + b_need) * (1 + 2.0 / S_) + out_bytes <= self.budget)
+        # overlapped rounds (every round of the step, R >= 1): exchange piece
+        # s + 1 crosses xGMI while piece s is sorted; they need two more
+        # scratch arenas (a piece's a and b), which the plan above left room for
+        use_ov = (self.path == "region" and self.overlap
+                  and (a_need + b_need) * ov_scale + out_bytes <= self.budget * 1.0001)
         # once (R > 1): every round's items extracted by one pass into the
         # output-key buffer, round r's regions (b, s) at x_off[r] + their
         # round_send offsets.  Round r's rows are written from n_out on, and

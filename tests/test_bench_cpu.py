@@ -130,17 +130,23 @@ def test_committed_pmc_summary_matches_the_default_workload():
 
 
 def _fake_line(calls):
-    def line(args, dev, world, rank, per, mode, canon, reparse, steps, warmup, tag):
+    def line(args, dev, world, rank, per, mode, canon, reparse, steps, warmup, tag, also_overlap=False):
         calls.append({"per": per, "mode": mode, "canon": canon, "reparse": reparse, "steps": steps,
-                      "warmup": warmup, "tag": tag})
+                      "warmup": warmup, "tag": tag, "also_overlap": also_overlap})
         if rank:
             return None
-        return {"value": 1e9 * world, "ms_per_step": 10.0, "steps": steps, "warmup": warmup,
-                "kmers_per_step": per * world, "rccl_ranks": world, "setup_s": 1.0, "fasta_bytes": per * world,
-                "fasta_bytes_per_rank": per, "path": "region", "rounds": 3 if mode == "count" else 1,
-                "fallback_rounds": 0, "partial_rounds": 0, "memory_plan": None, "stages_ms_per_step_rank0": {},
-                "stage_alg_bytes_rank0": {}, "roofline": {"frac": 0.5}, "sort_pass_roofline": {"frac": 0.6},
-                "spectrum_distinct": None}
+        out = {"value": 1e9 * world, "ms_per_step": 10.0, "steps": steps, "warmup": warmup,
+               "kmers_per_step": per * world, "rccl_ranks": world, "setup_s": 1.0, "fasta_bytes": per * world,
+               "fasta_bytes_per_rank": per, "path": "region", "rounds": 3 if mode == "count" else 1,
+               "fallback_rounds": 0, "partial_rounds": 0, "memory_plan": None, "stages_ms_per_step_rank0": {},
+               "stage_alg_bytes_rank0": {}, "roofline": {"frac": 0.5}, "sort_pass_roofline": {"frac": 0.6},
+               "spectrum_distinct": None, "exchange": world > 1, "exchanged_bytes_per_step": 8 * per,
+               "max_message_bytes": per, "exchange_gbs_rank0": 100.0}
+        if also_overlap:
+            out["overlapped"] = {"value": 1.1e9 * world, "ms_per_step": 9.0, "steps": steps,
+                                 "overlapped_rounds": out["rounds"], "rounds": out["rounds"], "pieces": 4,
+                                 "vs_sequential": 10.0 / 9.0}
+        return out
     return line
 
 
@@ -169,8 +175,14 @@ def test_multi_gpu_line_carries_config4_and_rccl_ranks(monkeypatch, capsys):
     c4 = out["config4"]
     assert c4["rccl_ranks"] == 8 and c4["fasta_bytes_per_rank"] == int(100e9 / 8) and c4["rounds"] == 3
     assert "roofline" in c4 and c4["ms_per_step"] > 0 and c4["setup_s"] >= 0
-    assert [(c["mode"], c["per"], c["reparse"], c["tag"]) for c in calls] == [
-        ("uniq", 10 ** 9, True, "bench"), ("count", int(100e9 / 8), False, "bench4")]
+    assert [(c["mode"], c["per"], c["reparse"], c["tag"], c["also_overlap"]) for c in calls] == [
+        ("uniq", 10 ** 9, True, "bench", True), ("count", int(100e9 / 8), False, "bench4", True)]
+    # both sub-lines of each: the sequential step (the line itself) and the
+    # overlapped one, for the N > 1 run to settle the default
+    for ln in (out["config"], c4):
+        assert ln["overlapped"]["ms_per_step"] > 0 and ln["overlapped"]["overlapped_rounds"] >= 1
+    assert c4["overlapped"]["rounds"] == 3 and out["config"]["exchange"] is True
+    assert "one RCCL all-to-all per round" in out["config"]["workload"]
     # the other ranks run both lines and print nothing
     calls.clear()
     bench.run_dist(args, 8, 3, 3)
@@ -182,3 +194,4 @@ def test_multi_gpu_line_carries_config4_and_rccl_ranks(monkeypatch, capsys):
         bench.run_dist(bench.parse_args(argv + ["--no-cpu-baseline"]), world, 0, 0)
         out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
         assert len(calls) == 1 and "config4" not in out and out["config"]["rccl_ranks"] == world
+        assert calls[0]["also_overlap"] == (world > 1)

@@ -87,7 +87,7 @@ def test_row_digest_matches_numpy(vb):
             dev.upload(dv, vals)
         got = _digest(dev, dk, dv if vb else None, vb, n)
         assert got == digest_np(keys, vals)
-        assert got[3] == 1
+        assert got[3] >= 1  # (the forced one; random 42-bit keys may repeat too)
         # slices combine (first = the slice's start)
         a = 1_234_567
         from kman_amd import _native as N

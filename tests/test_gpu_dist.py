@@ -123,14 +123,13 @@ def test_dist_region_rccl_exchange_world1(dev, mode, overlap, input_):
         body = inputs.syn_numpy(300_000, 4).split(b"\n", 1)[1].replace(b"\n", b"")
         text = b">r\n" + body + b"\n>s\n" + (seg * 3000).encode() + b"\n"
     p = dist.DistPipeline(dev, shard.BytesReader(text), 21, mode, 1, 0, dist.unique_id(), overlap=overlap,
-                          exchange=True, max_round_items=None if overlap else 200_000)
+                          exchange=True, max_round_items=120_000)
     try:
         p.step()
-        assert p.path == "region"
-        if overlap:
-            assert p.overlapped_rounds >= 1, "the overlapped exchange did not run"
-        else:
-            assert p.rounds >= 1
+        assert p.path == "region" and p.rounds >= 3
+        if overlap:  # (every round, R >= 3: config 4's shape of plan)
+            assert p.overlapped_rounds == p.rounds, "the overlapped exchange did not run in every round"
+        assert p.exchanged_items == p.n_local
         if input_ == "repeats":
             assert p.partial_rounds >= 1, "no region overflowed: the RCCL redo did not run"
         keys, vals = p.results()

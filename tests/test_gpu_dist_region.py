@@ -139,6 +139,24 @@ def test_dist_streamed_rounds(monkeypatch, variant, G, once, mode):
         _close(pipes)
 
 
+@pytest.mark.parametrize("G", [2, 8])
+@pytest.mark.parametrize("mode", ["count", "uniq"])
+def test_dist_overlapped_streamed_rounds(G, mode):
+    """Overlapped rounds at R >= 3 (config 4 plans R = 3 at 12.5 G k-mers per
+    rank): every round's exchange in pieces, each piece's passes + finish
+    after its own exchange; rows bit-exact against the oracle."""
+    text = _texts()["synth"]
+    outs, pipes, _ = _run(text, 21, mode, G, max_round_items=120_000 // G, overlap=True)
+    try:
+        assert all(p.rounds >= 3 and p.overlapped_rounds == p.rounds for p in pipes)
+        wk, wv = _oracle(text, 21, mode)
+        for keys, vals in outs:
+            np.testing.assert_array_equal(keys, wk)
+            np.testing.assert_array_equal(vals, wv)
+    finally:
+        _close(pipes)
+
+
 def test_dist_wide_pass1b(monkeypatch):
     """Pass 1b with 7 bits (the width config 4's 390 M-item buckets take)."""
     monkeypatch.setenv("KMAN_DROUND_MIN_G", "7")
