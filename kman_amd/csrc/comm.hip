@@ -143,8 +143,23 @@ int alltoallv_on(kman_ctx *ctx, hipStream_t st, bool second, const void *d_send,
     // was observed to move only part of its bytes (RCCL 2.27, 2.4 GB to self);
     // both ends derive the same chunk sequence from the same count
     const uint64_t CH = (512ull << 20) / elem_bytes;
+    // the rank's own part is a device copy on the same stream (RCCL's
+    // send/recv to self moved 8 GB at 1.34 TB/s, `profiles/r06b_bench_d1_on.json`)
+    // (KMAN_RCCL_SELF=1: through RCCL as every other peer -- tests of the
+    // chunked send/recv at world size 1)
+    const char *rs = getenv("KMAN_RCCL_SELF");
+    const bool rccl_self = rs && rs[0] == '1';
+    const int me = rccl_self ? -1 : c->rank;
+    if (me >= 0 && send_counts[me] != recv_counts[me])
+        return kman_fail(ctx, KMAN_EINVAL, "alltoallv: %llu items sent to self, %llu expected",
+                         (unsigned long long)send_counts[me], (unsigned long long)recv_counts[me]);
+    if (me >= 0 && send_counts[me])
+        HIP_TRY(ctx, hipMemcpyAsync((char *)d_recv + recv_offsets[me] * elem_bytes,
+                                    (const char *)d_send + send_offsets[me] * elem_bytes, send_counts[me] * elem_bytes,
+                                    hipMemcpyDeviceToDevice, st));
     uint64_t rounds = 0;
     for (int p = 0; p < c->nranks; p++) {
+        if (p == me) continue;
         const uint64_t a = (send_counts[p] + CH - 1) / CH, b = (recv_counts[p] + CH - 1) / CH;
         rounds = a > rounds ? a : rounds;
         rounds = b > rounds ? b : rounds;
@@ -152,6 +167,7 @@ int alltoallv_on(kman_ctx *ctx, hipStream_t st, bool second, const void *d_send,
     for (uint64_t r = 0; r < rounds; r++) {
         NCCL_TRY(ctx, ncclGroupStart());
         for (int p = 0; p < c->nranks; p++) {
+            if (p == me) continue;
             const uint64_t o = r * CH;
             if (send_counts[p] > o) {
                 const uint64_t n = send_counts[p] - o < CH ? send_counts[p] - o : CH;

@@ -307,3 +307,31 @@ def _canonical_range_matches_general(dev, p, r):
     np.testing.assert_array_equal(dev.download(r.ukeys, i1 - i0, np.uint64, offset=8 * i0), want_k)
     np.testing.assert_array_equal(dev.download(r.counts, i1 - i0, cdt, offset=r.count_bytes * i0).astype(np.uint64),
                                   want_c.astype(np.uint64))
+
+
+@pytest.mark.parametrize("rccl_self", ["0", "1"])
+def test_world1_exchange_chunked_messages(monkeypatch, rccl_self):
+    """1 GB at world size 1 through a real RCCL communicator with the
+    exchange on: the rank's own part as a device copy (the default), or
+    (KMAN_RCCL_SELF=1) through RCCL send/recv to self in 512 MiB chunks -- an
+    8 GB message, 16 chunks, the loop every peer pair of an N > 1 run takes.
+    Rows equal the exchange-free run's (kman_row_digest)."""
+    import inputs
+    from kman_amd import dist, engine, shard
+
+    monkeypatch.setenv("KMAN_RCCL_SELF", rccl_self)
+    lay = inputs.SynthLayout(1_000_000_000, 1)
+    rd = shard.SynthReader(lay)
+    dev = engine.default_device()
+    got = {}
+    for xch in (False, True):
+        p = dist.DistPipeline(dev, rd, K, "count", 1, 0, dist.unique_id(), chunk_bytes=1 << 30, exchange=xch)
+        try:
+            p.step()
+            if xch:
+                assert p.exchanged_items == p.n_local and p.max_message > 8 * (512 << 20)
+            ok_, ov_, vb = p._out
+            got[xch] = (p.n_out, _digest(dev, ok_, ov_, vb, p.n_out))
+        finally:
+            p.free()
+    assert got[True] == got[False] and got[True][1][3] == 0

@@ -1,0 +1,25 @@
+# round 6: the multi-GPU tests + the world-1 lines of the N > 1 data path
+# (exchange on = what every rank of an N > 1 run does; off = the one-GPU
+# shortcut), config 4's 12.5 GB shard both ways and with overlapped rounds
+set -e
+TAG=${1:-r06b}
+R=$GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest -q --timeout 300 --timeout-method thread -m gpu -x \
+  tests/test_gpu_dist.py tests/test_gpu_dist_region.py > gpurun_out/dist_tests_$TAG.log 2>&1 \
+  || { tail -60 gpurun_out/dist_tests_$TAG.log; exit 1; }
+tail -2 gpurun_out/dist_tests_$TAG.log
+cd /tmp
+for X in on off; do
+  timeout -k 10 300 python3 $R/bench.py --dist --exchange $X --no-cpu-baseline --steps 5 --warmup 2 > $R/gpurun_out/d1_${X}_$TAG.json 2> $R/gpurun_out/d1_${X}_$TAG.err
+  timeout -k 10 400 python3 $R/bench.py --dist --exchange $X --mode count --shard-gb 12.5 --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/cfg4_${X}_$TAG.json 2> $R/gpurun_out/cfg4_${X}_$TAG.err
+done
+KMAN_DIST_OVERLAP=1 timeout -k 10 400 python3 $R/bench.py --dist --exchange on --mode count --shard-gb 12.5 --steps 3 --warmup 1 --no-cpu-baseline > $R/gpurun_out/cfg4_ov_$TAG.json 2> $R/gpurun_out/cfg4_ov_$TAG.err
+cd $R
+python3 - <<PY
+import json
+for n in ("d1_on", "d1_off", "cfg4_on", "cfg4_off", "cfg4_ov"):
+    d = json.load(open("gpurun_out/%s_$TAG.json" % n)); c = d["config"]
+    print(n, round(d["value"] / 1e9, 2), "G/s", round(d["ms_per_step"], 2), "ms", "R", c.get("rounds"), "xch", c.get("exchange"),
+          "xch GB/s", c.get("exchange_gbs_rank0"), "maxmsg", c.get("max_message_bytes"), c.get("stages_ms_per_step_rank0"))
+PY
