@@ -658,7 +658,7 @@ constexpr int fin_waves() {
     return sizeof(T) == 4 || (ATOMIC && CAP <= GCAP) ? 6 : 4;
 }
 
-template <int MODE, typename O, bool ATOMIC, typename T = uint64_t, int CHK = 0, int CAP = FCAP, bool W2 = false>
+template <int MODE, typename O, bool ATOMIC, typename T = uint64_t, int CHK = 0, int CAP = FCAP>
 __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     const uint64_t *__restrict__ in, uint64_t C1, const uint32_t *__restrict__ cnt1, uint32_t Q, uint32_t rest,
     uint32_t rc, uint64_t rbase, uint32_t tag_shift, uint32_t fsub, uint64_t *__restrict__ okeys,
@@ -768,20 +768,7 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     // to a word (a wave ranks <= 64 * IPT items), same-word LDS atomics of one
     // wave return in lane order (probed: ATOMIC), else ballot match-any.
     const bool two = TWO_OK && rest >= 2 && rest <= 21;
-    // WIDE2 (8-byte items of an FCAP region, 24..26 rest bits: the uniq
-    // finish at k = 21): two passes instead of three -- the first by rest - 12
-    // bits on ONE block-wide counter array (unstable, as a first LSD pass may
-    // be), the second, stable, by 12 bits on per-wave counters of 2048 words.
-    // Both counter arrays live in the item buffer s, which is free while the
-    // items sit in registers: counted, scanned, every slot read, then one
-    // barrier before the first item is written
-    constexpr bool WIDE_OK = PIPE && W2;  // (the host picks W2 for 24..26 rest bits: launch_finish)
-    constexpr uint32_t W2B = 12, W2S = (1u << (W2B - 1)) + 64;  // pass-2 bits; words per wave (+ spare words)
-    static_assert(!WIDE_OK || (size_t)CAP * sizeof(T) >= (size_t)NW_ * W2S * 4, "per-wave counters fit the items");
-    static_assert(!WIDE_OK || (1u << (W2B - 1)) == 4 * NT, "the pass-2 scan: four words per thread");
-    static_assert(!W2 || PIPE, "the two-pass wide finish ranks with lane-ordered atomics");
-    const bool wide2 = WIDE_OK;
-    const uint32_t np = two || wide2 ? 2u : (rest + FBITS - 1) / FBITS;
+    const uint32_t np = two ? 2u : (rest + FBITS - 1) / FBITS;
     const uint32_t bw_two = rest / 2;  // (two: the stable second pass's bits, <= 10)
     // EARLY (uniq): the region's row count is found after the second-to-last
     // pass, when equal keys already share a run of equal low bits (a run of
@@ -846,188 +833,10 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
             p0 = 1;
         }
     }
-    // EARLY's marks (see above), after the second-to-last pass
-    auto early_marks = [&]() {
-            // The items are sorted by their low `at` rest bits, and x holds
-            // them wave-striped (item (i, lane) at position pw + i * 64), so a
-            // neighbour in position is a neighbouring lane (DPP) or the next /
-            // previous row's edge lane (readlane); only the wave's two edges
-            // come from LDS.  A key is a singleton iff no item of its run of
-            // equal low bits has its whole rest: runs of one or two decide
-            // from the neighbours, the rare runs of three or more scan LDS.
-            const uint64_t lm = ((1ull << at) - 1) << Q, km = rmask << Q;
-            const uint32_t wb = (uint32_t)w * (IPT * 64), we = wb + IPT * 64;
-            auto rl64 = [](uint64_t v, int l) -> uint64_t {
-                return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-            };
-            auto eq = [](uint64_t a, uint64_t b, uint64_t mask) { return !((a ^ b) & mask); };
-            // the wave's edges: positions wb - 2, wb - 1 and we, we + 1
-            const uint64_t eL = wb >= 1 && wb - 1 < m ? (uint64_t)s[wb - 1] : 0;
-            const uint64_t eLL = wb >= 2 && wb - 2 < m ? (uint64_t)s[wb - 2] : 0;
-            const uint64_t eR = we < m ? (uint64_t)s[we] : 0;
-            const uint64_t eRR = we + 1 < m ? (uint64_t)s[we + 1] : 0;
-            // LE / FE bit i: item (i, lane) has the low bits / the whole rest
-            // of its left neighbour (position - 1)
-            uint32_t LE = 0, FE = 0, V = 0;
-#pragma unroll
-            for (int i = 0; i < IPT; i++) {
-                const uint32_t pos = pw + i * 64;
-                const uint64_t v = x[i];
-                const uint64_t left = wave_shr1(v, i ? rl64(x[i - 1], 63) : eL);
-                const bool ok = pos < m && pos > 0;
-                const bool le = ok && eq(left, v, lm);
-                LE |= (uint32_t)le << i;
-                FE |= (uint32_t)(le && eq(left, v, km)) << i;
-                V |= (uint32_t)(pos < m) << i;
-            }
-            // the same of position + 1 (RE, RF), of position - 1 (LL) and of
-            // position + 2 (RR): lane shifts, rows carried through lanes 0 / 63
-            const uint64_t vlast = rl64(x[IPT - 1], 63);
-            const bool eRle = we < m && eq(eR, vlast, lm), eRfe = eRle && eq(eR, vlast, km);
-            const bool eRRle = we + 1 < m && eq(eRR, eR, lm);
-            const bool eLle = wb >= 2 && wb - 1 < m && eq(eL, eLL, lm);
-            const uint32_t top = 1u << (IPT - 1);
-            const uint32_t RE = wave_shl1(LE, ((uint32_t)__builtin_amdgcn_readlane((int)LE, 0) >> 1) | (eRle ? top : 0u));
-            const uint32_t RF = wave_shl1(FE, ((uint32_t)__builtin_amdgcn_readlane((int)FE, 0) >> 1) | (eRfe ? top : 0u));
-            const uint32_t LL = wave_shr1(LE, ((uint32_t)__builtin_amdgcn_readlane((int)LE, 63) << 1) | (eLle ? 1u : 0u));
-            const uint32_t RR = wave_shl1(RE, ((uint32_t)__builtin_amdgcn_readlane((int)RE, 0) >> 1) | (eRRle ? top : 0u));
-            const uint32_t lng = ((LE & RE) | (LE & LL) | (RE & RR)) & V;  // in a run of three or more
-            uint32_t S = V & ~FE & ~RF & ~lng;
-            for (uint32_t sl = lng; sl;) {  // (rare: the exact scan over the run in LDS)
-                const int i = __ffs(sl) - 1;
-                sl &= sl - 1;
-                const uint32_t q = pw + (uint32_t)i * 64;
-                const uint64_t v = s[q];
-                bool single = true;
-                for (uint32_t a2 = q; single && a2 > 0;) {
-                    const uint64_t u = s[--a2];
-                    if (!eq(u, v, lm)) break;
-                    if (eq(u, v, km)) single = false;
-                }
-                for (uint32_t a2 = q + 1; single && a2 < m; a2++) {
-                    const uint64_t u = s[a2];
-                    if (!eq(u, v, lm)) break;
-                    if (eq(u, v, km)) single = false;
-                }
-                S |= (uint32_t)single << i;
-            }
-            if (CHK == 2 && r == hook && t == 0) S ^= 1u;  // (the check's own test: one wrong mark)
-            // (bit 63 is the top bit of the region's pass-1 digit before it
-            // becomes the mark: set or cleared on every item)
-#pragma unroll
-            for (int i = 0; i < IPT; i++) x[i] = (x[i] & ~(T)MARK) | (((S >> i) & 1u) ? (T)MARK : (T)0);
-            (void)block_exclusive_scan1<NT>((uint32_t)__popc(S), SumU32(), 0u, lds_scan2, &etot);
-            if (t == 0) publish_agg<0>(status, r, etot, epoch);
-    };
-    if constexpr (WIDE_OK) {
-        if (wide2) {
-            for (uint32_t p = 0; p < 2; p++) {
-                const uint32_t bw = p == 0 ? rest - W2B : W2B;
-                const uint32_t sh = Q + at, dm = (1u << bw) - 1;
-                at += bw;
-                uint32_t *const cbase = reinterpret_cast<uint32_t *>(&s[0]);
-                const bool blk = p == 0;
-                const uint32_t nwd = 1u << (bw - 1);  // counter words (u16 pairs) of one array
-                uint32_t *const wc = blk ? cbase : cbase + w * W2S;
-                if (!blk) __syncthreads();  // (every read of the items in s is done: the counters overwrite them)
-                if (blk) {
-                    for (uint32_t q = 4 * t; q < nwd; q += 4 * NT) *reinterpret_cast<uint4 *>(&wc[q]) = make_uint4(0, 0, 0, 0);
-                    __syncthreads();
-                } else {
-                    for (uint32_t q = 4 * lane; q < nwd; q += 256) *reinterpret_cast<uint4 *>(&wc[q]) = make_uint4(0, 0, 0, 0);
-                    __builtin_amdgcn_wave_barrier();
-                }
-                uint32_t rk[IPT];
-    #pragma unroll
-                for (int i = 0; i < IPT; i++) {
-                    const bool valid = pw + i * 64 < m;
-                    const uint32_t d = (uint32_t)(x[i] >> sh) & dm, hs = (d & 1u) * 16u;
-                    rk[i] = (atomicAdd(&wc[valid ? d >> 1 : nwd + lane], 1u << hs) >> hs) & 0xffffu;
-                }
-                __syncthreads();
-                if (blk) {
-                    // thread t: words [t wp, (t + 1) wp), wp = nwd / NT in 4..16
-                    // (digits in order: even digit in the low half)
-                    const uint32_t wp = nwd / NT;
-                    uint32_t *const mine = cbase + t * wp;
-                    uint32_t sum = 0;
-                    for (uint32_t q = 0; q < wp; q += 4) {
-                        const uint4 v = *reinterpret_cast<const uint4 *>(&mine[q]);
-                        sum += (v.x & 0xffffu) + (v.x >> 16) + (v.y & 0xffffu) + (v.y >> 16) + (v.z & 0xffffu) +
-                               (v.z >> 16) + (v.w & 0xffffu) + (v.w >> 16);
-                    }
-                    uint32_t run = block_exclusive_scan1<NT>(sum, SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
-                    auto starts = [&](uint32_t c) {  // a word of two counts -> a word of their two starts
-                        const uint32_t lo = run, hi = run + (c & 0xffffu);
-                        run = hi + (c >> 16);
-                        return lo | (hi << 16);
-                    };
-                    for (uint32_t q = 0; q < wp; q += 4) {
-                        const uint4 v = *reinterpret_cast<const uint4 *>(&mine[q]);
-                        uint4 o;
-                        o.x = starts(v.x);
-                        o.y = starts(v.y);
-                        o.z = starts(v.z);
-                        o.w = starts(v.w);
-                        *reinterpret_cast<uint4 *>(&mine[q]) = o;
-                    }
-                } else {
-                    // thread t: words [4t, 4t + 4) of every wave's array (digits
-                    // 8t .. 8t + 7); each wave's first slot per digit = digit
-                    // start + the earlier waves' counts (stable)
-                    uint32_t tot[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    #pragma unroll
-                    for (int ww = 0; ww < NW_; ww++) {
-                        const uint4 v = *reinterpret_cast<const uint4 *>(&cbase[ww * W2S + 4 * t]);
-                        tot[0] += v.x & 0xffffu, tot[1] += v.x >> 16, tot[2] += v.y & 0xffffu, tot[3] += v.y >> 16;
-                        tot[4] += v.z & 0xffffu, tot[5] += v.z >> 16, tot[6] += v.w & 0xffffu, tot[7] += v.w >> 16;
-                    }
-                    uint32_t run = block_exclusive_scan1<NT>(tot[0] + tot[1] + tot[2] + tot[3] + tot[4] + tot[5] + tot[6] +
-                                                                 tot[7],
-                                                             SumU32(), 0u, lds_scan, (uint32_t *)nullptr);
-                    uint32_t st[8];
-    #pragma unroll
-                    for (int j = 0; j < 8; j++) st[j] = run, run += tot[j];
-    #pragma unroll
-                    for (int ww = 0; ww < NW_; ww++) {
-                        uint4 *const a = reinterpret_cast<uint4 *>(&cbase[ww * W2S + 4 * t]);
-                        const uint4 v = *a;
-                        uint4 o;
-                        o.x = st[0] | (st[1] << 16), st[0] += v.x & 0xffffu, st[1] += v.x >> 16;
-                        o.y = st[2] | (st[3] << 16), st[2] += v.y & 0xffffu, st[3] += v.y >> 16;
-                        o.z = st[4] | (st[5] << 16), st[4] += v.z & 0xffffu, st[5] += v.z >> 16;
-                        o.w = st[6] | (st[7] << 16), st[6] += v.w & 0xffffu, st[7] += v.w >> 16;
-                        *a = o;
-                    }
-                }
-                __syncthreads();
-    #pragma unroll
-                for (int i = 0; i < IPT; i++) {
-                    const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
-                    rk[i] += (wc[d >> 1] >> ((d & 1u) * 16u)) & 0xffffu;
-                }
-                __syncthreads();  // (the block's slot reads before the first item lands on a counter)
-    #pragma unroll
-                for (int i = 0; i < IPT; i++)
-                    if (pw + i * 64 < m) s[rk[i]] = x[i];
-                __syncthreads();
-                if (p == 0) {
-#pragma unroll
-                    for (int i = 0; i < IPT; i++)
-                        if (pw + i * 64 < m) x[i] = s[pw + i * 64];
-                    if (early) early_marks();
-                }
-            }
-            p0 = np;
-        }
-    }
-    if constexpr (!W2)
     for (uint32_t p = p0; p < np; p++) {
         const uint32_t bw = two ? bw_two : (rest - at + (np - p) - 1) / (np - p);
         const uint32_t sh = Q + at, dm = (1u << bw) - 1;
         at += bw;
-        {
         // (two: the second pass's per-wave counters, 2^(bw - 1) <= 512 words)
         const uint32_t nwd = two ? 1u << (bw - 1) : (uint32_t)FWORD;
         if (TWO_OK && two) {
@@ -1120,14 +929,85 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        }  // (the per-wave passes of <= 9 bits)
         __syncthreads();
         if (p + 1 < np) {
 #pragma unroll
             for (int i = 0; i < IPT; i++)
                 if (pw + i * 64 < m) x[i] = s[pw + i * 64];
         }
-        if (early && p + 2 == np) early_marks();
+        if (early && p + 2 == np) {
+            // The items are sorted by their low `at` rest bits, and x holds
+            // them wave-striped (item (i, lane) at position pw + i * 64), so a
+            // neighbour in position is a neighbouring lane (DPP) or the next /
+            // previous row's edge lane (readlane); only the wave's two edges
+            // come from LDS.  A key is a singleton iff no item of its run of
+            // equal low bits has its whole rest: runs of one or two decide
+            // from the neighbours, the rare runs of three or more scan LDS.
+            const uint64_t lm = ((1ull << at) - 1) << Q, km = rmask << Q;
+            const uint32_t wb = (uint32_t)w * (IPT * 64), we = wb + IPT * 64;
+            auto rl64 = [](uint64_t v, int l) -> uint64_t {
+                return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+            };
+            auto eq = [](uint64_t a, uint64_t b, uint64_t mask) { return !((a ^ b) & mask); };
+            // the wave's edges: positions wb - 2, wb - 1 and we, we + 1
+            const uint64_t eL = wb >= 1 && wb - 1 < m ? (uint64_t)s[wb - 1] : 0;
+            const uint64_t eLL = wb >= 2 && wb - 2 < m ? (uint64_t)s[wb - 2] : 0;
+            const uint64_t eR = we < m ? (uint64_t)s[we] : 0;
+            const uint64_t eRR = we + 1 < m ? (uint64_t)s[we + 1] : 0;
+            // LE / FE bit i: item (i, lane) has the low bits / the whole rest
+            // of its left neighbour (position - 1)
+            uint32_t LE = 0, FE = 0, V = 0;
+#pragma unroll
+            for (int i = 0; i < IPT; i++) {
+                const uint32_t pos = pw + i * 64;
+                const uint64_t v = x[i];
+                const uint64_t left = wave_shr1(v, i ? rl64(x[i - 1], 63) : eL);
+                const bool ok = pos < m && pos > 0;
+                const bool le = ok && eq(left, v, lm);
+                LE |= (uint32_t)le << i;
+                FE |= (uint32_t)(le && eq(left, v, km)) << i;
+                V |= (uint32_t)(pos < m) << i;
+            }
+            // the same of position + 1 (RE, RF), of position - 1 (LL) and of
+            // position + 2 (RR): lane shifts, rows carried through lanes 0 / 63
+            const uint64_t vlast = rl64(x[IPT - 1], 63);
+            const bool eRle = we < m && eq(eR, vlast, lm), eRfe = eRle && eq(eR, vlast, km);
+            const bool eRRle = we + 1 < m && eq(eRR, eR, lm);
+            const bool eLle = wb >= 2 && wb - 1 < m && eq(eL, eLL, lm);
+            const uint32_t top = 1u << (IPT - 1);
+            const uint32_t RE = wave_shl1(LE, ((uint32_t)__builtin_amdgcn_readlane((int)LE, 0) >> 1) | (eRle ? top : 0u));
+            const uint32_t RF = wave_shl1(FE, ((uint32_t)__builtin_amdgcn_readlane((int)FE, 0) >> 1) | (eRfe ? top : 0u));
+            const uint32_t LL = wave_shr1(LE, ((uint32_t)__builtin_amdgcn_readlane((int)LE, 63) << 1) | (eLle ? 1u : 0u));
+            const uint32_t RR = wave_shl1(RE, ((uint32_t)__builtin_amdgcn_readlane((int)RE, 0) >> 1) | (eRRle ? top : 0u));
+            const uint32_t lng = ((LE & RE) | (LE & LL) | (RE & RR)) & V;  // in a run of three or more
+            uint32_t S = V & ~FE & ~RF & ~lng;
+            for (uint32_t sl = lng; sl;) {  // (rare: the exact scan over the run in LDS)
+                const int i = __ffs(sl) - 1;
+                sl &= sl - 1;
+                const uint32_t q = pw + (uint32_t)i * 64;
+                const uint64_t v = s[q];
+                bool single = true;
+                for (uint32_t a2 = q; single && a2 > 0;) {
+                    const uint64_t u = s[--a2];
+                    if (!eq(u, v, lm)) break;
+                    if (eq(u, v, km)) single = false;
+                }
+                for (uint32_t a2 = q + 1; single && a2 < m; a2++) {
+                    const uint64_t u = s[a2];
+                    if (!eq(u, v, lm)) break;
+                    if (eq(u, v, km)) single = false;
+                }
+                S |= (uint32_t)single << i;
+            }
+            if (CHK == 2 && r == hook && t == 0) S ^= 1u;  // (the check's own test: one wrong mark)
+            // (bit 63 is the top bit of the region's pass-1 digit before it
+            // becomes the mark: set or cleared on every item)
+#pragma unroll
+            for (int i = 0; i < IPT; i++) x[i] = (x[i] & ~(T)MARK) | (((S >> i) & 1u) ? (T)MARK : (T)0);
+            (void)block_exclusive_scan1<NT>((uint32_t)__popc(S), SumU32(), 0u, lds_scan2, &etot);
+            if (t == 0) publish_agg<0>(status, r, etot, epoch);
+        }
     }
     if (np == 0) {
 #pragma unroll
@@ -1387,10 +1267,10 @@ struct FinishArgs {
     bool in4 = false;  // 4-byte items (the pass wrote them narrow: only with the narrow finish, narrow_ok)
 };
 
-template <int MODE, typename O, int CAP, bool ATOMIC, typename T = uint64_t, int CHK = 0, bool W2 = false>
+template <int MODE, typename O, int CAP, bool ATOMIC, typename T = uint64_t, int CHK = 0>
 void launch_finish_as(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ovals, uint32_t epoch,
                       uint32_t *counter, uint32_t hook, uint64_t *stp) {
-    hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, T, CHK, CAP, W2>), dim3(f.nreg), dim3(FT), 0, ctx->stream, f.in, f.C1,
+    hipLaunchKernelGGL((rg_finish<MODE, O, ATOMIC, T, CHK, CAP>), dim3(f.nreg), dim3(FT), 0, ctx->stream, f.in, f.C1,
                        f.cnt, f.Q, f.rest, f.rc, f.rbase, f.tag_shift, f.fsub, okeys, (O *)ovals, ctx->d_status,
                        counter, epoch, ctx->d_err, hook, stp, f.nreg, f.freg, (uint32_t)f.in4);
 }
@@ -1432,28 +1312,6 @@ void launch_finish(kman_ctx *ctx, const FinishArgs &f, uint64_t *okeys, void *ov
     if (!ctx->lds_atomic_ordered) {
         launch_finish_as<MODE, O, CAP, false>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
         return;
-    }
-    // 8-byte items with 24..26 rest bits (uniq at k = 21) in an FCAP region:
-    // the two-pass finish (W2; KMAN_FIN_W2=0 keeps the three 9-bit passes)
-    if constexpr (CAP == FCAP) {
-        const char *e = getenv("KMAN_FIN_W2");
-        if (f.rest >= 24 && f.rest <= 26 && !(e && !strcmp(e, "0"))) {
-            if constexpr (MODE == RG_UNIQ) {
-                const EarlyCheck ck = early_check();
-                if (ck.chk == 1) {
-                    launch_finish_as<MODE, O, CAP, true, uint64_t, 1, true>(ctx, f, okeys, ovals, epoch, counter, ~0u,
-                                                                           stp);
-                    return;
-                }
-                if (ck.chk == 2) {
-                    launch_finish_as<MODE, O, CAP, true, uint64_t, 2, true>(ctx, f, okeys, ovals, epoch, counter,
-                                                                           ck.hook, stp);
-                    return;
-                }
-            }
-            launch_finish_as<MODE, O, CAP, true, uint64_t, 0, true>(ctx, f, okeys, ovals, epoch, counter, ~0u, stp);
-            return;
-        }
     }
     if constexpr (MODE == RG_UNIQ) {
         const EarlyCheck ck = early_check();
