@@ -768,7 +768,16 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     // to a word (a wave ranks <= 64 * IPT items), same-word LDS atomics of one
     // wave return in lane order (probed: ATOMIC), else ballot match-any.
     const bool two = TWO_OK && rest >= 2 && rest <= 21;
-    const uint32_t np = two ? 2u : (rest + FBITS - 1) / FBITS;
+    // U32C (8-byte items of an FCAP region: the uniq finish): a block-wide
+    // first pass of <= 11 bits, then 8-bit passes on u32 counters (below)
+#ifdef KMAN_FIN_U16
+    constexpr bool U32C = false;  // (A/B builds: the u16-pair counters, 9-bit passes)
+#else
+    constexpr bool U32C = PIPE;
+#endif
+    static_assert(!U32C || (NW_ * (FWORD + 64) >= 2048 + 64 && FWORD + 64 >= 256 + 64), "u32 counters fit wh");
+    static_assert(!U32C || NT * IPT <= CAP, "an item past m writes its own position");
+    const uint32_t np = two ? 2u : U32C ? (rest <= 11 ? 1u : 1u + (rest - 11 + 7) / 8) : (rest + FBITS - 1) / FBITS;
     const uint32_t bw_two = rest / 2;  // (two: the stable second pass's bits, <= 10)
     // EARLY (uniq): the region's row count is found after the second-to-last
     // pass, when equal keys already share a run of equal low bits (a run of
@@ -833,6 +842,167 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
             p0 = 1;
         }
     }
+    // EARLY's marks, after the second-to-last pass (items sorted by their low
+    // `at` rest bits, wave-striped in x)
+    auto early_marks = [&]() {
+            // The items are sorted by their low `at` rest bits, and x holds
+            // them wave-striped (item (i, lane) at position pw + i * 64), so a
+            // neighbour in position is a neighbouring lane (DPP) or the next /
+            // previous row's edge lane (readlane); only the wave's two edges
+            // come from LDS.  A key is a singleton iff no item of its run of
+            // equal low bits has its whole rest: runs of one or two decide
+            // from the neighbours, the rare runs of three or more scan LDS.
+            const uint64_t lm = ((1ull << at) - 1) << Q, km = rmask << Q;
+            const uint32_t wb = (uint32_t)w * (IPT * 64), we = wb + IPT * 64;
+            auto rl64 = [](uint64_t v, int l) -> uint64_t {
+                return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+            };
+            auto eq = [](uint64_t a, uint64_t b, uint64_t mask) { return !((a ^ b) & mask); };
+            // the wave's edges: positions wb - 2, wb - 1 and we, we + 1
+            const uint64_t eL = wb >= 1 && wb - 1 < m ? (uint64_t)s[wb - 1] : 0;
+            const uint64_t eLL = wb >= 2 && wb - 2 < m ? (uint64_t)s[wb - 2] : 0;
+            const uint64_t eR = we < m ? (uint64_t)s[we] : 0;
+            const uint64_t eRR = we + 1 < m ? (uint64_t)s[we + 1] : 0;
+            // LE / FE bit i: item (i, lane) has the low bits / the whole rest
+            // of its left neighbour (position - 1)
+            uint32_t LE = 0, FE = 0, V = 0;
+#pragma unroll
+            for (int i = 0; i < IPT; i++) {
+                const uint32_t pos = pw + i * 64;
+                const uint64_t v = x[i];
+                const uint64_t left = wave_shr1(v, i ? rl64(x[i - 1], 63) : eL);
+                const bool ok = pos < m && pos > 0;
+                const bool le = ok && eq(left, v, lm);
+                LE |= (uint32_t)le << i;
+                FE |= (uint32_t)(le && eq(left, v, km)) << i;
+                V |= (uint32_t)(pos < m) << i;
+            }
+            // the same of position + 1 (RE, RF), of position - 1 (LL) and of
+            // position + 2 (RR): lane shifts, rows carried through lanes 0 / 63
+            const uint64_t vlast = rl64(x[IPT - 1], 63);
+            const bool eRle = we < m && eq(eR, vlast, lm), eRfe = eRle && eq(eR, vlast, km);
+            const bool eRRle = we + 1 < m && eq(eRR, eR, lm);
+            const bool eLle = wb >= 2 && wb - 1 < m && eq(eL, eLL, lm);
+            const uint32_t top = 1u << (IPT - 1);
+            const uint32_t RE = wave_shl1(LE, ((uint32_t)__builtin_amdgcn_readlane((int)LE, 0) >> 1) | (eRle ? top : 0u));
+            const uint32_t RF = wave_shl1(FE, ((uint32_t)__builtin_amdgcn_readlane((int)FE, 0) >> 1) | (eRfe ? top : 0u));
+            const uint32_t LL = wave_shr1(LE, ((uint32_t)__builtin_amdgcn_readlane((int)LE, 63) << 1) | (eLle ? 1u : 0u));
+            const uint32_t RR = wave_shl1(RE, ((uint32_t)__builtin_amdgcn_readlane((int)RE, 0) >> 1) | (eRRle ? top : 0u));
+            const uint32_t lng = ((LE & RE) | (LE & LL) | (RE & RR)) & V;  // in a run of three or more
+            uint32_t S = V & ~FE & ~RF & ~lng;
+            for (uint32_t sl = lng; sl;) {  // (rare: the exact scan over the run in LDS)
+                const int i = __ffs(sl) - 1;
+                sl &= sl - 1;
+                const uint32_t q = pw + (uint32_t)i * 64;
+                const uint64_t v = s[q];
+                bool single = true;
+                for (uint32_t a2 = q; single && a2 > 0;) {
+                    const uint64_t u = s[--a2];
+                    if (!eq(u, v, lm)) break;
+                    if (eq(u, v, km)) single = false;
+                }
+                for (uint32_t a2 = q + 1; single && a2 < m; a2++) {
+                    const uint64_t u = s[a2];
+                    if (!eq(u, v, lm)) break;
+                    if (eq(u, v, km)) single = false;
+                }
+                S |= (uint32_t)single << i;
+            }
+            if (CHK == 2 && r == hook && t == 0) S ^= 1u;  // (the check's own test: one wrong mark)
+            // (bit 63 is the top bit of the region's pass-1 digit before it
+            // becomes the mark: set or cleared on every item)
+#pragma unroll
+            for (int i = 0; i < IPT; i++) x[i] = (x[i] & ~(T)MARK) | (((S >> i) & 1u) ? (T)MARK : (T)0);
+            (void)block_exclusive_scan1<NT>((uint32_t)__popc(S), SumU32(), 0u, lds_scan2, &etot);
+            if (t == 0) publish_agg<0>(status, r, etot, epoch);
+    };
+    if constexpr (U32C) {
+        // the 8-byte-item finish: a first pass by up to 11 bits on ONE
+        // block-wide array of u32 counters (unstable, as a first LSD pass may
+        // be), then stable passes of <= 8 bits on per-wave u32 counters (256
+        // words: no u16 halves to shift in and out); every item's LDS write
+        // and read unconditional (an item past m writes its own position,
+        // >= m, so no branch per item)
+        uint32_t *const flat = &wh[0][0];
+        for (uint32_t p = 0; p < np; p++) {
+            const bool blk = p == 0;
+            const uint32_t bw = blk ? rest - 8 * (np - 1) : 8u;
+            const uint32_t sh = Q + at, dm = (1u << bw) - 1;
+            at += bw;
+            const uint32_t nd = 1u << bw;  // counters of the array
+            uint32_t *const wc = blk ? flat : &wh[w][0];
+            if (blk) {
+                for (uint32_t q = t; q < nd; q += NT) flat[q] = 0;
+                __syncthreads();
+            } else {
+#pragma unroll
+                for (int q = 0; q < 256 / 64; q++) wc[lane + 64 * q] = 0;
+                __builtin_amdgcn_wave_barrier();
+            }
+            uint32_t rk[IPT];
+#pragma unroll
+            for (int i = 0; i < IPT; i++) {
+                const bool valid = pw + i * 64 < m;
+                const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
+                rk[i] = atomicAdd(&wc[valid ? d : nd + lane], 1u);
+            }
+            __syncthreads();
+            if (blk) {
+                // thread t: counters [t * cp, (t + 1) * cp), cp = nd / NT (<= 4)
+                const uint32_t cp = nd > (uint32_t)NT ? nd / NT : 1u;
+                uint32_t c[4] = {0, 0, 0, 0};
+                const uint32_t b0 = t * cp;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++)
+                    if (q < cp && b0 + q < nd) c[q] = flat[b0 + q];
+                uint32_t run = block_exclusive_scan1<NT>(c[0] + c[1] + c[2] + c[3], SumU32(), 0u, lds_scan,
+                                                         (uint32_t *)nullptr);
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++)
+                    if (q < cp && b0 + q < nd) flat[b0 + q] = run, run += c[q];
+            } else {
+                // thread t < 256: digit t -> its total over the waves, block
+                // scan -> digit start, each wave's first slot in place
+                uint32_t cw[NW_], tot = 0;
+                if (t < 256) {
+#pragma unroll
+                    for (int ww = 0; ww < NW_; ww++) tot += (cw[ww] = wh[ww][t]);
+                }
+                uint32_t run = block_exclusive_scan1<NT>(t < 256 ? tot : 0u, SumU32(), 0u, lds_scan,
+                                                         (uint32_t *)nullptr);
+                if (t < 256) {
+#pragma unroll
+                    for (int ww = 0; ww < NW_; ww++) wh[ww][t] = run, run += cw[ww];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < IPT; i++) rk[i] += wc[(uint32_t)(x[i] >> sh) & dm];
+#ifdef KMAN_FIN_UNCOND
+#pragma unroll
+            for (int i = 0; i < IPT; i++) {
+                const uint32_t pos = pw + i * 64;
+                s[pos < m ? rk[i] : pos] = x[i];
+            }
+#else
+            // (only the items: the slot grid past m is 12-14 % of a region's
+            // LDS, and writing it unconditionally cost more LDS cycles than
+            // the branches: 5.72 vs 5.21 ms, `r06e`)
+#pragma unroll
+            for (int i = 0; i < IPT; i++)
+                if (pw + i * 64 < m) s[rk[i]] = x[i];
+#endif
+            __syncthreads();
+            if (p + 1 < np) {
+#pragma unroll
+                for (int i = 0; i < IPT; i++)
+                    if (pw + i * 64 < m) x[i] = s[pw + i * 64];
+            }
+            if (early && p + 2 == np) early_marks();
+        }
+    }
+    if constexpr (!U32C)
     for (uint32_t p = p0; p < np; p++) {
         const uint32_t bw = two ? bw_two : (rest - at + (np - p) - 1) / (np - p);
         const uint32_t sh = Q + at, dm = (1u << bw) - 1;
@@ -935,79 +1105,7 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
             for (int i = 0; i < IPT; i++)
                 if (pw + i * 64 < m) x[i] = s[pw + i * 64];
         }
-        if (early && p + 2 == np) {
-            // The items are sorted by their low `at` rest bits, and x holds
-            // them wave-striped (item (i, lane) at position pw + i * 64), so a
-            // neighbour in position is a neighbouring lane (DPP) or the next /
-            // previous row's edge lane (readlane); only the wave's two edges
-            // come from LDS.  A key is a singleton iff no item of its run of
-            // equal low bits has its whole rest: runs of one or two decide
-            // from the neighbours, the rare runs of three or more scan LDS.
-            const uint64_t lm = ((1ull << at) - 1) << Q, km = rmask << Q;
-            const uint32_t wb = (uint32_t)w * (IPT * 64), we = wb + IPT * 64;
-            auto rl64 = [](uint64_t v, int l) -> uint64_t {
-                return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
-                       (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
-            };
-            auto eq = [](uint64_t a, uint64_t b, uint64_t mask) { return !((a ^ b) & mask); };
-            // the wave's edges: positions wb - 2, wb - 1 and we, we + 1
-            const uint64_t eL = wb >= 1 && wb - 1 < m ? (uint64_t)s[wb - 1] : 0;
-            const uint64_t eLL = wb >= 2 && wb - 2 < m ? (uint64_t)s[wb - 2] : 0;
-            const uint64_t eR = we < m ? (uint64_t)s[we] : 0;
-            const uint64_t eRR = we + 1 < m ? (uint64_t)s[we + 1] : 0;
-            // LE / FE bit i: item (i, lane) has the low bits / the whole rest
-            // of its left neighbour (position - 1)
-            uint32_t LE = 0, FE = 0, V = 0;
-#pragma unroll
-            for (int i = 0; i < IPT; i++) {
-                const uint32_t pos = pw + i * 64;
-                const uint64_t v = x[i];
-                const uint64_t left = wave_shr1(v, i ? rl64(x[i - 1], 63) : eL);
-                const bool ok = pos < m && pos > 0;
-                const bool le = ok && eq(left, v, lm);
-                LE |= (uint32_t)le << i;
-                FE |= (uint32_t)(le && eq(left, v, km)) << i;
-                V |= (uint32_t)(pos < m) << i;
-            }
-            // the same of position + 1 (RE, RF), of position - 1 (LL) and of
-            // position + 2 (RR): lane shifts, rows carried through lanes 0 / 63
-            const uint64_t vlast = rl64(x[IPT - 1], 63);
-            const bool eRle = we < m && eq(eR, vlast, lm), eRfe = eRle && eq(eR, vlast, km);
-            const bool eRRle = we + 1 < m && eq(eRR, eR, lm);
-            const bool eLle = wb >= 2 && wb - 1 < m && eq(eL, eLL, lm);
-            const uint32_t top = 1u << (IPT - 1);
-            const uint32_t RE = wave_shl1(LE, ((uint32_t)__builtin_amdgcn_readlane((int)LE, 0) >> 1) | (eRle ? top : 0u));
-            const uint32_t RF = wave_shl1(FE, ((uint32_t)__builtin_amdgcn_readlane((int)FE, 0) >> 1) | (eRfe ? top : 0u));
-            const uint32_t LL = wave_shr1(LE, ((uint32_t)__builtin_amdgcn_readlane((int)LE, 63) << 1) | (eLle ? 1u : 0u));
-            const uint32_t RR = wave_shl1(RE, ((uint32_t)__builtin_amdgcn_readlane((int)RE, 0) >> 1) | (eRRle ? top : 0u));
-            const uint32_t lng = ((LE & RE) | (LE & LL) | (RE & RR)) & V;  // in a run of three or more
-            uint32_t S = V & ~FE & ~RF & ~lng;
-            for (uint32_t sl = lng; sl;) {  // (rare: the exact scan over the run in LDS)
-                const int i = __ffs(sl) - 1;
-                sl &= sl - 1;
-                const uint32_t q = pw + (uint32_t)i * 64;
-                const uint64_t v = s[q];
-                bool single = true;
-                for (uint32_t a2 = q; single && a2 > 0;) {
-                    const uint64_t u = s[--a2];
-                    if (!eq(u, v, lm)) break;
-                    if (eq(u, v, km)) single = false;
-                }
-                for (uint32_t a2 = q + 1; single && a2 < m; a2++) {
-                    const uint64_t u = s[a2];
-                    if (!eq(u, v, lm)) break;
-                    if (eq(u, v, km)) single = false;
-                }
-                S |= (uint32_t)single << i;
-            }
-            if (CHK == 2 && r == hook && t == 0) S ^= 1u;  // (the check's own test: one wrong mark)
-            // (bit 63 is the top bit of the region's pass-1 digit before it
-            // becomes the mark: set or cleared on every item)
-#pragma unroll
-            for (int i = 0; i < IPT; i++) x[i] = (x[i] & ~(T)MARK) | (((S >> i) & 1u) ? (T)MARK : (T)0);
-            (void)block_exclusive_scan1<NT>((uint32_t)__popc(S), SumU32(), 0u, lds_scan2, &etot);
-            if (t == 0) publish_agg<0>(status, r, etot, epoch);
-        }
+        if (early && p + 2 == np) early_marks();
     }
     if (np == 0) {
 #pragma unroll
