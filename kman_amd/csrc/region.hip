@@ -63,7 +63,10 @@ constexpr uint32_t B1 = 8;        // pass-0 digit: top 8 key bits
 // ms, and the 512-bucket pass 0 4.0 vs 3.6 ms)
 // (Round 5, with the cursor adds cheap: 9 + 8 bits measured equal to 8 + 9,
 // `r05xy_pass_geometry_ab.txt`)
-constexpr uint32_t G1 = B1;
+#ifndef KMAN_G1
+#define KMAN_G1 8
+#endif
+constexpr uint32_t G1 = KMAN_G1;
 // finish capacities (items): FCAP (68 KiB of 8-byte items, two blocks per
 // CU) and GCAP (40 KiB, three blocks per CU) for the round path's small
 // regions (a pass 1b over many ranks' items leaves ~4 K per region)
@@ -371,6 +374,7 @@ struct PassArgs {
     // path then leaves them out and redoes only their keys)
     uint8_t *fail;
     uint32_t fail_div, fail_shift;
+    uint32_t big;  // a pass of <= 8 bits on the 1024-thread instance anyway (8192-item tiles: 256-byte digit runs)
 };
 
 // Persistent 1024-thread blocks (one per CU; 141 KiB of LDS), block-owned
@@ -1289,7 +1293,9 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
     // B2: fewest bits with an expected region fill <= FFILL_T (at most 9); up
     // to FFILL_M expected keeps > 10 sd (uniform data) below the capacity
     uint32_t b2 = 1;
-    while (b2 < 9 && (p.W >> (G1 + b2)) > FFILL_T) b2++;
+    // (17 region bits in all while their fill stays <= FFILL_M: the finish's
+    // per-region costs make more, smaller regions slower)
+    while (b2 < 9 && (p.W >> (G1 + b2)) > FFILL_T && (G1 + b2 < 17 || (p.W >> (G1 + b2)) > FFILL_M)) b2++;
     if ((p.W >> (G1 + b2)) > FFILL_M) return KMAN_EFALLBACK;
     if (p.K < G1 + b2 + 1) return KMAN_EFALLBACK;
     p.B2 = b2;
@@ -1330,7 +1336,7 @@ template <typename TI, typename TO>
 void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint64_t *stp) {
     // radix <= 256: the 512-thread instance, two blocks per CU (KMAN_PASS_SMALL=0: the 1024-thread one)
     static const bool small_ok = !getenv("KMAN_PASS_SMALL") || strcmp(getenv("KMAN_PASS_SMALL"), "0") != 0;
-    if (small_ok && pa.bits <= 8) {
+    if (small_ok && pa.bits <= 8 && !pa.big) {
         const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, (const void *)rg_pass<TI, TO, 512, 256>, 512,
                                                              (uint64_t)pa.nbk * pa.H);
         hipLaunchKernelGGL((rg_pass<TI, TO, 512, 256>), dim3(grid), dim3(512), 0, ctx->stream, pa, counter,
@@ -1637,6 +1643,7 @@ int groups_tail(kman_ctx *ctx, const GroupsCall &g, int mode, uint64_t *d_okeys,
         pa.out = g.r1;
         pa.C1 = p.C1h;
         pa.cnt1 = g.c1;
+        pa.big = 1;
         launch_pass(ctx, pa, counter, stamps[1], false, narrow4);
         HIP_TRY(ctx, hipGetLastError());
     }
