@@ -652,7 +652,11 @@ class DistPipeline:
         S_ = self.pieces
         # overlapped rounds hold a piece's two scratch arenas beside A and B
         # (about 2 / S of them): their plan leaves room for those
-        ov_scale = 1.0 + 2.0 / S_ if (self.overlap and self.path == "region") else 1.0
+        # (a piece holds about 1 / S of a round's items: its two scratch
+        # arenas about (a + b) / S, planned here with a margin; each round
+        # checks the pieces' real plans against the budget before it runs
+        # overlapped, _overlapped_round)
+        ov_scale = 1.0 + 1.25 / S_ if (self.overlap and self.path == "region") else 1.0
         R, cuts, a_need, b_need = pl.plan(C, max(1, int((self.budget - out_bytes) / ov_scale)), self.max_round_items)
         self.rounds = R
         self.plan_info = {"budget_gb": self.budget / 1e9, "out_gb": out_bytes / 1e9, "arena_a_gb": a_need / 1e9,
@@ -797,6 +801,14 @@ class DistPipeline:
                 bad |= ret != N.KMAN_OK
             plans.append(cnt)
             a2, b2 = max(a2, int(a.value)), max(b2, int(b.value))
+        # the round's arenas plus the pieces' must fit this rank's budget (the
+        # plan's margin is an estimate): otherwise every rank runs this round
+        # the sequential way
+        rtab_, sc_, _ = round_send(H, cuts, G, R, r)
+        _, _, _, rcnt_, _ = round_recv(C, cuts, R, me, r)
+        need = (max(a_need, 8 * int(sc_.sum())) + max(b_need, 8 * int(rcnt_.sum())) + a2 + b2
+                + self.out_keys.buf.nbytes + self.out_vals.buf.nbytes)
+        bad |= need > self.budget
         f = yield ("allreduce", np.array([bad], np.uint64))
         if int(f[0]):
             return None
