@@ -669,7 +669,13 @@ def run_dist(args, world: int, rank: int, local: int):
                                    % (ln["fasta_bytes"] / 1e9, world, per / 1e9, args.k,
                                       "canonical count + all-reduced abundance spectrum (config 5's pipeline)"
                                       if canon else args.mode,
-                                      " + one RCCL all-to-all per round" if ln.get("exchange") else
+                                      (" + one all-to-all per round (kman_alltoallv: RCCL send/recv between "
+                                       "ranks, each rank's own part a device-to-device copy%s)"
+                                       % ("; at one rank the whole exchange is that copy"
+                                          if world == 1 and os.environ.get("KMAN_RCCL_SELF") != "1" else
+                                          "; KMAN_RCCL_SELF=1: the own part through RCCL too"
+                                          if os.environ.get("KMAN_RCCL_SELF") == "1" else ""))
+                                      if ln.get("exchange") else
                                       " without an exchange (one rank, --exchange off: a one-GPU-only shortcut, "
                                       "not the per-rank step of an N > 1 run)",
                                       "" if not canon else "; the synthetic input stands in for GRCh38"),

@@ -140,7 +140,7 @@ def _fake_line(calls):
                "fasta_bytes_per_rank": per, "path": "region", "rounds": 3 if mode == "count" else 1,
                "fallback_rounds": 0, "partial_rounds": 0, "memory_plan": None, "stages_ms_per_step_rank0": {},
                "stage_alg_bytes_rank0": {}, "roofline": {"frac": 0.5}, "sort_pass_roofline": {"frac": 0.6},
-               "spectrum_distinct": None, "exchange": world > 1, "exchanged_bytes_per_step": 8 * per,
+               "spectrum_distinct": None, "exchange": args.exchange == "on", "exchanged_bytes_per_step": 8 * per,
                "max_message_bytes": per, "exchange_gbs_rank0": 100.0}
         if also_overlap:
             out["overlapped"] = {"value": 1.1e9 * world, "ms_per_step": 9.0, "steps": steps,
@@ -182,7 +182,8 @@ def test_multi_gpu_line_carries_config4_and_rccl_ranks(monkeypatch, capsys):
     for ln in (out["config"], c4):
         assert ln["overlapped"]["ms_per_step"] > 0 and ln["overlapped"]["overlapped_rounds"] >= 1
     assert c4["overlapped"]["rounds"] == 3 and out["config"]["exchange"] is True
-    assert "one RCCL all-to-all per round" in out["config"]["workload"]
+    assert "one all-to-all per round (kman_alltoallv: RCCL send/recv between ranks" in out["config"]["workload"]
+    assert "at one rank" not in out["config"]["workload"]
     # the other ranks run both lines and print nothing
     calls.clear()
     bench.run_dist(args, 8, 3, 3)
@@ -195,3 +196,5 @@ def test_multi_gpu_line_carries_config4_and_rccl_ranks(monkeypatch, capsys):
         out = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
         assert len(calls) == 1 and "config4" not in out and out["config"]["rccl_ranks"] == world
         assert calls[0]["also_overlap"] == (world > 1)
+        if world == 1:
+            assert "at one rank the whole exchange is that copy" in out["config"]["workload"]
