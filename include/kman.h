@@ -345,6 +345,29 @@ int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_t k, uint32
  * kman_extract_marked + kman_sort_range + kman_finish and merge in
  * (kman_merge_runs). */
 int kman_dround_failed(kman_ctx *ctx, uint64_t *ranges, uint64_t cap, uint64_t *n);
+/* Heavy keys of the last kman_dround_finish (*n; 0 when none or off): keys
+ * that every S-th received item's sample saw at least twice (at most 2048,
+ * the most often sampled) are counted apart in its pass 1 -- count mode
+ * keeps one copy per pass-1 chain and adds the others to the key's row after
+ * the finish, uniq mode drops them all (they occur more than once) -- so a
+ * repeat with 10^5 copies does not overflow its regions.  KMAN_HEAVY=0 turns
+ * it off, KMAN_HEAVY=1 applies it to rounds of any size (default: >= 2^20
+ * items).  Not in the reference: the rows are the same either way. */
+int kman_dround_heavy(kman_ctx *ctx, uint32_t *n);
+/* After kman_dround_finish (before its arena A is reused): the items of the
+ * regions it left out, gathered from its pass-1 output instead of
+ * re-extracted from the codes (kman_extract_marked) -- full keys in d_keys
+ * and, uniq, the pos its finish would have emitted in d_pos; *n = items
+ * (NULL d_keys: count only; cap = room in d_keys / d_pos).  KMAN_EFALLBACK
+ * when its pass 1 itself overflowed (its output lacks items): then the
+ * marked extraction.  The items' sort + run-length rows equal the left-out
+ * regions' rows once kman_dround_heavy_fix has added the heavy keys' dropped
+ * copies (count mode).  Not in the reference. */
+int kman_dround_left(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_pos, uint64_t cap, uint64_t *n);
+/* Adds the last kman_dround_finish's heavy keys' dropped copies to the rows
+ * (d_keys sorted) that hold them: for rows built from kman_dround_left's
+ * items (count mode; uniq rows and rows recounted from the codes need none). */
+int kman_dround_heavy_fix(kman_ctx *ctx, const uint64_t *d_keys, void *d_vals, uint32_t val_bytes, uint64_t n);
 
 /* Abundance spectrum of a count output (BASELINE config 5; not
  * in the reference): d_hist[c] = number of distinct k-mers seen c times, the

@@ -152,6 +152,9 @@ SIGNATURES = {
          c_uint64, c_void_p, c_uint64, c_void_p, c_void_p, c_uint32, POINTER(c_uint64)],
     ),
     "kman_dround_failed": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
+    "kman_dround_heavy": (c_int, [c_void_p, POINTER(c_uint32)]),
+    "kman_dround_left": (c_int, [c_void_p, c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
+    "kman_dround_heavy_fix": (c_int, [c_void_p, c_void_p, c_void_p, c_uint32, c_uint64]),
     "kman_extract_marked": (
         c_int,
         [c_void_p, c_void_p, c_uint64, c_uint32, c_uint32, c_void_p, c_uint32, c_uint32, c_void_p, c_void_p, c_uint32,

@@ -67,6 +67,25 @@ struct kman_ctx {
     // key ranges [lo, hi] (pairs) that the last kman_dround_finish left out
     // (KMAN_EPARTIAL): regions that overflowed a capacity
     std::vector<uint64_t> failed;
+    // heavy keys of the last kman_dround_finish (counted apart in its pass 1)
+    // and their scratch (table, drop counts, samples)
+    uint32_t heavy_keys = 0;
+    int heavy_mode = 0;
+    void *d_hv = nullptr;
+    size_t hv_bytes = 0;
+    // the last kman_dround_finish's pass-1 output, for kman_dround_left (its
+    // left-out regions' items gathered from there): valid when pass 1 lost
+    // nothing; bd = the (bucket, digit) sub-buckets whose regions were left out
+    struct LeftRound {
+        bool valid = false;
+        const void *r1 = nullptr;
+        const uint32_t *c1 = nullptr;
+        uint64_t C1s = 0;
+        uint32_t nb = 0, G = 0, H = 0, K = 0, Q = 0, b_lo = 0;
+        bool rc = false, narrow = false;
+        int mode = 0;
+        std::vector<uint32_t> bd;
+    } left;
     // kman_groups_begin .. kman_groups_end: pass 0 by tile ranges as the
     // codes arrive (the look-back epoch it runs in, the next tile)
     uint32_t grp_epoch = 0;

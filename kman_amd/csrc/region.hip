@@ -375,7 +375,25 @@ struct PassArgs {
     uint8_t *fail;
     uint32_t fail_div, fail_shift;
     uint32_t big;  // a pass of <= 8 bits on the 1024-thread instance anyway (8192-item tiles: 256-byte digit runs)
+    // optional (pass 1 of a key round, rg_pass<..., HV = true): the heavy
+    // keys of the round (hv_keys: an open-addressing table of HV_SLOTS full
+    // keys, HV_EMPTY where free).  An item whose key ((hv_base + b / gsub) <<
+    // hv_kb | item >> hv_q) is in it is counted in LDS per chain; count mode
+    // keeps the chain's first copy (hv_keep = 1) and drops the rest, uniq mode
+    // drops every copy (a heavy key occurs more than once: no uniq row); the
+    // dropped copies are added to hv_drop[slot] when the chain ends
+    const uint64_t *hv_keys;
+    uint64_t *hv_drop;
+    uint32_t hv_base, hv_kb, hv_q, hv_keep;
 };
+
+// heavy keys of a key round (kman_dround_finish): found by sampling the
+// received items, counted apart in pass 1 so that a satellite or repeat-family
+// k-mer with 10^5 copies does not overflow its regions (and send the key range
+// through the partial redo)
+constexpr uint32_t HV_SLOTS = 4096, HV_MAX = 2048;
+constexpr uint64_t HV_EMPTY = ~0ull;
+__host__ __device__ inline uint32_t hv_hash(uint64_t key) { return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 52); }
 
 // Persistent 1024-thread blocks (one per CU; 141 KiB of LDS), block-owned
 // chains: a block takes a whole chain (bucket b, part h: the h-th of H runs of
@@ -405,7 +423,7 @@ struct PassArgs {
 // lines, ~69 KiB: two blocks per CU, so one block's loads, rank and scatter
 // run while the other's stores stream)
 constexpr int PT_NT = 1024, PT_SI = 8;
-template <typename TI, typename TO, int NT_ = PT_NT, int RB = R1>
+template <typename TI, typename TO, int NT_ = PT_NT, int RB = R1, bool HV = false>
 __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
                                                  uint32_t *__restrict__ err, uint64_t *__restrict__ stp) {
     constexpr int NT = NT_, SI = PT_SI, TILE = NT * SI, NWAVE = NT / 64;
@@ -439,6 +457,8 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
     __shared__ uint32_t lds_scan[NWAVE];
     __shared__ uint32_t s_items;
     __shared__ uint32_t lds_tile;
+    // HV: the chain's copies of each heavy key (by table slot)
+    __shared__ uint32_t hcnt[HV ? HV_SLOTS : 1];
     const uint32_t shift = pa.shift, bits = pa.bits, nsg = pa.nsg, H = pa.H;
     const uint64_t C1 = pa.C1;
     const int lane = lane_id();
@@ -465,6 +485,8 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
             if (threadIdx.x == 63) s_items = inc;
         }
         if (threadIdx.x < RB) run[threadIdx.x] = 0;
+        if constexpr (HV)
+            for (uint32_t s = threadIdx.x; s < HV_SLOTS; s += NT) hcnt[s] = 0;
         __syncthreads();
         const uint32_t items = s_items;
         const uint32_t tiles = (items + TILE - 1) / TILE;
@@ -553,8 +575,31 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
                 }
             }
 #define PDIGIT(x) ((uint32_t)((x) >> shift) & dmask)
+            // the items that stay (bit i): all but dropped heavy copies
+            uint32_t vm = 0;
 #pragma unroll
-            for (int i = 0; i < SI; i++) rank[i] = ib + i * 64 < n ? atomicAdd(&thist[PDIGIT(key[i])], 1u) : 0u;
+            for (int i = 0; i < SI; i++) vm |= (ib + i * 64 < n ? 1u : 0u) << i;
+            if constexpr (HV) {
+                const uint64_t hb = (uint64_t)(pa.hv_base + b / pa.gsub) << pa.hv_kb;
+#pragma unroll
+                for (int i = 0; i < SI; i++) {
+                    if (!((vm >> i) & 1u)) continue;
+                    const uint64_t full = hb | ((uint64_t)key[i] >> pa.hv_q);
+                    uint32_t sl = hv_hash(full);
+                    for (;;) {
+                        const uint64_t t = pa.hv_keys[sl];
+                        if (t == full) {
+                            const uint32_t old = atomicAdd(&hcnt[sl], 1u);
+                            if (!(pa.hv_keep && old == 0)) vm &= ~(1u << i);
+                            break;
+                        }
+                        if (t == HV_EMPTY) break;
+                        sl = (sl + 1) & (HV_SLOTS - 1);
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < SI; i++) rank[i] = (vm >> i) & 1u ? atomicAdd(&thist[PDIGIT(key[i])], 1u) : 0u;
             __syncthreads();
             const uint32_t ls = block_exclusive_scan1<NT>(threadIdx.x < RB ? thist[threadIdx.x] : 0u, SumU32(), 0u,
                                                           lds_scan, (uint32_t *)nullptr);
@@ -562,7 +607,9 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
             __syncthreads();
 #pragma unroll
             for (int i = 0; i < SI; i++)
-                if (ib + i * 64 < n) skeys[lstart[PDIGIT(key[i])] + rank[i]] = key[i];
+                if ((vm >> i) & 1u) skeys[lstart[PDIGIT(key[i])] + rank[i]] = key[i];
+            // (HV: the tile's items that stay, packed at the front of skeys)
+            const uint32_t nk = HV ? lstart[RB - 1] + thist[RB - 1] : n;
             __syncthreads();
             RSTAMP(r, 1);
             // a digit whose partial line completes in this tile: its pending
@@ -591,7 +638,7 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
 #pragma unroll
             for (int rr = 0; rr < SI; rr++) {
                 const uint32_t q = threadIdx.x + rr * NT;
-                if (q < n) {
+                if (q < nk) {
                     const uint64_t kk = skeys[q];
                     const uint32_t d = PDIGIT(kk);
                     const uint64_t qp = qpar[d];
@@ -630,6 +677,14 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
                 }
             }
             if (d < radix) pa.cnt1[SUBREG(d)] = run[d] < C1 ? run[d] : (uint32_t)C1;
+        }
+        if constexpr (HV) {
+            // the chain's dropped copies of each heavy key (hcnt is cleared by
+            // the next chain only after grab_tile's barriers)
+            for (uint32_t s = threadIdx.x; s < HV_SLOTS; s += NT) {
+                const uint32_t c = hcnt[s];
+                if (c > pa.hv_keep) atomicAdd((unsigned long long *)&pa.hv_drop[s], (unsigned long long)(c - pa.hv_keep));
+            }
         }
 #undef SUBREG
     }
@@ -1334,6 +1389,15 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
 
 template <typename TI, typename TO>
 void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint64_t *stp) {
+    if constexpr (sizeof(TI) == 8) {
+        if (pa.hv_keys) {  // (pass 1 of a key round with heavy keys: 9 bits, the 1024-thread instance)
+            const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, (const void *)rg_pass<TI, TO, PT_NT, R1, true>,
+                                                                 PT_NT, (uint64_t)pa.nbk * pa.H);
+            hipLaunchKernelGGL((rg_pass<TI, TO, PT_NT, R1, true>), dim3(grid), dim3(PT_NT), 0, ctx->stream, pa, counter,
+                               ctx->d_err, stp);
+            return;
+        }
+    }
     // radix <= 256: the 512-thread instance, two blocks per CU (KMAN_PASS_SMALL=0: the 1024-thread one)
     static const bool small_ok = !getenv("KMAN_PASS_SMALL") || strcmp(getenv("KMAN_PASS_SMALL"), "0") != 0;
     if (small_ok && pa.bits <= 8 && !pa.big) {
@@ -2088,7 +2152,7 @@ void launch_extract_ex(kman_ctx *ctx, const RegionPlan &p, const uint8_t *codes,
 // repeat fills, which overflow at any g and are redone by key range), never
 // above the plan's.  Pass 1 flagged overflowing sub-buckets per (b, d);
 // they are spread over their 2^g regions here.
-int refit_g(kman_ctx *ctx, RoundPlan &d, const uint32_t *c1, uint8_t *freg, uint32_t G) {
+int refit_g(kman_ctx *ctx, RoundPlan &d, const uint32_t *c1, uint8_t *freg, uint32_t G, bool *p1_lost) {
     const uint64_t nbd = (uint64_t)d.nb * 512, gh = (uint64_t)G * d.H;
     std::vector<uint32_t> hc(d.nsub);
     std::vector<uint8_t> hf(nbd);
@@ -2132,6 +2196,7 @@ int refit_g(kman_ctx *ctx, RoundPlan &d, const uint32_t *c1, uint8_t *freg, uint
     // pass 1's (b, d) flags -> the regions they feed
     bool any = false;
     for (uint64_t j = 0; j < nbd; j++) any |= hf[j] != 0;
+    *p1_lost = any;
     if (any) {
         std::vector<uint8_t> fr(d.nreg, 0);
         for (uint64_t j = 0; j < nbd; j++)
@@ -2141,6 +2206,221 @@ int refit_g(kman_ctx *ctx, RoundPlan &d, const uint32_t *c1, uint8_t *freg, uint
     } else {
         HIP_TRY(ctx, hipMemsetAsync(freg, 0, nbd, ctx->stream));
     }
+    return KMAN_OK;
+}
+
+// ---------------------------------------------------------------- heavy keys
+// A key round's heavy keys (PassArgs::hv_keys): every S-th received item's
+// full key is sampled, the samples sorted and run-length counted, and the
+// keys sampled at least twice (so they occur at least twice: a uniq round may
+// drop all their copies) -- at most HV_MAX of them, the most often sampled --
+// go into an open-addressing table that pass 1 probes per item.  Pass 1 adds
+// each key's dropped copies to drop[slot]; rg_hv_fix then adds them to the
+// key's row (count mode: pass 1 kept one copy per chain, so the row exists
+// unless its region was left out, in which case the partial redo recounts
+// the whole key range from the codes).
+constexpr uint32_t HV_CAND = 1u << 16;  // candidates downloaded to pick the table from
+
+// sample i = the item at i * S; runs (src, j) lie in src-major order, run t =
+// src * nb + j starting at rs[t] (the last run starting at or before p holds p)
+__global__ __launch_bounds__(256) void rg_hv_sample(const uint64_t *__restrict__ in, const uint64_t *__restrict__ rs,
+                                                    uint32_t nrun, uint32_t nb, uint64_t S, uint64_t ns, uint32_t b_lo,
+                                                    uint32_t kb, uint32_t q, uint64_t *__restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= ns) return;
+    const uint64_t p = i * S;
+    uint32_t lo = 0, hi = nrun;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (rs[mid] <= p) lo = mid;
+        else hi = mid;
+    }
+    out[i] = ((uint64_t)(b_lo + lo % nb) << kb) | (in[p] >> q);
+}
+
+// hist[min(c, 63)] of the sample counts >= 2; with T > 0, the keys sampled
+// >= T times into cand (key, count), at most HV_CAND (ncand counts them all)
+__global__ __launch_bounds__(256) void rg_hv_select(const uint64_t *__restrict__ ukeys,
+                                                    const uint32_t *__restrict__ cnt, uint64_t nu, uint32_t T,
+                                                    uint32_t *__restrict__ hist, uint32_t *__restrict__ ncand,
+                                                    uint64_t *__restrict__ cand) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= nu) return;
+    const uint32_t c = cnt[i];
+    if (c < 2) return;
+    if (!T) {
+        atomicAdd(&hist[c < 63 ? c : 63], 1u);
+        return;
+    }
+    if (c < T) return;
+    const uint32_t at = atomicAdd(ncand, 1u);
+    if (at < HV_CAND) {
+        cand[2 * at] = ukeys[i];
+        cand[2 * at + 1] = c;
+    }
+}
+
+// each heavy key's dropped copies onto its row (rows sorted by key)
+template <typename V>
+__global__ __launch_bounds__(256) void rg_hv_fix(const uint64_t *__restrict__ tab, const uint64_t *__restrict__ drop,
+                                                 const uint64_t *__restrict__ okeys, V *__restrict__ ovals,
+                                                 uint64_t n) {
+    const uint32_t s = blockIdx.x * 256 + threadIdx.x;
+    if (s >= HV_SLOTS) return;
+    const uint64_t key = tab[s], d = drop[s];
+    if (key == HV_EMPTY || !d || !n) return;
+    uint64_t lo = 0, hi = n;  // first row >= key
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (okeys[mid] < key) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo < n && okeys[lo] == key) ovals[lo] += (V)d;
+}
+
+// kman_dround_left: the items of the left-out sub-buckets' pass-1
+// sub-regions (bd, src, h) = subs[i] as full keys (+ uniq pos, as the finish
+// emits them), sub-region i at offs[i]
+template <typename TI>
+__global__ __launch_bounds__(256) void rg_left_gather(const TI *__restrict__ r1, uint64_t C1s,
+                                                      const uint32_t *__restrict__ subs,
+                                                      const uint32_t *__restrict__ cnts,
+                                                      const uint64_t *__restrict__ offs, uint32_t G, uint32_t H,
+                                                      uint32_t b_lo, uint32_t kb, uint32_t Q, uint32_t rc,
+                                                      uint64_t *__restrict__ okeys, uint64_t *__restrict__ opos) {
+    const uint32_t i = blockIdx.x;
+    const uint32_t s = subs[i], n = cnts[i];
+    const uint32_t bd = s / (G * H), src = (s / H) % G;
+    const uint64_t hi = (uint64_t)(b_lo + (bd >> 9)) << kb;
+    const uint64_t kmask = (1ull << kb) - 1, qmask = Q ? (1ull << Q) - 1 : 0ull;
+    const TI *in = r1 + (uint64_t)s * C1s;
+    const uint64_t o = offs[i];
+    for (uint32_t j = blockIdx.y * 256 + threadIdx.x; j < n; j += gridDim.y * 256) {
+        const uint64_t v = in[j];
+        if constexpr (sizeof(TI) == 4) {
+            okeys[o + j] = hi | ((uint64_t)(bd & 511u) << (kb - 9)) | (v & ((1ull << (kb - 9)) - 1));
+        } else {
+            okeys[o + j] = hi | ((v >> Q) & kmask);
+            if (opos) {
+                const uint64_t idx = v & qmask;
+                opos[o + j] = (rc ? idx : idx << 1) | ((uint64_t)src << 56);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void rg_left_counts(const uint32_t *__restrict__ c1, const uint32_t *__restrict__ subs,
+                                                      uint32_t n, uint64_t C1s, uint32_t *__restrict__ cnts) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i < n) {
+        const uint32_t c = c1[subs[i]];
+        cnts[i] = c < C1s ? c : (uint32_t)C1s;
+    }
+}
+
+struct HeavyRound {
+    uint32_t n = 0;  // heavy keys in the table (0: none, pass 1 as usual)
+    uint64_t *tab = nullptr, *drop = nullptr;
+};
+
+int hv_buffer(kman_ctx *ctx, size_t bytes, char **p) {
+    if (bytes > ctx->hv_bytes) {
+        if (ctx->d_hv) {
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            HIP_TRY(ctx, hipFree(ctx->d_hv));
+            ctx->d_hv = nullptr;
+            ctx->hv_bytes = 0;
+        }
+        HIP_TRY(ctx, hipMalloc(&ctx->d_hv, bytes));
+        ctx->hv_bytes = bytes;
+    }
+    *p = (char *)ctx->d_hv;
+    return KMAN_OK;
+}
+
+// The round's heavy keys (see above).  hb[j * G + src] = run (j, src)'s start
+// in d_recv, total = the round's items.  KMAN_HEAVY=0 turns it off.
+int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const std::vector<uint64_t> &hb,
+               uint64_t total, uint32_t b_lo, HeavyRound *hv) {
+    hv->n = 0;
+    const char *e = getenv("KMAN_HEAVY");  // "0": off; "1": any round (tests); else rounds of >= 2^20 items
+    if (e && !strcmp(e, "0")) return KMAN_OK;
+    const bool force = e && !strcmp(e, "1");
+    if (d.K > 62 || (!force && total < (1u << 20)) || !total) return KMAN_OK;  // (table keys < HV_EMPTY)
+    const uint32_t nb = d.nb, G = d.G, nrun = nb * G;
+    // samples: every S-th item, S >= 64, at most HV_NS
+    const uint64_t HV_NS = 1ull << 22;
+    const uint64_t S = std::max<uint64_t>(64, ceil_div(total, HV_NS));
+    const uint64_t ns = ceil_div(total, S);
+    const size_t o_drop = HV_SLOTS * 8, o_misc = 2 * HV_SLOTS * 8, o_cand = o_misc + 512,
+                 o_rs = o_cand + (size_t)HV_CAND * 16, o_s = o_rs + ceil_div(nrun * 8, 256) * 256,
+                 o_a = o_s + ns * 8, o_u = o_a + ns * 8, o_c = o_u + ns * 8, bytes = o_c + ns * 4 + 256;
+    char *w;
+    KMAN_TRY(hv_buffer(ctx, bytes, &w));
+    uint64_t *tab = (uint64_t *)w, *drop = (uint64_t *)(w + o_drop), *cand = (uint64_t *)(w + o_cand);
+    uint32_t *hist = (uint32_t *)(w + o_misc), *ncand = hist + 64;
+    uint64_t *rs = (uint64_t *)(w + o_rs), *smp = (uint64_t *)(w + o_s), *alt = (uint64_t *)(w + o_a),
+             *uk = (uint64_t *)(w + o_u);
+    uint32_t *uc = (uint32_t *)(w + o_c);
+    std::vector<uint64_t> hrs(nrun);
+    for (uint32_t src = 0; src < G; src++)
+        for (uint32_t j = 0; j < nb; j++) hrs[(size_t)src * nb + j] = hb[(size_t)j * G + src];
+    HIP_TRY(ctx, hipMemcpyAsync(rs, hrs.data(), nrun * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(hist, 0, 512, ctx->stream));
+    {
+        KTimer kt_(ctx, "heavy_sample");
+        hipLaunchKernelGGL(rg_hv_sample, dim3((uint32_t)ceil_div(ns, 256)), dim3(256), 0, ctx->stream, d_recv, rs,
+                           nrun, nb, S, ns, b_lo, d.K - B1, d.Q, smp);
+        HIP_TRY(ctx, hipGetLastError());
+    }
+    int in_alt = 0;
+    KMAN_TRY(kman_sort(ctx, smp, alt, nullptr, nullptr, 0, ns, d.K, nullptr, &in_alt));
+    uint64_t nu = 0;
+    KMAN_TRY(kman_rle_count(ctx, in_alt ? alt : smp, ns, uk, uc, 4, &nu));  // (synchronises)
+    if (nu == ns) return KMAN_OK;  // every sample distinct: no heavy key
+    const uint32_t gx = (uint32_t)ceil_div(nu, 256);
+    hipLaunchKernelGGL(rg_hv_select, dim3(gx), dim3(256), 0, ctx->stream, uk, uc, nu, 0u, hist, ncand, cand);
+    HIP_TRY(ctx, hipGetLastError());
+    uint32_t hh[64];
+    HIP_TRY(ctx, hipMemcpyAsync(hh, hist, sizeof(hh), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    // the lowest threshold >= 2 whose candidates fit HV_CAND
+    uint64_t above = 0;
+    uint32_t T = 63;
+    for (uint32_t t = 63; t >= 2; t--) {
+        above += hh[t];
+        if (above > HV_CAND) break;
+        T = t;
+    }
+    if (!above) return KMAN_OK;
+    hipLaunchKernelGGL(rg_hv_select, dim3(gx), dim3(256), 0, ctx->stream, uk, uc, nu, T, hist, ncand, cand);
+    HIP_TRY(ctx, hipGetLastError());
+    uint32_t nc = 0;
+    HIP_TRY(ctx, hipMemcpyAsync(&nc, ncand, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    nc = std::min(nc, HV_CAND);
+    std::vector<uint64_t> hc((size_t)nc * 2);
+    if (nc) HIP_TRY(ctx, hipMemcpy(hc.data(), cand, (size_t)nc * 16, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> order(nc);
+    for (uint32_t i = 0; i < nc; i++) order[i] = i;
+    // the most often sampled first (ties by key: the table is the same whatever the atomics' order)
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        return hc[2 * a + 1] != hc[2 * b + 1] ? hc[2 * a + 1] > hc[2 * b + 1] : hc[2 * a] < hc[2 * b];
+    });
+    const uint32_t m = std::min<uint32_t>(nc, HV_MAX);
+    std::vector<uint64_t> ht(HV_SLOTS, HV_EMPTY);
+    for (uint32_t i = 0; i < m; i++) {
+        const uint64_t key = hc[2 * order[i]];
+        uint32_t sl = hv_hash(key);
+        while (ht[sl] != HV_EMPTY) sl = (sl + 1) & (HV_SLOTS - 1);
+        ht[sl] = key;
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(tab, ht.data(), HV_SLOTS * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(drop, 0, HV_SLOTS * 8, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (ht leaves scope)
+    hv->n = m;
+    hv->tab = tab;
+    hv->drop = drop;
     return KMAN_OK;
 }
 
@@ -2253,6 +2533,9 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     uint8_t *freg = (uint8_t *)(wa + d.off_fail);
     const uint32_t G = world;
     ctx->failed.clear();
+    ctx->heavy_keys = 0;
+    ctx->left.valid = false;
+    ctx->left.bd.clear();
     // pass-1 segments: bucket (b, src) = one contiguous run of src's chunk
     std::vector<uint64_t> hb((size_t)nb * G);
     std::vector<uint32_t> hn((size_t)nb * G);
@@ -2269,10 +2552,13 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     HIP_TRY(ctx, hipMemcpyAsync(scnt, hn.data(), hn.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(c1, 0, d.nsub * 4, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(freg, 0, d.nreg, ctx->stream));
+    HeavyRound hv;
+    KMAN_TRY(find_heavy(ctx, d, d_recv, hb, roff, b_lo, &hv));
     uint32_t epoch, *counter;
     // 4-byte count items out of pass 1 when the key bits below its digit
     // (rest + g, whatever refit_g makes of the split) fit 32 bits
     const bool narrow1 = narrow_ok(ctx, mode, d.Q, d.K - B1 - 9, 0) && !getenv("KMAN_WIDE_ITEMS");
+    bool p1_lost = true;  // (g = 0: the finish reads pass 1's output, whose overflow loses items)
     // pass 1: by the 9 bits below the bucket, H chains per (b, src) into
     // sub-regions (b, d, src, h)
     {
@@ -2294,12 +2580,20 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         pa.fail = freg;  // sub-region (b, d, src, h) -> flag (b, d) (spread over its 2^g regions below)
         pa.fail_div = G * d.H;
         pa.fail_shift = 0;
+        if (hv.n) {
+            pa.hv_keys = hv.tab;
+            pa.hv_drop = hv.drop;
+            pa.hv_base = b_lo;
+            pa.hv_kb = d.K - B1;
+            pa.hv_q = d.Q;
+            pa.hv_keep = mode == KMAN_FINISH_COUNT;
+        }
         launch_pass(ctx, pa, counter, nullptr, false, narrow1);
         HIP_TRY(ctx, hipGetLastError());
     }
     KMAN_TRY(rg_check(ctx, "pass 1", c1, d.nsub));
     if (d.g > 0) {
-        KMAN_TRY(refit_g(ctx, d, c1, freg, G));
+        KMAN_TRY(refit_g(ctx, d, c1, freg, G, &p1_lost));
         c2 = (uint32_t *)(wb + d.off_c2);
     }
     uint64_t *fst = nullptr;
@@ -2353,6 +2647,19 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         HIP_TRY(ctx, hipGetLastError());
     }
     KMAN_TRY(rg_check(ctx, "pass 1b", c2, d.nreg));
+    if (const char *t = getenv("KMAN_TEST_LEAVE_OUT")) {
+        // tests: every n-th region left out as if it had overflowed (the
+        // partial redo's paths on inputs too small to overflow)
+        const uint64_t every = strtoull(t, nullptr, 10);
+        if (every) {
+            std::vector<uint8_t> fr(d.nreg);
+            HIP_TRY(ctx, hipMemcpy(fr.data(), freg, d.nreg, hipMemcpyDeviceToHost));
+            for (uint64_t r = 0; r < d.nreg; r += every) fr[r] = 1;
+            HIP_TRY(ctx, hipMemcpy(freg, fr.data(), d.nreg, hipMemcpyHostToDevice));
+            const uint32_t ev = ERR_REGION;
+            HIP_TRY(ctx, hipMemcpy(ctx->d_err, &ev, 4, hipMemcpyHostToDevice));
+        }
+    }
     {
         FinishArgs f{r2, d.C1, c2, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << (9 + d.g),
                      mode == KMAN_FINISH_UNIQ ? d.Q + d.rest + d.g : 0u, (uint32_t)d.nreg};
@@ -2370,6 +2677,36 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     if (((wd >> 56) & 63u) != ctx->epoch || (wd >> 62) != ST_INCL)
         return kman_fail(ctx, KMAN_EHIP, "region output total not published");
     *n_out = wd & ST_VMASK;
+    ctx->heavy_keys = hv.n;
+    ctx->heavy_mode = mode;
+    {
+        // pass 1's output stays in arena A until the caller reuses it
+        auto &L = ctx->left;
+        L.valid = !e || (d.g > 0 && !p1_lost);
+        L.r1 = r1;
+        L.c1 = c1;
+        L.C1s = d.C1s;
+        L.nb = nb;
+        L.G = G;
+        L.H = d.H;
+        L.K = d.K;
+        L.Q = d.Q;
+        L.b_lo = b_lo;
+        L.rc = d.rc;
+        L.narrow = narrow1;
+        L.mode = mode;
+    }
+    if (hv.n && mode == KMAN_FINISH_COUNT && *n_out) {
+        // the heavy keys' dropped copies onto their rows
+        KTimer kt_(ctx, "heavy_fix");
+        if (oval_bytes == 4)
+            hipLaunchKernelGGL(rg_hv_fix<uint32_t>, dim3(HV_SLOTS / 256), dim3(256), 0, ctx->stream, hv.tab, hv.drop,
+                               d_okeys, (uint32_t *)d_ovals, *n_out);
+        else
+            hipLaunchKernelGGL(rg_hv_fix<uint64_t>, dim3(HV_SLOTS / 256), dim3(256), 0, ctx->stream, hv.tab, hv.drop,
+                               d_okeys, (uint64_t *)d_ovals, *n_out);
+        HIP_TRY(ctx, hipGetLastError());
+    }
     if (!e) return KMAN_OK;
     // regions that overflowed a capacity (skewed keys: repeats) emitted
     // nothing; the rows of every other region are in place, in key order.
@@ -2380,6 +2717,8 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     const uint64_t top = d.rest >= 64 ? ~0ull : ((1ull << d.rest) - 1);
     for (uint64_t r = 0; r < d.nreg; r++) {
         if (!hf[r]) continue;
+        if (ctx->left.valid && (ctx->left.bd.empty() || ctx->left.bd.back() != (uint32_t)(r >> d.g)))
+            ctx->left.bd.push_back((uint32_t)(r >> d.g));
         const uint64_t lo = (rbase + r) << d.rest, hi = lo | top;
         if (!ctx->failed.empty() && ctx->failed.back() + 1 == lo) ctx->failed.back() = hi;
         else {
@@ -2390,6 +2729,96 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     if (ctx->failed.empty())  // (an overflow that flagged no region: not expected)
         return kman_fail(ctx, KMAN_EHIP, "kman_dround_finish: overflow without a flagged region");
     return KMAN_EPARTIAL;
+}
+
+extern "C" int kman_dround_left(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_pos, uint64_t cap, uint64_t *n) {
+    if (!ctx || !n) return KMAN_EINVAL;
+    *n = 0;
+    const auto &L = ctx->left;
+    if (!L.valid) return KMAN_EFALLBACK;
+    if (L.bd.empty()) return KMAN_OK;
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const uint32_t GH = L.G * L.H;
+    const uint32_t ns = (uint32_t)L.bd.size() * GH;
+    std::vector<uint32_t> subs(ns);
+    for (size_t i = 0; i < L.bd.size(); i++)
+        for (uint32_t q = 0; q < GH; q++) subs[i * GH + q] = L.bd[i] * GH + q;
+    // (the heavy-key scratch holds the sub-region list, counts and offsets)
+    const size_t o_subs = 2 * HV_SLOTS * 8, o_cnt = o_subs + ceil_div((uint64_t)ns * 4, 256) * 256,
+                 o_off = o_cnt + ceil_div((uint64_t)ns * 4, 256) * 256, bytes = o_off + (size_t)ns * 8 + 256;
+    if (bytes > ctx->hv_bytes) {
+        // (grows the buffer: its heavy table is copied along)
+        void *nb_ = nullptr;
+        HIP_TRY(ctx, hipMalloc(&nb_, bytes));
+        if (ctx->d_hv) {
+            HIP_TRY(ctx, hipMemcpyAsync(nb_, ctx->d_hv, 2 * HV_SLOTS * 8, hipMemcpyDeviceToDevice, ctx->stream));
+            HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+            HIP_TRY(ctx, hipFree(ctx->d_hv));
+        }
+        ctx->d_hv = nb_;
+        ctx->hv_bytes = bytes;
+    }
+    char *w = (char *)ctx->d_hv;
+    uint32_t *d_subs = (uint32_t *)(w + o_subs), *d_cnt = (uint32_t *)(w + o_cnt);
+    uint64_t *d_off = (uint64_t *)(w + o_off);
+    HIP_TRY(ctx, hipMemcpyAsync(d_subs, subs.data(), (size_t)ns * 4, hipMemcpyHostToDevice, ctx->stream));
+    hipLaunchKernelGGL(rg_left_counts, dim3((ns + 255) / 256), dim3(256), 0, ctx->stream, L.c1, d_subs, ns, L.C1s,
+                       d_cnt);
+    HIP_TRY(ctx, hipGetLastError());
+    std::vector<uint32_t> cnt(ns);
+    HIP_TRY(ctx, hipMemcpyAsync(cnt.data(), d_cnt, (size_t)ns * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    std::vector<uint64_t> off(ns);
+    uint64_t tot = 0;
+    uint32_t mx = 0;
+    for (uint32_t i = 0; i < ns; i++) {
+        off[i] = tot;
+        tot += cnt[i];
+        mx = std::max(mx, cnt[i]);
+    }
+    *n = tot;
+    if (!d_keys) return KMAN_OK;
+    if (cap < tot) return kman_fail(ctx, KMAN_ECAP, "kman_dround_left: %llu items > cap %llu",
+                                    (unsigned long long)tot, (unsigned long long)cap);
+    if (L.mode == KMAN_FINISH_UNIQ && !d_pos) return kman_fail(ctx, KMAN_EINVAL, "uniq: null pos");
+    if (!tot) return KMAN_OK;
+    HIP_TRY(ctx, hipMemcpyAsync(d_off, off.data(), (size_t)ns * 8, hipMemcpyHostToDevice, ctx->stream));
+    KTimer kt_(ctx, "left_gather");
+    const dim3 grid(ns, std::max<uint32_t>(1, std::min<uint32_t>(64, (mx + 2047) / 2048)));
+    uint64_t *pos = L.mode == KMAN_FINISH_UNIQ ? d_pos : nullptr;
+    if (L.narrow)
+        hipLaunchKernelGGL(rg_left_gather<uint32_t>, grid, dim3(256), 0, ctx->stream, (const uint32_t *)L.r1, L.C1s,
+                           d_subs, d_cnt, d_off, L.G, L.H, L.b_lo, L.K - B1, L.Q, (uint32_t)L.rc, d_keys, pos);
+    else
+        hipLaunchKernelGGL(rg_left_gather<uint64_t>, grid, dim3(256), 0, ctx->stream, (const uint64_t *)L.r1, L.C1s,
+                           d_subs, d_cnt, d_off, L.G, L.H, L.b_lo, L.K - B1, L.Q, (uint32_t)L.rc, d_keys, pos);
+    HIP_TRY(ctx, hipGetLastError());
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (off / subs leave scope)
+    return KMAN_OK;
+}
+
+extern "C" int kman_dround_heavy_fix(kman_ctx *ctx, const uint64_t *d_keys, void *d_vals, uint32_t val_bytes,
+                                     uint64_t n) {
+    if (!ctx) return KMAN_EINVAL;
+    if (!ctx->heavy_keys || ctx->heavy_mode != KMAN_FINISH_COUNT || !n) return KMAN_OK;
+    if (!d_keys || !d_vals) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
+    if (val_bytes != 4 && val_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "val_bytes must be 4 or 8");
+    HIP_TRY(ctx, hipSetDevice(ctx->device));
+    const uint64_t *tab = (const uint64_t *)ctx->d_hv, *drop = tab + HV_SLOTS;
+    if (val_bytes == 4)
+        hipLaunchKernelGGL(rg_hv_fix<uint32_t>, dim3(HV_SLOTS / 256), dim3(256), 0, ctx->stream, tab, drop, d_keys,
+                           (uint32_t *)d_vals, n);
+    else
+        hipLaunchKernelGGL(rg_hv_fix<uint64_t>, dim3(HV_SLOTS / 256), dim3(256), 0, ctx->stream, tab, drop, d_keys,
+                           (uint64_t *)d_vals, n);
+    HIP_TRY(ctx, hipGetLastError());
+    return KMAN_OK;
+}
+
+extern "C" int kman_dround_heavy(kman_ctx *ctx, uint32_t *n) {
+    if (!ctx || !n) return KMAN_EINVAL;
+    *n = ctx->heavy_keys;
+    return KMAN_OK;
 }
 
 extern "C" int kman_dround_failed(kman_ctx *ctx, uint64_t *ranges, uint64_t cap, uint64_t *n) {

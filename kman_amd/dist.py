@@ -44,7 +44,7 @@ from __future__ import annotations
 import ctypes
 import os
 import time
-from ctypes import byref, c_int, c_uint64, c_void_p
+from ctypes import byref, c_int, c_uint32, c_uint64, c_void_p
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -671,6 +671,8 @@ class DistPipeline:
         self.partial_rounds = 0
         self.redone_kmers = 0
         self.overlapped_rounds = 0
+        self.heavy_keys = 0  # keys its rounds' pass 1 counted apart (kman_dround_heavy, summed over rounds)
+        self.local_redo_kmers = 0  # of redone_kmers, gathered from the finish's pass-1 output (kman_dround_left)
         self.exchanged_items = 0  # items this rank sent through kman_alltoallv (its rounds)
         self.max_message = 0  # bytes of its largest message to one peer
         # overlapped rounds (every round of the step, R >= 1): exchange piece
@@ -737,6 +739,7 @@ class DistPipeline:
                                            byref(got))
                 fb = 1 if ret == N.KMAN_EFALLBACK else 0
                 part = 1 if ret == N.KMAN_EPARTIAL else 0
+                self._note_heavy()
                 if not fb and not part:
                     N.check(ctx, ret, "kman_dround_finish")
                 lap("finish")
@@ -857,14 +860,22 @@ class DistPipeline:
                 mine.append(self._failed_ranges())
             elif ret != N.KMAN_OK:
                 N.check(ctx, ret, "kman_dround_finish")
+            self._note_heavy()
             n_out += int(got.value)
         f = yield ("allreduce", np.array([0, len(mine)], np.uint64))
         if int(f[1]):
             self.partial_rounds += 1
             mine = np.concatenate(mine) if mine else np.zeros((0, 2), np.uint64)
-            rows = yield from self._redo_ranges(mine, n_out - start, A, B, ok_, ov_, start, vb)
+            rows = yield from self._redo_ranges(mine, n_out - start, A, B, ok_, ov_, start, vb, local=False)
             n_out = start + rows
         return n_out
+
+    def _note_heavy(self) -> None:
+        """Adds the heavy keys of the last kman_dround_finish (counted apart
+        in its pass 1) to the step's total."""
+        n = c_uint32(0)
+        N.check(self.dev.ctx, N.lib().kman_dround_heavy(self.dev.ctx, byref(n)), "kman_dround_heavy")
+        self.heavy_keys += int(n.value)
 
     def _failed_ranges(self) -> np.ndarray:
         """[lo, hi] key ranges the last kman_dround_finish left out."""
@@ -877,7 +888,8 @@ class DistPipeline:
                     "kman_dround_failed")
         return out
 
-    def _redo_ranges(self, mine: np.ndarray, n_region: int, A, B, ok_, ov_, n_out: int, vb: int):
+    def _redo_ranges(self, mine: np.ndarray, n_region: int, A, B, ok_, ov_, n_out: int, vb: int,
+                     local: bool = True):
         """The key ranges each rank's round finish left out (mine: this
         rank's), through the general path: every rank extracts the k-mers of
         each destination's ranges (kman_extract_marked), one exchange, then the
@@ -898,6 +910,32 @@ class DistPipeline:
                 self.phase_ms["redo_" + tag] = self.phase_ms.get("redo_" + tag, 0.0) + (t - tick[0]) * 1e3
                 tick[0] = t
 
+        # local: each rank's left-out items are still in its last finish's
+        # pass-1 output (kman_dround_left; not after overlapped pieces, whose
+        # scratch the later pieces reused) -- no re-extraction, no exchange.
+        # Every rank or none (a rank whose pass 1 itself overflowed needs the
+        # others' marked extraction)
+        n_left = c_uint64(0)
+        local = local and os.environ.get("KMAN_LOCAL_REDO", "1") != "0"
+        rc_ = L.kman_dround_left(ctx, None, None, 0, byref(n_left)) if local else N.KMAN_EFALLBACK
+        if rc_ not in (N.KMAN_OK, N.KMAN_EFALLBACK):
+            N.check(ctx, rc_, "kman_dround_left")
+        f = yield ("allreduce", np.array([0 if rc_ == N.KMAN_OK else 1], np.uint64))
+        if int(f[0]) == 0:
+            nr = int(n_left.value)
+            if vb == 4 and nr > 0xFFFFFFFF:
+                raise NotImplementedError("a redone key range of more than 2^32 k-mers would need u64 counts")
+            rk, ak = (self.gen_bufs[i].get(8 * max(1, nr)) for i in (1, 2))
+            rp = ap = None
+            if uniq:
+                rp, ap = (self.gen_bufs[i].get(8 * max(1, nr)) for i in (4, 5))
+            got = c_uint64(0)
+            N.check(ctx, L.kman_dround_left(ctx, c_void_p(rk.ptr), c_void_p(rp.ptr) if uniq else None, nr,
+                                            byref(got)), "kman_dround_left")
+            self.redone_kmers += nr
+            self.local_redo_kmers += nr
+            lap("gather")
+            return (yield from self._redo_rows(rk, ak, rp, ap, nr, n_region, A, B, ok_, ov_, n_out, vb, lap, True))
         cnt = yield ("allgather", np.array([len(mine)], np.uint64))
         cnt = np.asarray(cnt, np.uint64).reshape(G)
         m = max(1, int(cnt.max()))
@@ -977,6 +1015,17 @@ class DistPipeline:
         if uniq:
             yield ("alltoallv", (sp.ptr, sc, so, rp.ptr, rcnt, roff, 8))
         lap("exchange")
+        return (yield from self._redo_rows(rk, ak, rp, ap, nr, n_region, A, B, ok_, ov_, n_out, vb, lap, False))
+
+    def _redo_rows(self, rk, ak, rp, ap, nr, n_region, A, B, ok_, ov_, n_out, vb, lap, heavy_fix):
+        """The redone items rk (+ pos rp) -> rows: a full-key sort, run-length,
+        and (ordered) a merge with the n_region region rows at ok_/ov_[n_out].
+        heavy_fix: the items came from the finish's pass-1 output
+        (kman_dround_left), so the heavy keys' dropped copies are added to
+        their rows.  Generator (no collective); returns the rows at n_out."""
+        L, ctx, k = N.lib(), self.dev.ctx, self.k
+        uniq = self.mode == "uniq"
+        me = self.rank
         n_gen = 0
         if self.ordered:
             gk, gv = self.part_bufs[0].get(8 * max(1, nr)), self.part_bufs[1].get(vb * max(1, nr))
@@ -1009,6 +1058,9 @@ class DistPipeline:
                 N.check(ctx, L.kman_rle_count(ctx, c_void_p(keys.ptr), nr, c_void_p(gk.ptr), c_void_p(gv.ptr), vb,
                                               byref(out)), "kman_rle_count")
             n_gen = int(out.value)
+            if heavy_fix and not uniq:
+                N.check(ctx, L.kman_dround_heavy_fix(ctx, c_void_p(gk.ptr), c_void_p(gv.ptr), vb, n_gen),
+                        "kman_dround_heavy_fix")
             lap("finish")
         if n_gen and self.ordered:
             # the region rows move to the (now free) round arenas, then the two
@@ -1023,6 +1075,7 @@ class DistPipeline:
                                            c_void_p(ov_.ptr + vb * n_out), None, None), "kman_merge_runs")
             lap("merge")
         return n_region + n_gen
+        yield  # (a generator: the callers delegate with yield from)
 
     def _vb(self, C) -> int:
         """Output value bytes: uniq pos are u64 (source rank in bits 56-63);
@@ -1230,7 +1283,8 @@ def local_groups(p: engine.Parsed, k: int, rc: bool, mode: str, canonical: bool 
         LAST_LOCAL.clear()
         LAST_LOCAL.update(setup_ms=(t1 - t0) * 1e3, step_ms=(t2 - t1) * 1e3, rounds=pipe.rounds,
                           fallback_rounds=pipe.fallback_rounds, partial_rounds=pipe.partial_rounds,
-                          redone_kmers=pipe.redone_kmers, plan=getattr(pipe, "plan_info", None),
+                          redone_kmers=pipe.redone_kmers, heavy_keys=pipe.heavy_keys,
+                          plan=getattr(pipe, "plan_info", None),
                           phases_ms=dict(pipe.phase_ms))
         return pipe.take_result()
     finally:

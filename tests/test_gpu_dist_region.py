@@ -490,3 +490,87 @@ def test_dist_grch38_skewed_canonical(G):
             np.testing.assert_array_equal(h, want)
     finally:
         _close(pipes)
+
+
+@pytest.mark.parametrize("G", [1, 2, 3])
+@pytest.mark.parametrize("mode", ["count", "uniq"])
+@pytest.mark.parametrize("canonical", [False, True], ids=["fwd", "canon"])
+def test_dist_heavy_keys_counted_apart(G, mode, canonical, monkeypatch):
+    """Heavy keys (kman_dround_heavy): a round's sampled-twice keys are
+    counted apart in pass 1 -- count mode keeps one copy per chain and adds
+    the dropped ones to the row after the finish, uniq mode drops them all.
+    On a repeat-rich input (inputs.grch38_like: a few 300-bp elements copied
+    every 2.5 kb, a satellite array) with the table forced on (KMAN_HEAVY=1,
+    any round size) and also split into 3 rounds, the rows equal the oracle's
+    and equal the rows with the table off (KMAN_HEAVY=0); with it on, fewer
+    k-mers go through the partial redo."""
+    import inputs
+
+    text = inputs.grch38_like(11, n_bases=2_000_000, n_records=2)
+    wk, wv = _oracle(text, 21, mode, canonical=canonical)
+    redone = {}
+    for hv in ("1", "0"):
+        monkeypatch.setenv("KMAN_HEAVY", hv)
+        for mri in (None, 700_000):
+            kw = {"canonical": canonical} if canonical else {}
+            if mri:
+                kw["max_round_items"] = mri
+            outs, pipes, _ = _run(text, 21, mode, G, **kw)
+            try:
+                for keys, vals in outs:
+                    np.testing.assert_array_equal(keys, wk)
+                    np.testing.assert_array_equal(vals, wv)
+                heavy = sum(p.heavy_keys for p in pipes)
+                if hv == "1":
+                    assert heavy > 0, "no heavy key sampled on a repeat-rich input"
+                else:
+                    assert heavy == 0
+                if mri:
+                    assert max(p.rounds for p in pipes) >= 2
+                redone[hv, mri] = sum(p.redone_kmers for p in pipes)
+            finally:
+                _close(pipes)
+    assert redone["1", None] <= redone["0", None]
+
+
+@pytest.mark.parametrize("G", [1, 2, 3])
+@pytest.mark.parametrize("mode", ["count", "uniq"])
+@pytest.mark.parametrize("ordered", [True, False], ids=["ordered", "multiset"])
+def test_dist_left_out_regions_redone_locally(G, mode, ordered, monkeypatch):
+    """kman_dround_left: the regions a round's finish left out are redone
+    from its pass-1 output (no re-extraction from the codes, no exchange),
+    the heavy keys' dropped copies added back (kman_dround_heavy_fix).  Every
+    7th region is left out (KMAN_TEST_LEAVE_OUT, as if it had overflowed) on
+    the repeat-rich grch38_like input, with the heavy-key table on and off and
+    in 1 or 3 rounds: the rows equal the oracle's (as a multiset when
+    unordered) and equal those of the marked-extraction redo
+    (KMAN_LOCAL_REDO=0)."""
+    import inputs
+
+    text = inputs.grch38_like(12, n_bases=1_500_000, n_records=2)
+    wk, wv = _oracle(text, 21, mode)
+    monkeypatch.setenv("KMAN_TEST_LEAVE_OUT", "7")
+    monkeypatch.setenv("KMAN_DROUND_MIN_G", "1")  # (the leave-out hook acts on pass 1b's regions)
+    for hv in ("1", "0"):
+        monkeypatch.setenv("KMAN_HEAVY", hv)
+        for mri in (None, 600_000):
+            for loc in ("1", "0"):
+                monkeypatch.setenv("KMAN_LOCAL_REDO", loc)
+                kw = {"ordered": ordered}
+                if mri:
+                    kw["max_round_items"] = mri
+                outs, pipes, _ = _run(text, 21, mode, G, **kw)
+                try:
+                    for keys, vals in outs:
+                        if not ordered:
+                            q = np.lexsort((vals, keys))
+                            keys, vals = keys[q], vals[q]
+                        np.testing.assert_array_equal(keys, wk)
+                        np.testing.assert_array_equal(vals, wv)
+                    assert sum(p.partial_rounds for p in pipes) > 0
+                    local = sum(p.local_redo_kmers for p in pipes)
+                    assert (local > 0) == (loc == "1"), (local, loc)
+                    if hv == "1":
+                        assert sum(p.heavy_keys for p in pipes) > 0
+                finally:
+                    _close(pipes)

@@ -89,6 +89,7 @@ def run(name, dev, text_reader, k, mode, rc=False, canonical=False, steps=3, his
         dist.LAST_LOCAL.clear()
         dist.LAST_LOCAL.update(rounds=lr.pipe.rounds, fallback_rounds=lr.pipe.fallback_rounds,
                                partial_rounds=lr.pipe.partial_rounds, redone_kmers=lr.pipe.redone_kmers,
+                               heavy_keys=lr.pipe.heavy_keys,
                                plan=getattr(lr.pipe, "plan_info", None), phases_ms=dict(lr.pipe.phase_ms))
         lr.free()
     ms = 1e3 * sum(times) / len(times)
