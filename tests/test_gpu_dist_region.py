@@ -511,7 +511,7 @@ def test_dist_heavy_keys_counted_apart(G, mode, canonical, monkeypatch):
     redone = {}
     for hv in ("1", "0"):
         monkeypatch.setenv("KMAN_HEAVY", hv)
-        for mri in (None, 700_000):
+        for mri in (None, 250_000):
             kw = {"canonical": canonical} if canonical else {}
             if mri:
                 kw["max_round_items"] = mri
@@ -553,7 +553,7 @@ def test_dist_left_out_regions_redone_locally(G, mode, ordered, monkeypatch):
     monkeypatch.setenv("KMAN_DROUND_MIN_G", "1")  # (the leave-out hook acts on pass 1b's regions)
     for hv in ("1", "0"):
         monkeypatch.setenv("KMAN_HEAVY", hv)
-        for mri in (None, 600_000):
+        for mri in (None, 250_000):
             for loc in ("1", "0"):
                 monkeypatch.setenv("KMAN_LOCAL_REDO", loc)
                 kw = {"ordered": ordered}
