@@ -493,8 +493,8 @@ def test_dist_grch38_skewed_canonical(G):
 
 
 @pytest.mark.parametrize("G", [1, 2, 3])
-@pytest.mark.parametrize("mode", ["count", "uniq"])
-@pytest.mark.parametrize("canonical", [False, True], ids=["fwd", "canon"])
+@pytest.mark.parametrize("mode,canonical", [("count", False), ("uniq", False), ("count", True)],
+                         ids=["count", "uniq", "canon"])
 def test_dist_heavy_keys_counted_apart(G, mode, canonical, monkeypatch):
     """Heavy keys (kman_dround_heavy): a round's sampled-twice keys are
     counted apart in pass 1 -- count mode keeps one copy per chain and adds
