@@ -81,7 +81,8 @@ struct kman_ctx {
         const void *r1 = nullptr;
         const uint32_t *c1 = nullptr;
         uint64_t C1s = 0;
-        uint32_t nb = 0, G = 0, H = 0, K = 0, Q = 0, b_lo = 0;
+        uint32_t nb = 0, G = 0, H = 0, K = 0, Q = 0, b_lo = 0, g = 0;
+        const uint8_t *freg = nullptr;  // the round's left-out regions (arena A)
         bool rc = false, narrow = false;
         int mode = 0;
         std::vector<uint32_t> bd;

@@ -2278,32 +2278,51 @@ __global__ __launch_bounds__(256) void rg_hv_fix(const uint64_t *__restrict__ ta
     if (lo < n && okeys[lo] == key) ovals[lo] += (V)d;
 }
 
-// kman_dround_left: the items of the left-out sub-buckets' pass-1
-// sub-regions (bd, src, h) = subs[i] as full keys (+ uniq pos, as the finish
-// emits them), sub-region i at offs[i]
+// kman_dround_left: the items of the left-out regions, from the pass-1
+// sub-regions (bd, src, h) = subs[i] of their sub-buckets bd (a sub-bucket's
+// 2^g regions are left out one by one: an item is kept when freg flags its
+// region) as full keys (+ uniq pos, as the finish emits them), appended at
+// *cursor by one atomic per wave (the rows are sorted afterwards); okeys
+// null: counted only
 template <typename TI>
 __global__ __launch_bounds__(256) void rg_left_gather(const TI *__restrict__ r1, uint64_t C1s,
                                                       const uint32_t *__restrict__ subs,
-                                                      const uint32_t *__restrict__ cnts,
-                                                      const uint64_t *__restrict__ offs, uint32_t G, uint32_t H,
-                                                      uint32_t b_lo, uint32_t kb, uint32_t Q, uint32_t rc,
+                                                      const uint32_t *__restrict__ cnts, const uint8_t *__restrict__ freg,
+                                                      uint32_t g, uint32_t G, uint32_t H, uint32_t b_lo, uint32_t kb,
+                                                      uint32_t Q, uint32_t rc, unsigned long long *__restrict__ cursor,
                                                       uint64_t *__restrict__ okeys, uint64_t *__restrict__ opos) {
     const uint32_t i = blockIdx.x;
     const uint32_t s = subs[i], n = cnts[i];
     const uint32_t bd = s / (G * H), src = (s / H) % G;
     const uint64_t hi = (uint64_t)(b_lo + (bd >> 9)) << kb;
     const uint64_t kmask = (1ull << kb) - 1, qmask = Q ? (1ull << Q) - 1 : 0ull;
+    const uint32_t rsh = kb - 9 - g;  // key bits below the region
     const TI *in = r1 + (uint64_t)s * C1s;
-    const uint64_t o = offs[i];
-    for (uint32_t j = blockIdx.y * 256 + threadIdx.x; j < n; j += gridDim.y * 256) {
-        const uint64_t v = in[j];
-        if constexpr (sizeof(TI) == 4) {
-            okeys[o + j] = hi | ((uint64_t)(bd & 511u) << (kb - 9)) | (v & ((1ull << (kb - 9)) - 1));
-        } else {
-            okeys[o + j] = hi | ((v >> Q) & kmask);
-            if (opos) {
-                const uint64_t idx = v & qmask;
-                opos[o + j] = (rc ? idx : idx << 1) | ((uint64_t)src << 56);
+    const int lane = lane_id();
+    for (uint32_t j0 = (blockIdx.y * 256 + (threadIdx.x & ~63u)); j0 < n; j0 += gridDim.y * 256) {
+        const uint32_t j = j0 + (uint32_t)lane;
+        uint64_t key = 0, v = 0;
+        bool keep = false;
+        if (j < n) {
+            v = in[j];
+            if constexpr (sizeof(TI) == 4) key = hi | ((uint64_t)(bd & 511u) << (kb - 9)) | (v & ((1ull << (kb - 9)) - 1));
+            else key = hi | ((v >> Q) & kmask);
+            const uint64_t r = ((uint64_t)bd << g) | ((key >> rsh) & ((1ull << g) - 1));
+            keep = freg[r] != 0;
+        }
+        const uint64_t m = __ballot(keep);
+        if (!m) continue;
+        unsigned long long base = 0;
+        if (lane == __ffsll((unsigned long long)m) - 1) base = atomicAdd(cursor, (unsigned long long)__popcll(m));
+        base = __shfl(base, __ffsll((unsigned long long)m) - 1);
+        if (keep && okeys) {
+            const uint64_t at = base + (uint64_t)__popcll(m & lanemask_lt());
+            okeys[at] = key;
+            if constexpr (sizeof(TI) == 8) {
+                if (opos) {
+                    const uint64_t idx = v & qmask;
+                    opos[at] = (rc ? idx : idx << 1) | ((uint64_t)src << 56);
+                }
             }
         }
     }
@@ -2695,6 +2714,8 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         L.rc = d.rc;
         L.narrow = narrow1;
         L.mode = mode;
+        L.g = d.g;
+        L.freg = freg;
     }
     if (hv.n && mode == KMAN_FINISH_COUNT && *n_out) {
         // the heavy keys' dropped copies onto their rows
@@ -2745,7 +2766,7 @@ extern "C" int kman_dround_left(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_pos
         for (uint32_t q = 0; q < GH; q++) subs[i * GH + q] = L.bd[i] * GH + q;
     // (the heavy-key scratch holds the sub-region list, counts and offsets)
     const size_t o_subs = 2 * HV_SLOTS * 8, o_cnt = o_subs + ceil_div((uint64_t)ns * 4, 256) * 256,
-                 o_off = o_cnt + ceil_div((uint64_t)ns * 4, 256) * 256, bytes = o_off + (size_t)ns * 8 + 256;
+                 o_off = o_cnt + ceil_div((uint64_t)ns * 4, 256) * 256, bytes = o_off + 256;
     if (bytes > ctx->hv_bytes) {
         // (grows the buffer: its heavy table is copied along)
         void *nb_ = nullptr;
@@ -2760,7 +2781,7 @@ extern "C" int kman_dround_left(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_pos
     }
     char *w = (char *)ctx->d_hv;
     uint32_t *d_subs = (uint32_t *)(w + o_subs), *d_cnt = (uint32_t *)(w + o_cnt);
-    uint64_t *d_off = (uint64_t *)(w + o_off);
+    uint64_t *d_cur = (uint64_t *)(w + o_off);
     HIP_TRY(ctx, hipMemcpyAsync(d_subs, subs.data(), (size_t)ns * 4, hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(rg_left_counts, dim3((ns + 255) / 256), dim3(256), 0, ctx->stream, L.c1, d_subs, ns, L.C1s,
                        d_cnt);
@@ -2768,32 +2789,35 @@ extern "C" int kman_dround_left(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_pos
     std::vector<uint32_t> cnt(ns);
     HIP_TRY(ctx, hipMemcpyAsync(cnt.data(), d_cnt, (size_t)ns * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    std::vector<uint64_t> off(ns);
-    uint64_t tot = 0;
     uint32_t mx = 0;
-    for (uint32_t i = 0; i < ns; i++) {
-        off[i] = tot;
-        tot += cnt[i];
-        mx = std::max(mx, cnt[i]);
-    }
-    *n = tot;
-    if (!d_keys) return KMAN_OK;
-    if (cap < tot) return kman_fail(ctx, KMAN_ECAP, "kman_dround_left: %llu items > cap %llu",
-                                    (unsigned long long)tot, (unsigned long long)cap);
-    if (L.mode == KMAN_FINISH_UNIQ && !d_pos) return kman_fail(ctx, KMAN_EINVAL, "uniq: null pos");
-    if (!tot) return KMAN_OK;
-    HIP_TRY(ctx, hipMemcpyAsync(d_off, off.data(), (size_t)ns * 8, hipMemcpyHostToDevice, ctx->stream));
+    for (uint32_t i = 0; i < ns; i++) mx = std::max(mx, cnt[i]);
+    if (d_keys && L.mode == KMAN_FINISH_UNIQ && !d_pos) return kman_fail(ctx, KMAN_EINVAL, "uniq: null pos");
+    HIP_TRY(ctx, hipMemsetAsync(d_cur, 0, 8, ctx->stream));
     KTimer kt_(ctx, "left_gather");
     const dim3 grid(ns, std::max<uint32_t>(1, std::min<uint32_t>(64, (mx + 2047) / 2048)));
     uint64_t *pos = L.mode == KMAN_FINISH_UNIQ ? d_pos : nullptr;
-    if (L.narrow)
-        hipLaunchKernelGGL(rg_left_gather<uint32_t>, grid, dim3(256), 0, ctx->stream, (const uint32_t *)L.r1, L.C1s,
-                           d_subs, d_cnt, d_off, L.G, L.H, L.b_lo, L.K - B1, L.Q, (uint32_t)L.rc, d_keys, pos);
-    else
-        hipLaunchKernelGGL(rg_left_gather<uint64_t>, grid, dim3(256), 0, ctx->stream, (const uint64_t *)L.r1, L.C1s,
-                           d_subs, d_cnt, d_off, L.G, L.H, L.b_lo, L.K - B1, L.Q, (uint32_t)L.rc, d_keys, pos);
-    HIP_TRY(ctx, hipGetLastError());
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (off / subs leave scope)
+    // (a first launch counts: the caller's cap is checked before any write)
+    for (int pass = d_keys ? 0 : 1; pass < 2; pass++) {
+        uint64_t *ok = pass ? d_keys : nullptr;
+        if (pass && d_keys) HIP_TRY(ctx, hipMemsetAsync(d_cur, 0, 8, ctx->stream));
+        if (L.narrow)
+            hipLaunchKernelGGL(rg_left_gather<uint32_t>, grid, dim3(256), 0, ctx->stream, (const uint32_t *)L.r1,
+                               L.C1s, d_subs, d_cnt, L.freg, L.g, L.G, L.H, L.b_lo, L.K - B1, L.Q, (uint32_t)L.rc,
+                               (unsigned long long *)d_cur, ok, ok ? pos : nullptr);
+        else
+            hipLaunchKernelGGL(rg_left_gather<uint64_t>, grid, dim3(256), 0, ctx->stream, (const uint64_t *)L.r1,
+                               L.C1s, d_subs, d_cnt, L.freg, L.g, L.G, L.H, L.b_lo, L.K - B1, L.Q, (uint32_t)L.rc,
+                               (unsigned long long *)d_cur, ok, ok ? pos : nullptr);
+        HIP_TRY(ctx, hipGetLastError());
+        uint64_t tot = 0;
+        HIP_TRY(ctx, hipMemcpyAsync(&tot, d_cur, 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+        *n = tot;
+        if (!pass && tot > cap)
+            return kman_fail(ctx, KMAN_ECAP, "kman_dround_left: %llu items > cap %llu", (unsigned long long)tot,
+                             (unsigned long long)cap);
+        if (!d_keys) break;
+    }
     return KMAN_OK;
 }
 
