@@ -376,13 +376,17 @@ struct PassArgs {
     uint32_t fail_div, fail_shift;
     uint32_t big;  // a pass of <= 8 bits on the 1024-thread instance anyway (8192-item tiles: 256-byte digit runs)
     // optional (pass 1 of a key round, rg_pass<..., HV = true): the heavy
-    // keys of the round (hv_keys: an open-addressing table of HV_SLOTS full
+    // keys of the round (hv_keys: an open-addressing table of HV_TAB full
     // keys, HV_EMPTY where free).  An item whose key ((hv_base + b / gsub) <<
     // hv_kb | item >> hv_q) is in it is counted in LDS per chain; count mode
     // keeps the chain's first copy (hv_keep = 1) and drops the rest, uniq mode
     // drops every copy (a heavy key occurs more than once: no uniq row); the
-    // dropped copies are added to hv_drop[slot] when the chain ends
+    // dropped copies are added to hv_drop[i] when the chain ends (i =
+    // hv_idx[slot], the key's index in the sorted heavy list); hv_bm: a
+    // 2^16-bit filter of the keys' hashes, so only ~3 % of the other items
+    // probe the table
     const uint64_t *hv_keys;
+    const uint32_t *hv_idx, *hv_bm;
     uint64_t *hv_drop;
     uint32_t hv_base, hv_kb, hv_q, hv_keep;
 };
@@ -391,9 +395,14 @@ struct PassArgs {
 // received items, counted apart in pass 1 so that a satellite or repeat-family
 // k-mer with 10^5 copies does not overflow its regions (and send the key range
 // through the partial redo)
-constexpr uint32_t HV_SLOTS = 4096, HV_MAX = 2048;
+constexpr uint32_t HV_MAX = 2048, HV_TAB = 16384, HV_BM = 1u << 16;
 constexpr uint64_t HV_EMPTY = ~0ull;
-__host__ __device__ inline uint32_t hv_hash(uint64_t key) { return (uint32_t)((key * 0x9E3779B97F4A7C15ull) >> 52); }
+__host__ __device__ inline uint64_t hv_hash(uint64_t key) { return key * 0x9E3779B97F4A7C15ull; }
+__host__ __device__ inline uint32_t hv_slot(uint64_t h) { return (uint32_t)(h >> 50); }  // 14 bits
+__host__ __device__ inline uint32_t hv_bit(uint64_t h) { return (uint32_t)(h >> 48); }   // 16 bits
+// the heavy-key scratch (kman_ctx::d_hv): what outlives find_heavy
+constexpr size_t HVO_TAB = 0, HVO_IDX = HVO_TAB + HV_TAB * 8, HVO_KEYS = HVO_IDX + HV_TAB * 4,
+                 HVO_DROP = HVO_KEYS + HV_MAX * 8, HVO_BM = HVO_DROP + HV_MAX * 8, HVO_END = HVO_BM + HV_BM / 8;
 
 // Persistent 1024-thread blocks (one per CU; 141 KiB of LDS), block-owned
 // chains: a block takes a whole chain (bucket b, part h: the h-th of H runs of
@@ -458,7 +467,12 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
     __shared__ uint32_t s_items;
     __shared__ uint32_t lds_tile;
     // HV: the chain's copies of each heavy key (by table slot)
-    __shared__ uint32_t hcnt[HV ? HV_SLOTS : 1];
+    __shared__ uint32_t hcnt[HV ? HV_MAX : 1];
+    __shared__ uint32_t hbm[HV ? HV_BM / 32 : 1];
+    if constexpr (HV) {
+        for (uint32_t s = threadIdx.x; s < HV_BM / 32; s += NT) hbm[s] = pa.hv_bm[s];
+        // (visible after grab_tile's barriers)
+    }
     const uint32_t shift = pa.shift, bits = pa.bits, nsg = pa.nsg, H = pa.H;
     const uint64_t C1 = pa.C1;
     const int lane = lane_id();
@@ -486,7 +500,7 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
         }
         if (threadIdx.x < RB) run[threadIdx.x] = 0;
         if constexpr (HV)
-            for (uint32_t s = threadIdx.x; s < HV_SLOTS; s += NT) hcnt[s] = 0;
+            for (uint32_t s = threadIdx.x; s < HV_MAX; s += NT) hcnt[s] = 0;
         __syncthreads();
         const uint32_t items = s_items;
         const uint32_t tiles = (items + TILE - 1) / TILE;
@@ -585,16 +599,19 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
                 for (int i = 0; i < SI; i++) {
                     if (!((vm >> i) & 1u)) continue;
                     const uint64_t full = hb | ((uint64_t)key[i] >> pa.hv_q);
-                    uint32_t sl = hv_hash(full);
+                    const uint64_t hs = hv_hash(full);
+                    const uint32_t bi = hv_bit(hs);
+                    if (!((hbm[bi >> 5] >> (bi & 31)) & 1u)) continue;
+                    uint32_t sl = hv_slot(hs);
                     for (;;) {
                         const uint64_t t = pa.hv_keys[sl];
                         if (t == full) {
-                            const uint32_t old = atomicAdd(&hcnt[sl], 1u);
+                            const uint32_t old = atomicAdd(&hcnt[pa.hv_idx[sl]], 1u);
                             if (!(pa.hv_keep && old == 0)) vm &= ~(1u << i);
                             break;
                         }
                         if (t == HV_EMPTY) break;
-                        sl = (sl + 1) & (HV_SLOTS - 1);
+                        sl = (sl + 1) & (HV_TAB - 1);
                     }
                 }
             }
@@ -681,7 +698,7 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
         if constexpr (HV) {
             // the chain's dropped copies of each heavy key (hcnt is cleared by
             // the next chain only after grab_tile's barriers)
-            for (uint32_t s = threadIdx.x; s < HV_SLOTS; s += NT) {
+            for (uint32_t s = threadIdx.x; s < HV_MAX; s += NT) {
                 const uint32_t c = hcnt[s];
                 if (c > pa.hv_keep) atomicAdd((unsigned long long *)&pa.hv_drop[s], (unsigned long long)(c - pa.hv_keep));
             }
@@ -2262,13 +2279,13 @@ __global__ __launch_bounds__(256) void rg_hv_select(const uint64_t *__restrict__
 
 // each heavy key's dropped copies onto its row (rows sorted by key)
 template <typename V>
-__global__ __launch_bounds__(256) void rg_hv_fix(const uint64_t *__restrict__ tab, const uint64_t *__restrict__ drop,
-                                                 const uint64_t *__restrict__ okeys, V *__restrict__ ovals,
+__global__ __launch_bounds__(256) void rg_hv_fix(const uint64_t *__restrict__ keys, const uint64_t *__restrict__ drop,
+                                                 uint32_t m, const uint64_t *__restrict__ okeys, V *__restrict__ ovals,
                                                  uint64_t n) {
     const uint32_t s = blockIdx.x * 256 + threadIdx.x;
-    if (s >= HV_SLOTS) return;
-    const uint64_t key = tab[s], d = drop[s];
-    if (key == HV_EMPTY || !d || !n) return;
+    if (s >= m) return;
+    const uint64_t key = keys[s], d = drop[s];
+    if (!d || !n) return;
     uint64_t lo = 0, hi = n;  // first row >= key
     while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
@@ -2339,8 +2356,21 @@ __global__ __launch_bounds__(256) void rg_left_counts(const uint32_t *__restrict
 
 struct HeavyRound {
     uint32_t n = 0;  // heavy keys in the table (0: none, pass 1 as usual)
-    uint64_t *tab = nullptr, *drop = nullptr;
+    char *w = nullptr;  // kman_ctx::d_hv (HVO_* parts)
 };
+
+int hv_fix(kman_ctx *ctx, const char *w, uint32_t m, const uint64_t *okeys, void *ovals, uint32_t vb, uint64_t n) {
+    const uint64_t *keys = (const uint64_t *)(w + HVO_KEYS), *drop = (const uint64_t *)(w + HVO_DROP);
+    const dim3 grid((m + 255) / 256);
+    if (vb == 4)
+        hipLaunchKernelGGL(rg_hv_fix<uint32_t>, grid, dim3(256), 0, ctx->stream, keys, drop, m, okeys,
+                           (uint32_t *)ovals, n);
+    else
+        hipLaunchKernelGGL(rg_hv_fix<uint64_t>, grid, dim3(256), 0, ctx->stream, keys, drop, m, okeys,
+                           (uint64_t *)ovals, n);
+    HIP_TRY(ctx, hipGetLastError());
+    return KMAN_OK;
+}
 
 int hv_buffer(kman_ctx *ctx, size_t bytes, char **p) {
     if (bytes > ctx->hv_bytes) {
@@ -2371,12 +2401,12 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
     const uint64_t HV_NS = 1ull << 22;
     const uint64_t S = std::max<uint64_t>(64, ceil_div(total, HV_NS));
     const uint64_t ns = ceil_div(total, S);
-    const size_t o_drop = HV_SLOTS * 8, o_misc = 2 * HV_SLOTS * 8, o_cand = o_misc + 512,
-                 o_rs = o_cand + (size_t)HV_CAND * 16, o_s = o_rs + ceil_div(nrun * 8, 256) * 256,
-                 o_a = o_s + ns * 8, o_u = o_a + ns * 8, o_c = o_u + ns * 8, bytes = o_c + ns * 4 + 256;
+    const size_t o_misc = HVO_END, o_cand = o_misc + 512, o_rs = o_cand + (size_t)HV_CAND * 16,
+                 o_s = o_rs + ceil_div(nrun * 8, 256) * 256, o_a = o_s + ns * 8, o_u = o_a + ns * 8, o_c = o_u + ns * 8,
+                 bytes = o_c + ns * 4 + 256;
     char *w;
     KMAN_TRY(hv_buffer(ctx, bytes, &w));
-    uint64_t *tab = (uint64_t *)w, *drop = (uint64_t *)(w + o_drop), *cand = (uint64_t *)(w + o_cand);
+    uint64_t *cand = (uint64_t *)(w + o_cand);
     uint32_t *hist = (uint32_t *)(w + o_misc), *ncand = hist + 64;
     uint64_t *rs = (uint64_t *)(w + o_rs), *smp = (uint64_t *)(w + o_s), *alt = (uint64_t *)(w + o_a),
              *uk = (uint64_t *)(w + o_u);
@@ -2427,19 +2457,29 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
         return hc[2 * a + 1] != hc[2 * b + 1] ? hc[2 * a + 1] > hc[2 * b + 1] : hc[2 * a] < hc[2 * b];
     });
     const uint32_t m = std::min<uint32_t>(nc, HV_MAX);
-    std::vector<uint64_t> ht(HV_SLOTS, HV_EMPTY);
+    // the table (slots -> key, index in the sorted list), the sorted list,
+    // the filter bits
+    std::vector<uint64_t> keys(m);
+    for (uint32_t i = 0; i < m; i++) keys[i] = hc[2 * order[i]];
+    std::sort(keys.begin(), keys.end());
+    std::vector<uint64_t> ht(HV_TAB, HV_EMPTY);
+    std::vector<uint32_t> hi(HV_TAB, 0), bm(HV_BM / 32, 0);
     for (uint32_t i = 0; i < m; i++) {
-        const uint64_t key = hc[2 * order[i]];
-        uint32_t sl = hv_hash(key);
-        while (ht[sl] != HV_EMPTY) sl = (sl + 1) & (HV_SLOTS - 1);
-        ht[sl] = key;
+        const uint64_t h = hv_hash(keys[i]);
+        uint32_t sl = hv_slot(h);
+        while (ht[sl] != HV_EMPTY) sl = (sl + 1) & (HV_TAB - 1);
+        ht[sl] = keys[i];
+        hi[sl] = i;
+        bm[hv_bit(h) >> 5] |= 1u << (hv_bit(h) & 31);
     }
-    HIP_TRY(ctx, hipMemcpyAsync(tab, ht.data(), HV_SLOTS * 8, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(drop, 0, HV_SLOTS * 8, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (ht leaves scope)
+    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_TAB, ht.data(), HV_TAB * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_IDX, hi.data(), HV_TAB * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_KEYS, keys.data(), (size_t)m * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_BM, bm.data(), HV_BM / 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemsetAsync(w + HVO_DROP, 0, HV_MAX * 8, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (the host vectors leave scope)
     hv->n = m;
-    hv->tab = tab;
-    hv->drop = drop;
+    hv->w = w;
     return KMAN_OK;
 }
 
@@ -2600,8 +2640,10 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         pa.fail_div = G * d.H;
         pa.fail_shift = 0;
         if (hv.n) {
-            pa.hv_keys = hv.tab;
-            pa.hv_drop = hv.drop;
+            pa.hv_keys = (const uint64_t *)(hv.w + HVO_TAB);
+            pa.hv_idx = (const uint32_t *)(hv.w + HVO_IDX);
+            pa.hv_bm = (const uint32_t *)(hv.w + HVO_BM);
+            pa.hv_drop = (uint64_t *)(hv.w + HVO_DROP);
             pa.hv_base = b_lo;
             pa.hv_kb = d.K - B1;
             pa.hv_q = d.Q;
@@ -2720,13 +2762,8 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     if (hv.n && mode == KMAN_FINISH_COUNT && *n_out) {
         // the heavy keys' dropped copies onto their rows
         KTimer kt_(ctx, "heavy_fix");
-        if (oval_bytes == 4)
-            hipLaunchKernelGGL(rg_hv_fix<uint32_t>, dim3(HV_SLOTS / 256), dim3(256), 0, ctx->stream, hv.tab, hv.drop,
-                               d_okeys, (uint32_t *)d_ovals, *n_out);
-        else
-            hipLaunchKernelGGL(rg_hv_fix<uint64_t>, dim3(HV_SLOTS / 256), dim3(256), 0, ctx->stream, hv.tab, hv.drop,
-                               d_okeys, (uint64_t *)d_ovals, *n_out);
-        HIP_TRY(ctx, hipGetLastError());
+        KMAN_TRY(hv_fix(ctx, hv.w, hv.n, d_okeys, d_ovals, oval_bytes, *n_out));
+        
     }
     if (!e) return KMAN_OK;
     // regions that overflowed a capacity (skewed keys: repeats) emitted
@@ -2747,6 +2784,14 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
             ctx->failed.push_back(hi);
         }
     }
+    if (getenv("KMAN_DROUND_LOG")) {
+        uint64_t nf = 0;
+        for (uint64_t r = 0; r < d.nreg; r++) nf += hf[r] != 0;
+        fprintf(stderr, "kman_dround_finish: %llu items, nb %u G %u H %u g %u C1s %llu C1 %llu, heavy %u, pass 1 %s, "
+                "%llu of %llu regions left out (%zu sub-buckets for a local redo)\n", (unsigned long long)roff, nb, G,
+                d.H, d.g, (unsigned long long)d.C1s, (unsigned long long)d.C1, hv.n, p1_lost ? "lost items" : "complete",
+                (unsigned long long)nf, (unsigned long long)d.nreg, ctx->left.bd.size());
+    }
     if (ctx->failed.empty())  // (an overflow that flagged no region: not expected)
         return kman_fail(ctx, KMAN_EHIP, "kman_dround_finish: overflow without a flagged region");
     return KMAN_EPARTIAL;
@@ -2765,14 +2810,15 @@ extern "C" int kman_dround_left(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_pos
     for (size_t i = 0; i < L.bd.size(); i++)
         for (uint32_t q = 0; q < GH; q++) subs[i * GH + q] = L.bd[i] * GH + q;
     // (the heavy-key scratch holds the sub-region list, counts and offsets)
-    const size_t o_subs = 2 * HV_SLOTS * 8, o_cnt = o_subs + ceil_div((uint64_t)ns * 4, 256) * 256,
+    const size_t o_subs = HVO_END, o_cnt = o_subs + ceil_div((uint64_t)ns * 4, 256) * 256,
                  o_off = o_cnt + ceil_div((uint64_t)ns * 4, 256) * 256, bytes = o_off + 256;
     if (bytes > ctx->hv_bytes) {
         // (grows the buffer: its heavy table is copied along)
         void *nb_ = nullptr;
         HIP_TRY(ctx, hipMalloc(&nb_, bytes));
         if (ctx->d_hv) {
-            HIP_TRY(ctx, hipMemcpyAsync(nb_, ctx->d_hv, 2 * HV_SLOTS * 8, hipMemcpyDeviceToDevice, ctx->stream));
+            HIP_TRY(ctx, hipMemcpyAsync(nb_, ctx->d_hv, std::min(ctx->hv_bytes, HVO_END), hipMemcpyDeviceToDevice,
+                                        ctx->stream));
             HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
             HIP_TRY(ctx, hipFree(ctx->d_hv));
         }
@@ -2828,14 +2874,7 @@ extern "C" int kman_dround_heavy_fix(kman_ctx *ctx, const uint64_t *d_keys, void
     if (!d_keys || !d_vals) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
     if (val_bytes != 4 && val_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "val_bytes must be 4 or 8");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    const uint64_t *tab = (const uint64_t *)ctx->d_hv, *drop = tab + HV_SLOTS;
-    if (val_bytes == 4)
-        hipLaunchKernelGGL(rg_hv_fix<uint32_t>, dim3(HV_SLOTS / 256), dim3(256), 0, ctx->stream, tab, drop, d_keys,
-                           (uint32_t *)d_vals, n);
-    else
-        hipLaunchKernelGGL(rg_hv_fix<uint64_t>, dim3(HV_SLOTS / 256), dim3(256), 0, ctx->stream, tab, drop, d_keys,
-                           (uint64_t *)d_vals, n);
-    HIP_TRY(ctx, hipGetLastError());
+    KMAN_TRY(hv_fix(ctx, (const char *)ctx->d_hv, ctx->heavy_keys, d_keys, d_vals, val_bytes, n));
     return KMAN_OK;
 }
 

@@ -7,7 +7,7 @@ timeout -k 10 700 python -u -m pytest -v --timeout 300 --timeout-method thread -
   tests/test_gpu_dist_region.py -k "heavy or left_out or grch38 or streamed or overlapped" \
   > gpurun_out/heavy_tests_$TAG.log 2>&1 || { tail -80 gpurun_out/heavy_tests_$TAG.log; exit 1; }
 tail -5 gpurun_out/heavy_tests_$TAG.log
-KMAN_DIST_TIMES=1 timeout -k 10 600 python -u tools/widebench.py grch38 --steps 3 \
+KMAN_DROUND_LOG=1 KMAN_DIST_TIMES=1 timeout -k 10 600 python -u tools/widebench.py grch38 --steps 3 \
   > gpurun_out/wide_$TAG.json 2> gpurun_out/wide_$TAG.err || { tail -40 gpurun_out/wide_$TAG.err; exit 1; }
 cat gpurun_out/wide_$TAG.json
 timeout -k 10 500 python -u -m pytest -v --timeout 400 --timeout-method thread -m gpu -x \
