@@ -78,6 +78,10 @@ extern "C" {
                              * (every window kept; the rounds' items in one buffer, round-major), so
                              * both use the tiles of a shard that one round takes (16 windows per
                              * thread, 8 with KMAN_RC); the same flags on both calls */
+#define KMAN_ROOMY 32u      /* kman_dround_plan / _finish: pass-1 sub-regions planned at twice their
+                             * expected fill (a genome's repeat families then fit, so regions its
+                             * finish leaves out can be redone from pass 1's output, kman_dround_left);
+                             * the same flags on both calls */
 /* kman_extract: accumulate d_hist for the passes over bits [b, 2k) only
  * (the prefix passes of kman_split_bits); default b = 0, every bit */
 #define KMAN_HIST_LO(b) (((uint32_t)(b) & 0x7fu) << 8)

@@ -35,6 +35,7 @@ KMAN_WANT_POS = 2
 KMAN_CANONICAL = 4
 KMAN_MIXED = 8
 KMAN_ONCE = 16
+KMAN_ROOMY = 32
 KMAN_FINISH_SORT = 0
 KMAN_FINISH_COUNT = 1
 KMAN_FINISH_UNIQ = 2

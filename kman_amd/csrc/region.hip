@@ -2109,7 +2109,7 @@ int make_rplan(uint32_t k, uint32_t flags, int mode, uint32_t world, uint64_t n_
     d.g = g;
     d.rest = d.K - B1 - 9 - g;
     const uint64_t e1 = maxsb / (512ull * d.H);
-    d.C1s = round_cap(e1, 256);
+    d.C1s = round_cap((flags & KMAN_ROOMY) ? 2 * e1 : e1, 256);
     if ((uint64_t)512 * world * d.H * d.C1s >= (1ull << 31)) return KMAN_EFALLBACK;  // (32-bit WC offsets)
     const uint64_t e2 = (maxb >> 9) >> g;
     const uint64_t c2 = round_cap(e2, 512);

@@ -212,6 +212,31 @@ class RoundPlanner:
             return None
         return int(a.value), max(int(b.value), 8 * int(rc.sum()))
 
+    def roomy(self, C, cuts, R: int, budget: int, a: int, b: int) -> Tuple[bool, int, int]:
+        """(True, a, b) when the same rounds fit `budget` with KMAN_ROOMY
+        (pass-1 sub-regions at twice their expected fill: a genome's repeat
+        families fit them, so a left-out region is redone from pass 1's
+        output), else (False, a, b) unchanged.  The caller then passes
+        self.flags | KMAN_ROOMY to every kman_dround_* call of the step."""
+        if os.environ.get("KMAN_ROOMY", "1") == "0":
+            return False, a, b
+        base, self.flags = self.flags, self.flags | N.KMAN_ROOMY
+        try:
+            a2 = b2 = 0
+            for q in range(self.G):
+                for r in range(R):
+                    ab = self.arenas(C, cuts, R, q, r)
+                    if ab is None:
+                        return False, a, b
+                    a2, b2 = max(a2, ab[0]), max(b2, ab[1])
+            send, _ = round_sizes(C, cuts, self.G, R)
+            a2 = max(a2, 8 * int(send.max()))
+            if a2 + b2 > budget:
+                return False, a, b
+            return True, a2, b2
+        finally:
+            self.flags = base
+
     def plan(self, C, budget: int, max_round_items: Optional[int] = None, max_rounds: int = 64):
         """(R, cuts, a_bytes, b_bytes): the fewest rounds whose largest arenas
         (over ranks and rounds) fit `budget` bytes (and whose rounds receive
@@ -657,10 +682,16 @@ class DistPipeline:
         # checks the pieces' real plans against the budget before it runs
         # overlapped, _overlapped_round)
         ov_scale = 1.0 + 1.25 / S_ if (self.overlap and self.path == "region") else 1.0
-        R, cuts, a_need, b_need = pl.plan(C, max(1, int((self.budget - out_bytes) / ov_scale)), self.max_round_items)
+        room = max(1, int((self.budget - out_bytes) / ov_scale))
+        R, cuts, a_need, b_need = pl.plan(C, room, self.max_round_items)
+        roomy = False
+        if self.path == "region":
+            roomy, a_need, b_need = pl.roomy(C, cuts, R, room, a_need, b_need)
+        # the flags of this step's kman_dround_* calls
+        self.rflags = self.flags | (N.KMAN_ROOMY if roomy else 0)
         self.rounds = R
         self.plan_info = {"budget_gb": self.budget / 1e9, "out_gb": out_bytes / 1e9, "arena_a_gb": a_need / 1e9,
-                          "arena_b_gb": b_need / 1e9, "rounds": R}
+                          "arena_b_gb": b_need / 1e9, "rounds": R, "roomy": roomy}
         _, recv = round_sizes(C, cuts, G, R)
         cap = int(recv[me].sum())
         vb = self._vb(C)
@@ -732,7 +763,7 @@ class DistPipeline:
                     self.max_message = max(self.max_message, 8 * int(np.asarray(sc, np.uint64).max()))
                     lap("exchange")
                 got = c_uint64(0)
-                ret = L.kman_dround_finish(ctx, c_void_p(rin), self.k, self.flags, self.fmode, G, self.n_bases_q,
+                ret = L.kman_dround_finish(ctx, c_void_p(rin), self.k, self.rflags, self.fmode, G, self.n_bases_q,
                                            lo, nb, _u64p(np.ascontiguousarray(counts.reshape(-1))),
                                            c_void_p(A.ptr), A.nbytes, c_void_p(B.ptr), B.nbytes,
                                            c_void_p(ok_.ptr + 8 * n_out), c_void_p(ov_.ptr + vb * n_out), vb,
@@ -799,7 +830,7 @@ class DistPipeline:
             cnt = np.ascontiguousarray(C[:, b0:b1])
             a, b = c_uint64(0), c_uint64(0)
             if b1 > b0:
-                ret = L.kman_dround_plan(self.k, self.flags, self.fmode, G, self.n_bases_q, b1 - b0,
+                ret = L.kman_dround_plan(self.k, self.rflags, self.fmode, G, self.n_bases_q, b1 - b0,
                                          _u64p(cnt.reshape(-1)), byref(a), byref(b))
                 bad |= ret != N.KMAN_OK
             plans.append(cnt)
@@ -852,7 +883,7 @@ class DistPipeline:
             if b1 <= b0:
                 continue
             got = c_uint64(0)
-            ret = L.kman_dround_finish(ctx, c_void_p(B.ptr + 8 * recv_at[s_]), self.k, self.flags, self.fmode, G,
+            ret = L.kman_dround_finish(ctx, c_void_p(B.ptr + 8 * recv_at[s_]), self.k, self.rflags, self.fmode, G,
                                        self.n_bases_q, b0, b1 - b0, _u64p(plans[s_].reshape(-1)),
                                        c_void_p(A2.ptr), A2.nbytes, c_void_p(B2.ptr), B2.nbytes,
                                        c_void_p(ok_.ptr + 8 * n_out), c_void_p(ov_.ptr + vb * n_out), vb, byref(got))

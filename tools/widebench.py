@@ -52,6 +52,10 @@ def run(name, dev, text_reader, k, mode, rc=False, canonical=False, steps=3, his
     # outside kman_groups: the key rounds with their buffers held across
     # steps (as bench.py holds ResidentPipeline's)
     lr = None if in_groups else dist.LocalRounds(p, k, rc, mode, canonical, ordered=ordered)
+    tags = ("region_extract", "region_pass", "region_pass1b", "region_finish", "heavy_sample", "left_gather",
+            "extract_marked", "extract", "sort_pass", "sort_hist", "heavy_fix")
+    if lr is not None:
+        lr.pipe.timing(True)
     for s in range(steps + 1):
         dev.sync()
         t = time.perf_counter()
@@ -91,6 +95,8 @@ def run(name, dev, text_reader, k, mode, rc=False, canonical=False, steps=3, his
                                partial_rounds=lr.pipe.partial_rounds, redone_kmers=lr.pipe.redone_kmers,
                                heavy_keys=lr.pipe.heavy_keys,
                                plan=getattr(lr.pipe, "plan_info", None), phases_ms=dict(lr.pipe.phase_ms))
+        kern = {t: lr.pipe.timed(t)[1] / (steps + 1) for t in tags}
+        dist.LAST_LOCAL["kernels_ms_per_step"] = {t: round(v, 3) for t, v in kern.items() if v}
         lr.free()
     ms = 1e3 * sum(times) / len(times)
     out = {"line": name, "value": n_k / (ms / 1e3) if n_k else None, "unit": "k-mers/s", "ms_per_step": ms,
