@@ -376,17 +376,17 @@ struct PassArgs {
     uint32_t fail_div, fail_shift;
     uint32_t big;  // a pass of <= 8 bits on the 1024-thread instance anyway (8192-item tiles: 256-byte digit runs)
     // optional (pass 1 of a key round, rg_pass<..., HV = true): the heavy
-    // keys of the round (hv_keys: an open-addressing table of HV_TAB full
+    // keys of the round (hv_tab: an open-addressing table of HV_TAB full
     // keys, HV_EMPTY where free).  An item whose key ((hv_base + b / gsub) <<
     // hv_kb | item >> hv_q) is in it is counted in LDS per chain; count mode
     // keeps the chain's first copy (hv_keep = 1) and drops the rest, uniq mode
     // drops every copy (a heavy key occurs more than once: no uniq row); the
     // dropped copies are added to hv_drop[i] when the chain ends (i =
-    // hv_idx[slot], the key's index in the sorted heavy list); hv_bm: a
+    // the key's index in the sorted heavy list, beside it in the table); hv_bm: a
     // 2^16-bit filter of the keys' hashes, so only ~3 % of the other items
     // probe the table
-    const uint64_t *hv_keys;
-    const uint32_t *hv_idx, *hv_bm;
+    const ulonglong2 *hv_tab;  // (key, index in the sorted list)
+    const uint32_t *hv_bm;
     uint64_t *hv_drop;
     uint32_t hv_base, hv_kb, hv_q, hv_keep;
 };
@@ -401,7 +401,7 @@ __host__ __device__ inline uint64_t hv_hash(uint64_t key) { return key * 0x9E377
 __host__ __device__ inline uint32_t hv_slot(uint64_t h) { return (uint32_t)(h >> 50); }  // 14 bits
 __host__ __device__ inline uint32_t hv_bit(uint64_t h) { return (uint32_t)(h >> 48); }   // 16 bits
 // the heavy-key scratch (kman_ctx::d_hv): what outlives find_heavy
-constexpr size_t HVO_TAB = 0, HVO_IDX = HVO_TAB + HV_TAB * 8, HVO_KEYS = HVO_IDX + HV_TAB * 4,
+constexpr size_t HVO_TAB = 0, HVO_KEYS = HVO_TAB + HV_TAB * 16,
                  HVO_DROP = HVO_KEYS + HV_MAX * 8, HVO_BM = HVO_DROP + HV_MAX * 8, HVO_END = HVO_BM + HV_BM / 8;
 
 // Persistent 1024-thread blocks (one per CU; 141 KiB of LDS), block-owned
@@ -595,23 +595,40 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
             for (int i = 0; i < SI; i++) vm |= (ib + i * 64 < n ? 1u : 0u) << i;
             if constexpr (HV) {
                 const uint64_t hb = (uint64_t)(pa.hv_base + b / pa.gsub) << pa.hv_kb;
+                // the filter first; then the candidates' first table slots
+                // loaded PB at a time (one round trip per batch, not per item)
+                constexpr int PB = 4;
 #pragma unroll
-                for (int i = 0; i < SI; i++) {
-                    if (!((vm >> i) & 1u)) continue;
-                    const uint64_t full = hb | ((uint64_t)key[i] >> pa.hv_q);
-                    const uint64_t hs = hv_hash(full);
-                    const uint32_t bi = hv_bit(hs);
-                    if (!((hbm[bi >> 5] >> (bi & 31)) & 1u)) continue;
-                    uint32_t sl = hv_slot(hs);
-                    for (;;) {
-                        const uint64_t t = pa.hv_keys[sl];
-                        if (t == full) {
-                            const uint32_t old = atomicAdd(&hcnt[pa.hv_idx[sl]], 1u);
-                            if (!(pa.hv_keep && old == 0)) vm &= ~(1u << i);
-                            break;
+                for (int i0 = 0; i0 < SI; i0 += PB) {
+                    uint32_t sl[PB], cand = 0;
+                    ulonglong2 e[PB];
+#pragma unroll
+                    for (int u = 0; u < PB; u++) {
+                        const int i = i0 + u;
+                        const uint64_t full = hb | ((uint64_t)key[i] >> pa.hv_q);
+                        const uint64_t hs = hv_hash(full);
+                        const uint32_t bi = hv_bit(hs);
+                        sl[u] = hv_slot(hs);
+                        if (((vm >> i) & 1u) && ((hbm[bi >> 5] >> (bi & 31)) & 1u)) cand |= 1u << u;
+                    }
+#pragma unroll
+                    for (int u = 0; u < PB; u++)
+                        if ((cand >> u) & 1u) e[u] = pa.hv_tab[sl[u]];
+#pragma unroll
+                    for (int u = 0; u < PB; u++) {
+                        if (!((cand >> u) & 1u)) continue;
+                        const int i = i0 + u;
+                        const uint64_t full = hb | ((uint64_t)key[i] >> pa.hv_q);
+                        ulonglong2 t = e[u];
+                        uint32_t q = sl[u];
+                        while (t.x != full && t.x != HV_EMPTY) {  // (a collision: rare at 1/8 load)
+                            q = (q + 1) & (HV_TAB - 1);
+                            t = pa.hv_tab[q];
                         }
-                        if (t == HV_EMPTY) break;
-                        sl = (sl + 1) & (HV_TAB - 1);
+                        if (t.x == full) {
+                            const uint32_t old = atomicAdd(&hcnt[(uint32_t)t.y], 1u);
+                            if (!(pa.hv_keep && old == 0)) vm &= ~(1u << i);
+                        }
                     }
                 }
             }
@@ -1407,7 +1424,7 @@ int make_plan(uint64_t n_bases, uint32_t k, uint32_t flags, int mode, RegionPlan
 template <typename TI, typename TO>
 void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint64_t *stp) {
     if constexpr (sizeof(TI) == 8) {
-        if (pa.hv_keys) {  // (pass 1 of a key round with heavy keys: 9 bits, the 1024-thread instance)
+        if (pa.hv_tab) {  // (pass 1 of a key round with heavy keys: 9 bits, the 1024-thread instance)
             const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, (const void *)rg_pass<TI, TO, PT_NT, R1, true>,
                                                                  PT_NT, (uint64_t)pa.nbk * pa.H);
             hipLaunchKernelGGL((rg_pass<TI, TO, PT_NT, R1, true>), dim3(grid), dim3(PT_NT), 0, ctx->stream, pa, counter,
@@ -2227,7 +2244,7 @@ int refit_g(kman_ctx *ctx, RoundPlan &d, const uint32_t *c1, uint8_t *freg, uint
 }
 
 // ---------------------------------------------------------------- heavy keys
-// A key round's heavy keys (PassArgs::hv_keys): every S-th received item's
+// A key round's heavy keys (PassArgs::hv_tab): every S-th received item's
 // full key is sampled, the samples sorted and run-length counted, and the
 // keys sampled at least twice (so they occur at least twice: a uniq round may
 // drop all their copies) -- at most HV_MAX of them, the most often sampled --
@@ -2298,50 +2315,81 @@ __global__ __launch_bounds__(256) void rg_hv_fix(const uint64_t *__restrict__ ke
 // kman_dround_left: the items of the left-out regions, from the pass-1
 // sub-regions (bd, src, h) = subs[i] of their sub-buckets bd (a sub-bucket's
 // 2^g regions are left out one by one: an item is kept when freg flags its
-// region) as full keys (+ uniq pos, as the finish emits them), appended at
-// *cursor by one atomic per wave (the rows are sorted afterwards); okeys
-// null: counted only
-template <typename TI>
+// region) as full keys (+ uniq pos, as the finish emits them).  Block
+// (i, y) takes the sub-region's 2048-item chunks y, y + Y, ...; WRITE = false
+// counts its items into bcnt[block], WRITE = true writes them from
+// boff[block] on (a scan of those counts), in chunk order
+template <typename TI, bool WRITE>
 __global__ __launch_bounds__(256) void rg_left_gather(const TI *__restrict__ r1, uint64_t C1s,
                                                       const uint32_t *__restrict__ subs,
                                                       const uint32_t *__restrict__ cnts, const uint8_t *__restrict__ freg,
                                                       uint32_t g, uint32_t G, uint32_t H, uint32_t b_lo, uint32_t kb,
-                                                      uint32_t Q, uint32_t rc, unsigned long long *__restrict__ cursor,
+                                                      uint32_t Q, uint32_t rc, uint64_t *__restrict__ bco,
                                                       uint64_t *__restrict__ okeys, uint64_t *__restrict__ opos) {
-    const uint32_t i = blockIdx.x;
+    constexpr int E = 8;
+    __shared__ uint32_t wsum[4];
+    const uint32_t i = blockIdx.x, bid = blockIdx.x * gridDim.y + blockIdx.y;
     const uint32_t s = subs[i], n = cnts[i];
     const uint32_t bd = s / (G * H), src = (s / H) % G;
     const uint64_t hi = (uint64_t)(b_lo + (bd >> 9)) << kb;
     const uint64_t kmask = (1ull << kb) - 1, qmask = Q ? (1ull << Q) - 1 : 0ull;
     const uint32_t rsh = kb - 9 - g;  // key bits below the region
     const TI *in = r1 + (uint64_t)s * C1s;
-    const int lane = lane_id();
-    for (uint32_t j0 = (blockIdx.y * 256 + (threadIdx.x & ~63u)); j0 < n; j0 += gridDim.y * 256) {
-        const uint32_t j = j0 + (uint32_t)lane;
-        uint64_t key = 0, v = 0;
-        bool keep = false;
-        if (j < n) {
-            v = in[j];
-            if constexpr (sizeof(TI) == 4) key = hi | ((uint64_t)(bd & 511u) << (kb - 9)) | (v & ((1ull << (kb - 9)) - 1));
-            else key = hi | ((v >> Q) & kmask);
-            const uint64_t r = ((uint64_t)bd << g) | ((key >> rsh) & ((1ull << g) - 1));
-            keep = freg[r] != 0;
-        }
-        const uint64_t m = __ballot(keep);
-        if (!m) continue;
-        unsigned long long base = 0;
-        if (lane == __ffsll((unsigned long long)m) - 1) base = atomicAdd(cursor, (unsigned long long)__popcll(m));
-        base = __shfl(base, __ffsll((unsigned long long)m) - 1);
-        if (keep && okeys) {
-            const uint64_t at = base + (uint64_t)__popcll(m & lanemask_lt());
-            okeys[at] = key;
-            if constexpr (sizeof(TI) == 8) {
-                if (opos) {
-                    const uint64_t idx = v & qmask;
-                    opos[at] = (rc ? idx : idx << 1) | ((uint64_t)src << 56);
-                }
+    const int lane = lane_id(), w = threadIdx.x >> 6;
+    uint64_t base = WRITE ? bco[bid] : 0;
+    uint32_t mine = 0;
+    for (uint32_t c0 = blockIdx.y * 256 * E; c0 < n; c0 += gridDim.y * 256 * E) {
+        uint64_t kk[E], vv[E];
+        uint32_t km = 0;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            const uint32_t j = c0 + e * 256 + threadIdx.x;
+            kk[e] = vv[e] = 0;
+            if (j < n) {
+                const uint64_t v = in[j];
+                uint64_t key;
+                if constexpr (sizeof(TI) == 4) key = hi | ((uint64_t)(bd & 511u) << (kb - 9)) | (v & ((1ull << (kb - 9)) - 1));
+                else key = hi | ((v >> Q) & kmask);
+                const uint64_t r = ((uint64_t)bd << g) | ((key >> rsh) & ((1ull << g) - 1));
+                if (freg[r]) km |= 1u << e;
+                kk[e] = key;
+                vv[e] = v;
             }
         }
+        const uint32_t c = (uint32_t)__popc(km);
+        if constexpr (!WRITE) {
+            mine += c;
+            continue;
+        }
+        // the chunk's block-wide exclusive offsets
+        const uint32_t inc = wave_inclusive_scan(c, SumU32());
+        if (lane == 63) wsum[w] = inc;
+        __syncthreads();
+        uint32_t before = 0, tot = 0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            before += q < w ? wsum[q] : 0u;
+            tot += wsum[q];
+        }
+        __syncthreads();
+        uint64_t at = base + before + inc - c;
+#pragma unroll
+        for (int e = 0; e < E; e++) {
+            if (!((km >> e) & 1u)) continue;
+            okeys[at] = kk[e];
+            if (sizeof(TI) == 8 && opos) {
+                const uint64_t idx = vv[e] & qmask;
+                opos[at] = (rc ? idx : idx << 1) | ((uint64_t)src << 56);
+            }
+            at++;
+        }
+        base += tot;
+    }
+    if constexpr (!WRITE) {
+        const uint32_t inc = wave_inclusive_scan(mine, SumU32());
+        if (lane == 63) wsum[w] = inc;
+        __syncthreads();
+        if (threadIdx.x == 0) bco[bid] = (uint64_t)wsum[0] + wsum[1] + wsum[2] + wsum[3];
     }
 }
 
@@ -2462,18 +2510,18 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
     std::vector<uint64_t> keys(m);
     for (uint32_t i = 0; i < m; i++) keys[i] = hc[2 * order[i]];
     std::sort(keys.begin(), keys.end());
-    std::vector<uint64_t> ht(HV_TAB, HV_EMPTY);
-    std::vector<uint32_t> hi(HV_TAB, 0), bm(HV_BM / 32, 0);
+    std::vector<uint64_t> ht(2 * HV_TAB, 0);
+    std::vector<uint32_t> bm(HV_BM / 32, 0);
+    for (uint32_t s = 0; s < HV_TAB; s++) ht[2 * s] = HV_EMPTY;
     for (uint32_t i = 0; i < m; i++) {
         const uint64_t h = hv_hash(keys[i]);
         uint32_t sl = hv_slot(h);
-        while (ht[sl] != HV_EMPTY) sl = (sl + 1) & (HV_TAB - 1);
-        ht[sl] = keys[i];
-        hi[sl] = i;
+        while (ht[2 * sl] != HV_EMPTY) sl = (sl + 1) & (HV_TAB - 1);
+        ht[2 * sl] = keys[i];
+        ht[2 * sl + 1] = i;
         bm[hv_bit(h) >> 5] |= 1u << (hv_bit(h) & 31);
     }
-    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_TAB, ht.data(), HV_TAB * 8, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_IDX, hi.data(), HV_TAB * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_TAB, ht.data(), HV_TAB * 16, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(w + HVO_KEYS, keys.data(), (size_t)m * 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(w + HVO_BM, bm.data(), HV_BM / 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(w + HVO_DROP, 0, HV_MAX * 8, ctx->stream));
@@ -2640,8 +2688,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         pa.fail_div = G * d.H;
         pa.fail_shift = 0;
         if (hv.n) {
-            pa.hv_keys = (const uint64_t *)(hv.w + HVO_TAB);
-            pa.hv_idx = (const uint32_t *)(hv.w + HVO_IDX);
+            pa.hv_tab = (const ulonglong2 *)(hv.w + HVO_TAB);
             pa.hv_bm = (const uint32_t *)(hv.w + HVO_BM);
             pa.hv_drop = (uint64_t *)(hv.w + HVO_DROP);
             pa.hv_base = b_lo;
@@ -2811,7 +2858,7 @@ extern "C" int kman_dround_left(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_pos
         for (uint32_t q = 0; q < GH; q++) subs[i * GH + q] = L.bd[i] * GH + q;
     // (the heavy-key scratch holds the sub-region list, counts and offsets)
     const size_t o_subs = HVO_END, o_cnt = o_subs + ceil_div((uint64_t)ns * 4, 256) * 256,
-                 o_off = o_cnt + ceil_div((uint64_t)ns * 4, 256) * 256, bytes = o_off + 256;
+                 o_off = o_cnt + ceil_div((uint64_t)ns * 4, 256) * 256, bytes = o_off + (size_t)ns * 16 * 8 + 256;
     if (bytes > ctx->hv_bytes) {
         // (grows the buffer: its heavy table is copied along)
         void *nb_ = nullptr;
@@ -2827,7 +2874,7 @@ extern "C" int kman_dround_left(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_pos
     }
     char *w = (char *)ctx->d_hv;
     uint32_t *d_subs = (uint32_t *)(w + o_subs), *d_cnt = (uint32_t *)(w + o_cnt);
-    uint64_t *d_cur = (uint64_t *)(w + o_off);
+    uint64_t *d_bco = (uint64_t *)(w + o_off);  // (ns x Y <= 16 per-block counts / offsets)
     HIP_TRY(ctx, hipMemcpyAsync(d_subs, subs.data(), (size_t)ns * 4, hipMemcpyHostToDevice, ctx->stream));
     hipLaunchKernelGGL(rg_left_counts, dim3((ns + 255) / 256), dim3(256), 0, ctx->stream, L.c1, d_subs, ns, L.C1s,
                        d_cnt);
@@ -2838,32 +2885,53 @@ extern "C" int kman_dround_left(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_pos
     uint32_t mx = 0;
     for (uint32_t i = 0; i < ns; i++) mx = std::max(mx, cnt[i]);
     if (d_keys && L.mode == KMAN_FINISH_UNIQ && !d_pos) return kman_fail(ctx, KMAN_EINVAL, "uniq: null pos");
-    HIP_TRY(ctx, hipMemsetAsync(d_cur, 0, 8, ctx->stream));
     KTimer kt_(ctx, "left_gather");
-    const dim3 grid(ns, std::max<uint32_t>(1, std::min<uint32_t>(64, (mx + 2047) / 2048)));
-    uint64_t *pos = L.mode == KMAN_FINISH_UNIQ ? d_pos : nullptr;
-    // (a first launch counts: the caller's cap is checked before any write)
-    for (int pass = d_keys ? 0 : 1; pass < 2; pass++) {
-        uint64_t *ok = pass ? d_keys : nullptr;
-        if (pass && d_keys) HIP_TRY(ctx, hipMemsetAsync(d_cur, 0, 8, ctx->stream));
-        if (L.narrow)
-            hipLaunchKernelGGL(rg_left_gather<uint32_t>, grid, dim3(256), 0, ctx->stream, (const uint32_t *)L.r1,
-                               L.C1s, d_subs, d_cnt, L.freg, L.g, L.G, L.H, L.b_lo, L.K - B1, L.Q, (uint32_t)L.rc,
-                               (unsigned long long *)d_cur, ok, ok ? pos : nullptr);
-        else
-            hipLaunchKernelGGL(rg_left_gather<uint64_t>, grid, dim3(256), 0, ctx->stream, (const uint64_t *)L.r1,
-                               L.C1s, d_subs, d_cnt, L.freg, L.g, L.G, L.H, L.b_lo, L.K - B1, L.Q, (uint32_t)L.rc,
-                               (unsigned long long *)d_cur, ok, ok ? pos : nullptr);
-        HIP_TRY(ctx, hipGetLastError());
-        uint64_t tot = 0;
-        HIP_TRY(ctx, hipMemcpyAsync(&tot, d_cur, 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-        *n = tot;
-        if (!pass && tot > cap)
-            return kman_fail(ctx, KMAN_ECAP, "kman_dround_left: %llu items > cap %llu", (unsigned long long)tot,
-                             (unsigned long long)cap);
-        if (!d_keys) break;
+    const uint32_t Y = std::max<uint32_t>(1, std::min<uint32_t>(16, (mx + 2047) / 2048));
+    const dim3 grid(ns, Y);
+    const uint64_t nbk = (uint64_t)ns * Y;
+    // the per-block counts, then (writing) their exclusive scan, in d_bco
+    const auto launch = [&](bool write) {
+        uint64_t *pos = write && L.mode == KMAN_FINISH_UNIQ ? d_pos : nullptr;
+        uint64_t *ok = write ? d_keys : nullptr;
+        if (L.narrow) {
+            if (write)
+                hipLaunchKernelGGL((rg_left_gather<uint32_t, true>), grid, dim3(256), 0, ctx->stream,
+                                   (const uint32_t *)L.r1, L.C1s, d_subs, d_cnt, L.freg, L.g, L.G, L.H, L.b_lo,
+                                   L.K - B1, L.Q, (uint32_t)L.rc, d_bco, ok, pos);
+            else
+                hipLaunchKernelGGL((rg_left_gather<uint32_t, false>), grid, dim3(256), 0, ctx->stream,
+                                   (const uint32_t *)L.r1, L.C1s, d_subs, d_cnt, L.freg, L.g, L.G, L.H, L.b_lo,
+                                   L.K - B1, L.Q, (uint32_t)L.rc, d_bco, ok, pos);
+        } else {
+            if (write)
+                hipLaunchKernelGGL((rg_left_gather<uint64_t, true>), grid, dim3(256), 0, ctx->stream,
+                                   (const uint64_t *)L.r1, L.C1s, d_subs, d_cnt, L.freg, L.g, L.G, L.H, L.b_lo,
+                                   L.K - B1, L.Q, (uint32_t)L.rc, d_bco, ok, pos);
+            else
+                hipLaunchKernelGGL((rg_left_gather<uint64_t, false>), grid, dim3(256), 0, ctx->stream,
+                                   (const uint64_t *)L.r1, L.C1s, d_subs, d_cnt, L.freg, L.g, L.G, L.H, L.b_lo,
+                                   L.K - B1, L.Q, (uint32_t)L.rc, d_bco, ok, pos);
+        }
+        return hipGetLastError();
+    };
+    HIP_TRY(ctx, launch(false));
+    std::vector<uint64_t> bc(nbk);
+    HIP_TRY(ctx, hipMemcpyAsync(bc.data(), d_bco, nbk * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    uint64_t tot = 0;
+    for (uint64_t q = 0; q < nbk; q++) {
+        const uint64_t c = bc[q];
+        bc[q] = tot;
+        tot += c;
     }
+    *n = tot;
+    if (!d_keys || !tot) return KMAN_OK;
+    if (tot > cap)
+        return kman_fail(ctx, KMAN_ECAP, "kman_dround_left: %llu items > cap %llu", (unsigned long long)tot,
+                         (unsigned long long)cap);
+    HIP_TRY(ctx, hipMemcpyAsync(d_bco, bc.data(), nbk * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, launch(true));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (bc leaves scope)
     return KMAN_OK;
 }
 
