@@ -350,8 +350,9 @@ int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_t k, uint32
  * (kman_merge_runs). */
 int kman_dround_failed(kman_ctx *ctx, uint64_t *ranges, uint64_t cap, uint64_t *n);
 /* Heavy keys of the last kman_dround_finish (*n; 0 when none or off): keys
- * that every S-th received item's sample saw at least twice (at most 2048,
- * the most often sampled) are counted apart in its pass 1 -- count mode
+ * that every S-th received item's sample saw at least twice (the most often
+ * sampled, at most 256 per bucket of the round, held in the pass's LDS while
+ * a chain of the bucket runs) are counted apart in its pass 1 -- count mode
  * keeps one copy per pass-1 chain and adds the others to the key's row after
  * the finish, uniq mode drops them all (they occur more than once) -- so a
  * repeat with 10^5 copies does not overflow its regions.  KMAN_HEAVY=0 turns

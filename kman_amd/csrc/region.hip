@@ -376,33 +376,30 @@ struct PassArgs {
     uint32_t fail_div, fail_shift;
     uint32_t big;  // a pass of <= 8 bits on the 1024-thread instance anyway (8192-item tiles: 256-byte digit runs)
     // optional (pass 1 of a key round, rg_pass<..., HV = true): the heavy
-    // keys of the round (hv_tab: an open-addressing table of HV_TAB full
-    // keys, HV_EMPTY where free).  An item whose key ((hv_base + b / gsub) <<
-    // hv_kb | item >> hv_q) is in it is counted in LDS per chain; count mode
-    // keeps the chain's first copy (hv_keep = 1) and drops the rest, uniq mode
-    // drops every copy (a heavy key occurs more than once: no uniq row); the
-    // dropped copies are added to hv_drop[i] when the chain ends (i =
-    // the key's index in the sorted heavy list, beside it in the table); hv_bm: a
-    // 2^16-bit filter of the keys' hashes, so only ~3 % of the other items
-    // probe the table
-    const ulonglong2 *hv_tab;  // (key, index in the sorted list)
-    const uint32_t *hv_bm;
+    // keys of the round, per bucket j of the round an open-addressing table
+    // of HV_BSLOTS key rests (the item's key bits, item >> hv_q; HV_EMPTY
+    // where free) at hv_tab[j * HV_BSLOTS], copied to LDS when a chain of
+    // the bucket starts (a bucket holds <= HV_BMAX of them).  An item whose
+    // key rest is in it is counted per slot in LDS; count mode keeps the
+    // chain's first copy (hv_keep = 1) and drops the rest, uniq mode drops
+    // every copy (a heavy key occurs more than once: no uniq row); the chain's
+    // dropped copies go to hv_drop[hv_idx[j * HV_BSLOTS + slot]] when it ends
+    const uint64_t *hv_tab;
+    const uint32_t *hv_idx;
     uint64_t *hv_drop;
-    uint32_t hv_base, hv_kb, hv_q, hv_keep;
+    uint32_t hv_q, hv_keep;
 };
 
 // heavy keys of a key round (kman_dround_finish): found by sampling the
 // received items, counted apart in pass 1 so that a satellite or repeat-family
 // k-mer with 10^5 copies does not overflow its regions (and send the key range
 // through the partial redo)
-constexpr uint32_t HV_MAX = 2048, HV_TAB = 16384, HV_BM = 1u << 16;
+constexpr uint32_t HV_BSLOTS = 1024, HV_BMAX = 256, HV_MAX = 1u << 16;
 constexpr uint64_t HV_EMPTY = ~0ull;
-__host__ __device__ inline uint64_t hv_hash(uint64_t key) { return key * 0x9E3779B97F4A7C15ull; }
-__host__ __device__ inline uint32_t hv_slot(uint64_t h) { return (uint32_t)(h >> 50); }  // 14 bits
-__host__ __device__ inline uint32_t hv_bit(uint64_t h) { return (uint32_t)(h >> 48); }   // 16 bits
+__host__ __device__ inline uint32_t hv_slot(uint64_t rest) { return (uint32_t)((rest * 0x9E3779B97F4A7C15ull) >> 54); }
 // the heavy-key scratch (kman_ctx::d_hv): what outlives find_heavy
-constexpr size_t HVO_TAB = 0, HVO_KEYS = HVO_TAB + HV_TAB * 16,
-                 HVO_DROP = HVO_KEYS + HV_MAX * 8, HVO_BM = HVO_DROP + HV_MAX * 8, HVO_END = HVO_BM + HV_BM / 8;
+constexpr size_t HVO_TAB = 0, HVO_IDX = HVO_TAB + 256 * HV_BSLOTS * 8, HVO_KEYS = HVO_IDX + 256 * HV_BSLOTS * 4,
+                 HVO_DROP = HVO_KEYS + HV_MAX * 8, HVO_END = HVO_DROP + HV_MAX * 8;
 
 // Persistent 1024-thread blocks (one per CU; 141 KiB of LDS), block-owned
 // chains: a block takes a whole chain (bucket b, part h: the h-th of H runs of
@@ -467,12 +464,8 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
     __shared__ uint32_t s_items;
     __shared__ uint32_t lds_tile;
     // HV: the chain's copies of each heavy key (by table slot)
-    __shared__ uint32_t hcnt[HV ? HV_MAX : 1];
-    __shared__ uint32_t hbm[HV ? HV_BM / 32 : 1];
-    if constexpr (HV) {
-        for (uint32_t s = threadIdx.x; s < HV_BM / 32; s += NT) hbm[s] = pa.hv_bm[s];
-        // (visible after grab_tile's barriers)
-    }
+    __shared__ uint64_t htab[HV ? HV_BSLOTS : 1];
+    __shared__ uint32_t hcnt[HV ? HV_BSLOTS : 1];
     const uint32_t shift = pa.shift, bits = pa.bits, nsg = pa.nsg, H = pa.H;
     const uint64_t C1 = pa.C1;
     const int lane = lane_id();
@@ -500,7 +493,10 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
         }
         if (threadIdx.x < RB) run[threadIdx.x] = 0;
         if constexpr (HV)
-            for (uint32_t s = threadIdx.x; s < HV_MAX; s += NT) hcnt[s] = 0;
+            for (uint32_t s = threadIdx.x; s < HV_BSLOTS; s += NT) {
+                htab[s] = pa.hv_tab[(uint64_t)(b / pa.gsub) * HV_BSLOTS + s];
+                hcnt[s] = 0;
+            }
         __syncthreads();
         const uint32_t items = s_items;
         const uint32_t tiles = (items + TILE - 1) / TILE;
@@ -594,41 +590,19 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
 #pragma unroll
             for (int i = 0; i < SI; i++) vm |= (ib + i * 64 < n ? 1u : 0u) << i;
             if constexpr (HV) {
-                const uint64_t hb = (uint64_t)(pa.hv_base + b / pa.gsub) << pa.hv_kb;
-                // the filter first; then the candidates' first table slots
-                // loaded PB at a time (one round trip per batch, not per item)
-                constexpr int PB = 4;
 #pragma unroll
-                for (int i0 = 0; i0 < SI; i0 += PB) {
-                    uint32_t sl[PB], cand = 0;
-                    ulonglong2 e[PB];
-#pragma unroll
-                    for (int u = 0; u < PB; u++) {
-                        const int i = i0 + u;
-                        const uint64_t full = hb | ((uint64_t)key[i] >> pa.hv_q);
-                        const uint64_t hs = hv_hash(full);
-                        const uint32_t bi = hv_bit(hs);
-                        sl[u] = hv_slot(hs);
-                        if (((vm >> i) & 1u) && ((hbm[bi >> 5] >> (bi & 31)) & 1u)) cand |= 1u << u;
+                for (int i = 0; i < SI; i++) {
+                    if (!((vm >> i) & 1u)) continue;
+                    const uint64_t kr = (uint64_t)key[i] >> pa.hv_q;
+                    uint32_t sl = hv_slot(kr);
+                    uint64_t t = htab[sl];
+                    while (t != kr && t != HV_EMPTY) {  // (<= 1/4 full: short)
+                        sl = (sl + 1) & (HV_BSLOTS - 1);
+                        t = htab[sl];
                     }
-#pragma unroll
-                    for (int u = 0; u < PB; u++)
-                        if ((cand >> u) & 1u) e[u] = pa.hv_tab[sl[u]];
-#pragma unroll
-                    for (int u = 0; u < PB; u++) {
-                        if (!((cand >> u) & 1u)) continue;
-                        const int i = i0 + u;
-                        const uint64_t full = hb | ((uint64_t)key[i] >> pa.hv_q);
-                        ulonglong2 t = e[u];
-                        uint32_t q = sl[u];
-                        while (t.x != full && t.x != HV_EMPTY) {  // (a collision: rare at 1/8 load)
-                            q = (q + 1) & (HV_TAB - 1);
-                            t = pa.hv_tab[q];
-                        }
-                        if (t.x == full) {
-                            const uint32_t old = atomicAdd(&hcnt[(uint32_t)t.y], 1u);
-                            if (!(pa.hv_keep && old == 0)) vm &= ~(1u << i);
-                        }
+                    if (t == kr) {
+                        const uint32_t old = atomicAdd(&hcnt[sl], 1u);
+                        if (!(pa.hv_keep && old == 0)) vm &= ~(1u << i);
                     }
                 }
             }
@@ -715,9 +689,11 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
         if constexpr (HV) {
             // the chain's dropped copies of each heavy key (hcnt is cleared by
             // the next chain only after grab_tile's barriers)
-            for (uint32_t s = threadIdx.x; s < HV_MAX; s += NT) {
+            for (uint32_t s = threadIdx.x; s < HV_BSLOTS; s += NT) {
                 const uint32_t c = hcnt[s];
-                if (c > pa.hv_keep) atomicAdd((unsigned long long *)&pa.hv_drop[s], (unsigned long long)(c - pa.hv_keep));
+                if (c > pa.hv_keep)
+                    atomicAdd((unsigned long long *)&pa.hv_drop[pa.hv_idx[(uint64_t)(b / pa.gsub) * HV_BSLOTS + s]],
+                              (unsigned long long)(c - pa.hv_keep));
             }
         }
 #undef SUBREG
@@ -2247,13 +2223,13 @@ int refit_g(kman_ctx *ctx, RoundPlan &d, const uint32_t *c1, uint8_t *freg, uint
 // A key round's heavy keys (PassArgs::hv_tab): every S-th received item's
 // full key is sampled, the samples sorted and run-length counted, and the
 // keys sampled at least twice (so they occur at least twice: a uniq round may
-// drop all their copies) -- at most HV_MAX of them, the most often sampled --
+// drop all their copies) -- the most often sampled, at most HV_BMAX per bucket --
 // go into an open-addressing table that pass 1 probes per item.  Pass 1 adds
 // each key's dropped copies to drop[slot]; rg_hv_fix then adds them to the
 // key's row (count mode: pass 1 kept one copy per chain, so the row exists
 // unless its region was left out, in which case the partial redo recounts
 // the whole key range from the codes).
-constexpr uint32_t HV_CAND = 1u << 16;  // candidates downloaded to pick the table from
+constexpr uint32_t HV_CAND = 1u << 17;  // candidates downloaded to pick the tables from
 
 // sample i = the item at i * S; runs (src, j) lie in src-major order, run t =
 // src * nb + j starting at rs[t] (the last run starting at or before p holds p)
@@ -2446,7 +2422,7 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
     if (d.K > 62 || (!force && total < (1u << 20)) || !total) return KMAN_OK;  // (table keys < HV_EMPTY)
     const uint32_t nb = d.nb, G = d.G, nrun = nb * G;
     // samples: every S-th item, S >= 64, at most HV_NS
-    const uint64_t HV_NS = 1ull << 22;
+    const uint64_t HV_NS = 1ull << 23;
     const uint64_t S = std::max<uint64_t>(64, ceil_div(total, HV_NS));
     const uint64_t ns = ceil_div(total, S);
     const size_t o_misc = HVO_END, o_cand = o_misc + 512, o_rs = o_cand + (size_t)HV_CAND * 16,
@@ -2504,26 +2480,32 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
     std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
         return hc[2 * a + 1] != hc[2 * b + 1] ? hc[2 * a + 1] > hc[2 * b + 1] : hc[2 * a] < hc[2 * b];
     });
-    const uint32_t m = std::min<uint32_t>(nc, HV_MAX);
-    // the table (slots -> key, index in the sorted list), the sorted list,
-    // the filter bits
-    std::vector<uint64_t> keys(m);
-    for (uint32_t i = 0; i < m; i++) keys[i] = hc[2 * order[i]];
-    std::sort(keys.begin(), keys.end());
-    std::vector<uint64_t> ht(2 * HV_TAB, 0);
-    std::vector<uint32_t> bm(HV_BM / 32, 0);
-    for (uint32_t s = 0; s < HV_TAB; s++) ht[2 * s] = HV_EMPTY;
-    for (uint32_t i = 0; i < m; i++) {
-        const uint64_t h = hv_hash(keys[i]);
-        uint32_t sl = hv_slot(h);
-        while (ht[2 * sl] != HV_EMPTY) sl = (sl + 1) & (HV_TAB - 1);
-        ht[2 * sl] = keys[i];
-        ht[2 * sl + 1] = i;
-        bm[hv_bit(h) >> 5] |= 1u << (hv_bit(h) & 31);
+    // per bucket of the round at most HV_BMAX keys, the most often sampled;
+    // per bucket a table of their key rests (and their index in keys)
+    const uint32_t kb = d.K - B1;
+    std::vector<uint32_t> per(nb, 0);
+    std::vector<uint64_t> keys;
+    for (uint32_t i = 0; i < nc && keys.size() < HV_MAX; i++) {
+        const uint64_t key = hc[2 * order[i]];
+        const uint32_t j = (uint32_t)(key >> kb) - b_lo;
+        if (j >= nb || per[j] >= HV_BMAX) continue;
+        per[j]++;
+        keys.push_back(key);
     }
-    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_TAB, ht.data(), HV_TAB * 16, hipMemcpyHostToDevice, ctx->stream));
+    const uint32_t m = (uint32_t)keys.size();
+    std::vector<uint64_t> ht((size_t)nb * HV_BSLOTS, HV_EMPTY);
+    std::vector<uint32_t> hi((size_t)nb * HV_BSLOTS, 0);
+    for (uint32_t i = 0; i < m; i++) {
+        const uint32_t j = (uint32_t)(keys[i] >> kb) - b_lo;
+        const uint64_t kr = keys[i] & ((1ull << kb) - 1);
+        uint32_t sl = hv_slot(kr);
+        while (ht[(size_t)j * HV_BSLOTS + sl] != HV_EMPTY) sl = (sl + 1) & (HV_BSLOTS - 1);
+        ht[(size_t)j * HV_BSLOTS + sl] = kr;
+        hi[(size_t)j * HV_BSLOTS + sl] = i;
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_TAB, ht.data(), ht.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_IDX, hi.data(), hi.size() * 4, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(w + HVO_KEYS, keys.data(), (size_t)m * 8, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_BM, bm.data(), HV_BM / 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(w + HVO_DROP, 0, HV_MAX * 8, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (the host vectors leave scope)
     hv->n = m;
@@ -2688,11 +2670,9 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         pa.fail_div = G * d.H;
         pa.fail_shift = 0;
         if (hv.n) {
-            pa.hv_tab = (const ulonglong2 *)(hv.w + HVO_TAB);
-            pa.hv_bm = (const uint32_t *)(hv.w + HVO_BM);
+            pa.hv_tab = (const uint64_t *)(hv.w + HVO_TAB);
+            pa.hv_idx = (const uint32_t *)(hv.w + HVO_IDX);
             pa.hv_drop = (uint64_t *)(hv.w + HVO_DROP);
-            pa.hv_base = b_lo;
-            pa.hv_kb = d.K - B1;
             pa.hv_q = d.Q;
             pa.hv_keep = mode == KMAN_FINISH_COUNT;
         }
