@@ -36,6 +36,7 @@
 #include "kmer.h"
 #include "onesweep.h"
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -2440,17 +2441,24 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
         for (uint32_t j = 0; j < nb; j++) hrs[(size_t)src * nb + j] = hb[(size_t)j * G + src];
     HIP_TRY(ctx, hipMemcpyAsync(rs, hrs.data(), nrun * 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(hist, 0, 512, ctx->stream));
-    {
-        KTimer kt_(ctx, "heavy_sample");
-        hipLaunchKernelGGL(rg_hv_sample, dim3((uint32_t)ceil_div(ns, 256)), dim3(256), 0, ctx->stream, d_recv, rs,
-                           nrun, nb, S, ns, b_lo, d.K - B1, d.Q, smp);
-        HIP_TRY(ctx, hipGetLastError());
-    }
-    int in_alt = 0;
-    KMAN_TRY(kman_sort(ctx, smp, alt, nullptr, nullptr, 0, ns, d.K, nullptr, &in_alt));
+    // the samples sorted and run-length counted: first 2^18 of them (every
+    // S1-th item; all distinct -- uniform keys -- ends it here), then ns
     uint64_t nu = 0;
-    KMAN_TRY(kman_rle_count(ctx, in_alt ? alt : smp, ns, uk, uc, 4, &nu));  // (synchronises)
-    if (nu == ns) return KMAN_OK;  // every sample distinct: no heavy key
+    for (int stage = 0; stage < 2; stage++) {
+        const uint64_t S_ = stage ? S : std::max<uint64_t>(S, ceil_div(total, 1ull << 18)),
+                       ns_ = stage ? ns : ceil_div(total, S_);
+        if (stage && S_ == std::max<uint64_t>(S, ceil_div(total, 1ull << 18))) break;  // (stage 0 took them all)
+        {
+            KTimer kt_(ctx, "heavy_sample");
+            hipLaunchKernelGGL(rg_hv_sample, dim3((uint32_t)ceil_div(ns_, 256)), dim3(256), 0, ctx->stream, d_recv,
+                               rs, nrun, nb, S_, ns_, b_lo, d.K - B1, d.Q, smp);
+            HIP_TRY(ctx, hipGetLastError());
+        }
+        int in_alt = 0;
+        KMAN_TRY(kman_sort(ctx, smp, alt, nullptr, nullptr, 0, ns_, d.K, nullptr, &in_alt));
+        KMAN_TRY(kman_rle_count(ctx, in_alt ? alt : smp, ns_, uk, uc, 4, &nu));  // (synchronises)
+        if (nu == ns_) return KMAN_OK;  // every sample distinct: no heavy key
+    }
     const uint32_t gx = (uint32_t)ceil_div(nu, 256);
     hipLaunchKernelGGL(rg_hv_select, dim3(gx), dim3(256), 0, ctx->stream, uk, uc, nu, 0u, hist, ncand, cand);
     HIP_TRY(ctx, hipGetLastError());
@@ -2474,19 +2482,18 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
     nc = std::min(nc, HV_CAND);
     std::vector<uint64_t> hc((size_t)nc * 2);
     if (nc) HIP_TRY(ctx, hipMemcpy(hc.data(), cand, (size_t)nc * 16, hipMemcpyDeviceToHost));
-    std::vector<uint32_t> order(nc);
-    for (uint32_t i = 0; i < nc; i++) order[i] = i;
-    // the most often sampled first (ties by key: the table is the same whatever the atomics' order)
-    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
-        return hc[2 * a + 1] != hc[2 * b + 1] ? hc[2 * a + 1] > hc[2 * b + 1] : hc[2 * a] < hc[2 * b];
-    });
+    // the most often sampled first (ties by key: the tables are the same
+    // whatever the order the atomics gave)
+    std::vector<std::pair<uint64_t, uint64_t>> byh(nc);
+    for (uint32_t i = 0; i < nc; i++) byh[i] = {~hc[2 * i + 1], hc[2 * i]};
+    std::sort(byh.begin(), byh.end());
     // per bucket of the round at most HV_BMAX keys, the most often sampled;
     // per bucket a table of their key rests (and their index in keys)
     const uint32_t kb = d.K - B1;
     std::vector<uint32_t> per(nb, 0);
     std::vector<uint64_t> keys;
     for (uint32_t i = 0; i < nc && keys.size() < HV_MAX; i++) {
-        const uint64_t key = hc[2 * order[i]];
+        const uint64_t key = byh[i].second;
         const uint32_t j = (uint32_t)(key >> kb) - b_lo;
         if (j >= nb || per[j] >= HV_BMAX) continue;
         per[j]++;
@@ -2642,7 +2649,9 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     HIP_TRY(ctx, hipMemsetAsync(c1, 0, d.nsub * 4, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(freg, 0, d.nreg, ctx->stream));
     HeavyRound hv;
+    const auto t_hv0 = std::chrono::steady_clock::now();
     KMAN_TRY(find_heavy(ctx, d, d_recv, hb, roff, b_lo, &hv));
+    const double hv_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_hv0).count();
     uint32_t epoch, *counter;
     // 4-byte count items out of pass 1 when the key bits below its digit
     // (rest + g, whatever refit_g makes of the split) fit 32 bits
@@ -2815,9 +2824,10 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         uint64_t nf = 0;
         for (uint64_t r = 0; r < d.nreg; r++) nf += hf[r] != 0;
         fprintf(stderr, "kman_dround_finish: %llu items, nb %u G %u H %u g %u C1s %llu C1 %llu, heavy %u, pass 1 %s, "
-                "%llu of %llu regions left out (%zu sub-buckets for a local redo)\n", (unsigned long long)roff, nb, G,
-                d.H, d.g, (unsigned long long)d.C1s, (unsigned long long)d.C1, hv.n, p1_lost ? "lost items" : "complete",
-                (unsigned long long)nf, (unsigned long long)d.nreg, ctx->left.bd.size());
+                "%llu of %llu regions left out (%zu sub-buckets for a local redo); finding the heavy keys %.2f ms\n",
+                (unsigned long long)roff, nb, G, d.H, d.g, (unsigned long long)d.C1s, (unsigned long long)d.C1, hv.n,
+                p1_lost ? "lost items" : "complete", (unsigned long long)nf, (unsigned long long)d.nreg,
+                ctx->left.bd.size(), hv_ms);
     }
     if (ctx->failed.empty())  // (an overflow that flagged no region: not expected)
         return kman_fail(ctx, KMAN_EHIP, "kman_dround_finish: overflow without a flagged region");
