@@ -2465,14 +2465,15 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
     uint32_t hh[64];
     HIP_TRY(ctx, hipMemcpyAsync(hh, hist, sizeof(hh), hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    // the lowest threshold >= 2 whose candidates fit HV_CAND
+    // the lowest threshold >= 2 whose candidates fit HV_MAX
     uint64_t above = 0;
     uint32_t T = 63;
     for (uint32_t t = 63; t >= 2; t--) {
+        if (above + hh[t] > HV_MAX) break;
         above += hh[t];
-        if (above > HV_CAND) break;
         T = t;
     }
+    if (!above && hh[63]) above = hh[63];  // (more than HV_MAX keys sampled >= 63 times: HV_CAND of them)
     if (!above) return KMAN_OK;
     hipLaunchKernelGGL(rg_hv_select, dim3(gx), dim3(256), 0, ctx->stream, uk, uc, nu, T, hist, ncand, cand);
     HIP_TRY(ctx, hipGetLastError());
@@ -2480,41 +2481,67 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
     HIP_TRY(ctx, hipMemcpyAsync(&nc, ncand, 4, hipMemcpyDeviceToHost, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     nc = std::min(nc, HV_CAND);
-    std::vector<uint64_t> hc((size_t)nc * 2);
-    if (nc) HIP_TRY(ctx, hipMemcpy(hc.data(), cand, (size_t)nc * 16, hipMemcpyDeviceToHost));
-    // the most often sampled first (ties by key: the tables are the same
-    // whatever the order the atomics gave)
-    std::vector<std::pair<uint64_t, uint64_t>> byh(nc);
-    for (uint32_t i = 0; i < nc; i++) byh[i] = {~hc[2 * i + 1], hc[2 * i]};
-    std::sort(byh.begin(), byh.end());
-    // per bucket of the round at most HV_BMAX keys, the most often sampled;
-    // per bucket a table of their key rests (and their index in keys)
+    // pinned staging: the candidates down, the tables up
+    const size_t tab_b = (size_t)nb * HV_BSLOTS * 8, idx_b = (size_t)nb * HV_BSLOTS * 4;
+    const size_t stage_b = std::max((size_t)HV_CAND * 16, tab_b + idx_b + (size_t)HV_MAX * 8);
+    if (stage_b > ctx->hv_host_bytes) {
+        if (ctx->h_hv) HIP_TRY(ctx, hipHostFree(ctx->h_hv));
+        ctx->h_hv = nullptr;
+        ctx->hv_host_bytes = 0;
+        HIP_TRY(ctx, hipHostMalloc(&ctx->h_hv, stage_b, hipHostMallocDefault));
+        ctx->hv_host_bytes = stage_b;
+    }
+    const uint64_t *hc = (const uint64_t *)ctx->h_hv;
+    if (nc) {
+        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_hv, cand, (size_t)nc * 16, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    // per bucket of the round at most HV_BMAX keys: the most often sampled
+    // (ties by key, so the tables do not depend on the atomics' order), in
+    // key order; per bucket a table of their key rests and their index in keys
     const uint32_t kb = d.K - B1;
-    std::vector<uint32_t> per(nb, 0);
-    std::vector<uint64_t> keys;
-    for (uint32_t i = 0; i < nc && keys.size() < HV_MAX; i++) {
-        const uint64_t key = byh[i].second;
-        const uint32_t j = (uint32_t)(key >> kb) - b_lo;
-        if (j >= nb || per[j] >= HV_BMAX) continue;
-        per[j]++;
-        keys.push_back(key);
+    std::vector<uint32_t> start(nb + 1, 0);
+    for (uint32_t i = 0; i < nc; i++) {
+        const uint32_t j = (uint32_t)(hc[2 * i] >> kb) - b_lo;
+        if (j < nb) start[j + 1]++;
     }
-    const uint32_t m = (uint32_t)keys.size();
-    std::vector<uint64_t> ht((size_t)nb * HV_BSLOTS, HV_EMPTY);
-    std::vector<uint32_t> hi((size_t)nb * HV_BSLOTS, 0);
-    for (uint32_t i = 0; i < m; i++) {
-        const uint32_t j = (uint32_t)(keys[i] >> kb) - b_lo;
-        const uint64_t kr = keys[i] & ((1ull << kb) - 1);
-        uint32_t sl = hv_slot(kr);
-        while (ht[(size_t)j * HV_BSLOTS + sl] != HV_EMPTY) sl = (sl + 1) & (HV_BSLOTS - 1);
-        ht[(size_t)j * HV_BSLOTS + sl] = kr;
-        hi[(size_t)j * HV_BSLOTS + sl] = i;
+    for (uint32_t j = 0; j < nb; j++) start[j + 1] += start[j];
+    std::vector<std::pair<uint64_t, uint64_t>> byb(start[nb]);  // (~hits, key) grouped by bucket
+    {
+        std::vector<uint32_t> at(start.begin(), start.end() - 1);
+        for (uint32_t i = 0; i < nc; i++) {
+            const uint32_t j = (uint32_t)(hc[2 * i] >> kb) - b_lo;
+            if (j < nb) byb[at[j]++] = {~hc[2 * i + 1], hc[2 * i]};
+        }
     }
-    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_TAB, ht.data(), ht.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_IDX, hi.data(), hi.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_KEYS, keys.data(), (size_t)m * 8, hipMemcpyHostToDevice, ctx->stream));
+    uint64_t *ht = (uint64_t *)ctx->h_hv;  // (the candidates are in byb now)
+    uint32_t *hi = (uint32_t *)((char *)ctx->h_hv + tab_b);
+    uint64_t *keys = (uint64_t *)((char *)ctx->h_hv + tab_b + idx_b);
+    std::fill(ht, ht + (size_t)nb * HV_BSLOTS, HV_EMPTY);
+    uint32_t m = 0;
+    for (uint32_t j = 0; j < nb; j++) {
+        auto b0 = byb.begin() + start[j], b1 = byb.begin() + start[j + 1];
+        if (b1 - b0 > (long)HV_BMAX) {
+            std::nth_element(b0, b0 + HV_BMAX, b1);
+            b1 = b0 + HV_BMAX;
+        }
+        std::sort(b0, b1, [](const std::pair<uint64_t, uint64_t> &x, const std::pair<uint64_t, uint64_t> &y) {
+            return x.second < y.second;
+        });
+        for (auto it = b0; it != b1; ++it, ++m) {
+            const uint64_t kr = it->second & ((1ull << kb) - 1);
+            uint32_t sl = hv_slot(kr);
+            while (ht[(size_t)j * HV_BSLOTS + sl] != HV_EMPTY) sl = (sl + 1) & (HV_BSLOTS - 1);
+            ht[(size_t)j * HV_BSLOTS + sl] = kr;
+            hi[(size_t)j * HV_BSLOTS + sl] = m;
+            keys[m] = it->second;
+        }
+    }
+    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_TAB, ht, tab_b, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_IDX, hi, idx_b, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_KEYS, keys, (size_t)m * 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(w + HVO_DROP, 0, HV_MAX * 8, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (the host vectors leave scope)
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (the staging is reused by the next round)
     hv->n = m;
     hv->w = w;
     return KMAN_OK;
