@@ -397,7 +397,9 @@ struct PassArgs {
 // through the partial redo)
 constexpr uint32_t HV_BSLOTS = 1024, HV_BMAX = 256, HV_MAX = 1u << 16;
 constexpr uint64_t HV_EMPTY = ~0ull;
-__host__ __device__ inline uint32_t hv_slot(uint64_t rest) { return (uint32_t)((rest * 0x9E3779B97F4A7C15ull) >> 54); }
+__host__ __device__ inline uint32_t hv_slot(uint64_t rest) {
+    return (((uint32_t)rest ^ (uint32_t)(rest >> 29)) * 0x9E3779B1u) >> 22;  // (one 32-bit multiply)
+}
 // the heavy-key scratch (kman_ctx::d_hv): what outlives find_heavy
 constexpr size_t HVO_TAB = 0, HVO_IDX = HVO_TAB + 256 * HV_BSLOTS * 8, HVO_KEYS = HVO_IDX + 256 * HV_BSLOTS * 4,
                  HVO_DROP = HVO_KEYS + HV_MAX * 8, HVO_END = HVO_DROP + HV_MAX * 8;
@@ -2444,6 +2446,10 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
     // the samples sorted and run-length counted: first 2^18 of them (every
     // S1-th item; all distinct -- uniform keys -- ends it here), then ns
     uint64_t nu = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto ms_since = [&](std::chrono::steady_clock::time_point a) {
+        return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+    };
     for (int stage = 0; stage < 2; stage++) {
         const uint64_t S_ = stage ? S : std::max<uint64_t>(S, ceil_div(total, 1ull << 18)),
                        ns_ = stage ? ns : ceil_div(total, S_);
@@ -2459,6 +2465,8 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
         KMAN_TRY(kman_rle_count(ctx, in_alt ? alt : smp, ns_, uk, uc, 4, &nu));  // (synchronises)
         if (nu == ns_) return KMAN_OK;  // every sample distinct: no heavy key
     }
+    const double t_sort = ms_since(t0);
+    const auto t1 = std::chrono::steady_clock::now();
     const uint32_t gx = (uint32_t)ceil_div(nu, 256);
     hipLaunchKernelGGL(rg_hv_select, dim3(gx), dim3(256), 0, ctx->stream, uk, uc, nu, 0u, hist, ncand, cand);
     HIP_TRY(ctx, hipGetLastError());
@@ -2496,6 +2504,8 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
         HIP_TRY(ctx, hipMemcpyAsync(ctx->h_hv, cand, (size_t)nc * 16, hipMemcpyDeviceToHost, ctx->stream));
         HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     }
+    const double t_sel = ms_since(t1);
+    const auto t2 = std::chrono::steady_clock::now();
     // per bucket of the round at most HV_BMAX keys: the most often sampled
     // (ties by key, so the tables do not depend on the atomics' order), in
     // key order; per bucket a table of their key rests and their index in keys
@@ -2537,11 +2547,17 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
             keys[m] = it->second;
         }
     }
+    const double t_build = ms_since(t2);
+    const auto t3 = std::chrono::steady_clock::now();
     HIP_TRY(ctx, hipMemcpyAsync(w + HVO_TAB, ht, tab_b, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(w + HVO_IDX, hi, idx_b, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemcpyAsync(w + HVO_KEYS, keys, (size_t)m * 8, hipMemcpyHostToDevice, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(w + HVO_DROP, 0, HV_MAX * 8, ctx->stream));
     HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (the staging is reused by the next round)
+    if (getenv("KMAN_DROUND_LOG"))
+        fprintf(stderr, "find_heavy: %llu samples, %llu distinct, %u candidates (>= %u hits), %u keys; sample + sort "
+                "%.2f ms, select %.2f, tables %.2f, upload %.2f\n", (unsigned long long)ns, (unsigned long long)nu, nc,
+                T, m, t_sort, t_sel, t_build, ms_since(t3));
     hv->n = m;
     hv->w = w;
     return KMAN_OK;
