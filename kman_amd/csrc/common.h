@@ -69,12 +69,10 @@ struct kman_ctx {
     std::vector<uint64_t> failed;
     // heavy keys of the last kman_dround_finish (counted apart in its pass 1)
     // and their scratch (table, drop counts, samples)
-    uint32_t heavy_keys = 0;
+    uint32_t heavy_keys = 0, heavy_slots = 0;
     int heavy_mode = 0;
     void *d_hv = nullptr;
     size_t hv_bytes = 0;
-    void *h_hv = nullptr;  // (pinned staging of the heavy-key tables)
-    size_t hv_host_bytes = 0;
     // the last kman_dround_finish's pass-1 output, for kman_dround_left (its
     // left-out regions' items gathered from there): valid when pass 1 lost
     // nothing; bd = the (bucket, digit) sub-buckets whose regions were left out

@@ -2232,7 +2232,6 @@ int refit_g(kman_ctx *ctx, RoundPlan &d, const uint32_t *c1, uint8_t *freg, uint
 // key's row (count mode: pass 1 kept one copy per chain, so the row exists
 // unless its region was left out, in which case the partial redo recounts
 // the whole key range from the codes).
-constexpr uint32_t HV_CAND = 1u << 17;  // candidates downloaded to pick the tables from
 
 // sample i = the item at i * S; runs (src, j) lie in src-major order, run t =
 // src * nb + j starting at rs[t] (the last run starting at or before p holds p)
@@ -2251,26 +2250,91 @@ __global__ __launch_bounds__(256) void rg_hv_sample(const uint64_t *__restrict__
     out[i] = ((uint64_t)(b_lo + lo % nb) << kb) | (in[p] >> q);
 }
 
-// hist[min(c, 63)] of the sample counts >= 2; with T > 0, the keys sampled
-// >= T times into cand (key, count), at most HV_CAND (ncand counts them all)
-__global__ __launch_bounds__(256) void rg_hv_select(const uint64_t *__restrict__ ukeys,
-                                                    const uint32_t *__restrict__ cnt, uint64_t nu, uint32_t T,
-                                                    uint32_t *__restrict__ hist, uint32_t *__restrict__ ncand,
-                                                    uint64_t *__restrict__ cand) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= nu) return;
-    const uint32_t c = cnt[i];
-    if (c < 2) return;
-    if (!T) {
-        atomicAdd(&hist[c < 63 ? c : 63], 1u);
-        return;
+// One block per bucket j of the round: its sampled keys (the run-length
+// output ukeys / cnt, sorted) seen >= 2 times, the most often sampled of them
+// (hits >= a cut-off that leaves <= HV_BMAX; the first HV_BMAX in key order
+// when more than that were sampled >= 63 times) into the bucket's table of key
+// rests (an LDS open-addressing table of HV_BSLOTS, filled by CAS, then
+// written out with each slot's index j * HV_BMAX + i into keys), *total +=
+// the keys taken
+__global__ __launch_bounds__(256) void rg_hv_build(const uint64_t *__restrict__ ukeys, const uint32_t *__restrict__ cnt,
+                                                   uint64_t nu, uint32_t b_lo, uint32_t kb, uint64_t *__restrict__ tab,
+                                                   uint32_t *__restrict__ idx, uint64_t *__restrict__ keys,
+                                                   uint32_t *__restrict__ total) {
+    __shared__ unsigned long long t_[HV_BSLOTS];
+    __shared__ uint32_t ti[HV_BSLOTS];
+    __shared__ uint32_t hist[64], wsum[4], s_cut;
+    __shared__ uint64_t s_lo, s_hi;
+    const uint32_t j = blockIdx.x, tid = threadIdx.x;
+    const int lane = lane_id(), w = tid >> 6;
+    for (uint32_t q = tid; q < HV_BSLOTS; q += 256) {
+        t_[q] = HV_EMPTY;
+        ti[q] = 0;
     }
-    if (c < T) return;
-    const uint32_t at = atomicAdd(ncand, 1u);
-    if (at < HV_CAND) {
-        cand[2 * at] = ukeys[i];
-        cand[2 * at + 1] = c;
+    if (tid < 64) hist[tid] = 0;
+    if (tid < 2) {  // the bucket's range [lo, hi) of ukeys
+        const uint64_t want = (uint64_t)(b_lo + j + tid) << kb;
+        uint64_t lo = 0, hi = nu;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (ukeys[mid] < want) lo = mid + 1;
+            else hi = mid;
+        }
+        if (tid == 0) s_lo = lo;
+        else s_hi = lo;
     }
+    __syncthreads();
+    const uint64_t lo = s_lo, hi = s_hi;
+    for (uint64_t i = lo + tid; i < hi; i += 256) {
+        const uint32_t c = cnt[i];
+        if (c >= 2) atomicAdd(&hist[c < 63 ? c : 63], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t above = 0, cut = 64;
+        for (uint32_t t = 63; t >= 2; t--) {
+            if (above + hist[t] > HV_BMAX) break;
+            above += hist[t];
+            cut = t;
+        }
+        s_cut = cut == 64 && hist[63] ? 63 : cut;  // (64: none)
+    }
+    __syncthreads();
+    const uint32_t cut = s_cut;
+    // the keys >= cut in key order, 256 at a time (cut 64: none; the
+    // bucket's table and keys are written empty all the same -- they hold a
+    // previous round's otherwise)
+    uint32_t base = 0;
+    for (uint64_t c0 = lo; cut < 64 && c0 < hi && base < HV_BMAX; c0 += 256) {
+        const uint64_t i = c0 + tid;
+        const bool take = i < hi && cnt[i] >= cut;
+        const uint64_t m = __ballot(take);
+        if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t before = 0, tot = 0;
+        for (int q = 0; q < 4; q++) {
+            before += q < w ? wsum[q] : 0u;
+            tot += wsum[q];
+        }
+        const uint32_t at = base + before + (uint32_t)__popcll(m & lanemask_lt());
+        if (take && at < HV_BMAX) {
+            const uint64_t key = ukeys[i], kr = key & ((1ull << kb) - 1);
+            uint32_t sl = hv_slot(kr);
+            while (atomicCAS(&t_[sl], (unsigned long long)HV_EMPTY, (unsigned long long)kr) != HV_EMPTY)
+                sl = (sl + 1) & (HV_BSLOTS - 1);
+            ti[sl] = j * HV_BMAX + at;
+            keys[(uint64_t)j * HV_BMAX + at] = key;
+        }
+        base += tot;
+        __syncthreads();
+    }
+    const uint32_t n = base < HV_BMAX ? base : HV_BMAX;
+    for (uint32_t q = n + tid; q < HV_BMAX; q += 256) keys[(uint64_t)j * HV_BMAX + q] = HV_EMPTY;
+    for (uint32_t q = tid; q < HV_BSLOTS; q += 256) {
+        tab[(uint64_t)j * HV_BSLOTS + q] = t_[q];
+        idx[(uint64_t)j * HV_BSLOTS + q] = ti[q];
+    }
+    if (tid == 0) atomicAdd(total, n);
 }
 
 // each heavy key's dropped copies onto its row (rows sorted by key)
@@ -2281,7 +2345,7 @@ __global__ __launch_bounds__(256) void rg_hv_fix(const uint64_t *__restrict__ ke
     const uint32_t s = blockIdx.x * 256 + threadIdx.x;
     if (s >= m) return;
     const uint64_t key = keys[s], d = drop[s];
-    if (!d || !n) return;
+    if (!d || !n || key == HV_EMPTY) return;
     uint64_t lo = 0, hi = n;  // first row >= key
     while (lo < hi) {
         const uint64_t mid = (lo + hi) >> 1;
@@ -2383,6 +2447,7 @@ __global__ __launch_bounds__(256) void rg_left_counts(const uint32_t *__restrict
 
 struct HeavyRound {
     uint32_t n = 0;  // heavy keys in the table (0: none, pass 1 as usual)
+    uint32_t slots = 0;  // the keys list's length (HV_BMAX per bucket, HV_EMPTY where unused)
     char *w = nullptr;  // kman_ctx::d_hv (HVO_* parts)
 };
 
@@ -2428,13 +2493,10 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
     const uint64_t HV_NS = 1ull << 23;
     const uint64_t S = std::max<uint64_t>(64, ceil_div(total, HV_NS));
     const uint64_t ns = ceil_div(total, S);
-    const size_t o_misc = HVO_END, o_cand = o_misc + 512, o_rs = o_cand + (size_t)HV_CAND * 16,
-                 o_s = o_rs + ceil_div(nrun * 8, 256) * 256, o_a = o_s + ns * 8, o_u = o_a + ns * 8, o_c = o_u + ns * 8,
+    const size_t o_misc = HVO_END, o_rs = o_misc + 512, o_s = o_rs + ceil_div(nrun * 8, 256) * 256, o_a = o_s + ns * 8, o_u = o_a + ns * 8, o_c = o_u + ns * 8,
                  bytes = o_c + ns * 4 + 256;
     char *w;
     KMAN_TRY(hv_buffer(ctx, bytes, &w));
-    uint64_t *cand = (uint64_t *)(w + o_cand);
-    uint32_t *hist = (uint32_t *)(w + o_misc), *ncand = hist + 64;
     uint64_t *rs = (uint64_t *)(w + o_rs), *smp = (uint64_t *)(w + o_s), *alt = (uint64_t *)(w + o_a),
              *uk = (uint64_t *)(w + o_u);
     uint32_t *uc = (uint32_t *)(w + o_c);
@@ -2442,7 +2504,6 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
     for (uint32_t src = 0; src < G; src++)
         for (uint32_t j = 0; j < nb; j++) hrs[(size_t)src * nb + j] = hb[(size_t)j * G + src];
     HIP_TRY(ctx, hipMemcpyAsync(rs, hrs.data(), nrun * 8, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemsetAsync(hist, 0, 512, ctx->stream));
     // the samples sorted and run-length counted: first 2^18 of them (every
     // S1-th item; all distinct -- uniform keys -- ends it here), then ns
     uint64_t nu = 0;
@@ -2467,98 +2528,23 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
     }
     const double t_sort = ms_since(t0);
     const auto t1 = std::chrono::steady_clock::now();
-    const uint32_t gx = (uint32_t)ceil_div(nu, 256);
-    hipLaunchKernelGGL(rg_hv_select, dim3(gx), dim3(256), 0, ctx->stream, uk, uc, nu, 0u, hist, ncand, cand);
-    HIP_TRY(ctx, hipGetLastError());
-    uint32_t hh[64];
-    HIP_TRY(ctx, hipMemcpyAsync(hh, hist, sizeof(hh), hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    // the lowest threshold >= 2 whose candidates fit HV_MAX
-    uint64_t above = 0;
-    uint32_t T = 63;
-    for (uint32_t t = 63; t >= 2; t--) {
-        if (above + hh[t] > HV_MAX) break;
-        above += hh[t];
-        T = t;
-    }
-    if (!above && hh[63]) above = hh[63];  // (more than HV_MAX keys sampled >= 63 times: HV_CAND of them)
-    if (!above) return KMAN_OK;
-    hipLaunchKernelGGL(rg_hv_select, dim3(gx), dim3(256), 0, ctx->stream, uk, uc, nu, T, hist, ncand, cand);
-    HIP_TRY(ctx, hipGetLastError());
-    uint32_t nc = 0;
-    HIP_TRY(ctx, hipMemcpyAsync(&nc, ncand, 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    nc = std::min(nc, HV_CAND);
-    // pinned staging: the candidates down, the tables up
-    const size_t tab_b = (size_t)nb * HV_BSLOTS * 8, idx_b = (size_t)nb * HV_BSLOTS * 4;
-    const size_t stage_b = std::max((size_t)HV_CAND * 16, tab_b + idx_b + (size_t)HV_MAX * 8);
-    if (stage_b > ctx->hv_host_bytes) {
-        if (ctx->h_hv) HIP_TRY(ctx, hipHostFree(ctx->h_hv));
-        ctx->h_hv = nullptr;
-        ctx->hv_host_bytes = 0;
-        HIP_TRY(ctx, hipHostMalloc(&ctx->h_hv, stage_b, hipHostMallocDefault));
-        ctx->hv_host_bytes = stage_b;
-    }
-    const uint64_t *hc = (const uint64_t *)ctx->h_hv;
-    if (nc) {
-        HIP_TRY(ctx, hipMemcpyAsync(ctx->h_hv, cand, (size_t)nc * 16, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
-    }
-    const double t_sel = ms_since(t1);
-    const auto t2 = std::chrono::steady_clock::now();
-    // per bucket of the round at most HV_BMAX keys: the most often sampled
-    // (ties by key, so the tables do not depend on the atomics' order), in
-    // key order; per bucket a table of their key rests and their index in keys
-    const uint32_t kb = d.K - B1;
-    std::vector<uint32_t> start(nb + 1, 0);
-    for (uint32_t i = 0; i < nc; i++) {
-        const uint32_t j = (uint32_t)(hc[2 * i] >> kb) - b_lo;
-        if (j < nb) start[j + 1]++;
-    }
-    for (uint32_t j = 0; j < nb; j++) start[j + 1] += start[j];
-    std::vector<std::pair<uint64_t, uint64_t>> byb(start[nb]);  // (~hits, key) grouped by bucket
-    {
-        std::vector<uint32_t> at(start.begin(), start.end() - 1);
-        for (uint32_t i = 0; i < nc; i++) {
-            const uint32_t j = (uint32_t)(hc[2 * i] >> kb) - b_lo;
-            if (j < nb) byb[at[j]++] = {~hc[2 * i + 1], hc[2 * i]};
-        }
-    }
-    uint64_t *ht = (uint64_t *)ctx->h_hv;  // (the candidates are in byb now)
-    uint32_t *hi = (uint32_t *)((char *)ctx->h_hv + tab_b);
-    uint64_t *keys = (uint64_t *)((char *)ctx->h_hv + tab_b + idx_b);
-    std::fill(ht, ht + (size_t)nb * HV_BSLOTS, HV_EMPTY);
-    uint32_t m = 0;
-    for (uint32_t j = 0; j < nb; j++) {
-        auto b0 = byb.begin() + start[j], b1 = byb.begin() + start[j + 1];
-        if (b1 - b0 > (long)HV_BMAX) {
-            std::nth_element(b0, b0 + HV_BMAX, b1);
-            b1 = b0 + HV_BMAX;
-        }
-        std::sort(b0, b1, [](const std::pair<uint64_t, uint64_t> &x, const std::pair<uint64_t, uint64_t> &y) {
-            return x.second < y.second;
-        });
-        for (auto it = b0; it != b1; ++it, ++m) {
-            const uint64_t kr = it->second & ((1ull << kb) - 1);
-            uint32_t sl = hv_slot(kr);
-            while (ht[(size_t)j * HV_BSLOTS + sl] != HV_EMPTY) sl = (sl + 1) & (HV_BSLOTS - 1);
-            ht[(size_t)j * HV_BSLOTS + sl] = kr;
-            hi[(size_t)j * HV_BSLOTS + sl] = m;
-            keys[m] = it->second;
-        }
-    }
-    const double t_build = ms_since(t2);
-    const auto t3 = std::chrono::steady_clock::now();
-    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_TAB, ht, tab_b, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_IDX, hi, idx_b, hipMemcpyHostToDevice, ctx->stream));
-    HIP_TRY(ctx, hipMemcpyAsync(w + HVO_KEYS, keys, (size_t)m * 8, hipMemcpyHostToDevice, ctx->stream));
+    // the tables built on the device (the buckets without a key sampled
+    // twice get empty ones: their chains probe and find nothing)
+    uint32_t *d_total = (uint32_t *)(w + o_misc);
+    HIP_TRY(ctx, hipMemsetAsync(d_total, 0, 4, ctx->stream));
     HIP_TRY(ctx, hipMemsetAsync(w + HVO_DROP, 0, HV_MAX * 8, ctx->stream));
-    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));  // (the staging is reused by the next round)
+    hipLaunchKernelGGL(rg_hv_build, dim3(nb), dim3(256), 0, ctx->stream, uk, uc, nu, b_lo, d.K - B1,
+                       (uint64_t *)(w + HVO_TAB), (uint32_t *)(w + HVO_IDX), (uint64_t *)(w + HVO_KEYS), d_total);
+    HIP_TRY(ctx, hipGetLastError());
+    uint32_t m = 0;
+    HIP_TRY(ctx, hipMemcpyAsync(&m, d_total, 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(ctx, hipStreamSynchronize(ctx->stream));
     if (getenv("KMAN_DROUND_LOG"))
-        fprintf(stderr, "find_heavy: %llu samples, %llu distinct, %u candidates (>= %u hits), %u keys; sample + sort "
-                "%.2f ms, select %.2f, tables %.2f, upload %.2f\n", (unsigned long long)ns, (unsigned long long)nu, nc,
-                T, m, t_sort, t_sel, t_build, ms_since(t3));
+        fprintf(stderr, "find_heavy: %llu samples, %llu distinct, %u keys; sample + sort %.2f ms, tables %.2f\n",
+                (unsigned long long)ns, (unsigned long long)nu, m, t_sort, ms_since(t1));
+    if (!m) return KMAN_OK;
     hv->n = m;
+    hv->slots = nb * HV_BMAX;
     hv->w = w;
     return KMAN_OK;
 }
@@ -2818,6 +2804,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         return kman_fail(ctx, KMAN_EHIP, "region output total not published");
     *n_out = wd & ST_VMASK;
     ctx->heavy_keys = hv.n;
+    ctx->heavy_slots = hv.slots;
     ctx->heavy_mode = mode;
     {
         // pass 1's output stays in arena A until the caller reuses it
@@ -2841,7 +2828,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     if (hv.n && mode == KMAN_FINISH_COUNT && *n_out) {
         // the heavy keys' dropped copies onto their rows
         KTimer kt_(ctx, "heavy_fix");
-        KMAN_TRY(hv_fix(ctx, hv.w, hv.n, d_okeys, d_ovals, oval_bytes, *n_out));
+        KMAN_TRY(hv_fix(ctx, hv.w, hv.slots, d_okeys, d_ovals, oval_bytes, *n_out));
         
     }
     if (!e) return KMAN_OK;
@@ -2975,7 +2962,7 @@ extern "C" int kman_dround_heavy_fix(kman_ctx *ctx, const uint64_t *d_keys, void
     if (!d_keys || !d_vals) return kman_fail(ctx, KMAN_EINVAL, "null buffer");
     if (val_bytes != 4 && val_bytes != 8) return kman_fail(ctx, KMAN_EINVAL, "val_bytes must be 4 or 8");
     HIP_TRY(ctx, hipSetDevice(ctx->device));
-    KMAN_TRY(hv_fix(ctx, (const char *)ctx->d_hv, ctx->heavy_keys, d_keys, d_vals, val_bytes, n));
+    KMAN_TRY(hv_fix(ctx, (const char *)ctx->d_hv, ctx->heavy_slots, d_keys, d_vals, val_bytes, n));
     return KMAN_OK;
 }
 

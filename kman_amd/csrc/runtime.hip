@@ -267,7 +267,6 @@ void kman_destroy(kman_ctx *ctx) {
     if (ctx->d_scratch) (void)hipFree(ctx->d_scratch);
     if (ctx->d_aux) (void)hipFree(ctx->d_aux);
     if (ctx->d_hv) (void)hipFree(ctx->d_hv);
-    if (ctx->h_hv) (void)hipHostFree(ctx->h_hv);
     if (ctx->d_counters) (void)hipFree(ctx->d_counters);
     if (ctx->d_xcounters) (void)hipFree(ctx->d_xcounters);
     if (ctx->d_cursors) (void)hipFree(ctx->d_cursors);
