@@ -197,25 +197,33 @@ def test_dist_canonical_count_and_hist(G):
 
 
 @pytest.mark.parametrize("G", [1, 2, 3])
-def test_dist_region_overflow_redoes_only_its_keys(G):
+@pytest.mark.parametrize("heavy", ["0", "1"], ids=["table-off", "table-on"])
+def test_dist_region_overflow_redoes_only_its_keys(G, heavy, monkeypatch):
     """A key repeated far more often than a region holds: its regions emit
     nothing (kman_dround_finish -> KMAN_EPARTIAL, kman_dround_failed) and only
     their key ranges go through the general path on every rank, merged into
-    the region rows; results stay exact."""
+    the region rows; results stay exact.  With the heavy-key table on
+    (KMAN_HEAVY=1) the repeat's keys are counted apart in pass 1 instead and
+    nothing overflows."""
     import inputs
 
+    monkeypatch.setenv("KMAN_HEAVY", heavy)
     rep = b"ACGTTGCAAGGCTTACGATCGATCGGATCC"
     body = inputs.SynthLayout(200_000, 4, record_len=50_000).read(0, 10**9)
     text = body + b">rep\n" + b"\n".join([rep * 2] * 30_000) + b"\n"
     for mode in ("count", "uniq"):
         outs, pipes, _ = _run(text, 21, mode, G)
         try:
-            assert sum(p.partial_rounds for p in pipes) >= 1
             assert all(p.fallback_rounds == 0 for p in pipes)
-            # only the left-out ranges were redone: the repeat's 1.8 M k-mers,
-            # not the 0.2 M of the random body
             redone, total = sum(p.redone_kmers for p in pipes), sum(p.n_kmers for p in pipes)
-            assert 0 < redone < total - 150_000
+            if heavy == "1":
+                assert sum(p.heavy_keys for p in pipes) > 0
+                assert redone < total - 150_000
+            else:
+                assert sum(p.partial_rounds for p in pipes) >= 1
+                # only the left-out ranges were redone: the repeat's 1.8 M
+                # k-mers, not the 0.2 M of the random body
+                assert 0 < redone < total - 150_000
             wk, wv = _oracle(text, 21, mode)
             for o in outs:
                 np.testing.assert_array_equal(o[0], wk)
@@ -225,9 +233,10 @@ def test_dist_region_overflow_redoes_only_its_keys(G):
 
 
 @pytest.mark.parametrize("G", [1, 3])
-def test_dist_overflow_redo_canonical_and_rc(G):
+def test_dist_overflow_redo_canonical_and_rc(G, monkeypatch):
     """The partial redo with canonical keys (config 5's count) and with -r
     uniq: left-out ranges of min(fwd, rc) keys, and of both strands."""
+    monkeypatch.setenv("KMAN_HEAVY", "0")  # (the partial redo itself; tables: test_dist_heavy_keys_counted_apart)
     import inputs
 
     rep = b"TTGACCATGACCGATTACAGATTGGC"
@@ -245,10 +254,11 @@ def test_dist_overflow_redo_canonical_and_rc(G):
 
 
 @pytest.mark.parametrize("G", [1, 3])
-def test_dist_unordered_redo_spectrum(G):
+def test_dist_unordered_redo_spectrum(G, monkeypatch):
     """ordered=False (the abundance spectrum, config 5): a redone key range is
     appended after the region rows, not merged -- the rows are the oracle's
     as a multiset and the all-reduced spectrum is exact."""
+    monkeypatch.setenv("KMAN_HEAVY", "0")  # (the partial redo itself; tables: test_dist_heavy_keys_counted_apart)
     import inputs
     from kman_amd import dist, engine
 
