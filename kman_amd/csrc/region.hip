@@ -2504,7 +2504,7 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
     for (uint32_t src = 0; src < G; src++)
         for (uint32_t j = 0; j < nb; j++) hrs[(size_t)src * nb + j] = hb[(size_t)j * G + src];
     HIP_TRY(ctx, hipMemcpyAsync(rs, hrs.data(), nrun * 8, hipMemcpyHostToDevice, ctx->stream));
-    // the samples sorted and run-length counted: first 2^18 of them (every
+    // the samples sorted and run-length counted: first 2^16 of them (every
     // S1-th item; all distinct -- uniform keys -- ends it here), then ns
     uint64_t nu = 0;
     const auto t0 = std::chrono::steady_clock::now();
@@ -2512,9 +2512,9 @@ int find_heavy(kman_ctx *ctx, const RoundPlan &d, const uint64_t *d_recv, const 
         return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
     };
     for (int stage = 0; stage < 2; stage++) {
-        const uint64_t S_ = stage ? S : std::max<uint64_t>(S, ceil_div(total, 1ull << 18)),
+        const uint64_t S_ = stage ? S : std::max<uint64_t>(S, ceil_div(total, 1ull << 16)),
                        ns_ = stage ? ns : ceil_div(total, S_);
-        if (stage && S_ == std::max<uint64_t>(S, ceil_div(total, 1ull << 18))) break;  // (stage 0 took them all)
+        if (stage && S_ == std::max<uint64_t>(S, ceil_div(total, 1ull << 16))) break;  // (stage 0 took them all)
         {
             KTimer kt_(ctx, "heavy_sample");
             hipLaunchKernelGGL(rg_hv_sample, dim3((uint32_t)ceil_div(ns_, 256)), dim3(256), 0, ctx->stream, d_recv,

@@ -264,6 +264,52 @@ def test_config4_plan_fits_one_mi355x():
             assert pl.arenas(C, cuts, R, q, r) is not None
 
 
+def test_roomy_plan_only_when_the_rounds_still_fit():
+    """KMAN_ROOMY (pass-1 sub-regions at twice the expected fill, so that a
+    left-out region can be redone from pass 1's output): kman_dround_plan's
+    arena A grows by the pass-1 sub-regions' extra room, arena B does not;
+    RoundPlanner.roomy takes it only when the same rounds fit the budget --
+    so config 4's rank shape keeps its plain plan on one MI355X -- and
+    KMAN_ROOMY=0 turns it off."""
+    import os
+    from ctypes import byref, c_uint64
+
+    from kman_amd import _native as N
+    from kman_amd import dist
+
+    L = N.lib()
+    counts = np.full(256, 12_000_000, dtype=np.uint64)
+    ab = {}
+    for fl in (0, N.KMAN_ROOMY):
+        a, b = c_uint64(0), c_uint64(0)
+        assert L.kman_dround_plan(21, fl, N.KMAN_FINISH_COUNT, 1, 3 * 10**9, 256, dist._u64p(counts), byref(a),
+                                  byref(b)) == N.KMAN_OK
+        ab[fl] = (a.value, b.value)
+    extra = ab[N.KMAN_ROOMY][0] - ab[0][0]
+    assert ab[N.KMAN_ROOMY][1] == ab[0][1]
+    # the pass-1 items (8 bytes) of every sub-region once more, about
+    assert 0.9 * 8 * counts.sum() < extra < 1.3 * 8 * counts.sum()
+    C = counts.reshape(1, 256)
+    pl = dist.RoundPlanner(21, 0, N.KMAN_FINISH_COUNT, 1, 3 * 10**9)
+    R, cuts, a, b = pl.plan(C, 1 << 40)
+    assert pl.roomy(C, cuts, R, 1 << 40, a, b) == (True, ab[N.KMAN_ROOMY][0], ab[0][1])
+    assert pl.roomy(C, cuts, R, a + b, a, b) == (False, a, b)
+    assert pl.flags == 0
+    os.environ["KMAN_ROOMY"] = "0"
+    try:
+        assert pl.roomy(C, cuts, R, 1 << 40, a, b) == (False, a, b)
+    finally:
+        del os.environ["KMAN_ROOMY"]
+    # config 4's rank shape on one MI355X: the plain plan
+    nbase = 12_500_000_000
+    G = 8
+    C4 = np.full((G, 256), nbase // 256, dtype=np.uint64)
+    budget = int(0.85 * 288 * 10**9) - nbase - 12 * (nbase + (1 << 20))
+    pl4 = dist.RoundPlanner(21, 0, N.KMAN_FINISH_COUNT, G, nbase)
+    R4, cuts4, a4, b4 = pl4.plan(C4, budget)
+    assert pl4.roomy(C4, cuts4, R4, budget, a4, b4)[0] is False
+
+
 @pytest.mark.parametrize("G,S", [(1, 4), (2, 4), (3, 2), (8, 4)])
 def test_round_pieces_partition_each_part(G, S):
     """The overlapped rounds' pieces (dist.round_pieces): each destination's
