@@ -691,7 +691,9 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
         }
         if constexpr (HV) {
             // the chain's dropped copies of each heavy key (hcnt is cleared by
-            // the next chain only after grab_tile's barriers)
+            // the next chain only after grab_tile's barriers; the barrier here
+            // keeps the index loads below from waiting on the stores above)
+            __syncthreads();
             for (uint32_t s = threadIdx.x; s < HV_BSLOTS; s += NT) {
                 const uint32_t c = hcnt[s];
                 if (c > pa.hv_keep)
