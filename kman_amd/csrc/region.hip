@@ -397,7 +397,6 @@ struct PassArgs {
 // through the partial redo)
 constexpr uint32_t HV_BSLOTS = 1024, HV_BMAX = 256, HV_MAX = 1u << 16;
 constexpr uint64_t HV_EMPTY = ~0ull;
-constexpr uint32_t HV_EMPTY_LO = ~0u;  // (keys whose low word is this are never heavy)
 __host__ __device__ inline uint32_t hv_slot(uint64_t rest) {
     return (((uint32_t)rest ^ (uint32_t)(rest >> 29)) * 0x9E3779B1u) >> 22;  // (one 32-bit multiply)
 }
@@ -468,9 +467,7 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
     __shared__ uint32_t s_items;
     __shared__ uint32_t lds_tile;
     // HV: the chain's copies of each heavy key (by table slot)
-    // (the table's key rests as low / high words: the first probe of every
-    // item reads one 4-byte word, HV_EMPTY_LO where free)
-    __shared__ uint32_t hlo[HV ? HV_BSLOTS : 1], hhi[HV ? HV_BSLOTS : 1];
+    __shared__ uint64_t htab[HV ? HV_BSLOTS : 1];
     __shared__ uint32_t hcnt[HV ? HV_BSLOTS : 1];
     const uint32_t shift = pa.shift, bits = pa.bits, nsg = pa.nsg, H = pa.H;
     const uint64_t C1 = pa.C1;
@@ -500,9 +497,7 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
         if (threadIdx.x < RB) run[threadIdx.x] = 0;
         if constexpr (HV)
             for (uint32_t s = threadIdx.x; s < HV_BSLOTS; s += NT) {
-                const uint64_t t = pa.hv_tab[(uint64_t)(b / pa.gsub) * HV_BSLOTS + s];
-                hlo[s] = (uint32_t)t;
-                hhi[s] = (uint32_t)(t >> 32);
+                htab[s] = pa.hv_tab[(uint64_t)(b / pa.gsub) * HV_BSLOTS + s];
                 hcnt[s] = 0;
             }
         __syncthreads();
@@ -598,37 +593,19 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
 #pragma unroll
             for (int i = 0; i < SI; i++) vm |= (ib + i * 64 < n ? 1u : 0u) << i;
             if constexpr (HV) {
-                // first probes of 4 items issued together; an empty first
-                // slot (most items: the tables are <= 1/4 full) ends an item
-                constexpr int PB = 4;
 #pragma unroll
-                for (int i0 = 0; i0 < SI; i0 += PB) {
-                    uint32_t sl[PB], lo[PB];
-#pragma unroll
-                    for (int u = 0; u < PB; u++) {
-                        sl[u] = hv_slot((uint64_t)key[i0 + u] >> pa.hv_q);
-                        lo[u] = hlo[sl[u]];
+                for (int i = 0; i < SI; i++) {
+                    if (!((vm >> i) & 1u)) continue;
+                    const uint64_t kr = (uint64_t)key[i] >> pa.hv_q;
+                    uint32_t sl = hv_slot(kr);
+                    uint64_t t = htab[sl];
+                    while (t != kr && t != HV_EMPTY) {  // (<= 1/4 full: short)
+                        sl = (sl + 1) & (HV_BSLOTS - 1);
+                        t = htab[sl];
                     }
-#pragma unroll
-                    for (int u = 0; u < PB; u++) {
-                        const int i = i0 + u;
-                        if (!((vm >> i) & 1u) || lo[u] == HV_EMPTY_LO) continue;
-                        const uint64_t kr = (uint64_t)key[i] >> pa.hv_q;
-                        uint32_t q = sl[u], l = lo[u];
-                        bool hit = false;
-                        for (;;) {  // (<= 1/4 full: short)
-                            if (l == (uint32_t)kr && hhi[q] == (uint32_t)(kr >> 32)) {
-                                hit = true;
-                                break;
-                            }
-                            q = (q + 1) & (HV_BSLOTS - 1);
-                            l = hlo[q];
-                            if (l == HV_EMPTY_LO) break;
-                        }
-                        if (hit) {
-                            const uint32_t old = atomicAdd(&hcnt[q], 1u);
-                            if (!(pa.hv_keep && old == 0)) vm &= ~(1u << i);
-                        }
+                    if (t == kr) {
+                        const uint32_t old = atomicAdd(&hcnt[sl], 1u);
+                        if (!(pa.hv_keep && old == 0)) vm &= ~(1u << i);
                     }
                 }
             }
@@ -2332,7 +2309,7 @@ __global__ __launch_bounds__(256) void rg_hv_build(const uint64_t *__restrict__ 
     uint32_t base = 0;
     for (uint64_t c0 = lo; cut < 64 && c0 < hi && base < HV_BMAX; c0 += 256) {
         const uint64_t i = c0 + tid;
-        const bool take = i < hi && cnt[i] >= cut && (uint32_t)ukeys[i] != HV_EMPTY_LO;
+        const bool take = i < hi && cnt[i] >= cut;
         const uint64_t m = __ballot(take);
         if (lane == 0) wsum[w] = (uint32_t)__popcll(m);
         __syncthreads();
