@@ -435,7 +435,7 @@ constexpr int PT_NT = 1024, PT_SI = 8;
 template <typename TI, typename TO, int NT_ = PT_NT, int RB = R1, bool HV = false>
 __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
                                                  uint32_t *__restrict__ err, uint64_t *__restrict__ stp) {
-    constexpr int NT = NT_, SI = PT_SI, TILE = NT * SI, NWAVE = NT / 64;
+    constexpr int NT = NT_, SI = HV ? PT_SI - 1 : PT_SI, TILE = NT * SI, NWAVE = NT / 64;  // (HV: 7 items, no spills)
     // items per write-combining line (128 bytes)
     constexpr uint32_t WLB = sizeof(TO) == 8 ? 4 : 5, WL = 1u << WLB, WM = WL - 1;
     static_assert(NT >= RB && NT / WL <= RB, "a thread per digit");
