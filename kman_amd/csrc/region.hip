@@ -397,6 +397,8 @@ struct PassArgs {
 // through the partial redo)
 constexpr uint32_t HV_BSLOTS = 1024, HV_BMAX = 256, HV_MAX = 1u << 16;
 constexpr uint64_t HV_EMPTY = ~0ull;
+constexpr uint32_t HV_FBITS = 1u << 16;
+__host__ __device__ inline uint32_t hv_fbit(uint64_t rest) { return ((uint32_t)rest * 0x85EBCA6Bu) >> 16; }
 __host__ __device__ inline uint32_t hv_slot(uint64_t rest) {
     return (((uint32_t)rest ^ (uint32_t)(rest >> 29)) * 0x9E3779B1u) >> 22;  // (one 32-bit multiply)
 }
@@ -469,6 +471,8 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
     // HV: the chain's copies of each heavy key (by table slot)
     __shared__ uint64_t htab[HV ? HV_BSLOTS : 1];
     __shared__ uint32_t hcnt[HV ? HV_BSLOTS : 1];
+    // a 2^16-bit filter of the table's keys: most items test one bit
+    __shared__ uint32_t hbits[HV ? HV_FBITS / 32 : 1];
     const uint32_t shift = pa.shift, bits = pa.bits, nsg = pa.nsg, H = pa.H;
     const uint64_t C1 = pa.C1;
     const int lane = lane_id();
@@ -495,12 +499,24 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
             if (threadIdx.x == 63) s_items = inc;
         }
         if (threadIdx.x < RB) run[threadIdx.x] = 0;
-        if constexpr (HV)
+        if constexpr (HV) {
             for (uint32_t s = threadIdx.x; s < HV_BSLOTS; s += NT) {
                 htab[s] = pa.hv_tab[(uint64_t)(b / pa.gsub) * HV_BSLOTS + s];
                 hcnt[s] = 0;
             }
+            for (uint32_t s = threadIdx.x; s < HV_FBITS / 32; s += NT) hbits[s] = 0;
+        }
         __syncthreads();
+        if constexpr (HV) {
+            for (uint32_t s = threadIdx.x; s < HV_BSLOTS; s += NT) {
+                const uint64_t t = htab[s];
+                if (t != HV_EMPTY) {
+                    const uint32_t bt = hv_fbit(t);
+                    atomicOr(&hbits[bt >> 5], 1u << (bt & 31));
+                }
+            }
+            __syncthreads();
+        }
         const uint32_t items = s_items;
         const uint32_t tiles = (items + TILE - 1) / TILE;
         const uint32_t per = (tiles + H - 1) / H;
@@ -597,6 +613,8 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
                 for (int i = 0; i < SI; i++) {
                     if (!((vm >> i) & 1u)) continue;
                     const uint64_t kr = (uint64_t)key[i] >> pa.hv_q;
+                    const uint32_t bt = hv_fbit(kr);
+                    if (!((hbits[bt >> 5] >> (bt & 31)) & 1u)) continue;
                     uint32_t sl = hv_slot(kr);
                     uint64_t t = htab[sl];
                     while (t != kr && t != HV_EMPTY) {  // (<= 1/4 full: short)
