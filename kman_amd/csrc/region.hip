@@ -609,21 +609,33 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
 #pragma unroll
             for (int i = 0; i < SI; i++) vm |= (ib + i * 64 < n ? 1u : 0u) << i;
             if constexpr (HV) {
+                // the filter over every item; then each lane probes only its
+                // candidates, one per trip (the trips: the most candidates
+                // any lane has, mostly 1 -- not one probe path per item)
+                uint32_t cm = 0;
 #pragma unroll
                 for (int i = 0; i < SI; i++) {
-                    if (!((vm >> i) & 1u)) continue;
-                    const uint64_t kr = (uint64_t)key[i] >> pa.hv_q;
-                    const uint32_t bt = hv_fbit(kr);
-                    if (!((hbits[bt >> 5] >> (bt & 31)) & 1u)) continue;
-                    uint32_t sl = hv_slot(kr);
-                    uint64_t t = htab[sl];
-                    while (t != kr && t != HV_EMPTY) {  // (<= 1/4 full: short)
-                        sl = (sl + 1) & (HV_BSLOTS - 1);
-                        t = htab[sl];
-                    }
-                    if (t == kr) {
-                        const uint32_t old = atomicAdd(&hcnt[sl], 1u);
-                        if (!(pa.hv_keep && old == 0)) vm &= ~(1u << i);
+                    const uint32_t bt = hv_fbit((uint64_t)key[i] >> pa.hv_q);
+                    cm |= (((vm >> i) & (hbits[bt >> 5] >> (bt & 31))) & 1u) << i;
+                }
+                while (__builtin_amdgcn_read_exec() & __ballot(cm != 0)) {
+                    if (cm) {
+                        const int i = __ffs(cm) - 1;
+                        cm &= cm - 1;
+                        uint64_t kk = key[0];
+#pragma unroll
+                        for (int u = 1; u < SI; u++) kk = i == u ? (uint64_t)key[u] : kk;
+                        const uint64_t kr = kk >> pa.hv_q;
+                        uint32_t sl = hv_slot(kr);
+                        uint64_t t = htab[sl];
+                        while (t != kr && t != HV_EMPTY) {  // (<= 1/4 full: short)
+                            sl = (sl + 1) & (HV_BSLOTS - 1);
+                            t = htab[sl];
+                        }
+                        if (t == kr) {
+                            const uint32_t old = atomicAdd(&hcnt[sl], 1u);
+                            if (!(pa.hv_keep && old == 0)) vm &= ~(1u << i);
+                        }
                     }
                 }
             }
