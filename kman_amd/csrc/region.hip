@@ -2780,17 +2780,30 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     {
         KMAN_TRY(kman_lookback_begin(ctx, 1, &epoch, &counter));
         KTimer kt_(ctx, "region_pass1b");
+        // count mode: a chain takes 2^m consecutive sub-buckets (their G x H
+        // sub-regions lie one after another) and sorts by the g bits and the
+        // low m bits of d above them -- the same regions, in the same order,
+        // from fewer and longer chains (a sub-bucket alone is a few tiles,
+        // whose per-chain setup and partial lines dominated); m keeps >= 1024
+        // chains, <= 64 segments, <= 8 bits, and the d bits a 4-byte item holds
+        uint32_t m = 0;
+        if (mode == KMAN_FINISH_COUNT && !getenv("KMAN_PASS1B_ONE")) {
+            const uint32_t kb = d.K - B1;
+            while (m < 5 && ((d.H * G) << (m + 1)) <= 64 && d.g + m + 1 <= 8 && ((nb * 512u) >> (m + 1)) >= 1024 &&
+                   (!narrow1 || m + 1 + (kb - 9) <= 32))
+                m++;
+        }
         PassArgs pa{};
         pa.in = r1;
         pa.seg_base = nullptr;
         pa.seg_cnt = c1;
         pa.stride = d.C1s;
-        pa.nbk = nb * 512;
-        pa.nsg = d.H * G;
+        pa.nbk = (nb * 512) >> m;
+        pa.nsg = (d.H * G) << m;
         pa.gsub = 1;
         pa.H = 1;
         pa.shift = d.Q + d.rest;
-        pa.bits = d.g;
+        pa.bits = d.g + m;
         pa.tag = mode == KMAN_FINISH_UNIQ;
         pa.tag_div = d.H;
         pa.tag_shift = d.Q + d.rest + d.g;
