@@ -2786,11 +2786,14 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         // from fewer and longer chains (a sub-bucket alone is a few tiles,
         // whose per-chain setup and partial lines dominated); m keeps >= 1024
         // chains, <= 64 segments, <= 8 bits, and the d bits a 4-byte item holds
+        // (and stops once a chain averages 64 K items: config 4's
+        // sub-buckets, ~100 K each, stay one per chain)
         uint32_t m = 0;
         if (mode == KMAN_FINISH_COUNT && !getenv("KMAN_PASS1B_ONE")) {
             const uint32_t kb = d.K - B1;
-            while (m < 5 && ((d.H * G) << (m + 1)) <= 64 && d.g + m + 1 <= 8 && ((nb * 512u) >> (m + 1)) >= 1024 &&
-                   (!narrow1 || m + 1 + (kb - 9) <= 32))
+            const uint64_t per_sub = roff / ((uint64_t)nb * 512);
+            while (m < 5 && (per_sub << m) < 65536 && ((d.H * G) << (m + 1)) <= 64 && d.g + m + 1 <= 8 &&
+                   ((nb * 512u) >> (m + 1)) >= 1024 && (!narrow1 || m + 1 + (kb - 9) <= 32))
                 m++;
         }
         PassArgs pa{};
