@@ -543,6 +543,43 @@ def test_dist_heavy_keys_counted_apart(G, mode, canonical, monkeypatch):
     assert redone["1", None] <= redone["0", None]
 
 
+def test_dist_heavy_keys_eight_ranks_canonical(monkeypatch):
+    """Config 5's shape across 8 simulated ranks: canonical counts of the
+    repeat-rich input with the heavy-key table forced on; each rank samples
+    the items it received, so the tables differ by rank -- the rows equal
+    the oracle's, in key order and as the mixed multiset, and the
+    all-reduced spectrum is exact."""
+    import inputs
+    import np_oracle
+
+    monkeypatch.setenv("KMAN_HEAVY", "1")
+    text = inputs.grch38_like(13, n_bases=2_000_000, n_records=3)
+    wk, wc = _oracle(text, 21, "count", canonical=True)
+    outs, pipes, _ = _run(text, 21, "count", 8, canonical=True)
+    try:
+        assert sum(p.heavy_keys for p in pipes) > 0
+        for keys, counts in outs:
+            np.testing.assert_array_equal(keys, wk)
+            np.testing.assert_array_equal(counts, wc)
+    finally:
+        _close(pipes)
+    outs, pipes, grp = _run(text, 21, "count", 8, canonical=True, ordered=False)
+    try:
+        mk = np_oracle.mix_keys(wk, 21)
+        o = np.argsort(mk, kind="stable")
+        for keys, counts in outs:
+            q = np.argsort(keys, kind="stable")
+            np.testing.assert_array_equal(keys[q], mk[o])
+            np.testing.assert_array_equal(counts[q], wc[o])
+        hs = grp.run(lambda p: p.hist_gen(1001))
+        want = np.bincount(np.minimum(wc.astype(np.int64), 1000), minlength=1001).astype(np.uint64)
+        want[0] = 0
+        for h in hs:
+            np.testing.assert_array_equal(h, want)
+    finally:
+        _close(pipes)
+
+
 @pytest.mark.parametrize("G", [1, 2, 3])
 @pytest.mark.parametrize("mode", ["count", "uniq"])
 @pytest.mark.parametrize("ordered", [True, False], ids=["ordered", "multiset"])
