@@ -2242,6 +2242,16 @@ int refit_g(kman_ctx *ctx, RoundPlan &d, const uint32_t *c1, uint8_t *freg, uint
     bool any = false;
     for (uint64_t j = 0; j < nbd; j++) any |= hf[j] != 0;
     *p1_lost = any;
+    if (any && getenv("KMAN_DROUND_LOG")) {
+        uint64_t nl = 0, big = 0;
+        for (uint64_t j = 0; j < nbd; j++)
+            if (hf[j]) {
+                nl++;
+                big = std::max(big, size[j]);
+            }
+        fprintf(stderr, "refit_g: pass 1 lost items in %llu of %llu sub-buckets (C1s %llu; the largest kept %llu)\n",
+                (unsigned long long)nl, (unsigned long long)nbd, (unsigned long long)d.C1s, (unsigned long long)big);
+    }
     if (any) {
         std::vector<uint8_t> fr(d.nreg, 0);
         for (uint64_t j = 0; j < nbd; j++)
