@@ -2721,7 +2721,17 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     HIP_TRY(ctx, hipMemsetAsync(freg, 0, d.nreg, ctx->stream));
     HeavyRound hv;
     const auto t_hv0 = std::chrono::steady_clock::now();
-    KMAN_TRY(find_heavy(ctx, d, d_recv, hb, roff, b_lo, &hv));
+    {
+        // (no room for the samples: the round runs without the table)
+        const int hr = find_heavy(ctx, d, d_recv, hb, roff, b_lo, &hv);
+        if (hr == KMAN_ENOMEM) {
+            hv = HeavyRound{};
+            ctx->err.clear();
+            (void)hipGetLastError();
+        } else if (hr != KMAN_OK) {
+            return hr;
+        }
+    }
     const double hv_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_hv0).count();
     uint32_t epoch, *counter;
     // 4-byte count items out of pass 1 when the key bits below its digit
@@ -2940,7 +2950,10 @@ extern "C" int kman_dround_left(kman_ctx *ctx, uint64_t *d_keys, uint64_t *d_pos
     if (bytes > ctx->hv_bytes) {
         // (grows the buffer: its heavy table is copied along)
         void *nb_ = nullptr;
-        HIP_TRY(ctx, hipMalloc(&nb_, bytes));
+        if (hipMalloc(&nb_, bytes) != hipSuccess) {  // (no room: the caller's marked-extraction redo)
+            (void)hipGetLastError();
+            return KMAN_EFALLBACK;
+        }
         if (ctx->d_hv) {
             HIP_TRY(ctx, hipMemcpyAsync(nb_, ctx->d_hv, std::min(ctx->hv_bytes, HVO_END), hipMemcpyDeviceToDevice,
                                         ctx->stream));
