@@ -72,8 +72,6 @@ constexpr uint32_t G1 = KMAN_G1;
 // CU) and GCAP (40 KiB, three blocks per CU) for the round path's small
 // regions (a pass 1b over many ranks' items leaves ~4 K per region)
 constexpr int GCAP = 5120;
-// the finish's top-bits sort with run fix-up (count keys of a long rest)
-constexpr uint32_t TOPFIX_MIN = 30, TOPFIX_RUN = 32;
 // expected region fills the plans aim at (<= T) and accept (<= M): M keeps
 // > 10 sd of a uniform fill below the capacity
 constexpr uint64_t FFILL_T = 6144, FFILL_M = 7800;
@@ -897,13 +895,6 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
     // (the round path's items carry the source rank in the 9 bits at
     // tag_shift, read as 8 bits below: bit 63 is free there as well)
     const bool early = MODE == RG_UNIQ && (!tag_shift || tag_shift + 8 <= 63) && np >= 2;
-    // TOPFIX (count, 8-byte items, a rest of >= TOPFIX_MIN bits): the top 16
-    // bits by two LSD passes, then the runs of equal top bits sorted in place
-#ifdef KMAN_NO_TOPFIX
-    constexpr bool topfix = false;  // (A/B builds: the full LSD)
-#else
-    const bool topfix = U32C && MODE == RG_COUNT && rest >= TOPFIX_MIN;
-#endif
     uint32_t etot = 0;
     uint32_t at = 0;
     uint32_t p0 = 0;
@@ -1038,125 +1029,81 @@ __global__ __launch_bounds__(FT, (fin_waves<T, ATOMIC, CAP>())) void rg_finish(
         // and read unconditional (an item past m writes its own position,
         // >= m, so no branch per item)
         uint32_t *const flat = &wh[0][0];
-        auto lsd = [&](uint32_t np_) {
-            for (uint32_t p = 0; p < np_; p++) {
-                const bool blk = p == 0;
-                const uint32_t bw = blk ? (rest - at) - 8 * (np_ - 1) : 8u;
-                const uint32_t sh = Q + at, dm = (1u << bw) - 1;
-                at += bw;
-                const uint32_t nd = 1u << bw;  // counters of the array
-                uint32_t *const wc = blk ? flat : &wh[w][0];
-                if (blk) {
-                    for (uint32_t q = t; q < nd; q += NT) flat[q] = 0;
-                    __syncthreads();
-                } else {
-    #pragma unroll
-                    for (int q = 0; q < 256 / 64; q++) wc[lane + 64 * q] = 0;
-                    __builtin_amdgcn_wave_barrier();
-                }
-                uint32_t rk[IPT];
-    #pragma unroll
-                for (int i = 0; i < IPT; i++) {
-                    const bool valid = pw + i * 64 < m;
-                    const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
-                    rk[i] = atomicAdd(&wc[valid ? d : nd + lane], 1u);
-                }
+        for (uint32_t p = 0; p < np; p++) {
+            const bool blk = p == 0;
+            const uint32_t bw = blk ? rest - 8 * (np - 1) : 8u;
+            const uint32_t sh = Q + at, dm = (1u << bw) - 1;
+            at += bw;
+            const uint32_t nd = 1u << bw;  // counters of the array
+            uint32_t *const wc = blk ? flat : &wh[w][0];
+            if (blk) {
+                for (uint32_t q = t; q < nd; q += NT) flat[q] = 0;
                 __syncthreads();
-                if (blk) {
-                    // thread t: counters [t * cp, (t + 1) * cp), cp = nd / NT (<= 4)
-                    const uint32_t cp = nd > (uint32_t)NT ? nd / NT : 1u;
-                    uint32_t c[4] = {0, 0, 0, 0};
-                    const uint32_t b0 = t * cp;
-    #pragma unroll
-                    for (uint32_t q = 0; q < 4; q++)
-                        if (q < cp && b0 + q < nd) c[q] = flat[b0 + q];
-                    uint32_t run = block_exclusive_scan1<NT>(c[0] + c[1] + c[2] + c[3], SumU32(), 0u, lds_scan,
-                                                             (uint32_t *)nullptr);
-    #pragma unroll
-                    for (uint32_t q = 0; q < 4; q++)
-                        if (q < cp && b0 + q < nd) flat[b0 + q] = run, run += c[q];
-                } else {
-                    // thread t < 256: digit t -> its total over the waves, block
-                    // scan -> digit start, each wave's first slot in place
-                    uint32_t cw[NW_], tot = 0;
-                    if (t < 256) {
-    #pragma unroll
-                        for (int ww = 0; ww < NW_; ww++) tot += (cw[ww] = wh[ww][t]);
-                    }
-                    uint32_t run = block_exclusive_scan1<NT>(t < 256 ? tot : 0u, SumU32(), 0u, lds_scan,
-                                                             (uint32_t *)nullptr);
-                    if (t < 256) {
-    #pragma unroll
-                        for (int ww = 0; ww < NW_; ww++) wh[ww][t] = run, run += cw[ww];
-                    }
-                }
-                __syncthreads();
-    #pragma unroll
-                for (int i = 0; i < IPT; i++) rk[i] += wc[(uint32_t)(x[i] >> sh) & dm];
-    #ifdef KMAN_FIN_UNCOND
-    #pragma unroll
-                for (int i = 0; i < IPT; i++) {
-                    const uint32_t pos = pw + i * 64;
-                    s[pos < m ? rk[i] : pos] = x[i];
-                }
-    #else
-                // (only the items: the slot grid past m is 12-14 % of a region's
-                // LDS, and writing it unconditionally cost more LDS cycles than
-                // the branches: 5.72 vs 5.21 ms, `r06e`)
-    #pragma unroll
-                for (int i = 0; i < IPT; i++)
-                    if (pw + i * 64 < m) s[rk[i]] = x[i];
-    #endif
-                __syncthreads();
-                if (p + 1 < np_) {
-    #pragma unroll
-                    for (int i = 0; i < IPT; i++)
-                        if (pw + i * 64 < m) x[i] = s[pw + i * 64];
-                }
-                if (early && p + 2 == np_) early_marks();
+            } else {
+#pragma unroll
+                for (int q = 0; q < 256 / 64; q++) wc[lane + 64 * q] = 0;
+                __builtin_amdgcn_wave_barrier();
             }
-        };
-        // TOPFIX: count keys of a long rest (k >= ~27): LSD by the rest's top
-        // 16 bits only (two passes), then each run of equal top bits -- a few
-        // items at most among ~8 K in a region -- sorted by its whole rest in
-        // place by the thread that holds its first item: 2 passes + that
-        // instead of 5.  A run longer than TOPFIX_RUN (repeats) sends the
-        // region through the full LSD after all.  (One call site of lsd: its
-        // copies would spill.)
-        uint32_t np_run = topfix ? 2u : np;
-        if (topfix) at = rest - 16;
-        for (int attempt = 0;; attempt++) {
-            lsd(np_run);
-            if (!topfix || attempt) break;
-            const uint64_t tmk = 0xffffull << (Q + rest - 16);
-            const uint32_t f0 = (uint32_t)t * IPT;
-            bool bad = false;
-            for (uint32_t q = f0; q < f0 + IPT && q < m; q++) {
-                const uint64_t v = (uint64_t)s[q];
-                if (q > 0 && !(((uint64_t)s[q - 1] ^ v) & tmk)) continue;  // (not a run's first item)
-                uint32_t e = q + 1;
-                while (e < m && e - q <= TOPFIX_RUN && !(((uint64_t)s[e] ^ v) & tmk)) e++;
-                if (e - q > TOPFIX_RUN) {
-                    bad = true;
-                    continue;
+            uint32_t rk[IPT];
+#pragma unroll
+            for (int i = 0; i < IPT; i++) {
+                const bool valid = pw + i * 64 < m;
+                const uint32_t d = (uint32_t)(x[i] >> sh) & dm;
+                rk[i] = atomicAdd(&wc[valid ? d : nd + lane], 1u);
+            }
+            __syncthreads();
+            if (blk) {
+                // thread t: counters [t * cp, (t + 1) * cp), cp = nd / NT (<= 4)
+                const uint32_t cp = nd > (uint32_t)NT ? nd / NT : 1u;
+                uint32_t c[4] = {0, 0, 0, 0};
+                const uint32_t b0 = t * cp;
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++)
+                    if (q < cp && b0 + q < nd) c[q] = flat[b0 + q];
+                uint32_t run = block_exclusive_scan1<NT>(c[0] + c[1] + c[2] + c[3], SumU32(), 0u, lds_scan,
+                                                         (uint32_t *)nullptr);
+#pragma unroll
+                for (uint32_t q = 0; q < 4; q++)
+                    if (q < cp && b0 + q < nd) flat[b0 + q] = run, run += c[q];
+            } else {
+                // thread t < 256: digit t -> its total over the waves, block
+                // scan -> digit start, each wave's first slot in place
+                uint32_t cw[NW_], tot = 0;
+                if (t < 256) {
+#pragma unroll
+                    for (int ww = 0; ww < NW_; ww++) tot += (cw[ww] = wh[ww][t]);
                 }
-                for (uint32_t a2 = q + 1; a2 < e; a2++) {
-                    const T u = s[a2];
-                    const uint64_t ku = ((uint64_t)u >> Q) & rmask;
-                    uint32_t b2 = a2;
-                    while (b2 > q && (((uint64_t)s[b2 - 1] >> Q) & rmask) > ku) {
-                        s[b2] = s[b2 - 1];
-                        b2--;
-                    }
-                    s[b2] = u;
+                uint32_t run = block_exclusive_scan1<NT>(t < 256 ? tot : 0u, SumU32(), 0u, lds_scan,
+                                                         (uint32_t *)nullptr);
+                if (t < 256) {
+#pragma unroll
+                    for (int ww = 0; ww < NW_; ww++) wh[ww][t] = run, run += cw[ww];
                 }
             }
-            if (!__syncthreads_or(bad)) break;  // (block-uniform)
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < IPT; i++) rk[i] += wc[(uint32_t)(x[i] >> sh) & dm];
+#ifdef KMAN_FIN_UNCOND
+#pragma unroll
+            for (int i = 0; i < IPT; i++) {
+                const uint32_t pos = pw + i * 64;
+                s[pos < m ? rk[i] : pos] = x[i];
+            }
+#else
+            // (only the items: the slot grid past m is 12-14 % of a region's
+            // LDS, and writing it unconditionally cost more LDS cycles than
+            // the branches: 5.72 vs 5.21 ms, `r06e`)
 #pragma unroll
             for (int i = 0; i < IPT; i++)
-                if (pw + i * 64 < m) x[i] = s[pw + i * 64];
-            at = 0;
-            np_run = np;
+                if (pw + i * 64 < m) s[rk[i]] = x[i];
+#endif
+            __syncthreads();
+            if (p + 1 < np) {
+#pragma unroll
+                for (int i = 0; i < IPT; i++)
+                    if (pw + i * 64 < m) x[i] = s[pw + i * 64];
+            }
+            if (early && p + 2 == np) early_marks();
         }
     }
     if constexpr (!U32C)
