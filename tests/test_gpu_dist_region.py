@@ -543,6 +543,36 @@ def test_dist_heavy_keys_counted_apart(G, mode, canonical, monkeypatch):
     assert redone["1", None] <= redone["0", None]
 
 
+@pytest.mark.parametrize("k,mode,rc", [(15, "count", False), (27, "count", False), (31, "count", False),
+                                        (21, "count", True), (21, "uniq", True), (25, "uniq", False)])
+def test_dist_heavy_keys_other_k_and_strands(k, mode, rc, monkeypatch):
+    """The heavy-key table at other widths of the key rest (k 15 .. 31: 4- and
+    8-byte pass-1 items, tables of longer rests) and with both strands (-r),
+    forced on, with every 5th region left out and redone from pass 1's
+    output, across 3 simulated ranks in 2+ rounds: the rows equal the
+    oracle's."""
+    import inputs
+    import np_oracle
+
+    monkeypatch.setenv("KMAN_HEAVY", "1")
+    monkeypatch.setenv("KMAN_TEST_LEAVE_OUT", "5")
+    monkeypatch.setenv("KMAN_DROUND_MIN_G", "1")
+    text = inputs.grch38_like(17, n_bases=800_000, n_records=2)
+    keys, pos = np_oracle.stream_kmers(np_oracle.parse_fasta(text), k, rc=rc)
+    sk, sp = np_oracle.stable_sort(keys, pos)
+    wk, wv = np_oracle.rle_count(sk) if mode == "count" else np_oracle.rle_uniq(sk, sp)
+    kw = {"rc": rc, "max_round_items": 300_000 if not rc else 600_000}
+    outs, pipes, _ = _run(text, k, mode, 3, **kw)
+    try:
+        if mode == "count":
+            assert sum(p.heavy_keys for p in pipes) > 0
+        for kk, vv in outs:
+            np.testing.assert_array_equal(kk, wk)
+            np.testing.assert_array_equal(vv, wv)
+    finally:
+        _close(pipes)
+
+
 def test_dist_heavy_keys_eight_ranks_canonical(monkeypatch):
     """Config 5's shape across 8 simulated ranks: canonical counts of the
     repeat-rich input with the heavy-key table forced on; each rank samples
