@@ -2055,6 +2055,7 @@ int make_shard_plan(uint64_t n_bases, uint64_t n_bases_q, uint32_t k, uint32_t f
 struct RoundPlan {
     uint32_t K, Q, g, rest, G, nb;
     uint32_t H;           // pass-1 chains per (bucket, source)
+    bool p1b;             // pass 1b runs (by g >= 0 bits); else the finish reads pass 1's sub-regions
     bool rc;
     uint64_t C1s, C1;     // pass-1 sub-region / pass-1b region capacities
     int cap;              // the finish's capacity: GCAP when the planned regions fit it (three blocks per CU)
@@ -2124,15 +2125,24 @@ int make_rplan(uint32_t k, uint32_t flags, int mode, uint32_t world, uint64_t n_
     // pass-1 sub-regions) when one rank's 9-bit regions already fit: with one
     // source and two chains (N > 1 needs pass 1b anyway, to tag each item with
     // its source rank for uniq and to merge the ranks' sub-regions)
+    // Pass 1b runs whenever the finish cannot read the pass-1 sub-regions
+    // itself (more than two per region: N > 1, or H > 2) -- with g = 0 bits
+    // (a pass that only merges the sources' sub-regions and tags uniq items
+    // with their rank) while a (b, d) region's expected fill is <= FFILL_M,
+    // as kman_groups keeps its 17-bit regions: N > 1 at 1 G k-mers per rank
+    // then finishes ~7.6 K-item regions, not twice as many of half the size
+    // (finish 6.3 vs 5.3 ms per 1 G uniq k-mers at world 1, KMAN_DROUND_P1B)
     uint32_t g = 0;
     {
         const char *e = getenv("KMAN_DROUND_MIN_G");  // tests: the wide pass-1b digits of huge rounds
         g = e ? (uint32_t)atoi(e) : 0u;
         g = g <= 9 ? g : 9;
     }
-    if (g == 0 && (world * d.H > 2 || (maxb >> 9) > FFILL_M)) g = 1;
-    while (g > 0 && g < 9 && ((maxb >> 9) >> g) > FFILL_T) g++;
-    if (((maxb >> 9) >> g) > FFILL_M) return KMAN_EFALLBACK;
+    const uint64_t e2f = maxb >> 9;
+    const bool p1b = g > 0 || getenv("KMAN_DROUND_P1B") != nullptr || world * d.H > 2 || e2f > FFILL_M;
+    while (p1b && g < 9 && (e2f >> g) > FFILL_T && (g > 0 || e2f > FFILL_M)) g++;
+    if ((e2f >> g) > FFILL_M) return KMAN_EFALLBACK;
+    d.p1b = p1b;
     if (d.K < B1 + 9 + g + 1) return KMAN_EFALLBACK;
     d.g = g;
     d.rest = d.K - B1 - 9 - g;
@@ -2152,8 +2162,8 @@ int make_rplan(uint32_t k, uint32_t flags, int mode, uint32_t world, uint64_t n_
     d.off_tab = ceil_div(d.off_c1 + d.nsub * 4, 64) * 64;
     d.off_fail = d.off_tab + ceil_div((uint64_t)nb * world * 12 + 64, 64) * 64;
     d.a_bytes = d.off_fail + ceil_div(d.nreg + 64, 64) * 64;
-    d.off_c2 = g ? d.nreg * d.C1 * 8 : 0;
-    d.b_bytes = g ? d.off_c2 + ceil_div(d.nreg * 4 + 64, 64) * 64 : 64;
+    d.off_c2 = p1b ? d.nreg * d.C1 * 8 : 0;
+    d.b_bytes = p1b ? d.off_c2 + ceil_div(d.nreg * 4 + 64, 64) * 64 : 64;
     *rp = d;
     return KMAN_OK;
 }
@@ -2737,7 +2747,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     // 4-byte count items out of pass 1 when the key bits below its digit
     // (rest + g, whatever refit_g makes of the split) fit 32 bits
     const bool narrow1 = narrow_ok(ctx, mode, d.Q, d.K - B1 - 9, 0) && !getenv("KMAN_WIDE_ITEMS");
-    bool p1_lost = true;  // (g = 0: the finish reads pass 1's output, whose overflow loses items)
+    bool p1_lost = true;  // (no pass 1b: the finish reads pass 1's output, whose overflow loses items)
     // pass 1: by the 9 bits below the bucket, H chains per (b, src) into
     // sub-regions (b, d, src, h)
     {
@@ -2770,7 +2780,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         HIP_TRY(ctx, hipGetLastError());
     }
     KMAN_TRY(rg_check(ctx, "pass 1", c1, d.nsub));
-    if (d.g > 0) {
+    if (d.p1b) {
         KMAN_TRY(refit_g(ctx, d, c1, freg, G, &p1_lost));
         c2 = (uint32_t *)(wb + d.off_c2);
     }
@@ -2781,7 +2791,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         HIP_TRY(ctx, hipMemsetAsync(fst, 0, d.nreg * 128, ctx->stream));
     }
 #endif
-    if (d.g == 0) {
+    if (!d.p1b) {
         // one source, two chains: the finish reads the pass-1 sub-regions
         FinishArgs f{r1, d.C1s, c1, d.Q, d.rest, (uint32_t)d.rc, (uint64_t)b_lo << 9, 0u, (uint32_t)d.nreg};
         f.fsub = d.H;
@@ -2877,7 +2887,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
     {
         // pass 1's output stays in arena A until the caller reuses it
         auto &L = ctx->left;
-        L.valid = !e || (d.g > 0 && !p1_lost);
+        L.valid = !e || (d.p1b && !p1_lost);
         L.r1 = r1;
         L.c1 = c1;
         L.C1s = d.C1s;
