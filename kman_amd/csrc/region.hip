@@ -639,8 +639,16 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
                     }
                 }
             }
+            if (!HV && bits == 0) {
+                // (a 0-bit pass, pass 1b merging the sources' sub-regions: every
+                // item to digit 0 in tile order -- no same-address atomics)
 #pragma unroll
-            for (int i = 0; i < SI; i++) rank[i] = (vm >> i) & 1u ? atomicAdd(&thist[PDIGIT(key[i])], 1u) : 0u;
+                for (int i = 0; i < SI; i++) rank[i] = ib + i * 64;
+                if (threadIdx.x == 0) thist[0] = n;
+            } else {
+#pragma unroll
+                for (int i = 0; i < SI; i++) rank[i] = (vm >> i) & 1u ? atomicAdd(&thist[PDIGIT(key[i])], 1u) : 0u;
+            }
             __syncthreads();
             const uint32_t ls = block_exclusive_scan1<NT>(threadIdx.x < RB ? thist[threadIdx.x] : 0u, SumU32(), 0u,
                                                           lds_scan, (uint32_t *)nullptr);
