@@ -2289,6 +2289,54 @@ int refit_g(kman_ctx *ctx, RoundPlan &d, const uint32_t *c1, uint8_t *freg, uint
     return KMAN_OK;
 }
 
+// ---------------------------------------------------------------- 0-bit pass 1b
+// Pass 1b with g = 0 bits is a merge: region r = (b, d) takes the G x H
+// pass-1 sub-regions (b, d, src, h) one after another (uniq: each item's d
+// field replaced by its source rank, src = segment / H, as rg_pass tags it).
+// One block per region, every item placed by its position (the segment from
+// a binary search over the <= 64 segment starts in LDS), so a block's loads
+// are independent; c2[r] = the region's size, clipped to C1 (past it the
+// region is flagged, as rg_pass flags it).
+template <typename T>
+__global__ __launch_bounds__(256) void rg_merge_regions(const T *__restrict__ in, uint64_t C1s,
+                                                        const uint32_t *__restrict__ c1, uint32_t nsg, uint32_t H,
+                                                        T *__restrict__ out, uint64_t C1, uint32_t *__restrict__ c2,
+                                                        uint8_t *__restrict__ freg, uint32_t *__restrict__ err,
+                                                        uint32_t tag, uint32_t tag_shift) {
+    __shared__ uint32_t pre[65];
+    const uint64_t r = blockIdx.x;
+    if (threadIdx.x < 64) {
+        const uint32_t c = threadIdx.x < nsg ? c1[r * nsg + threadIdx.x] : 0u;
+        const uint32_t inc = wave_inclusive_scan(c, SumU32());
+        pre[threadIdx.x] = inc - c;
+        if (threadIdx.x == 63) pre[64] = inc;
+    }
+    __syncthreads();
+    const uint32_t tot = pre[64];
+    const uint32_t lim = tot < C1 ? tot : (uint32_t)C1;
+    if (threadIdx.x == 0) {
+        c2[r] = lim;
+        if (tot > C1) {
+            freg[r] = 1;
+            atomicOr(err, ERR_REGION);
+        }
+    }
+    const uint64_t tm = tag ? 0x1ffull << tag_shift : 0ull;
+    T *const dst = out + r * C1;
+#pragma unroll 4
+    for (uint32_t p = threadIdx.x; p < lim; p += 256) {
+        uint32_t lo = 0, hi = nsg;  // the last segment starting at or before p
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (pre[mid] <= p) lo = mid;
+            else hi = mid;
+        }
+        T v = in[(r * nsg + lo) * C1s + (p - pre[lo])];
+        if (tag) v = (T)(((uint64_t)v & ~tm) | ((uint64_t)(lo / H) << tag_shift));
+        dst[p] = v;
+    }
+}
+
 // ---------------------------------------------------------------- heavy keys
 // A key round's heavy keys (PassArgs::hv_tab): every S-th received item's
 // full key is sampled, the samples sorted and run-length counted, and the
@@ -2841,6 +2889,19 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
                    ((nb * 512u) >> (m + 1)) >= 1024 && (!narrow1 || m + 1 + (kb - 9) <= 32))
                 m++;
         }
+        if (d.g == 0 && !getenv("KMAN_PASS1B_RG")) {
+            // (0 bits: a merge of the sources' sub-regions, rg_merge_regions)
+            const uint32_t nsg = d.H * G, tg = mode == KMAN_FINISH_UNIQ, ts = d.Q + d.rest;
+            if (narrow1b != narrow1) return kman_fail(ctx, KMAN_EHIP, "pass 1b: 0-bit merge changes the item width");
+            if (narrow1)
+                hipLaunchKernelGGL(rg_merge_regions<uint32_t>, dim3((uint32_t)d.nreg), dim3(256), 0, ctx->stream,
+                                   (const uint32_t *)r1, d.C1s, c1, nsg, d.H, (uint32_t *)r2, d.C1, c2, freg,
+                                   ctx->d_err, tg, ts);
+            else
+                hipLaunchKernelGGL(rg_merge_regions<uint64_t>, dim3((uint32_t)d.nreg), dim3(256), 0, ctx->stream,
+                                   (const uint64_t *)r1, d.C1s, c1, nsg, d.H, r2, d.C1, c2, freg, ctx->d_err, tg, ts);
+            HIP_TRY(ctx, hipGetLastError());
+        } else {
         PassArgs pa{};
         pa.in = r1;
         pa.seg_base = nullptr;
@@ -2864,6 +2925,7 @@ extern "C" int kman_dround_finish(kman_ctx *ctx, const uint64_t *d_recv, uint32_
         pa.fail_shift = 0;
         launch_pass(ctx, pa, counter, nullptr, narrow1, narrow1b);
         HIP_TRY(ctx, hipGetLastError());
+        }
     }
     KMAN_TRY(rg_check(ctx, "pass 1b", c2, d.nreg));
     if (const char *t = getenv("KMAN_TEST_LEAVE_OUT")) {
